@@ -1,0 +1,233 @@
+"""bench.py -- rasterizer forward+backward throughput on MI355X (BASELINE.json metric).
+
+Workload (N=1): BASELINE.json configs[2] "C3" -- 1M Gaussians, SH degree 3, 1920x1080, 16x16
+tiles, one view per step (synthetic scene per SURVEY.md §8d: frustum-uniform means, seed 0).
+One step = GaussianRasterizer forward + backward for one view (dL/dimage fixed, seed 1) through
+the drop-in package, i.e. exactly what train.py:86-93 runs on the rasterizer.  With --gpus N>1
+(torchrun, one rank per GPU, RCCL) every rank renders one view per step and the 59-float/Gaussian
+gradient bucket is all-reduced (view-parallel data parallelism, weak scaling).
+
+Output: one JSON line (rank 0) with the metric, a per-kernel HIP-event breakdown, the roofline of
+the dominant kernel and the CPU oracle baseline timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "gaussian-splatting-skysphere_amd"), ROOT]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import gs_scenes  # noqa: E402
+from diff_gaussian_rasterization import GaussianRasterizer, _C, _native  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E
+
+WORKLOADS = {
+    "c3": dict(P=1_000_000, deg=3, W=1920, H=1080, desc="C3: 1M Gaussians SH3 1920x1080, 16x16 tiles"),
+    "c2": dict(P=100_000, deg=3, W=800, H=800, desc="C2: 100k Gaussians SH3 800x800"),
+    "c1": dict(P=10_000, deg=0, W=256, H=256, desc="C1: 10k Gaussians SH0 256x256"),
+}
+
+
+def kernel_bytes(name, P, V, I, M, W, H, tiles):
+    """Algorithmic (minimum) HBM bytes of ONE launch of each kernel."""
+    npix = W * H
+    sh = 12 * M
+    return {
+        "preprocess": P * (44 + sh + 8) + V * (36 + 4 + 1),
+        "render_fwd": I * (4 + 4 + 36) + npix * 20 + tiles * 12,
+        "render_bwd": I * (4 + 4 + 36 + 36) + npix * 20 + tiles * 12,
+        "preprocess_bwd": P * (8 + 44 + sh + 1 + 32 + 24 + sh) + I * 36,
+        "duplicate": V * 24 + I * 8,
+        "ranges": I * 4 + tiles * 8,
+    }.get(name)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = all host cores, max 16)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    wl = WORKLOADS[args.workload]
+    P, deg, W, H = wl["P"], wl["deg"], wl["W"], wl["H"]
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=0)
+    settings = gs_scenes.raster_settings_for(cam, deg, device=dev)
+    d = sc.to(dev)
+    M = d.shs.shape[1]
+    params = [t.clone().requires_grad_(True) for t in (d.means3D, d.shs, d.opacities, d.scales, d.rotations)]
+    means2D = torch.zeros_like(params[0], requires_grad=True)
+    dpix = gs_scenes.dl_dimage(H, W, seed=1).to(dev)
+    rast = GaussianRasterizer(settings)
+    n_grad = sum(p.numel() for p in params)
+    flat = torch.empty((n_grad,), dtype=torch.float32, device=dev) if world > 1 else None
+
+    def step():
+        img, _ = rast(means3D=params[0], means2D=means2D, opacities=params[2], shs=params[1], scales=params[3],
+                      rotations=params[4])
+        img.backward(dpix)
+        if world > 1:
+            torch.cat([p.grad.reshape(-1) for p in params], out=flat)
+            dist.all_reduce(flat)
+        for p in params:
+            p.grad = None
+        means2D.grad = None
+
+    # workload counters (one extra forward, untimed)
+    e = torch.Tensor([])
+    num_rendered, _, radii, *_ = _C.rasterize_gaussians(
+        settings.bg, d.means3D, e, d.opacities, d.scales, d.rotations, 1.0, e, settings.viewmatrix,
+        settings.projmatrix, settings.tanfovx, settings.tanfovy, H, W, d.shs, deg, settings.campos, False, False)
+    visible = int((radii > 0).sum())
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    lib = _native.load()
+    lib.gs_profile_reset()
+    lib.gs_profile_enable(1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lib.gs_profile_enable(0)
+    prof = _native.profile_stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # render-only (no_grad forward) throughput
+    with torch.no_grad():
+        for _ in range(2):
+            rast(means3D=params[0], means2D=means2D, opacities=params[2], shs=params[1], scales=params[3],
+                 rotations=params[4])
+        torch.cuda.synchronize()
+        tr = time.perf_counter()
+        nr = max(5, args.steps // 2)
+        for _ in range(nr):
+            rast(means3D=params[0], means2D=means2D, opacities=params[2], shs=params[1], scales=params[3],
+                 rotations=params[4])
+        torch.cuda.synchronize()
+        t_render = (time.perf_counter() - tr) / nr
+
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = world * args.steps / elapsed
+
+    # per-kernel breakdown + roofline of the dominant kernel
+    kernels = {}
+    for name, (ms, n) in prof.items():
+        per_launch_ms = ms / max(n, 1)
+        b = kernel_bytes(name, P, visible, num_rendered, M, W, H, tiles)
+        kernels[name] = dict(total_ms_per_step=round(ms / args.steps, 4), launches_per_step=round(n / args.steps, 2),
+                             avg_us=round(1e3 * per_launch_ms, 2),
+                             algo_GBs=(round(b / (per_launch_ms * 1e-3) / 1e9, 1) if b else None))
+    dom = max(kernels, key=lambda k: kernels[k]["total_ms_per_step"])
+    dom_avg_ms = kernels[dom]["avg_us"] / 1e3
+    dom_bytes = kernel_bytes(dom, P, visible, num_rendered, M, W, H, tiles)
+    achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9 if dom_bytes else None
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get(args.workload, {}).get(dom)
+        except Exception:
+            traffic = None
+    roofline = dict(bound="hbm", kernel=dom, achieved=round(achieved, 1) if achieved else None, peak=HBM_PEAK_GBS,
+                    unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4) if achieved else None, traffic=traffic,
+                    algo_bytes_per_launch=dom_bytes)
+    # whole-step algorithmic bytes (P*a_G + I*a_I + Npix*a_px)
+    step_bytes = sum(kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles) or 0 for k in
+                     ("preprocess", "render_fwd", "render_bwd", "preprocess_bwd", "duplicate", "ranges"))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(sc, cam, deg, W, H, dpix.cpu(), args.cpu_threads)
+
+    out = {
+        "metric": "train iters/sec (fwd+bwd) + render Mpix/s @1080p, 1M Gaussians SH=3",
+        "value": round(value, 2),
+        "unit": "iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded; SURVEY.md §8d distribution)",
+        "config": {"workload": wl["desc"], "gaussians": P, "sh_degree": deg, "width": W, "height": H,
+                   "views_per_rank_per_step": 1, "parallelism": f"view-parallel dp{world}" +
+                   (" + RCCL all-reduce of 59 f32/Gaussian" if world > 1 else "")},
+        "render_mpix_s": round(W * H / t_render / 1e6, 1),
+        "render_ms": round(1e3 * t_render, 4),
+        "num_rendered": int(num_rendered),
+        "visible": visible,
+        "roofline": roofline,
+        "step_algo_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+        "kernels": kernels,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sc, cam, deg, W, H, dpix, threads):
+    """CPU oracle (oracle/gs_oracle.c: this repo's C restatement of the algorithm; the reference has
+    no CPU rasterizer) timed on the host for one full fwd+bwd step of the same workload."""
+    import numpy as np
+
+    from oracle import gs_oracle
+
+    gs_oracle.build()
+    n = threads or min(16, os.cpu_count() or 1)
+    gs_oracle.set_threads(n)
+    osc = gs_oracle.Scene(bg=np.zeros(3, np.float32), means3D=sc.means3D.numpy(), opacities=sc.opacities.numpy(),
+                          W=W, H=H, viewmatrix=cam.world_view_transform.numpy(),
+                          projmatrix=cam.full_proj_transform.numpy(), campos=cam.camera_center.numpy(),
+                          tanfovx=math.tan(cam.FoVx / 2), tanfovy=math.tan(cam.FoVy / 2), shs=sc.shs.numpy(),
+                          sh_degree=deg, scales=sc.scales.numpy(), rotations=sc.rotations.numpy())
+    t = time.perf_counter()
+    gs_oracle.forward(osc)
+    gs_oracle.backward(osc, dpix.numpy())
+    dt = time.perf_counter() - t
+    return {"value": round(1.0 / dt, 5), "unit": "iters/s", "cores": n, "kind": "port",
+            "sample": f"one full fwd+bwd step of the same workload ({sc.P} Gaussians, {W}x{H}), "
+                      f"{dt:.1f} s on {n} host threads"}
+
+
+if __name__ == "__main__":
+    main()

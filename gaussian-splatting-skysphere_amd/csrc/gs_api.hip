@@ -1,0 +1,395 @@
+// gs_api.hip -- C ABI (include/gsrast.h): argument validation, buffer layout, stage orchestration,
+// error capture, debug synchronisation and per-kernel HIP-event timing.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gsrast.h"
+#include "gs_internal.h"
+
+namespace gs {
+
+// ------------------------------------------------------------------------------------------
+// error / debug / timing state
+// ------------------------------------------------------------------------------------------
+static thread_local std::string t_err;
+static thread_local bool t_failed = false;
+static thread_local bool t_debug = false;
+
+static void set_error(const char* fmt, ...) {
+  if (t_failed) return;  // keep the first error
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  t_err = buf;
+  t_failed = true;
+}
+static void clear_error(int debug) {
+  t_err.clear();
+  t_failed = false;
+  t_debug = debug != 0;
+}
+
+struct ProfEntry {
+  std::string name;
+  double ms;
+  long long n;
+};
+struct Pending {
+  const char* name;
+  hipEvent_t a, b;
+};
+static std::mutex g_prof_mu;
+static bool g_prof_on = false;
+static std::vector<Pending> g_pending;
+static std::vector<hipEvent_t> g_pool;
+static std::vector<ProfEntry> g_stats;
+
+static hipEvent_t get_event() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void trace_begin(const char* name, hipStream_t st) {
+  if (!g_prof_on) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  hipEvent_t a = get_event();
+  (void)hipEventRecord(a, st);
+  g_pending.push_back(Pending{name, a, nullptr});
+}
+
+void trace_end(const char* name, hipStream_t st) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) set_error("kernel %s launch failed: %s", name, hipGetErrorString(e));
+  if (g_prof_on) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    hipEvent_t b = get_event();
+    (void)hipEventRecord(b, st);
+    if (!g_pending.empty() && g_pending.back().b == nullptr) g_pending.back().b = b;
+  }
+  if (t_debug) {
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) set_error("kernel %s failed: %s", name, hipGetErrorString(e));
+  }
+}
+
+static void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) set_error("%s failed: %s", what, hipGetErrorString(e));
+}
+
+static CameraArgs make_camera(const float* bg, int W, int H, const float* view, const float* proj, const float* campos,
+                              float tanfovx, float tanfovy, int prefiltered) {
+  CameraArgs c;
+  c.view = view;
+  c.proj = proj;
+  c.campos = campos;
+  c.bg = bg;
+  c.tanfovx = tanfovx;
+  c.tanfovy = tanfovy;
+  c.fy = (float)H / (2.0f * tanfovy);
+  c.fx = (float)W / (2.0f * tanfovx);
+  c.W = W;
+  c.H = H;
+  c.gx = (W + GS_TILE - 1) / GS_TILE;
+  c.gy = (H + GS_TILE - 1) / GS_TILE;
+  c.prefiltered = prefiltered;
+  return c;
+}
+
+static bool validate(int P, int D, int M, int W, int H, const float* means3D, const float* shs, const float* colors,
+                     const float* opac, const float* scales, const float* rots, const float* cov3D, const float* view,
+                     const float* proj, const float* campos, const float* bg, bool need_opac = true) {
+  if (P < 0) return set_error("P must be >= 0"), false;
+  if (W <= 0 || H <= 0) return set_error("image size must be positive (got %d x %d)", W, H), false;
+  if (P == 0) return true;
+  if (!means3D || (need_opac && !opac) || !view || !proj || !bg)
+    return set_error("missing required input pointer"), false;
+  if ((shs == nullptr) == (colors == nullptr))
+    return set_error("Please provide excatly one of either SHs or precomputed colors!"), false;
+  if (((scales == nullptr || rots == nullptr) && cov3D == nullptr) || ((scales || rots) && cov3D))
+    return set_error("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!"), false;
+  if (shs) {
+    if (D < 0 || D > 3) return set_error("SH degree must be in [0, 3] (got %d)", D), false;
+    if (M < (D + 1) * (D + 1)) return set_error("shs has %d coefficients, degree %d needs %d", M, D, (D + 1) * (D + 1)), false;
+    if (!campos) return set_error("campos is required with SHs"), false;
+  }
+  if ((size_t)P * 48 > ((size_t)1 << 40)) return set_error("P too large"), false;
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------
+// debug export kernel
+// ------------------------------------------------------------------------------------------
+__global__ void k_export_list(uint32_t I, const uint32_t* point_list, const uint32_t* presort_gid, uint32_t* out) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k < I) out[k] = presort_gid[point_list[k]];
+}
+__global__ void k_export_splat(int P, const float4* splat, float* xy, float* co, float* rgb, float* depth) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= P) return;
+  const float4 a = splat[3 * i], b = splat[3 * i + 1], d = splat[3 * i + 2];
+  if (xy) {
+    xy[2 * i] = a.x;
+    xy[2 * i + 1] = a.y;
+  }
+  if (co) {
+    co[4 * i] = a.z;
+    co[4 * i + 1] = a.w;
+    co[4 * i + 2] = b.x;
+    co[4 * i + 3] = b.y;
+  }
+  if (rgb) {
+    rgb[3 * i] = b.z;
+    rgb[3 * i + 1] = b.w;
+    rgb[3 * i + 2] = d.x;
+  }
+  if (depth) depth[i] = d.y;
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+extern "C" {
+
+int gs_abi_version(void) { return GSRAST_ABI_VERSION; }
+const char* gs_last_error(void) { return t_err.c_str(); }
+
+size_t gs_geom_buffer_bytes(int P) { return geom_layout((size_t)(P > 0 ? P : 1), nullptr, nullptr); }
+size_t gs_binning_buffer_bytes(long long num_rendered, int W, int H) {
+  int tiles = ((W + GS_TILE - 1) / GS_TILE) * ((H + GS_TILE - 1) / GS_TILE);
+  return bin_layout((size_t)(num_rendered > 0 ? num_rendered : 1), tiles, nullptr, nullptr);
+}
+size_t gs_image_buffer_bytes(int W, int H) { return img_layout(W, H, nullptr, nullptr); }
+size_t gs_grad_buffer_bytes(long long num_rendered) {
+  return align_up((size_t)(num_rendered > 0 ? num_rendered : 1) * GRAD_REC * sizeof(float));
+}
+
+int gs_forward_preprocess(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                          const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                          float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                          const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                          float tan_fovy, int prefiltered, int* radii_out, void* geom_buffer,
+                          long long* num_rendered_host, int debug, void* stream) {
+  clear_error(debug);
+  if (num_rendered_host) *num_rendered_host = 0;
+  if (!validate(P, D, M, W, H, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, viewmatrix,
+                projmatrix, campos, background))
+    return 1;
+  if (P == 0) return 0;
+  if (!radii_out || !geom_buffer || !num_rendered_host) return set_error("missing output pointer"), 1;
+  hipStream_t st = (hipStream_t)stream;
+  GeomPtrs geo;
+  geom_layout((size_t)P, &geo, (char*)geom_buffer);
+  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier};
+  CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, prefiltered);
+  fwd_preprocess(g, c, radii_out, geo, st);
+  fwd_order(P, geo, st);
+  uint32_t h[4] = {0, 0, 0, 0};
+  check_hip(hipMemcpyAsync(h, geo.counters, sizeof(h), hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
+  check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+  if (t_failed) return 1;
+  if (h[2] & 1u) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
+  *num_rendered_host = (long long)h[1];
+  return 0;
+}
+
+int gs_forward_render(int P, const float* background, int W, int H, const float* viewmatrix, const float* projmatrix,
+                      const float* campos, float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
+                      long long num_rendered, void* binning_buffer, void* image_buffer, float* out_color, int debug,
+                      void* stream) {
+  clear_error(debug);
+  if (P <= 0) return 0;
+  if (W <= 0 || H <= 0) return set_error("image size must be positive"), 1;
+  if (num_rendered < 0 || num_rendered > 0xFFFFFFFFll) return set_error("num_rendered out of range"), 1;
+  if (!geom_buffer || !binning_buffer || !image_buffer || !out_color || !radii)
+    return set_error("missing buffer pointer"), 1;
+  hipStream_t st = (hipStream_t)stream;
+  CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, 0);
+  GeomPtrs geo;
+  BinPtrs bin;
+  ImgPtrs img;
+  geom_layout((size_t)P, &geo, (char*)geom_buffer);
+  bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer);
+  img_layout(W, H, &img, (char*)image_buffer);
+  fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
+  fwd_render(c, geo, bin, img, out_color, st);
+  return t_failed ? 1 : 0;
+}
+
+long long gs_rasterize_forward(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                               const float* shs, const float* colors_precomp, const float* opacities,
+                               const float* scales, float scale_modifier, const float* rotations,
+                               const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                               const float* campos, float tan_fovx, float tan_fovy, int prefiltered, float* out_color,
+                               int* radii_out, gs_alloc_fn alloc, void* alloc_ctx, void** geom_out,
+                               void** binning_out, void** image_out, int debug, void* stream) {
+  if (!alloc) {
+    clear_error(debug);
+    set_error("alloc callback is NULL");
+    return -1;
+  }
+  void* geom = alloc(alloc_ctx, 0, gs_geom_buffer_bytes(P));
+  long long I = 0;
+  if (gs_forward_preprocess(P, D, M, background, W, H, means3D, shs, colors_precomp, opacities, scales,
+                            scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx,
+                            tan_fovy, prefiltered, radii_out, geom, &I, debug, stream))
+    return -1;
+  void* bin = alloc(alloc_ctx, 1, gs_binning_buffer_bytes(I, W, H));
+  void* img = alloc(alloc_ctx, 2, gs_image_buffer_bytes(W, H));
+  if (geom_out) *geom_out = geom;
+  if (binning_out) *binning_out = bin;
+  if (image_out) *image_out = img;
+  if (gs_forward_render(P, background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii_out, geom, I,
+                        bin, img, out_color, debug, stream))
+    return -1;
+  return I;
+}
+
+int gs_backward(int P, int D, int M, const float* background, int W, int H, const float* means3D, const float* shs,
+                const float* colors_precomp, const float* opacities, const float* scales, float scale_modifier,
+                const float* rotations, const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                const float* campos, float tan_fovx, float tan_fovy, const int* radii, const void* geom_buffer,
+                long long num_rendered, const void* binning_buffer, const void* image_buffer,
+                const float* dL_dout_color, void* grad_buffer, float* dL_dmeans2D, float* dL_dcolors,
+                float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                float* dL_drotations, int debug, void* stream) {
+  clear_error(debug);
+  (void)radii;
+  (void)opacities;  // the opacity is carried by the forward's splat records
+  if (!validate(P, D, M, W, H, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, viewmatrix,
+                projmatrix, campos, background, false))
+    return 1;
+  if (P == 0) return 0;
+  if (!geom_buffer || !binning_buffer || !image_buffer || !dL_dout_color || !grad_buffer)
+    return set_error("missing buffer pointer"), 1;
+  if (!dL_dmeans2D || !dL_dopacity || !dL_dmeans3D) return set_error("missing gradient output pointer"), 1;
+  if (num_rendered < 0 || num_rendered > 0xFFFFFFFFll) return set_error("num_rendered out of range"), 1;
+  hipStream_t st = (hipStream_t)stream;
+  CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, 0);
+  GeomPtrs geo;
+  BinPtrs bin;
+  ImgPtrs img;
+  geom_layout((size_t)P, &geo, (char*)geom_buffer);
+  bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer);
+  img_layout(W, H, &img, (char*)image_buffer);
+  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier};
+  float* gradrec = (float*)grad_buffer;
+  if (num_rendered > 0) bwd_render(c, geo, bin, img, dL_dout_color, gradrec, st);
+  GradOut out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, cov3D_precomp ? dL_dcov3D : nullptr,
+              shs ? dL_dsh : nullptr, cov3D_precomp ? nullptr : dL_dscales, cov3D_precomp ? nullptr : dL_drotations};
+  bwd_preprocess(g, c, geo, gradrec, out, st);
+  return t_failed ? 1 : 0;
+}
+
+int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
+                    void* stream) {
+  clear_error(0);
+  if (P < 0) return set_error("P must be >= 0"), 1;
+  if (P > 0 && (!means3D || !viewmatrix || !present)) return set_error("missing pointer"), 1;
+  mark_visible(P, means3D, viewmatrix, projmatrix, present, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
+size_t gs_knn_scratch_bytes(int P) { return knn_scratch_bytes(P); }
+
+int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, void* stream) {
+  clear_error(0);
+  if (P < 0) return set_error("P must be >= 0"), 1;
+  if (P == 0) return 0;
+  if (!points || !out || !scratch) return set_error("missing pointer"), 1;
+  knn_mean_dist2(P, points, out, (char*)scratch, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
+int gs_debug_export(int P, int W, int H, long long num_rendered, const void* geom_buffer, const void* binning_buffer,
+                    const void* image_buffer, uint32_t* point_list, uint32_t* ranges, float* xy, float* conic_opacity,
+                    float* rgb, float* depth, uint32_t* tiles_touched, float* final_T, uint32_t* n_contrib,
+                    void* stream) {
+  clear_error(0);
+  hipStream_t st = (hipStream_t)stream;
+  const int gx = (W + GS_TILE - 1) / GS_TILE, gy = (H + GS_TILE - 1) / GS_TILE;
+  if (P <= 0) return 0;
+  GeomPtrs geo;
+  BinPtrs bin;
+  ImgPtrs img;
+  geom_layout((size_t)P, &geo, (char*)geom_buffer);
+  bin_layout((size_t)num_rendered, gx * gy, &bin, (char*)binning_buffer);
+  img_layout(W, H, &img, (char*)image_buffer);
+  if (point_list && num_rendered > 0)
+    GS_LAUNCH("export_list", k_export_list, dim3((unsigned)((num_rendered + 255) / 256)), dim3(256), 0, st,
+              (uint32_t)num_rendered, bin.point_list, bin.presort_gid, point_list);
+  if (ranges) check_hip(hipMemcpyAsync(ranges, img.ranges, sizeof(uint2) * gx * gy, hipMemcpyDeviceToDevice, st), "copy");
+  if (xy || conic_opacity || rgb || depth)
+    GS_LAUNCH("export_splat", k_export_splat, dim3((P + 255) / 256), dim3(256), 0, st, P, geo.splat, xy, conic_opacity,
+              rgb, depth);
+  if (tiles_touched)
+    check_hip(hipMemcpyAsync(tiles_touched, geo.tiles, sizeof(uint32_t) * P, hipMemcpyDeviceToDevice, st), "copy");
+  if (final_T)
+    check_hip(hipMemcpyAsync(final_T, img.final_T, sizeof(float) * W * H, hipMemcpyDeviceToDevice, st), "copy");
+  if (n_contrib)
+    check_hip(hipMemcpyAsync(n_contrib, img.n_contrib, sizeof(uint32_t) * W * H, hipMemcpyDeviceToDevice, st), "copy");
+  return t_failed ? 1 : 0;
+}
+
+void gs_profile_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_on = on != 0;
+}
+
+int gs_profile_collect(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  int n = 0;
+  for (Pending& p : g_pending) {
+    if (!p.b) continue;
+    (void)hipEventSynchronize(p.b);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      bool found = false;
+      for (ProfEntry& e : g_stats)
+        if (e.name == p.name) {
+          e.ms += ms;
+          e.n += 1;
+          found = true;
+          break;
+        }
+      if (!found) g_stats.push_back(ProfEntry{p.name, (double)ms, 1});
+      n++;
+    }
+    g_pool.push_back(p.a);
+    g_pool.push_back(p.b);
+  }
+  g_pending.clear();
+  return n;
+}
+
+void gs_profile_reset(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_stats.clear();
+}
+
+int gs_profile_stat(int i, char* name, int name_len, double* total_ms, long long* launches) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  if (i < 0 || i >= (int)g_stats.size()) return 0;
+  if (name && name_len > 0) {
+    strncpy(name, g_stats[i].name.c_str(), name_len - 1);
+    name[name_len - 1] = 0;
+  }
+  if (total_ms) *total_ms = g_stats[i].ms;
+  if (launches) *launches = g_stats[i].n;
+  return 1;
+}
+
+}  // extern "C"

@@ -1,0 +1,464 @@
+// gs_backward.hip -- backward pass of the MI355X Gaussian rasterizer (gfx950).
+//
+// Restates the un-vendored upstream backward (spec SURVEY.md §8a a7-a8) without global atomics:
+//   k_render_bwd      one 256-lane workgroup per tile walks the tile's list back to front
+//                     (starting at the tile's max n_contrib -- later entries never contribute),
+//                     recovers T by division, computes the 9 per-(pixel, Gaussian) gradient terms,
+//                     sums them over each wave64 with DPP (row_bcast:15/31 tree) into an LDS slab per
+//                     wave, then sums the 4 wave slabs in fixed order and STORES one 9-float record
+//                     per (Gaussian, tile) instance at the instance's depth-ordered slot.
+//   k_preprocess_bwd  one lane per Gaussian sums its contiguous instance records (fixed order:
+//                     deterministic, no float atomics) and runs conic -> cov2D -> cov3D / mean,
+//                     projection, SH and scale/rotation gradients in one pass.
+// Upstream instead issues 9 float atomics per contributing (pixel, Gaussian) pair; on MI355X
+// per-lane scattered float atomics run at ~0.08 TB/s (MI355X_MICROARCH.md §Global float atomics),
+// while the record store + contiguous re-read moves the same information at HBM stream rates.
+#include "gs_internal.h"
+
+namespace gs {
+
+__global__ __launch_bounds__(GS_BLOCK) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
+                                                         const uint32_t* __restrict__ point_list,
+                                                         const uint32_t* __restrict__ presort_gid,
+                                                         const float4* __restrict__ splat,
+                                                         const float* __restrict__ final_T,
+                                                         const uint32_t* __restrict__ n_contrib,
+                                                         const uint32_t* __restrict__ tile_max,
+                                                         const float* __restrict__ dL_dpix,
+                                                         float* __restrict__ gradrec) {
+  __shared__ float2 s_xy[GS_BLOCK];
+  __shared__ float4 s_co[GS_BLOCK];
+  __shared__ float4 s_rgb[GS_BLOCK];
+  __shared__ uint32_t s_slot[GS_BLOCK];
+  __shared__ float s_acc[4][GRAD_REC][GS_BLOCK];
+  const uint32_t tile = blockIdx.x;
+  const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int px = tx * GS_TILE + (tid & 15), py = ty * GS_TILE + (tid >> 4);
+  const bool inside = px < c.W && py < c.H;
+  const float pfx = (float)px, pfy = (float)py;
+  const uint2 range = ranges[tile];
+  const uint32_t n = range.y - range.x;
+  const uint32_t n_eff = min(tile_max[tile], n);
+
+  // instances past the last contributor of every pixel get zero records
+  for (uint32_t e = n_eff + tid; e < n; e += GS_BLOCK) {
+    float* r = gradrec + (size_t)point_list[range.x + e] * GRAD_REC;
+#pragma unroll
+    for (int k = 0; k < GRAD_REC; k++) r[k] = 0.0f;
+  }
+
+  const size_t HW = (size_t)c.W * c.H, pix = inside ? (size_t)py * c.W + px : 0;
+  const float T_final = inside ? final_T[pix] : 0.0f;
+  float T = T_final;
+  const uint32_t last_contributor = inside ? n_contrib[pix] : 0u;
+  const float dp0 = inside ? dL_dpix[pix] : 0.0f;
+  const float dp1 = inside ? dL_dpix[HW + pix] : 0.0f;
+  const float dp2 = inside ? dL_dpix[2 * HW + pix] : 0.0f;
+  const float bg_dot = c.bg[0] * dp0 + c.bg[1] * dp1 + c.bg[2] * dp2;
+  float ar0 = 0.0f, ar1 = 0.0f, ar2 = 0.0f;  // accum_rec
+  float lc0 = 0.0f, lc1 = 0.0f, lc2 = 0.0f;  // last_color
+  float last_alpha = 0.0f;
+  const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
+  float* my_slab = &s_acc[wid][0][0];
+
+  for (uint32_t base = 0; base < n_eff; base += GS_BLOCK) {
+    const uint32_t cnt = min((uint32_t)GS_BLOCK, n_eff - base);
+    __syncthreads();
+    if ((uint32_t)tid < cnt) {
+      const uint32_t e = n_eff - 1 - (base + tid);
+      const uint32_t slot = point_list[range.x + e];
+      const uint32_t gid = presort_gid[slot];
+      const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
+      s_xy[tid] = make_float2(a.x, a.y);
+      s_co[tid] = make_float4(a.z, a.w, b.x, b.y);
+      s_rgb[tid] = make_float4(b.z, b.w, d.x, 0.0f);
+      s_slot[tid] = slot;
+    }
+    {
+      float4* z4 = reinterpret_cast<float4*>(my_slab);
+#pragma unroll
+      for (int k = 0; k < GRAD_REC * GS_BLOCK / 4 / 64; k++) z4[k * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j < cnt; j++) {
+      const uint32_t e = n_eff - 1 - (base + j);
+      bool contrib = false;
+      float v[GRAD_REC];
+#pragma unroll
+      for (int k = 0; k < GRAD_REC; k++) v[k] = 0.0f;
+      if (inside && e < last_contributor) {
+        const float2 xy = s_xy[j];
+        const float4 co = s_co[j];
+        const float dx = xy.x - pfx, dy = xy.y - pfy;
+        const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+        if (power <= 0.0f) {
+          const float G = gs_exp(power);
+          const float alpha = fminf(0.99f, co.w * G);
+          if (alpha >= 1.0f / 255.0f) {
+            contrib = true;
+            T = T / (1.f - alpha);
+            const float dchannel_dcolor = alpha * T;
+            const float4 rgb = s_rgb[j];
+            float dL_dalpha = 0.0f;
+            ar0 = last_alpha * lc0 + (1.f - last_alpha) * ar0;
+            lc0 = rgb.x;
+            dL_dalpha += (rgb.x - ar0) * dp0;
+            v[0] = dchannel_dcolor * dp0;
+            ar1 = last_alpha * lc1 + (1.f - last_alpha) * ar1;
+            lc1 = rgb.y;
+            dL_dalpha += (rgb.y - ar1) * dp1;
+            v[1] = dchannel_dcolor * dp1;
+            ar2 = last_alpha * lc2 + (1.f - last_alpha) * ar2;
+            lc2 = rgb.z;
+            dL_dalpha += (rgb.z - ar2) * dp2;
+            v[2] = dchannel_dcolor * dp2;
+            dL_dalpha *= T;
+            last_alpha = alpha;
+            dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+            const float dL_dG = co.w * dL_dalpha;
+            const float gdx = G * dx, gdy = G * dy;
+            const float dG_ddelx = -gdx * co.x - gdy * co.y;
+            const float dG_ddely = -gdy * co.z - gdx * co.y;
+            v[3] = dL_dG * dG_ddelx * ddelx_dx;
+            v[4] = dL_dG * dG_ddely * ddely_dy;
+            v[5] = -0.5f * gdx * dx * dL_dG;
+            v[6] = -0.5f * gdx * dy * dL_dG;
+            v[7] = -0.5f * gdy * dy * dL_dG;
+            v[8] = G * dL_dalpha;
+          }
+        }
+      }
+      if (__ballot(contrib) != 0) {
+#pragma unroll
+        for (int k = 0; k < GRAD_REC; k++) {
+          const float sum = wave_sum_to_lane63(v[k]);
+          if (lane == 63) my_slab[k * GS_BLOCK + j] = sum;
+        }
+      }
+    }
+    __syncthreads();
+    if ((uint32_t)tid < cnt) {
+      float* r = gradrec + (size_t)s_slot[tid] * GRAD_REC;
+#pragma unroll
+      for (int k = 0; k < GRAD_REC; k++)
+        r[k] = s_acc[0][k][tid] + s_acc[1][k][tid] + s_acc[2][k][tid] + s_acc[3][k][tid];
+    }
+  }
+}
+
+void bwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
+                const float* dL_dpix, float* gradrec, hipStream_t st) {
+  const int tiles = c.gx * c.gy;
+  GS_LAUNCH("render_bwd", k_render_bwd, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
+            bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, dL_dpix, gradrec);
+}
+
+// ------------------------------------------------------------------------------------------
+// preprocess backward
+// ------------------------------------------------------------------------------------------
+
+// SH backward for one Gaussian (order identical to oracle/gs_oracle.c sh_bwd_one).
+template <int DEG>
+__device__ __forceinline__ void sh_backward(const float* __restrict__ sh, int M, float vx, float vy, float vz,
+                                            uint32_t clamped, const float* dcol, float* __restrict__ dsh,
+                                            float* dmean) {
+  constexpr int K = (DEG + 1) * (DEG + 1);
+  const float len = sqrtf(vx * vx + vy * vy + vz * vz);
+  const float x = vx / len, y = vy / len, z = vz / len;
+  float g[3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ch++) g[ch] = ((clamped >> ch) & 1) ? 0.0f : dcol[ch];
+  float s[K * 3];
+#pragma unroll
+  for (int k = 0; k < K * 3; k++) s[k] = sh[k];
+  const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+  float b[16];
+  b[0] = SH_C0;
+  if (DEG > 0) {
+    b[1] = -SH_C1 * y;
+    b[2] = SH_C1 * z;
+    b[3] = -SH_C1 * x;
+  }
+  if (DEG > 1) {
+    b[4] = SH_C20 * xy;
+    b[5] = SH_C21 * yz;
+    b[6] = SH_C22 * (2.0f * zz - xx - yy);
+    b[7] = SH_C23 * xz;
+    b[8] = SH_C24 * (xx - yy);
+  }
+  if (DEG > 2) {
+    b[9] = (SH_C30 * y) * (3.0f * xx - yy);
+    b[10] = (SH_C31 * xy) * z;
+    b[11] = (SH_C32 * y) * (4.0f * zz - xx - yy);
+    b[12] = (SH_C33 * z) * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+    b[13] = (SH_C34 * x) * (4.0f * zz - xx - yy);
+    b[14] = (SH_C35 * z) * (xx - yy);
+    b[15] = (SH_C36 * x) * (xx - 3.0f * yy);
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++)
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) dsh[3 * k + ch] = b[k] * g[ch];
+  for (int k = 3 * K; k < 3 * M; k++) dsh[k] = 0.0f;
+  float ddx[3] = {0.f, 0.f, 0.f}, ddy[3] = {0.f, 0.f, 0.f}, ddz[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ch = 0; ch < 3; ch++) {
+#define S(k) s[3 * (k) + ch]
+    if (DEG > 0) {
+      ddx[ch] = -SH_C1 * S(3);
+      ddy[ch] = -SH_C1 * S(1);
+      ddz[ch] = SH_C1 * S(2);
+      if (DEG > 1) {
+        ddx[ch] = ddx[ch] + (SH_C20 * y) * S(4) + (SH_C22 * (-2.f * x)) * S(6) + (SH_C23 * z) * S(7) +
+                  (SH_C24 * (2.f * x)) * S(8);
+        ddy[ch] = ddy[ch] + (SH_C20 * x) * S(4) + (SH_C21 * z) * S(5) + (SH_C22 * (-2.f * y)) * S(6) +
+                  (SH_C24 * (-2.f * y)) * S(8);
+        ddz[ch] = ddz[ch] + (SH_C21 * y) * S(5) + (SH_C22 * (4.f * z)) * S(6) + (SH_C23 * x) * S(7);
+        if (DEG > 2) {
+          ddx[ch] = ddx[ch] + (SH_C30 * (6.f * xy)) * S(9) + (SH_C31 * yz) * S(10) + (SH_C32 * (-2.f * xy)) * S(11) +
+                    (SH_C33 * (-6.f * xz)) * S(12) + (SH_C34 * (-3.f * xx + 4.f * zz - yy)) * S(13) +
+                    (SH_C35 * (2.f * xz)) * S(14) + (SH_C36 * (3.f * (xx - yy))) * S(15);
+          ddy[ch] = ddy[ch] + (SH_C30 * (3.f * (xx - yy))) * S(9) + (SH_C31 * xz) * S(10) +
+                    (SH_C32 * (-3.f * yy + 4.f * zz - xx)) * S(11) + (SH_C33 * (-6.f * yz)) * S(12) +
+                    (SH_C34 * (-2.f * xy)) * S(13) + (SH_C35 * (-2.f * yz)) * S(14) + (SH_C36 * (-6.f * xy)) * S(15);
+          ddz[ch] = ddz[ch] + (SH_C31 * xy) * S(10) + (SH_C32 * (8.f * yz)) * S(11) +
+                    (SH_C33 * (3.f * (2.f * zz - xx - yy))) * S(12) + (SH_C34 * (8.f * xz)) * S(13) +
+                    (SH_C35 * (xx - yy)) * S(14);
+        }
+      }
+    }
+#undef S
+  }
+  const float d0 = ddx[0] * g[0] + ddx[1] * g[1] + ddx[2] * g[2];
+  const float d1 = ddy[0] * g[0] + ddy[1] * g[1] + ddy[2] * g[2];
+  const float d2 = ddz[0] * g[0] + ddz[1] * g[1] + ddz[2] * g[2];
+  const float sum2 = vx * vx + vy * vy + vz * vz;
+  const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+  dmean[0] = ((sum2 - vx * vx) * d0 - vy * vx * d1 - vz * vx * d2) * invsum32;
+  dmean[1] = (-vx * vy * d0 + (sum2 - vy * vy) * d1 - vz * vy * d2) * invsum32;
+  dmean[2] = (-vx * vz * d0 - vy * vz * d1 + (sum2 - vz * vz) * d2) * invsum32;
+}
+
+// cov3D backward (order identical to oracle/gs_oracle.c cov3d_bwd_one)
+__device__ __forceinline__ void cov3d_backward(float sx, float sy, float sz, float mod, float qr, float qx, float qy,
+                                               float qz, const float* dcov, float* dscale, float* drot) {
+  mat3 R = quat_rot(qr, qx, qy, qz);
+  float sv[3] = {mod * sx, mod * sy, mod * sz};
+  float m[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int a = 0; a < 3; a++) m[i][a] = sv[i] * R.m[a][i];
+  float g[3][3];
+  g[0][0] = dcov[0];
+  g[1][1] = dcov[3];
+  g[2][2] = dcov[5];
+  g[0][1] = g[1][0] = 0.5f * dcov[1];
+  g[0][2] = g[2][0] = 0.5f * dcov[2];
+  g[1][2] = g[2][1] = 0.5f * dcov[4];
+  float dm[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int a = 0; a < 3; a++) dm[i][a] = 2.0f * (m[i][0] * g[0][a] + m[i][1] * g[1][a] + m[i][2] * g[2][a]);
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    float ds = R.m[0][i] * dm[i][0] + R.m[1][i] * dm[i][1] + R.m[2][i] * dm[i][2];
+    dscale[i] = ds * mod;
+  }
+  float dR[3][3];
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int i = 0; i < 3; i++) dR[a][i] = sv[i] * dm[i][a];
+  const float r = qr, x = qx, y = qy, z = qz;
+  drot[0] = 2.f * z * (dR[1][0] - dR[0][1]) + 2.f * y * (dR[0][2] - dR[2][0]) + 2.f * x * (dR[2][1] - dR[1][2]);
+  drot[1] = 2.f * y * (dR[0][1] + dR[1][0]) + 2.f * z * (dR[0][2] + dR[2][0]) + 2.f * r * (dR[2][1] - dR[1][2]) -
+            4.f * x * (dR[1][1] + dR[2][2]);
+  drot[2] = 2.f * x * (dR[0][1] + dR[1][0]) + 2.f * r * (dR[0][2] - dR[2][0]) + 2.f * z * (dR[1][2] + dR[2][1]) -
+            4.f * y * (dR[0][0] + dR[2][2]);
+  drot[3] = 2.f * r * (dR[1][0] - dR[0][1]) + 2.f * x * (dR[0][2] + dR[2][0]) + 2.f * y * (dR[1][2] + dR[2][1]) -
+            4.f * z * (dR[0][0] + dR[1][1]);
+}
+
+template <int DEG>  // -1: colours precomputed (no SH gradient)
+__global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraArgs c,
+                                                        const uint32_t* __restrict__ tiles,
+                                                        const uint32_t* __restrict__ goff,
+                                                        const uint8_t* __restrict__ clamped,
+                                                        const float* __restrict__ gradrec, GradOut out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g.P) return;
+  const uint32_t cnt = tiles[i];
+  if (cnt == 0) {
+    // invisible: every gradient is zero (upstream: zero-initialised outputs, radii == 0 skipped)
+    out.dmean2D[3 * i] = 0.f;
+    out.dmean2D[3 * i + 1] = 0.f;
+    out.dmean2D[3 * i + 2] = 0.f;
+    if (out.dcolor) {
+      out.dcolor[3 * i] = 0.f;
+      out.dcolor[3 * i + 1] = 0.f;
+      out.dcolor[3 * i + 2] = 0.f;
+    }
+    out.dopacity[i] = 0.f;
+    out.dmean3D[3 * i] = 0.f;
+    out.dmean3D[3 * i + 1] = 0.f;
+    out.dmean3D[3 * i + 2] = 0.f;
+    if (out.dcov3D)
+      for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
+    if (out.dsh)
+      for (int k = 0; k < 3 * g.M; k++) out.dsh[(size_t)i * 3 * g.M + k] = 0.f;
+    if (out.dscale)
+      for (int k = 0; k < 3; k++) out.dscale[3 * i + k] = 0.f;
+    if (out.drot)
+      for (int k = 0; k < 4; k++) out.drot[4 * i + k] = 0.f;
+    return;
+  }
+  float a[GRAD_REC];
+#pragma unroll
+  for (int k = 0; k < GRAD_REC; k++) a[k] = 0.0f;
+  const float* rec = gradrec + (size_t)goff[i] * GRAD_REC;
+  for (uint32_t t = 0; t < cnt; t++) {
+#pragma unroll
+    for (int k = 0; k < GRAD_REC; k++) a[k] += rec[(size_t)t * GRAD_REC + k];
+  }
+  const float dcol[3] = {a[0], a[1], a[2]};
+  const float dm2x = a[3], dm2y = a[4];
+  const float dcon0 = a[5], dcon1 = a[6], dcon2 = a[7];
+  if (out.dcolor) {
+    out.dcolor[3 * i] = dcol[0];
+    out.dcolor[3 * i + 1] = dcol[1];
+    out.dcolor[3 * i + 2] = dcol[2];
+  }
+  out.dmean2D[3 * i] = dm2x;
+  out.dmean2D[3 * i + 1] = dm2y;
+  out.dmean2D[3 * i + 2] = 0.0f;
+  out.dopacity[i] = a[8];
+
+  const float px = g.means3D[3 * i], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
+  float cov3[6];
+  if (g.cov3D) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) cov3[k] = g.cov3D[6 * i + k];
+  } else {
+    cov3d(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
+          g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], cov3);
+  }
+  // conic -> cov2D -> cov3D and view-space mean
+  const Cov2D cv = cov2d(c.view, px, py, pz, cov3, c.fx, c.fy, c.tanfovx, c.tanfovy);
+  const float A = cv.a, Bv = cv.b, Cc = cv.c;
+  const float denom = A * Cc - Bv * Bv;
+  float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+  const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+  float dcv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float(*Tm)[3] = cv.T;
+  if (denom2inv != 0.0f) {
+    dL_da = denom2inv * (-Cc * Cc * dcon0 + 2.f * Bv * Cc * dcon1 + (denom - A * Cc) * dcon2);
+    dL_dc = denom2inv * (-A * A * dcon2 + 2.f * A * Bv * dcon1 + (denom - A * Cc) * dcon0);
+    dL_db = denom2inv * 2.f * (Bv * Cc * dcon0 - (denom + 2.f * Bv * Bv) * dcon1 + A * Bv * dcon2);
+    dcv[0] = Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc;
+    dcv[3] = Tm[0][1] * Tm[0][1] * dL_da + Tm[0][1] * Tm[1][1] * dL_db + Tm[1][1] * Tm[1][1] * dL_dc;
+    dcv[5] = Tm[0][2] * Tm[0][2] * dL_da + Tm[0][2] * Tm[1][2] * dL_db + Tm[1][2] * Tm[1][2] * dL_dc;
+    dcv[1] = 2.f * Tm[0][0] * Tm[0][1] * dL_da + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_db +
+             2.f * Tm[1][0] * Tm[1][1] * dL_dc;
+    dcv[2] = 2.f * Tm[0][0] * Tm[0][2] * dL_da + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_db +
+             2.f * Tm[1][0] * Tm[1][2] * dL_dc;
+    dcv[4] = 2.f * Tm[0][2] * Tm[0][1] * dL_da + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_db +
+             2.f * Tm[1][1] * Tm[1][2] * dL_dc;
+  }
+  const float V[3][3] = {{cov3[0], cov3[1], cov3[2]}, {cov3[1], cov3[3], cov3[4]}, {cov3[2], cov3[4], cov3[5]}};
+  float dT0[3], dT1[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const float tv0 = Tm[0][0] * V[r][0] + Tm[0][1] * V[r][1] + Tm[0][2] * V[r][2];
+    const float tv1 = Tm[1][0] * V[r][0] + Tm[1][1] * V[r][1] + Tm[1][2] * V[r][2];
+    dT0[r] = 2.f * tv0 * dL_da + tv1 * dL_db;
+    dT1[r] = 2.f * tv1 * dL_dc + tv0 * dL_db;
+  }
+  const float* v = c.view;
+  const float dJ00 = v[0] * dT0[0] + v[4] * dT0[1] + v[8] * dT0[2];
+  const float dJ02 = v[2] * dT0[0] + v[6] * dT0[1] + v[10] * dT0[2];
+  const float dJ11 = v[1] * dT1[0] + v[5] * dT1[1] + v[9] * dT1[2];
+  const float dJ12 = v[2] * dT1[0] + v[6] * dT1[1] + v[10] * dT1[2];
+  const float tz = 1.f / cv.tz, tz2 = tz * tz, tz3 = tz2 * tz;
+  const float dL_dtx = cv.gmx * -c.fx * tz2 * dJ02;
+  const float dL_dty = cv.gmy * -c.fy * tz2 * dJ12;
+  const float dL_dtz =
+      -c.fx * tz2 * dJ00 - c.fy * tz2 * dJ11 + (2.f * c.fx * cv.tx) * tz3 * dJ02 + (2.f * c.fy * cv.ty) * tz3 * dJ12;
+  float dmean[3];
+  dmean[0] = v[0] * dL_dtx + v[1] * dL_dty + v[2] * dL_dtz;
+  dmean[1] = v[4] * dL_dtx + v[5] * dL_dty + v[6] * dL_dtz;
+  dmean[2] = v[8] * dL_dtx + v[9] * dL_dty + v[10] * dL_dtz;
+  if (out.dcov3D)
+#pragma unroll
+    for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = dcv[k];
+  // projection: NDC mean2D -> mean3D
+  const float* P = c.proj;
+  const float hw = xf44w(P, px, py, pz);
+  const float m_w = 1.0f / (hw + 0.0000001f);
+  const float mul1 = (P[0] * px + P[4] * py + P[8] * pz + P[12]) * m_w * m_w;
+  const float mul2 = (P[1] * px + P[5] * py + P[9] * pz + P[13]) * m_w * m_w;
+  const float pm0 = (P[0] * m_w - P[3] * mul1) * dm2x + (P[1] * m_w - P[3] * mul2) * dm2y;
+  const float pm1 = (P[4] * m_w - P[7] * mul1) * dm2x + (P[5] * m_w - P[7] * mul2) * dm2y;
+  const float pm2 = (P[8] * m_w - P[11] * mul1) * dm2x + (P[9] * m_w - P[11] * mul2) * dm2y;
+  dmean[0] = dmean[0] + pm0;
+  dmean[1] = dmean[1] + pm1;
+  dmean[2] = dmean[2] + pm2;
+  if (DEG >= 0) {
+    float shm[3];
+    const float vx = px - c.campos[0], vy = py - c.campos[1], vz = pz - c.campos[2];
+    float* dsh = out.dsh + (size_t)i * 3 * g.M;
+    sh_backward<(DEG < 0 ? 0 : DEG)>(g.shs + (size_t)i * 3 * g.M, g.M, vx, vy, vz, clamped[i], dcol, dsh, shm);
+    dmean[0] = dmean[0] + shm[0];
+    dmean[1] = dmean[1] + shm[1];
+    dmean[2] = dmean[2] + shm[2];
+  }
+  out.dmean3D[3 * i] = dmean[0];
+  out.dmean3D[3 * i + 1] = dmean[1];
+  out.dmean3D[3 * i + 2] = dmean[2];
+  if (!g.cov3D && out.dscale && out.drot) {
+    float ds[3], dr[4];
+    cov3d_backward(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
+                   g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], dcv, ds, dr);
+    out.dscale[3 * i] = ds[0];
+    out.dscale[3 * i + 1] = ds[1];
+    out.dscale[3 * i + 2] = ds[2];
+    out.drot[4 * i] = dr[0];
+    out.drot[4 * i + 1] = dr[1];
+    out.drot[4 * i + 2] = dr[2];
+    out.drot[4 * i + 3] = dr[3];
+  }
+}
+
+void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const float* gradrec,
+                    const GradOut& out, hipStream_t st) {
+  if (g.P <= 0) return;
+  dim3 grid((g.P + 255) / 256), block(256);
+  const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
+  if (!sh) {
+    GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<-1>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+              gradrec, out);
+    return;
+  }
+  switch (g.D) {
+    case 0:
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<0>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+                gradrec, out);
+      break;
+    case 1:
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<1>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+                gradrec, out);
+      break;
+    case 2:
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<2>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+                gradrec, out);
+      break;
+    default:
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<3>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+                gradrec, out);
+      break;
+  }
+}
+
+}  // namespace gs

@@ -1,0 +1,208 @@
+// gs_common.h -- shared device helpers for the MI355X (gfx950, CDNA4) Gaussian rasterizer.
+//
+// Numerics contract: fp32, no implicit contraction (-ffp-contract=off),
+// every FMA explicit, fixed left-to-right operation order.  The CPU oracle (oracle/gs_oracle.c)
+// is an independent restatement of the same spec; the two agree bit-for-bit on every
+// per-Gaussian and per-pixel value of the forward pass, so every threshold decision of the
+// compositing loop (alpha < 1/255, T < 1e-4, power > 0) is identical on both sides.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GS_TILE 16
+#define GS_BLOCK 256  // pixels per tile = threads per render workgroup = 4 wave64
+#define GS_WAVE 64
+
+namespace gs {
+
+// ------------------------------------------------------------------------------------------
+// launch tracing (gs_api.cpp): error capture after every launch, optional per-launch sync
+// (settings.debug) and optional HIP-event timing per kernel name (bench / profiling).
+// ------------------------------------------------------------------------------------------
+void trace_begin(const char* name, hipStream_t st);
+void trace_end(const char* name, hipStream_t st);
+
+#define GS_LAUNCH(name, kern, grid, block, shm, st, ...)              \
+  do {                                                                \
+    ::gs::trace_begin(name, st);                                      \
+    hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__);      \
+    ::gs::trace_end(name, st);                                        \
+  } while (0)
+
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+constexpr float SH_C20 = 1.0925484305920792f, SH_C21 = -1.0925484305920792f, SH_C22 = 0.31539156525252005f,
+                SH_C23 = -1.0925484305920792f, SH_C24 = 0.5462742152960396f;
+constexpr float SH_C30 = -0.5900435899266435f, SH_C31 = 2.890611442640554f, SH_C32 = -0.4570457994644658f,
+                SH_C33 = 0.3731763325901154f, SH_C34 = -0.4570457994644658f, SH_C35 = 1.445305721320277f,
+                SH_C36 = -0.5900435899266435f;
+
+// exp(x) of the splat falloff (x = power <= 0).  Cody-Waite reduction + degree-6 minimax
+// polynomial from correctly rounded IEEE ops only: 2 mul, 1 rndne, 8 fma, 1 add, 1 shift -- about
+// the issue cost of ocml's expf, and reproducible bit-for-bit by the CPU oracle.
+__device__ __forceinline__ float gs_exp(float x) {
+  if (!(x >= -87.0f)) return 0.0f;
+  float t = x * 1.44269504088896341f;
+  float n = __builtin_rintf(t);
+  float r = __builtin_fmaf(n, -0.693359375f, x);
+  r = __builtin_fmaf(n, 2.12194440e-4f, r);
+  float z = r * r;
+  float p = 1.9875691500e-4f;
+  p = __builtin_fmaf(p, r, 1.3981999507e-3f);
+  p = __builtin_fmaf(p, r, 8.3334519073e-3f);
+  p = __builtin_fmaf(p, r, 4.1665795894e-2f);
+  p = __builtin_fmaf(p, r, 1.6666665459e-1f);
+  p = __builtin_fmaf(p, r, 5.0000001201e-1f);
+  p = __builtin_fmaf(p, z, r);
+  p = p + 1.0f;
+  int e = (int)n + 127;
+  return p * __uint_as_float((uint32_t)e << 23);
+}
+
+// m = 4x4 world_view_transform / full_proj_transform, row-major flattening of the torch tensor
+// (row-vector convention: translation in row 3; /root/reference/scene/cameras.py:54-56).
+struct float3v { float x, y, z; };
+
+__device__ __forceinline__ float3v xf43(const float* m, float px, float py, float pz) {
+  float3v o;
+  o.x = m[0] * px + m[4] * py + m[8] * pz + m[12];
+  o.y = m[1] * px + m[5] * py + m[9] * pz + m[13];
+  o.z = m[2] * px + m[6] * py + m[10] * pz + m[14];
+  return o;
+}
+__device__ __forceinline__ float xf44w(const float* m, float px, float py, float pz) {
+  return m[3] * px + m[7] * py + m[11] * pz + m[15];
+}
+
+__device__ __forceinline__ float ndc2pix(float v, int S) {
+  return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
+}
+
+// tile rectangle [rmin, rmax) touched by a splat of integer radius r centred at (x, y) (pixels)
+__device__ __forceinline__ void get_rect(float x, float y, int r, int gx, int gy, int& x0, int& y0, int& x1,
+                                         int& y1) {
+  float fr = (float)r;
+  x0 = min(gx, max(0, (int)((x - fr) / 16.0f)));
+  y0 = min(gy, max(0, (int)((y - fr) / 16.0f)));
+  x1 = min(gx, max(0, (int)((((x + fr) + 16.0f) - 1.0f) / 16.0f)));
+  y1 = min(gy, max(0, (int)((((y + fr) + 16.0f) - 1.0f) / 16.0f)));
+}
+
+// rotation of the (w, x, y, z) quaternion, un-normalised (the caller normalises:
+// /root/reference/scene/gaussian_model.py:41,100-101)
+struct mat3 { float m[3][3]; };
+__device__ __forceinline__ mat3 quat_rot(float r, float x, float y, float z) {
+  mat3 R;
+  R.m[0][0] = 1.f - 2.f * (y * y + z * z);
+  R.m[0][1] = 2.f * (x * y - r * z);
+  R.m[0][2] = 2.f * (x * z + r * y);
+  R.m[1][0] = 2.f * (x * y + r * z);
+  R.m[1][1] = 1.f - 2.f * (x * x + z * z);
+  R.m[1][2] = 2.f * (y * z - r * x);
+  R.m[2][0] = 2.f * (x * z - r * y);
+  R.m[2][1] = 2.f * (y * z + r * x);
+  R.m[2][2] = 1.f - 2.f * (x * x + y * y);
+  return R;
+}
+
+// cov3D 6-vector (xx, xy, xz, yy, yz, zz) of R diag(mod*s)^2 R^T
+__device__ __forceinline__ void cov3d(float sx, float sy, float sz, float mod, float qr, float qx, float qy,
+                                      float qz, float* cov) {
+  mat3 R = quat_rot(qr, qx, qy, qz);
+  float sv[3] = {mod * sx, mod * sy, mod * sz};
+  float m[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int a = 0; a < 3; a++) m[i][a] = sv[i] * R.m[a][i];
+#define GS_SIG(a, b) (m[0][a] * m[0][b] + m[1][a] * m[1][b] + m[2][a] * m[2][b])
+  cov[0] = GS_SIG(0, 0);
+  cov[1] = GS_SIG(0, 1);
+  cov[2] = GS_SIG(0, 2);
+  cov[3] = GS_SIG(1, 1);
+  cov[4] = GS_SIG(1, 2);
+  cov[5] = GS_SIG(2, 2);
+#undef GS_SIG
+}
+
+// EWA 2D covariance: returns (a, b, c) with the 0.3 low-pass dilation, plus the 2x3 Jacobian
+// product T = J Rw and the view-space point (clamped x, y).
+struct Cov2D {
+  float a, b, c;
+  float T[2][3];
+  float tx, ty, tz;
+  float gmx, gmy;  // 0 where the tx/tz (ty/tz) frustum clamp was active
+};
+
+__device__ __forceinline__ Cov2D cov2d(const float* view, float px, float py, float pz, const float* cov3,
+                                       float fx, float fy, float tanfovx, float tanfovy) {
+  Cov2D o;
+  float3v t = xf43(view, px, py, pz);
+  float limx = 1.3f * tanfovx, limy = 1.3f * tanfovy;
+  float txtz = t.x / t.z, tytz = t.y / t.z;
+  float cx = fminf(limx, fmaxf(-limx, txtz)), cy = fminf(limy, fmaxf(-limy, tytz));
+  o.gmx = (txtz < -limx || txtz > limx) ? 0.0f : 1.0f;
+  o.gmy = (tytz < -limy || tytz > limy) ? 0.0f : 1.0f;
+  t.x = cx * t.z;
+  t.y = cy * t.z;
+  float tz2 = t.z * t.z;
+  float J00 = fx / t.z, J02 = -(fx * t.x) / tz2;
+  float J11 = fy / t.z, J12 = -(fy * t.y) / tz2;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    o.T[0][r] = view[4 * r + 0] * J00 + view[4 * r + 2] * J02;
+    o.T[1][r] = view[4 * r + 1] * J11 + view[4 * r + 2] * J12;
+  }
+  float V[3][3] = {{cov3[0], cov3[1], cov3[2]}, {cov3[1], cov3[3], cov3[4]}, {cov3[2], cov3[4], cov3[5]}};
+  float U[2][3];
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int b = 0; b < 3; b++) U[i][b] = o.T[i][0] * V[0][b] + o.T[i][1] * V[1][b] + o.T[i][2] * V[2][b];
+  float c00 = U[0][0] * o.T[0][0] + U[0][1] * o.T[0][1] + U[0][2] * o.T[0][2];
+  float c01 = U[0][0] * o.T[1][0] + U[0][1] * o.T[1][1] + U[0][2] * o.T[1][2];
+  float c11 = U[1][0] * o.T[1][0] + U[1][1] * o.T[1][1] + U[1][2] * o.T[1][2];
+  o.a = c00 + 0.3f;
+  o.b = c01;
+  o.c = c11 + 0.3f;
+  o.tx = t.x;
+  o.ty = t.y;
+  o.tz = t.z;
+  return o;
+}
+
+// ------------------------------------------------------------------------------------------
+// wave64 helpers (CDNA: 64-lane wavefront, 64-bit ballots)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  uint32_t l = lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// DPP move helpers (gfx9 encodings: quad_perm, row_half_mirror, row_mirror, row_bcast15/31)
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF, bool BOUND_CTRL = false>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, BANK_MASK, BOUND_CTRL));
+}
+
+// Sum over the 64 lanes; the full sum lands in lane 63 (other lanes hold partials).
+// Inactive lanes must hold 0 (callers keep EXEC full and zero non-contributors).
+__device__ __forceinline__ float wave_sum_to_lane63(float v) {
+  v = v + dpp_f<0xB1>(v);        // quad_perm [1,0,3,2]
+  v = v + dpp_f<0x4E>(v);        // quad_perm [2,3,0,1]
+  v = v + dpp_f<0x141>(v);       // row_half_mirror
+  v = v + dpp_f<0x140>(v);       // row_mirror: every lane holds its row-of-16 sum
+  v = v + dpp_f<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+  v = v + dpp_f<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+__device__ __forceinline__ float readlane63(float v) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+}  // namespace gs

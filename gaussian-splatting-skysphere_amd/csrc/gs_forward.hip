@@ -1,0 +1,343 @@
+// gs_forward.hip -- forward pass of the MI355X Gaussian rasterizer (gfx950).
+//
+// Restates the un-vendored upstream forward (graphdeco-inria/diff-gaussian-rasterization,
+// /root/reference/.gitmodules:4-6; spec SURVEY.md §8a a4-a6) as:
+//   k_preprocess   one lane per Gaussian: cull, project, cov3D -> EWA cov2D -> conic, radius,
+//                  tile rectangle, SH -> RGB; writes the 48-B splat record used by render.
+//   fwd_order      visibility compaction (scan), stable 32-bit depth radix sort of the visible
+//                  Gaussians, exclusive scan of their tile counts in depth order.
+//   k_duplicate    one lane per depth-ranked Gaussian writes its (tile, slot) instances; slots of
+//                  a Gaussian are contiguous and in depth order.
+//   tile sort      stable radix sort of the instances by tile id only: because the input is
+//                  already depth-ordered (ties by Gaussian index) this equals upstream's sort by
+//                  the 64-bit key (tile << 32 | depth bits) with a ~3x smaller sort.
+//   k_ranges       per-tile [start, end) of the sorted list.
+//   k_render_fwd   one 256-lane workgroup (4 wave64) per 16x16 tile; Gaussians staged through LDS
+//                  256 at a time; front-to-back compositing with the block-wide early exit.
+#include "gs_internal.h"
+
+namespace gs {
+
+// ------------------------------------------------------------------------------------------
+// preprocess
+// ------------------------------------------------------------------------------------------
+
+// SH -> RGB for one Gaussian, channel-major evaluation order identical to oracle/gs_oracle.c
+// sh_eval_one (reference: /root/reference/utils/sh_utils.py:57-100, +0.5 and clamp_min(0) as
+// /root/reference/gaussian_renderer/__init__.py:77-78).
+template <int DEG>
+__device__ __forceinline__ void sh_to_rgb(const float* __restrict__ sh, int M, float x, float y, float z, float* rgb,
+                                          uint32_t& clamped) {
+  constexpr int K = (DEG + 1) * (DEG + 1);
+  float s[K * 3];
+  if (((M * 3) & 3) == 0) {
+    const float4* s4 = reinterpret_cast<const float4*>(sh);
+#pragma unroll
+    for (int v = 0; v < (K * 3 + 3) / 4; v++) {
+      float4 q = s4[v];
+      if (4 * v + 0 < K * 3) s[4 * v + 0] = q.x;
+      if (4 * v + 1 < K * 3) s[4 * v + 1] = q.y;
+      if (4 * v + 2 < K * 3) s[4 * v + 2] = q.z;
+      if (4 * v + 3 < K * 3) s[4 * v + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < K * 3; k++) s[k] = sh[k];
+  }
+  clamped = 0;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+#define S(k) s[3 * (k) + c]
+    float res = SH_C0 * S(0);
+    if (DEG > 0) {
+      res = res - (SH_C1 * y) * S(1) + (SH_C1 * z) * S(2) - (SH_C1 * x) * S(3);
+      if (DEG > 1) {
+        float xx = x * x, yy = y * y, zz = z * z;
+        float xy = x * y, yz = y * z, xz = x * z;
+        res = res + (SH_C20 * xy) * S(4) + (SH_C21 * yz) * S(5) + (SH_C22 * (2.0f * zz - xx - yy)) * S(6) +
+              (SH_C23 * xz) * S(7) + (SH_C24 * (xx - yy)) * S(8);
+        if (DEG > 2) {
+          res = res + ((SH_C30 * y) * (3.0f * xx - yy)) * S(9) + ((SH_C31 * xy) * z) * S(10) +
+                ((SH_C32 * y) * (4.0f * zz - xx - yy)) * S(11) +
+                ((SH_C33 * z) * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * S(12) +
+                ((SH_C34 * x) * (4.0f * zz - xx - yy)) * S(13) + ((SH_C35 * z) * (xx - yy)) * S(14) +
+                ((SH_C36 * x) * (xx - 3.0f * yy)) * S(15);
+        }
+      }
+    }
+#undef S
+    res = res + 0.5f;
+    if (res < 0.0f) clamped |= 1u << c;
+    rgb[c] = res < 0.0f ? 0.0f : res;
+  }
+}
+
+// DEG = -1: colours precomputed by the caller
+template <int DEG>
+__global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
+                                                    float4* __restrict__ splat, uint32_t* __restrict__ depth_key,
+                                                    uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
+                                                    uint32_t* __restrict__ counters) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g.P) return;
+  radii[i] = 0;
+  tiles[i] = 0;
+  const float px = g.means3D[3 * i + 0], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
+  const float3v pv = xf43(c.view, px, py, pz);
+  if (pv.z <= 0.2f) {
+    if (c.prefiltered) atomicOr(&counters[2], 1u);
+    return;
+  }
+  const float* P = c.proj;
+  const float hx = P[0] * px + P[4] * py + P[8] * pz + P[12];
+  const float hy = P[1] * px + P[5] * py + P[9] * pz + P[13];
+  const float hw = xf44w(P, px, py, pz);
+  const float pw = 1.0f / (hw + 0.0000001f);
+  const float projx = hx * pw, projy = hy * pw;
+
+  float cov3[6];
+  if (g.cov3D) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) cov3[k] = g.cov3D[6 * i + k];
+  } else {
+    cov3d(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
+          g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], cov3);
+  }
+  const Cov2D cv = cov2d(c.view, px, py, pz, cov3, c.fx, c.fy, c.tanfovx, c.tanfovy);
+  const float det = cv.a * cv.c - cv.b * cv.b;
+  if (det == 0.0f) return;
+  const float det_inv = 1.f / det;
+  const float cxx = cv.c * det_inv, cxy = -cv.b * det_inv, cyy = cv.a * det_inv;
+  const float mid = 0.5f * (cv.a + cv.c);
+  const float disc = fmaxf(0.1f, mid * mid - det);
+  const float l1 = mid + sqrtf(disc), l2 = mid - sqrtf(disc);
+  const int radius = (int)ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+  const float sx = ndc2pix(projx, c.W), sy = ndc2pix(projy, c.H);
+  int x0, y0, x1, y1;
+  get_rect(sx, sy, radius, c.gx, c.gy, x0, y0, x1, y1);
+  const int area = (x1 - x0) * (y1 - y0);
+  if (area == 0) return;
+
+  float rgb[3];
+  uint32_t cl = 0;
+  if (DEG < 0) {
+    rgb[0] = g.colors[3 * i];
+    rgb[1] = g.colors[3 * i + 1];
+    rgb[2] = g.colors[3 * i + 2];
+  } else {
+    float dx = px - c.campos[0], dy = py - c.campos[1], dz = pz - c.campos[2];
+    float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    sh_to_rgb<(DEG < 0 ? 0 : DEG)>(g.shs + (size_t)i * g.M * 3, g.M, dx / len, dy / len, dz / len, rgb, cl);
+  }
+  splat[3 * i + 0] = make_float4(sx, sy, cxx, cxy);
+  splat[3 * i + 1] = make_float4(cyy, g.opacities[i], rgb[0], rgb[1]);
+  splat[3 * i + 2] = make_float4(rgb[2], pv.z, 0.0f, 0.0f);
+  depth_key[i] = __float_as_uint(pv.z);
+  radii[i] = radius;
+  tiles[i] = (uint32_t)area;
+  clamped[i] = (uint8_t)cl;
+}
+
+void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st) {
+  (void)hipMemsetAsync(geo.counters, 0, 64, st);
+  dim3 grid((g.P + 255) / 256), block(256);
+  if (g.colors) {
+    GS_LAUNCH("preprocess", k_preprocess<-1>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+              geo.clamped, geo.counters);
+    return;
+  }
+  switch (g.D) {
+    case 0:
+      GS_LAUNCH("preprocess", k_preprocess<0>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+                geo.clamped, geo.counters);
+      break;
+    case 1:
+      GS_LAUNCH("preprocess", k_preprocess<1>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+                geo.clamped, geo.counters);
+      break;
+    case 2:
+      GS_LAUNCH("preprocess", k_preprocess<2>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+                geo.clamped, geo.counters);
+      break;
+    default:
+      GS_LAUNCH("preprocess", k_preprocess<3>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+                geo.clamped, geo.counters);
+      break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// ordering: compaction -> depth sort -> instance offsets
+// ------------------------------------------------------------------------------------------
+struct SrcVisible {
+  const uint32_t* tiles;
+  __device__ uint32_t operator()(uint32_t i) const { return tiles[i] > 0 ? 1u : 0u; }
+};
+struct DstCompact {
+  const uint32_t* depth_key;
+  uint32_t *keys, *vals;
+  __device__ void operator()(uint32_t i, uint32_t ex, uint32_t v) const {
+    if (v) {
+      keys[ex] = depth_key[i];
+      vals[ex] = i;
+    }
+  }
+};
+struct SrcTilesByRank {
+  const uint32_t *tiles, *sorted_gid;
+  __device__ uint32_t operator()(uint32_t s) const { return tiles[sorted_gid[s]]; }
+};
+
+void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
+  const uint32_t n = (uint32_t)P;
+  scan_exclusive(SrcVisible{geo.tiles}, DstCompact{geo.depth_key, geo.keys_a, geo.vals_a}, nullptr, n,
+                 geo.scan_partial, &geo.counters[0], st);
+  radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, false, &geo.counters[0], n, 32, geo.sort_scratch,
+                   st);
+  scan_exclusive(SrcTilesByRank{geo.tiles, geo.sorted_gid}, DstArray{geo.offsets}, &geo.counters[0], n,
+                 geo.scan_partial, &geo.counters[1], st);
+}
+
+// ------------------------------------------------------------------------------------------
+// binning
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* __restrict__ counters,
+                                                   const uint32_t* __restrict__ sorted_gid,
+                                                   const uint32_t* __restrict__ offsets, const int* __restrict__ radii,
+                                                   const float4* __restrict__ splat, int gx, int gy,
+                                                   uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
+                                                   uint32_t* __restrict__ presort_gid) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= P || s >= counters[0]) return;
+  const uint32_t gid = sorted_gid[s];
+  uint32_t off = offsets[s];
+  goff[gid] = off;
+  const float4 a = splat[3 * gid];
+  int x0, y0, x1, y1;
+  get_rect(a.x, a.y, radii[gid], gx, gy, x0, y0, x1, y1);
+  for (int y = y0; y < y1; y++)
+    for (int x = x0; x < x1; x++) {
+      tile_keys[off] = (uint32_t)(y * gx + x);
+      presort_gid[off] = gid;
+      off++;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __restrict__ tile, uint2* __restrict__ ranges) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= I) return;
+  const uint32_t t = tile[k];
+  if (k == 0 || tile[k - 1] != t) ranges[t].x = k;
+  if (k == I - 1 || tile[k + 1] != t) ranges[t].y = k + 1;
+}
+
+void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const GeomPtrs& geo, const BinPtrs& bin,
+             const ImgPtrs& img, hipStream_t st) {
+  const int tiles = c.gx * c.gy;
+  (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
+  if (I == 0) return;
+  GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
+            geo.sorted_gid, geo.offsets, radii, geo.splat, c.gx, c.gy, geo.goff, bin.keys_a, bin.presort_gid);
+  radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tile_bits(tiles),
+                   bin.sort_scratch, st);
+  GS_LAUNCH("ranges", k_ranges, dim3((I + 255) / 256), dim3(256), 0, st, I, bin.sorted_tile, img.ranges);
+}
+
+// ------------------------------------------------------------------------------------------
+// render forward
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uint2* __restrict__ ranges,
+                                                         const uint32_t* __restrict__ point_list,
+                                                         const uint32_t* __restrict__ presort_gid,
+                                                         const float4* __restrict__ splat, float* __restrict__ out,
+                                                         float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                                                         uint32_t* __restrict__ tile_max) {
+  __shared__ float2 s_xy[GS_BLOCK];
+  __shared__ float4 s_co[GS_BLOCK];
+  __shared__ float4 s_rgb[GS_BLOCK];
+  __shared__ uint32_t s_max;
+  const uint32_t tile = blockIdx.x;
+  const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
+  const int tid = threadIdx.x;
+  const int px = tx * GS_TILE + (tid & 15), py = ty * GS_TILE + (tid >> 4);
+  const bool inside = px < c.W && py < c.H;
+  const float pfx = (float)px, pfy = (float)py;
+  const uint2 range = ranges[tile];
+  const uint32_t n = range.y - range.x;
+  if (tid == 0) s_max = 0;
+  float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+  uint32_t contributor = 0, last = 0;
+  bool done = !inside;
+  for (uint32_t base = 0; base < n; base += GS_BLOCK) {
+    if (__syncthreads_and(done)) break;
+    if (base + tid < n) {
+      const uint32_t gid = presort_gid[point_list[range.x + base + tid]];
+      const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
+      s_xy[tid] = make_float2(a.x, a.y);
+      s_co[tid] = make_float4(a.z, a.w, b.x, b.y);
+      s_rgb[tid] = make_float4(b.z, b.w, d.x, 0.0f);
+    }
+    __syncthreads();
+    const uint32_t cnt = min((uint32_t)GS_BLOCK, n - base);
+    for (uint32_t j = 0; !done && j < cnt; j++) {
+      contributor++;
+      const float2 xy = s_xy[j];
+      const float4 co = s_co[j];
+      const float dx = xy.x - pfx, dy = xy.y - pfy;
+      const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+      if (power > 0.0f) continue;
+      const float alpha = fminf(0.99f, co.w * gs_exp(power));
+      if (alpha < 1.0f / 255.0f) continue;
+      const float test_T = T * (1.0f - alpha);
+      if (test_T < 0.0001f) {
+        done = true;
+        continue;
+      }
+      const float4 rgb = s_rgb[j];
+      C0 += rgb.x * alpha * T;
+      C1 += rgb.y * alpha * T;
+      C2 += rgb.z * alpha * T;
+      T = test_T;
+      last = contributor;
+    }
+  }
+  if (inside) {
+    const size_t pix = (size_t)py * c.W + px, HW = (size_t)c.W * c.H;
+    final_T[pix] = T;
+    n_contrib[pix] = last;
+    out[pix] = C0 + T * c.bg[0];
+    out[HW + pix] = C1 + T * c.bg[1];
+    out[2 * HW + pix] = C2 + T * c.bg[2];
+  }
+  __syncthreads();
+  if (last) atomicMax(&s_max, last);
+  __syncthreads();
+  if (tid == 0) tile_max[tile] = s_max;
+}
+
+void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
+                hipStream_t st) {
+  const int tiles = c.gx * c.gy;
+  GS_LAUNCH("render_fwd", k_render_fwd, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
+            bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
+}
+
+// ------------------------------------------------------------------------------------------
+// mark_visible (upstream checkFrustum: near-plane test, prefiltered = false)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means,
+                                                      const float* __restrict__ view, uint8_t* __restrict__ present) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= P) return;
+  const float3v pv = xf43(view, means[3 * i], means[3 * i + 1], means[3 * i + 2]);
+  present[i] = !(pv.z <= 0.2f);
+}
+
+void mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
+                  hipStream_t st) {
+  (void)proj;
+  if (P <= 0) return;
+  GS_LAUNCH("mark_visible", k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, st, P, means3D, view, present);
+}
+
+}  // namespace gs

@@ -1,0 +1,188 @@
+// gs_internal.h -- host/device shared structures of the rasterizer: argument packs and the HBM
+// layout of the three opaque state buffers that travel from forward to backward (the same role as
+// upstream's geomBuffer / binningBuffer / imgBuffer).
+//
+// Layout (all arrays 256-B aligned, structure-of-arrays except the 48-B splat record):
+//   geometry  (per Gaussian, P)      splat float4x3 | depth_key u32 | tiles u32 | goff u32 |
+//                                    clamped u8 | depth-sort keys/vals x2 u32 | offsets u32 |
+//                                    scan partials | sort scratch | counters
+//   binning   (per instance, I)      tile keys/vals x2 u32 | presort_gid u32 | sort scratch
+//   image     (per pixel / tile)     ranges uint2 | final_T f32 | n_contrib u32 | tile_max u32
+//   gradient  (per instance, I)      9 f32 per (Gaussian, tile) instance (backward scratch)
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gs_common.h"
+#include "gs_sortscan.h"
+
+namespace gs {
+
+constexpr int GRAD_REC = 9;  // dcolor(3), dmean2D(2), dconic(xx, xy, yy), dopacity
+
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct GaussianArgs {
+  int P, D, M;
+  const float* means3D;
+  const float* shs;        // [P, M, 3] or null
+  const float* colors;     // [P, 3] or null
+  const float* opacities;  // [P]
+  const float* scales;     // [P, 3] or null
+  const float* rotations;  // [P, 4] or null
+  const float* cov3D;      // [P, 6] or null
+  float scale_modifier;
+};
+
+struct CameraArgs {
+  const float* view;    // 16, device
+  const float* proj;    // 16, device
+  const float* campos;  // 3, device
+  const float* bg;      // 3, device
+  float tanfovx, tanfovy, fx, fy;
+  int W, H, gx, gy;
+  int prefiltered;
+};
+
+struct GeomPtrs {
+  float4* splat;  // 3 per Gaussian: (x, y, cxx, cxy) (cyy, opacity, r, g) (b, depth, -, -)
+  uint32_t* depth_key;
+  uint32_t* tiles;
+  uint32_t* goff;  // first instance slot of each visible Gaussian (depth order)
+  uint8_t* clamped;
+  uint32_t *keys_a, *vals_a, *keys_b, *vals_b;
+  uint32_t* offsets;  // per depth rank
+  uint32_t* scan_partial;
+  uint32_t* sort_scratch;
+  uint32_t* counters;  // [0] visible V, [1] instances I, [2] error flags
+  uint32_t* sorted_gid;  // = vals_a or vals_b after the depth sort
+};
+
+inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += align_up(bytes);
+    return o;
+  };
+  size_t Pn = P ? P : 1;
+  size_t o_splat = take(Pn * 48);
+  size_t o_dkey = take(Pn * 4), o_tiles = take(Pn * 4), o_goff = take(Pn * 4), o_cl = take(Pn);
+  size_t o_ka = take(Pn * 4), o_va = take(Pn * 4), o_kb = take(Pn * 4), o_vb = take(Pn * 4);
+  size_t o_offs = take(Pn * 4);
+  size_t o_sp = take((size_t)scan_plan(Pn).nb * 4 + 64);
+  size_t o_ss = take(sort_scratch_words(Pn) * 4);
+  size_t o_cnt = take(64);
+  if (out && base) {
+    out->splat = (float4*)(base + o_splat);
+    out->depth_key = (uint32_t*)(base + o_dkey);
+    out->tiles = (uint32_t*)(base + o_tiles);
+    out->goff = (uint32_t*)(base + o_goff);
+    out->clamped = (uint8_t*)(base + o_cl);
+    out->keys_a = (uint32_t*)(base + o_ka);
+    out->vals_a = (uint32_t*)(base + o_va);
+    out->keys_b = (uint32_t*)(base + o_kb);
+    out->vals_b = (uint32_t*)(base + o_vb);
+    out->offsets = (uint32_t*)(base + o_offs);
+    out->scan_partial = (uint32_t*)(base + o_sp);
+    out->sort_scratch = (uint32_t*)(base + o_ss);
+    out->counters = (uint32_t*)(base + o_cnt);
+    out->sorted_gid = (radix_passes(32) % 2 == 0) ? out->vals_a : out->vals_b;
+  }
+  return off;
+}
+
+struct BinPtrs {
+  uint32_t *keys_a, *vals_a, *keys_b, *vals_b;
+  uint32_t* presort_gid;
+  uint32_t* sort_scratch;
+  uint32_t* point_list;  // sorted presort slots (= vals_a or vals_b after the tile sort)
+  uint32_t* sorted_tile;
+};
+
+inline int tile_bits(int tiles) {
+  int b = 1;
+  while (b < 32 && ((uint64_t)1 << b) < (uint64_t)tiles) b++;
+  return b;
+}
+
+inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += align_up(bytes);
+    return o;
+  };
+  size_t In = I ? I : 1;
+  size_t o_ka = take(In * 4), o_va = take(In * 4), o_kb = take(In * 4), o_vb = take(In * 4);
+  size_t o_pg = take(In * 4);
+  size_t o_ss = take(sort_scratch_words(In) * 4);
+  if (out && base) {
+    out->keys_a = (uint32_t*)(base + o_ka);
+    out->vals_a = (uint32_t*)(base + o_va);
+    out->keys_b = (uint32_t*)(base + o_kb);
+    out->vals_b = (uint32_t*)(base + o_vb);
+    out->presort_gid = (uint32_t*)(base + o_pg);
+    out->sort_scratch = (uint32_t*)(base + o_ss);
+    bool in_b = radix_passes(tile_bits(tiles)) % 2 == 1;
+    out->point_list = in_b ? out->vals_b : out->vals_a;
+    out->sorted_tile = in_b ? out->keys_b : out->keys_a;
+  }
+  return off;
+}
+
+struct ImgPtrs {
+  uint2* ranges;
+  float* final_T;
+  uint32_t* n_contrib;
+  uint32_t* tile_max;
+};
+
+inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += align_up(bytes);
+    return o;
+  };
+  size_t tiles = (size_t)((W + GS_TILE - 1) / GS_TILE) * ((H + GS_TILE - 1) / GS_TILE);
+  size_t npix = (size_t)W * H;
+  if (tiles == 0) tiles = 1;
+  if (npix == 0) npix = 1;
+  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 4);
+  if (out && base) {
+    out->ranges = (uint2*)(base + o_r);
+    out->final_T = (float*)(base + o_t);
+    out->n_contrib = (uint32_t*)(base + o_n);
+    out->tile_max = (uint32_t*)(base + o_m);
+  }
+  return off;
+}
+
+// ---- stages (gs_forward.hip / gs_backward.hip) ----
+void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st);
+void fwd_order(int P, const GeomPtrs& geo, hipStream_t st);  // compaction, depth sort, instance offsets
+void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const GeomPtrs& geo, const BinPtrs& bin,
+             const ImgPtrs& img, hipStream_t st);
+void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
+                hipStream_t st);
+void mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
+                  hipStream_t st);
+void bwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
+                const float* dL_dpix, float* gradrec, hipStream_t st);
+struct GradOut {
+  float* dmean2D;   // [P, 3]
+  float* dcolor;    // [P, 3] or null
+  float* dopacity;  // [P]
+  float* dmean3D;   // [P, 3]
+  float* dcov3D;    // [P, 6] or null
+  float* dsh;       // [P, M, 3] or null
+  float* dscale;    // [P, 3] or null
+  float* drot;      // [P, 4] or null
+};
+void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const float* gradrec,
+                    const GradOut& out, hipStream_t st);
+void knn_mean_dist2(int P, const float* pts, float* out, char* scratch, hipStream_t st);
+size_t knn_scratch_bytes(int P);
+
+}  // namespace gs

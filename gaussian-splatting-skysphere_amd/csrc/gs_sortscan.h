@@ -1,0 +1,288 @@
+// gs_sortscan.h -- hand-written device-wide exclusive scan and stable LSD radix sort (u32 keys,
+// u32 values) for gfx950.  Used for: visibility compaction, per-Gaussian instance offsets, the
+// depth sort of visible Gaussians and the stable tile sort of (tile, presort-slot) instances.
+//
+// Scan: reduce -> single-workgroup partial scan -> down-sweep (3 launches).  Workgroup count is
+// capped at 1024 so the partial scan is one 1024-lane workgroup.
+// Radix sort: per pass (8-bit digit) upsweep histogram [digit][block] -> scan -> stable scatter.
+// The scatter ranks keys inside a 256-key tile with wave64 ballots (per-bit peer masks, the
+// CDNA analogue of match_any), combines the 4 waves through LDS and keeps a running per-digit
+// base per workgroup, so equal digits keep input order (LSD stability).
+//
+// Element counts may live on the device (`n_dev`, e.g. the number of visible Gaussians) with a
+// host-side upper bound `n_max` that sizes the grids; surplus workgroups see an empty range.
+#pragma once
+#include "gs_common.h"
+
+namespace gs {
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 4;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;  // 1024 elements per tile
+constexpr int SCAN_MAX_BLOCKS = 1024;
+
+struct ScanPlan {
+  uint32_t nb;     // workgroups
+  uint32_t chunk;  // elements per workgroup (multiple of SCAN_TILE)
+};
+
+inline ScanPlan scan_plan(uint64_t n_max) {
+  uint64_t tiles = (n_max + SCAN_TILE - 1) / SCAN_TILE;
+  if (tiles == 0) tiles = 1;
+  uint64_t per = (tiles + SCAN_MAX_BLOCKS - 1) / SCAN_MAX_BLOCKS;
+  ScanPlan p;
+  p.nb = (uint32_t)((tiles + per - 1) / per);
+  p.chunk = (uint32_t)(per * SCAN_TILE);
+  return p;
+}
+
+__device__ __forceinline__ uint32_t resolve_n(const uint32_t* n_dev, uint32_t n_max) {
+  if (n_dev == nullptr) return n_max;
+  uint32_t n = *n_dev;
+  return n < n_max ? n : n_max;
+}
+
+// inclusive wave64 scan (u32)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+
+// exclusive scan of one value per thread over a 256-thread workgroup; returns the exclusive
+// prefix and writes the workgroup total to *total.  `sh` needs 4 u32 of LDS.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  uint32_t inc = wave_incl_scan(v);
+  if (lane == 63) sh[wid] = inc;
+  __syncthreads();
+  uint32_t w0 = sh[0], w1 = sh[1], w2 = sh[2], w3 = sh[3];
+  uint32_t before = (wid > 0 ? w0 : 0) + (wid > 1 ? w1 : 0) + (wid > 2 ? w2 : 0);
+  *total = w0 + w1 + w2 + w3;
+  __syncthreads();
+  return before + inc - v;
+}
+
+template <class Src>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(Src src, const uint32_t* n_dev, uint32_t n_max,
+                                                              uint32_t chunk, uint32_t* partial) {
+  __shared__ uint32_t sh[4];
+  const uint32_t n = resolve_n(n_dev, n_max);
+  const uint64_t start = (uint64_t)blockIdx.x * chunk;
+  const uint64_t end = start + chunk < n ? start + chunk : n;
+  uint32_t s = 0;
+  for (uint64_t i = start + threadIdx.x; i < end; i += SCAN_THREADS) s += src((uint32_t)i);
+  uint32_t tot;
+  block_excl_scan(s, sh, &tot);
+  if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+// single workgroup (1024 lanes): exclusive scan of partial[0..nb) in place; total -> *total_out
+static __global__ __launch_bounds__(1024) void k_scan_partials(uint32_t* partial, uint32_t nb, uint32_t* total_out) {
+  __shared__ uint32_t sh[16];
+  const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < nb; base += 1024) {
+    uint32_t i = base + threadIdx.x;
+    uint32_t v = i < nb ? partial[i] : 0u;
+    uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) sh[wid] = inc;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+      uint32_t x = sh[w];
+      if (w < wid) before += x;
+      tot += x;
+    }
+    if (i < nb) partial[i] = carry + before + inc - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total_out) *total_out = carry;
+}
+
+template <class Src, class Dst>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_down(Src src, Dst dst, const uint32_t* n_dev,
+                                                            uint32_t n_max, uint32_t chunk,
+                                                            const uint32_t* partial) {
+  __shared__ uint32_t sh[4];
+  const uint32_t n = resolve_n(n_dev, n_max);
+  const uint64_t start = (uint64_t)blockIdx.x * chunk;
+  const uint64_t end = start + chunk < n ? start + chunk : n;
+  uint32_t carry = partial[blockIdx.x];
+  for (uint64_t base = start; base < end; base += SCAN_TILE) {
+    uint64_t i0 = base + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS], loc = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+      v[k] = (i0 + k < end) ? src((uint32_t)(i0 + k)) : 0u;
+      loc += v[k];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(loc, sh, &tot) + carry;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+      if (i0 + k < end) dst((uint32_t)(i0 + k), ex, v[k]);
+      ex += v[k];
+    }
+    carry += tot;
+  }
+}
+
+// host: run the 3-launch scan.  partial must hold >= plan.nb u32.
+template <class Src, class Dst>
+inline void scan_exclusive(Src src, Dst dst, const uint32_t* n_dev, uint32_t n_max, uint32_t* partial,
+                           uint32_t* total_out, hipStream_t st) {
+  ScanPlan p = scan_plan(n_max);
+  GS_LAUNCH("scan_reduce", (k_scan_reduce<Src>), dim3(p.nb), dim3(SCAN_THREADS), 0, st, src, n_dev, n_max,
+            p.chunk, partial);
+  GS_LAUNCH("scan_partials", k_scan_partials, dim3(1), dim3(1024), 0, st, partial, p.nb, total_out);
+  GS_LAUNCH("scan_down", (k_scan_down<Src, Dst>), dim3(p.nb), dim3(SCAN_THREADS), 0, st, src, dst, n_dev, n_max,
+            p.chunk, partial);
+}
+
+// simple functors
+struct SrcArray {
+  const uint32_t* a;
+  __device__ uint32_t operator()(uint32_t i) const { return a[i]; }
+};
+struct DstArray {
+  uint32_t* a;
+  __device__ void operator()(uint32_t i, uint32_t ex, uint32_t) const { a[i] = ex; }
+};
+
+// ------------------------------------------------------------------------------------------
+// radix sort
+// ------------------------------------------------------------------------------------------
+constexpr int RADIX_BITS = 8;
+constexpr int RADIX = 1 << RADIX_BITS;
+constexpr int SORT_THREADS = 256;
+constexpr int SORT_MAX_BLOCKS = 1024;
+
+struct SortPlan {
+  uint32_t nb, chunk;
+};
+
+inline int radix_passes(int end_bit) { return (end_bit + RADIX_BITS - 1) / RADIX_BITS; }
+
+inline SortPlan sort_plan(uint64_t n_max) {
+  uint64_t tiles = (n_max + SORT_THREADS - 1) / SORT_THREADS;
+  if (tiles == 0) tiles = 1;
+  uint64_t per = (tiles + SORT_MAX_BLOCKS - 1) / SORT_MAX_BLOCKS;
+  SortPlan p;
+  p.nb = (uint32_t)((tiles + per - 1) / per);
+  p.chunk = (uint32_t)(per * SORT_THREADS);
+  return p;
+}
+
+// scratch words needed by radix_sort_pairs: histogram + its scan partials
+inline size_t sort_scratch_words(uint64_t n_max) {
+  SortPlan p = sort_plan(n_max);
+  size_t hist = (size_t)RADIX * p.nb;
+  return hist + scan_plan(hist).nb + 16;
+}
+
+static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys,
+                                                                     const uint32_t* n_dev, uint32_t n_max,
+                                                                     int shift, int bits, uint32_t chunk,
+                                                                     uint32_t nb, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[RADIX];
+  const uint32_t n = resolve_n(n_dev, n_max);
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t start = (uint64_t)blockIdx.x * chunk;
+  const uint64_t end = start + chunk < n ? start + chunk : n;
+  for (uint64_t i = start + threadIdx.x; i < end; i += SORT_THREADS) {
+    uint32_t d = (keys[i] >> shift) & ((1u << bits) - 1u);
+    // wave-aggregated LDS increment: one atomic per distinct digit per wave
+    uint64_t peers = __ballot(1);
+#pragma unroll
+    for (int b = 0; b < RADIX_BITS; b++) {
+      uint64_t bb = __ballot((d >> b) & 1);
+      peers &= ((d >> b) & 1) ? bb : ~bb;
+    }
+    if ((peers & lanemask_lt()) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  hist[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+
+static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
+    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
+    uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, int bits, uint32_t chunk,
+    uint32_t nb, const uint32_t* __restrict__ hist) {
+  __shared__ uint32_t base[RADIX];
+  __shared__ uint32_t wcnt[4][RADIX];
+  const uint32_t n = resolve_n(n_dev, n_max);
+  const uint32_t tid = threadIdx.x, wid = tid >> 6;
+  base[tid] = hist[(size_t)tid * nb + blockIdx.x];
+  const uint64_t start = (uint64_t)blockIdx.x * chunk;
+  const uint64_t end = start + chunk < n ? start + chunk : n;
+  const uint32_t mask = (1u << bits) - 1u;
+  for (uint64_t t0 = start; t0 < end; t0 += SORT_THREADS) {
+    const uint64_t i = t0 + tid;
+    const bool valid = i < end;
+    const uint32_t key = valid ? keys_in[i] : 0u;
+    const uint32_t val = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
+    const uint32_t d = (key >> shift) & mask;
+    wcnt[0][tid] = 0;
+    wcnt[1][tid] = 0;
+    wcnt[2][tid] = 0;
+    wcnt[3][tid] = 0;
+    __syncthreads();
+    uint64_t peers = __ballot(valid);
+    for (int b = 0; b < bits; b++) {
+      uint64_t bb = __ballot((d >> b) & 1);
+      peers &= ((d >> b) & 1) ? bb : ~bb;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+    if (valid && rank == 0) wcnt[wid][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    // thread `tid` owns digit `tid`: exclusive prefix over the 4 waves, tile total
+    uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
+    __syncthreads();
+    wcnt[0][tid] = 0;
+    wcnt[1][tid] = c0;
+    wcnt[2][tid] = c0 + c1;
+    wcnt[3][tid] = c0 + c1 + c2;
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = base[d] + wcnt[wid][d] + rank;
+      keys_out[pos] = key;
+      vals_out[pos] = val;
+    }
+    __syncthreads();
+    base[tid] += c0 + c1 + c2 + c3;
+  }
+}
+
+static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b,
+                                    bool vals_identity, const uint32_t* n_dev, uint32_t n_max, int end_bit,
+                                    uint32_t* scratch, hipStream_t st) {
+  SortPlan p = sort_plan(n_max);
+  uint32_t* hist = scratch;
+  const size_t hist_n = (size_t)RADIX * p.nb;
+  uint32_t* partial = scratch + hist_n;
+  uint32_t *kin = keys_a, *vin = vals_a, *kout = keys_b, *vout = vals_b;
+  bool in_b = false;
+  for (int shift = 0; shift < end_bit; shift += RADIX_BITS) {
+    int bits = end_bit - shift < RADIX_BITS ? end_bit - shift : RADIX_BITS;
+    GS_LAUNCH("radix_hist", k_radix_hist, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, n_dev, n_max, shift, bits,
+              p.chunk, p.nb, hist);
+    scan_exclusive(SrcArray{hist}, DstArray{hist}, nullptr, (uint32_t)hist_n, partial, nullptr, st);
+    const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
+    GS_LAUNCH("radix_scatter", k_radix_scatter, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, vsrc, kout, vout, n_dev,
+              n_max, shift, bits, p.chunk, p.nb, hist);
+    uint32_t* t;
+    t = kin; kin = kout; kout = t;
+    t = vin; vin = vout; vout = t;
+    in_b = !in_b;
+  }
+  return in_b;
+}
+
+}  // namespace gs

@@ -1,0 +1,133 @@
+"""diff_gaussian_rasterization -- MI355X-native drop-in for the 3DGS differentiable rasterizer.
+
+Public surface used by the reference's render adapter
+(/root/reference/gaussian_renderer/__init__.py:14 import, :36-49 settings, :51 rasterizer,
+:85-93 call):
+
+    GaussianRasterizationSettings(image_height, image_width, tanfovx, tanfovy, bg, scale_modifier,
+                                  viewmatrix, projmatrix, sh_degree, campos, prefiltered, debug)
+    GaussianRasterizer(raster_settings)(means3D, means2D, opacities, shs=None, colors_precomp=None,
+                                        scales=None, rotations=None, cov3D_precomp=None)
+        -> (color [3, H, W] fp32, radii [P] int32)
+    GaussianRasterizer.markVisible(positions) -> bool [P]
+    rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                        cov3Ds_precomp, raster_settings)
+
+This is the 2023 two-output API of graphdeco-inria/diff-gaussian-rasterization (the reference's
+un-vendored submodule, /root/reference/.gitmodules:4-6), implemented over libgsrast.so (hand-written
+HIP for gfx950, C ABI in include/gsrast.h).  Gradients flow to every tensor input that requires
+them, including `means2D`, whose .grad holds the NDC-space screen gradient read by densification
+(/root/reference/scene/gaussian_model.py:405-407).
+"""
+from __future__ import annotations
+
+from typing import NamedTuple
+
+import torch
+import torch.nn as nn
+
+from . import _C
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "cpu_deep_copy_tuple"]
+
+
+def cpu_deep_copy_tuple(input_tuple):
+    """CPU copies of every tensor in the tuple (used for the debug snapshot on failure)."""
+    return tuple(item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple)
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                        raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                                     cov3Ds_precomp, raster_settings)
+
+
+def _run_with_snapshot(fn, args, debug, dump_name, phase):
+    """settings.debug: keep CPU copies of the arguments and dump them if the native call fails."""
+    if not debug:
+        return fn(*args)
+    cpu_args = cpu_deep_copy_tuple(args)
+    try:
+        return fn(*args)
+    except Exception:
+        torch.save(cpu_args, dump_name)
+        print(f"\nAn error occured in {phase}. Please forward {dump_name} for debugging.")
+        raise
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                raster_settings):
+        s = raster_settings
+        args = (s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+                s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
+                s.campos, s.prefiltered, s.debug)
+        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _run_with_snapshot(
+            _C.rasterize_gaussians, args, s.debug, "snapshot_fw.dump", "forward")
+        ctx.raster_settings = s
+        ctx.num_rendered = num_rendered
+        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
+                              binningBuffer, imgBuffer)
+        ctx.mark_non_differentiable(radii)
+        return color, radii
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _grad_radii):
+        s = ctx.raster_settings
+        colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer, imgBuffer = (
+            ctx.saved_tensors)
+        args = (s.bg, means3D, radii, colors_precomp, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+                s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color.contiguous(), sh, s.sh_degree,
+                s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.debug)
+
+        def _bwd(*a):
+            return _C.backward_impl(*a, want_all=False)
+
+        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
+         grad_rotations) = _run_with_snapshot(_bwd, args, s.debug, "snapshot_bw.dump", "backward")
+        return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
+                grad_rotations, grad_cov3Ds_precomp, None)
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        with torch.no_grad():
+            s = self.raster_settings
+            return _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None):
+        s = self.raster_settings
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception("Please provide excatly one of either SHs or precomputed colors!")
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or (
+                (scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        empty = torch.Tensor([])
+        shs = empty if shs is None else shs
+        colors_precomp = empty if colors_precomp is None else colors_precomp
+        scales = empty if scales is None else scales
+        rotations = empty if rotations is None else rotations
+        cov3D_precomp = empty if cov3D_precomp is None else cov3D_precomp
+        return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                                   s)

@@ -1,0 +1,106 @@
+"""Loader for libgsrast.so, the MI355X (gfx950) HIP rasterizer behind include/gsrast.h.
+
+There is no fallback: if the shared library is missing or does not load, importing
+`diff_gaussian_rasterization._C` raises.  Build it with `make -C gaussian-splatting-skysphere_amd`
+(or `python __graft_entry__.py build`).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("GSRAST_LIB", os.path.join(_PKG_ROOT, "build", "libgsrast.so"))
+
+_c_p = ctypes.c_void_p
+_c_i = ctypes.c_int
+_c_f = ctypes.c_float
+_c_ll = ctypes.c_longlong
+_c_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/gsrast.h
+SIGNATURES = {
+    "gs_abi_version": (_c_i, []),
+    "gs_last_error": (ctypes.c_char_p, []),
+    "gs_geom_buffer_bytes": (_c_sz, [_c_i]),
+    "gs_binning_buffer_bytes": (_c_sz, [_c_ll, _c_i, _c_i]),
+    "gs_image_buffer_bytes": (_c_sz, [_c_i, _c_i]),
+    "gs_grad_buffer_bytes": (_c_sz, [_c_ll]),
+    "gs_forward_preprocess": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_f, _c_f, _c_i, _c_p, _c_p, ctypes.POINTER(_c_ll), _c_i, _c_p],
+    ),
+    "gs_forward_render": (
+        _c_i,
+        [_c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_i, _c_p],
+    ),
+    "gs_rasterize_forward": (
+        _c_ll,
+        [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_f, _c_f, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p],
+    ),
+    "gs_backward": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_i, _c_p],
+    ),
+    "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "gs_knn_scratch_bytes": (_c_sz, [_c_i]),
+    "gs_knn_mean_dist2": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p]),
+    "gs_debug_export": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
+    ),
+    "gs_profile_enable": (None, [_c_i]),
+    "gs_profile_collect": (_c_i, []),
+    "gs_profile_reset": (None, []),
+    "gs_profile_stat": (_c_i, [_c_i, ctypes.c_char_p, _c_i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_ll)]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libgsrast.so once and declare every C-ABI symbol.  Raises if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libgsrast.so not found at {LIB_PATH}; build it with "
+            f"`make -C {_PKG_ROOT}` (hipcc --offload-arch=gfx950). There is no CPU fallback."
+        )
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().gs_last_error()
+    return msg.decode() if msg else "unknown error"
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what}: {last_error()}")
+
+
+def profile_stats():
+    """Per-kernel (name -> (total_ms, launches)) collected with gs_profile_enable(1)."""
+    lib = load()
+    lib.gs_profile_collect()
+    out = {}
+    i = 0
+    buf = ctypes.create_string_buffer(128)
+    ms = ctypes.c_double()
+    n = ctypes.c_longlong()
+    while lib.gs_profile_stat(i, buf, 128, ctypes.byref(ms), ctypes.byref(n)):
+        out[buf.value.decode()] = (ms.value, n.value)
+        i += 1
+    return out

@@ -1,0 +1,134 @@
+/*
+ * gsrast.h -- C ABI of the MI355X-native differentiable Gaussian rasterizer (libgsrast.so).
+ *
+ * Drop-in boundary for the reference's native rasterizer.  The reference binds an un-vendored
+ * CUDA/C++ torch extension `diff_gaussian_rasterization._C` (/root/reference/.gitmodules:4-6)
+ * through `GaussianRasterizer(...)(...)` at /root/reference/gaussian_renderer/__init__.py:51,85-93
+ * (import at :14).  Each entry point below names the upstream native function it replaces
+ * (upstream signatures restated in SURVEY.md §8b):
+ *
+ *   gs_forward_preprocess + gs_forward_render  <-  _C.rasterize_gaussians(...)
+ *       (upstream runs both halves in one call with resize callbacks for its three scratch
+ *        buffers; here the caller sizes the binning buffer from the returned num_rendered, so no
+ *        callback into the host language is needed.  gs_rasterize_forward() is the one-call
+ *        variant with the upstream-style allocator callback.)
+ *   gs_backward                                <-  _C.rasterize_gaussians_backward(...)
+ *   gs_mark_visible                            <-  _C.mark_visible(...)
+ *   gs_knn_mean_dist2                          <-  simple_knn._C.distCUDA2(points)
+ *                                                  (/root/reference/scene/gaussian_model.py:20,134)
+ *
+ * Conventions
+ *   - Every pointer argument is a DEVICE pointer (HBM of the current HIP device) unless its name
+ *     ends in `_host`.  Arrays are dense row-major fp32 unless stated.  Optional inputs are NULL.
+ *   - viewmatrix / projmatrix are the 4x4 `world_view_transform` / `full_proj_transform` tensors
+ *     of /root/reference/scene/cameras.py:54-56 (row-vector convention), flattened row-major.
+ *   - The caller owns every buffer (the host framework's allocator); the library never allocates
+ *     or frees device memory.  Buffers returned by forward must stay alive until backward.
+ *   - stream: a hipStream_t; all work is enqueued on it.  gs_forward_preprocess synchronises the
+ *     stream once to read num_rendered (as upstream does).
+ *   - Return value: 0 on success, non-zero on error; gs_last_error() describes the last error of
+ *     the calling thread.  With debug != 0 every kernel is followed by a stream synchronisation
+ *     and an error check (upstream `debug` semantics).
+ */
+#ifndef GSRAST_H
+#define GSRAST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSRAST_ABI_VERSION 1
+
+int gs_abi_version(void);
+const char* gs_last_error(void);
+
+/* ---- scratch sizing (bytes) ---- */
+size_t gs_geom_buffer_bytes(int P);
+size_t gs_binning_buffer_bytes(long long num_rendered, int image_width, int image_height);
+size_t gs_image_buffer_bytes(int image_width, int image_height);
+size_t gs_grad_buffer_bytes(long long num_rendered);
+
+/* ---- forward, part 1: preprocess, cull, depth order, instance offsets ----
+ * P Gaussians; D = active SH degree; M = SH coefficients per colour (stride of shs, 0 if none).
+ * Exactly one of {shs, colors_precomp} and one of {(scales, rotations), cov3D_precomp} is non-NULL.
+ * Writes radii_out[P] (int32) and the geometry buffer; returns num_rendered in *num_rendered_host.
+ * Ref: upstream rasterize_gaussians (first half: preprocess, InclusiveSum, D2H of num_rendered). */
+int gs_forward_preprocess(int P, int D, int M, const float* background, int image_width, int image_height,
+                          const float* means3D, const float* shs, const float* colors_precomp,
+                          const float* opacities, const float* scales, float scale_modifier,
+                          const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                          const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                          int prefiltered, int* radii_out, void* geom_buffer, long long* num_rendered_host,
+                          int debug, void* stream);
+
+/* ---- forward, part 2: duplicate, tile sort, ranges, compositing ----
+ * out_color[3, H, W] fp32 (CHW).  binning_buffer >= gs_binning_buffer_bytes(num_rendered, W, H),
+ * image_buffer >= gs_image_buffer_bytes(W, H). */
+int gs_forward_render(int P, const float* background, int image_width, int image_height,
+                      const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                      float tan_fovy, const int* radii, void* geom_buffer, long long num_rendered,
+                      void* binning_buffer, void* image_buffer, float* out_color, int debug, void* stream);
+
+/* ---- one-call forward with an upstream-style allocator callback ----
+ * alloc(ctx, which, bytes) returns a device pointer of >= bytes (which: 0 geometry, 1 binning,
+ * 2 image) that stays valid until backward.  Returns num_rendered (>= 0) or -1 on error. */
+typedef void* (*gs_alloc_fn)(void* ctx, int which, size_t bytes);
+long long gs_rasterize_forward(int P, int D, int M, const float* background, int image_width, int image_height,
+                               const float* means3D, const float* shs, const float* colors_precomp,
+                               const float* opacities, const float* scales, float scale_modifier,
+                               const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                               const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                               int prefiltered, float* out_color, int* radii_out, gs_alloc_fn alloc,
+                               void* alloc_ctx, void** geom_out, void** binning_out, void** image_out, int debug,
+                               void* stream);
+
+/* ---- backward ----
+ * dL_dout_color[3, H, W].  grad_buffer >= gs_grad_buffer_bytes(num_rendered) (scratch).
+ * Outputs (P rows each): dL_dmeans2D[P,3] (gradient w.r.t. the NDC projected mean; column 2 = 0),
+ * dL_dcolors[P,3], dL_dopacity[P,1], dL_dmeans3D[P,3], dL_dcov3D[P,6], dL_dsh[P,M,3],
+ * dL_dscales[P,3], dL_drotations[P,4].  dL_dcolors, dL_dcov3D, dL_dsh, dL_dscales and
+ * dL_drotations may be NULL when the matching input was not given (they are then not computed).
+ * Ref: upstream rasterize_gaussians_backward. */
+int gs_backward(int P, int D, int M, const float* background, int image_width, int image_height,
+                const float* means3D, const float* shs, const float* colors_precomp, const float* opacities,
+                const float* scales, float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                float tan_fovy, const int* radii, const void* geom_buffer, long long num_rendered,
+                const void* binning_buffer, const void* image_buffer, const float* dL_dout_color,
+                void* grad_buffer, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                int debug, void* stream);
+
+/* ---- mark_visible: present[P] (uint8 0/1), near-plane test ---- */
+int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                    uint8_t* present, void* stream);
+
+/* ---- simple-knn: mean squared distance to the 3 nearest other points ---- */
+size_t gs_knn_scratch_bytes(int P);
+int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, void* stream);
+
+/* ---- debug export of forward intermediates (tests) ----
+ * Copies (device -> device) whichever outputs are non-NULL: point_list[num_rendered] (Gaussian ids
+ * of the tile-sorted instance list), ranges[tiles*2] (u32), xy[P*2], conic_opacity[P*4],
+ * rgb[P*3], depth[P], tiles_touched[P] (u32), final_T[H*W], n_contrib[H*W] (u32). */
+int gs_debug_export(int P, int image_width, int image_height, long long num_rendered, const void* geom_buffer,
+                    const void* binning_buffer, const void* image_buffer, uint32_t* point_list,
+                    uint32_t* ranges, float* xy, float* conic_opacity, float* rgb, float* depth,
+                    uint32_t* tiles_touched, float* final_T, uint32_t* n_contrib, void* stream);
+
+/* ---- per-kernel timing with HIP events on the launch stream (bench / profiling) ----
+ * While enabled every launch is bracketed by a hipEvent pair.  gs_profile_collect() waits for the
+ * recorded events and folds them into per-kernel totals; gs_profile_stat(i, ...) reads entry i
+ * (returns 0 past the end). */
+void gs_profile_enable(int on);
+int gs_profile_collect(void);
+void gs_profile_reset(void);
+int gs_profile_stat(int i, char* name, int name_len, double* total_ms, long long* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSRAST_H */

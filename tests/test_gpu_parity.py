@@ -1,0 +1,325 @@
+"""GPU parity: the HIP path (through the C ABI, via the drop-in package) against the CPU oracle on
+identical seeded inputs.
+
+Tolerances
+  - Forward (every integer and every float of the forward): BIT-EXACT.  The kernels and the
+    oracle follow one explicit operation order with no FMA contraction and the same exp
+    (DESIGN.md §Numerics), so radii, num_rendered, the tile-sorted instance list, ranges, splat
+    attributes, n_contrib, final_T and the image must be identical.
+  - Backward: the GPU sums per-pixel terms in fp32 (wave DPP tree -> 4 wave slabs -> per-instance
+    records -> per-Gaussian sequential sum); the oracle sums the identical fp32 terms in fp64.
+    Per tensor: |gpu - oracle| <= 1e-5 * |oracle| + 1e-5 * max|oracle|  (north-star 1e-5 rel fp32).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import gs_scenes
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def _tol_check(gpu, ref, name, rtol=RTOL, frac=RTOL):
+    gpu = np.asarray(gpu, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert gpu.shape == ref.shape, (name, gpu.shape, ref.shape)
+    scale = max(np.abs(ref).max(), 1e-30)
+    tol = rtol * np.abs(ref) + frac * scale
+    bad = np.abs(gpu - ref) > tol
+    assert not bad.any(), (f"{name}: {int(bad.sum())}/{bad.size} beyond tol; max|d|={np.abs(gpu - ref).max():.3e} "
+                           f"max|ref|={scale:.3e}")
+
+
+def _oracle_scene(oracle, cam, sc, bg, colors=None, cov3D=None, deg=None, mod=1.0):
+    deg = sc.sh_degree if deg is None else deg
+    return oracle.Scene(bg=bg, means3D=sc.means3D.numpy(), opacities=sc.opacities.numpy(), W=cam.image_width,
+                        H=cam.image_height, viewmatrix=cam.world_view_transform.numpy(),
+                        projmatrix=cam.full_proj_transform.numpy(), campos=cam.camera_center.numpy(),
+                        tanfovx=math.tan(cam.FoVx / 2), tanfovy=math.tan(cam.FoVy / 2),
+                        shs=None if colors is not None else sc.shs.numpy(), sh_degree=deg, colors_precomp=colors,
+                        scales=None if cov3D is not None else sc.scales.numpy(),
+                        rotations=None if cov3D is not None else sc.rotations.numpy(), cov3D_precomp=cov3D,
+                        scale_modifier=mod)
+
+
+def _gpu_run(cam, sc, device, bg, dpix, colors=None, cov3D=None, deg=None, mod=1.0, debug=False):
+    """Forward + backward through GaussianRasterizer exactly as the reference adapter calls it."""
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+
+    deg = sc.sh_degree if deg is None else deg
+    s = gs_scenes.raster_settings_for(cam, deg, bg=torch.tensor(bg, device=device), scale_modifier=mod,
+                                      debug=debug, device=device)
+    d = sc.to(device)
+    means3D = d.means3D.clone().requires_grad_(True)
+    means2D = torch.zeros_like(means3D, requires_grad=True)
+    opac = d.opacities.clone().requires_grad_(True)
+    kw = {}
+    leaves = dict(means3D=means3D, means2D=means2D, opacities=opac)
+    if colors is None:
+        kw["shs"] = leaves["shs"] = d.shs.clone().requires_grad_(True)
+    else:
+        kw["colors_precomp"] = leaves["colors"] = torch.tensor(colors, device=device).requires_grad_(True)
+    if cov3D is None:
+        kw["scales"] = leaves["scales"] = d.scales.clone().requires_grad_(True)
+        kw["rotations"] = leaves["rotations"] = d.rotations.clone().requires_grad_(True)
+    else:
+        kw["cov3D_precomp"] = leaves["cov3D"] = torch.tensor(cov3D, device=device).requires_grad_(True)
+    img, radii = GaussianRasterizer(s)(means3D=means3D, means2D=means2D, opacities=opac, **kw)
+    (img * torch.tensor(dpix, device=device)).sum().backward()
+    torch.cuda.synchronize()
+    return img, radii, leaves
+
+
+def _check_forward_exact(oracle_fw, cam, sc, device, colors=None, cov3D=None, deg=None):
+    """Bit-exact comparison of every forward intermediate (through _C + debug export)."""
+    from diff_gaussian_rasterization import _C
+
+    deg = sc.sh_degree if deg is None else deg
+    s = gs_scenes.raster_settings_for(cam, deg, bg=torch.tensor(oracle_fw["bg"], device=device), device=device)
+    d = sc.to(device)
+    e = torch.Tensor([])
+    num, color, radii, geom, binb, imgb = _C.rasterize_gaussians(
+        s.bg, d.means3D, e if colors is None else torch.tensor(colors, device=device), d.opacities,
+        d.scales if cov3D is None else e, d.rotations if cov3D is None else e, s.scale_modifier,
+        e if cov3D is None else torch.tensor(cov3D, device=device), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy,
+        s.image_height, s.image_width, d.shs if colors is None else e, deg, s.campos, False, False)
+    ex = _C.debug_export(sc.P, cam.image_width, cam.image_height, num, geom, binb, imgb, device)
+    torch.cuda.synchronize()
+    assert num == oracle_fw["num_rendered"]
+    np.testing.assert_array_equal(radii.cpu().numpy(), oracle_fw["radii"])
+    vis = oracle_fw["radii"] > 0
+    np.testing.assert_array_equal(ex["tiles_touched"].cpu().numpy().astype(np.uint32), oracle_fw["tiles_touched"])
+    np.testing.assert_array_equal(ex["point_list"].cpu().numpy().astype(np.uint32), oracle_fw["point_list"])
+    np.testing.assert_array_equal(ex["ranges"].cpu().numpy().astype(np.uint32), oracle_fw["ranges"])
+    np.testing.assert_array_equal(ex["xy"].cpu().numpy()[vis], oracle_fw["xy"][vis])
+    np.testing.assert_array_equal(ex["conic_opacity"].cpu().numpy()[vis], oracle_fw["conic_opacity"][vis])
+    np.testing.assert_array_equal(ex["rgb"].cpu().numpy()[vis], oracle_fw["rgb"][vis])
+    np.testing.assert_array_equal(ex["n_contrib"].cpu().numpy().astype(np.uint32), oracle_fw["n_contrib"])
+    np.testing.assert_array_equal(ex["final_T"].cpu().numpy(), oracle_fw["final_T"])
+    np.testing.assert_array_equal(color.cpu().numpy(), oracle_fw["color"])
+
+
+def _check_backward(gr, leaves, colors=None, cov3D=None, rtol=RTOL):
+    g = lambda k: leaves[k].grad.detach().cpu().numpy()  # noqa: E731
+    _tol_check(g("means2D"), gr["dmeans2D"], "dmeans2D", rtol, rtol)
+    _tol_check(g("opacities"), gr["dopacity"], "dopacity", rtol, rtol)
+    _tol_check(g("means3D"), gr["dmeans3D"], "dmeans3D", rtol, rtol)
+    if colors is None:
+        _tol_check(g("shs"), gr["dsh"], "dsh", rtol, rtol)
+    else:
+        _tol_check(g("colors"), gr["dcolors"], "dcolors", rtol, rtol)
+    if cov3D is None:
+        _tol_check(g("scales"), gr["dscales"], "dscales", rtol, rtol)
+        _tol_check(g("rotations"), gr["drotations"], "drotations", rtol, rtol)
+    else:
+        _tol_check(g("cov3D"), gr["dcov3D"], "dcov3D", rtol, rtol)
+
+
+CASES = [
+    # name, P, sh_degree, W, H, bg
+    ("tiny", 64, 3, 64, 48, 0.0),
+    ("C1_10k_sh0_256", 10_000, 0, 256, 256, 0.0),
+    ("ragged_sh1_bg", 3_000, 1, 203, 117, 0.5),
+    ("C2_100k_sh3_800", 100_000, 3, 800, 800, 0.0),
+]
+
+
+@pytest.mark.parametrize("name,P,deg,W,H,bgv", CASES, ids=[c[0] for c in CASES])
+def test_forward_bitexact_and_backward_vs_oracle(oracle, device, name, P, deg, W, H, bgv):
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=0)
+    bg = np.full(3, bgv, np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg)
+    ofw = oracle.forward(osc, intermediates=True)
+    ofw["bg"] = bg
+    _check_forward_exact(ofw, cam, sc, device)
+    dpix = gs_scenes.dl_dimage(H, W, seed=1).numpy()
+    img, radii, leaves = _gpu_run(cam, sc, device, bg, dpix)
+    np.testing.assert_array_equal(img.detach().cpu().numpy(), ofw["color"])
+    gr = oracle.backward(osc, dpix)
+    _check_backward(gr, leaves)
+
+
+def test_precomputed_colors_and_cov3d(oracle, device):
+    W, H = 160, 96
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(2000, 0, cam=cam, seed=3)
+    colors = np.random.default_rng(0).random((2000, 3), dtype=np.float32)
+    cov = oracle.cov3d(sc.scales.numpy(), 1.0, sc.rotations.numpy())
+    bg = np.array([0.2, 0.1, 0.0], np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg, colors=colors, cov3D=cov)
+    ofw = oracle.forward(osc, intermediates=True)
+    ofw["bg"] = bg
+    _check_forward_exact(ofw, cam, sc, device, colors=colors, cov3D=cov)
+    dpix = gs_scenes.dl_dimage(H, W, seed=2).numpy()
+    img, _, leaves = _gpu_run(cam, sc, device, bg, dpix, colors=colors, cov3D=cov)
+    gr = oracle.backward(osc, dpix)
+    _check_backward(gr, leaves, colors=colors, cov3D=cov)
+
+
+def test_active_degree_below_max_uses_stride_M(oracle, device):
+    """train.py raises the active SH degree every 1000 its (gaussian_model.py:120-122): shs keeps
+    M = 16 coefficients while D < 3; coefficients past (D+1)^2 get zero gradient."""
+    W, H = 128, 128
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(4000, 3, cam=cam, seed=4)
+    bg = np.zeros(3, np.float32)
+    for D in (0, 1, 2):
+        osc = _oracle_scene(oracle, cam, sc, bg, deg=D)
+        ofw = oracle.forward(osc, intermediates=True)
+        ofw["bg"] = bg
+        _check_forward_exact(ofw, cam, sc, device, deg=D)
+        dpix = gs_scenes.dl_dimage(H, W, seed=5).numpy()
+        img, _, leaves = _gpu_run(cam, sc, device, bg, dpix, deg=D)
+        gr = oracle.backward(osc, dpix)
+        _check_backward(gr, leaves)
+        assert torch.all(leaves["shs"].grad[:, (D + 1) ** 2:] == 0)
+
+
+def test_scale_modifier(oracle, device):
+    W, H = 96, 96
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(1500, 1, cam=cam, seed=6)
+    bg = np.zeros(3, np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg, mod=0.6)
+    ofw = oracle.forward(osc)
+    dpix = gs_scenes.dl_dimage(H, W, seed=7).numpy()
+    img, radii, leaves = _gpu_run(cam, sc, device, bg, dpix, mod=0.6)
+    np.testing.assert_array_equal(img.detach().cpu().numpy(), ofw["color"])
+    np.testing.assert_array_equal(radii.cpu().numpy(), ofw["radii"])
+    _check_backward(oracle.backward(osc, dpix), leaves)
+
+
+def test_empty_scene_returns_zero_image(device):
+    """Upstream skips all work for P == 0: all-zero image (background NOT composited), empty radii."""
+    cam = gs_scenes.identity_camera(64, 32)
+    sc = gs_scenes.random_gaussians(0, 0, cam=cam)
+    img, radii, leaves = _gpu_run(cam, sc, device, np.ones(3, np.float32), np.ones((3, 32, 64), np.float32))
+    assert img.shape == (3, 32, 64) and torch.all(img == 0) and radii.numel() == 0
+
+
+def test_all_culled_scene_is_background(oracle, device):
+    cam = gs_scenes.identity_camera(64, 48)
+    sc = gs_scenes.random_gaussians(500, 0, cam=cam, seed=9)
+    sc.means3D[:, 2] = -sc.means3D[:, 2]  # behind the camera
+    bg = np.array([0.25, 0.5, 0.75], np.float32)
+    dpix = gs_scenes.dl_dimage(48, 64).numpy()
+    img, radii, leaves = _gpu_run(cam, sc, device, bg, dpix)
+    assert torch.all(radii == 0)
+    ref = np.broadcast_to(bg[:, None, None], (3, 48, 64))
+    np.testing.assert_array_equal(img.detach().cpu().numpy(), ref)
+    for k, v in leaves.items():
+        assert torch.all(v.grad == 0), k
+
+
+def test_multi_view_circle_cameras(oracle, device):
+    """C4-style cameras (look-at, non-identity view) exercise the full view / projection path."""
+    cams = gs_scenes.circle_cameras(3, 6.0, 200, 150)
+    sc = gs_scenes.random_gaussians(5000, 3, seed=10, ball_radius=2.0)
+    bg = np.zeros(3, np.float32)
+    for cam in cams:
+        osc = _oracle_scene(oracle, cam, sc, bg)
+        ofw = oracle.forward(osc, intermediates=True)
+        ofw["bg"] = bg
+        _check_forward_exact(ofw, cam, sc, device)
+        dpix = gs_scenes.dl_dimage(150, 200, seed=11).numpy()
+        _, _, leaves = _gpu_run(cam, sc, device, bg, dpix)
+        _check_backward(oracle.backward(osc, dpix), leaves)
+
+
+def test_prefiltered_near_point_raises(device):
+    from diff_gaussian_rasterization import GaussianRasterizer
+
+    cam = gs_scenes.identity_camera(32, 32)
+    sc = gs_scenes.random_gaussians(10, 0, cam=cam, seed=1).to(device)
+    sc.means3D[0, 2] = 0.1
+    s = gs_scenes.raster_settings_for(cam, 0, device=device)._replace(prefiltered=True)
+    with pytest.raises(RuntimeError, match="prefiltered"):
+        GaussianRasterizer(s)(means3D=sc.means3D, means2D=torch.zeros_like(sc.means3D), opacities=sc.opacities,
+                              shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+
+
+def test_debug_mode_matches_normal_mode(device):
+    cam = gs_scenes.identity_camera(80, 64)
+    sc = gs_scenes.random_gaussians(800, 2, cam=cam, seed=12)
+    dpix = gs_scenes.dl_dimage(64, 80).numpy()
+    bg = np.zeros(3, np.float32)
+    a, _, la = _gpu_run(cam, sc, device, bg, dpix, debug=False)
+    b, _, lb = _gpu_run(cam, sc, device, bg, dpix, debug=True)
+    assert torch.equal(a, b)
+    for k in la:
+        assert torch.equal(la[k].grad, lb[k].grad), k
+
+
+def test_backward_is_deterministic(device):
+    """No float atomics anywhere: two backward passes are bit-identical."""
+    cam = gs_scenes.identity_camera(256, 256)
+    sc = gs_scenes.random_gaussians(20000, 3, cam=cam, seed=13)
+    dpix = gs_scenes.dl_dimage(256, 256).numpy()
+    bg = np.zeros(3, np.float32)
+    _, _, la = _gpu_run(cam, sc, device, bg, dpix)
+    _, _, lb = _gpu_run(cam, sc, device, bg, dpix)
+    for k in la:
+        assert torch.equal(la[k].grad, lb[k].grad), k
+
+
+def test_mark_visible(oracle, device):
+    from diff_gaussian_rasterization import GaussianRasterizer
+
+    cam = gs_scenes.identity_camera(64, 64)
+    sc = gs_scenes.random_gaussians(3000, 0, cam=cam, seed=14)
+    sc.means3D[::3, 2] *= -1
+    s = gs_scenes.raster_settings_for(cam, 0, device=device)
+    vis = GaussianRasterizer(s).markVisible(sc.means3D.to(device)).cpu().numpy()
+    ref = oracle.mark_visible(sc.means3D.numpy(), cam.world_view_transform.numpy(), cam.full_proj_transform.numpy())
+    np.testing.assert_array_equal(vis, ref)
+
+
+@pytest.mark.parametrize("P", [4, 100, 5000])
+def test_knn_matches_oracle(oracle, device, P):
+    from simple_knn._C import distCUDA2
+
+    g = torch.Generator().manual_seed(P)
+    pts = torch.randn((P, 3), generator=g) * torch.tensor([3.0, 1.0, 0.5])
+    got = distCUDA2(pts.to(device)).cpu().numpy()
+    ref = oracle.knn_mean_dist2(pts.numpy())
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=0)
+
+
+def test_large_c3_properties(device):
+    """C3 size (1M Gaussians SH3, 1920x1080) -- size-independent properties instead of the oracle:
+    the tile-sorted list is ordered by (tile, depth, index), ranges tile the list exactly,
+    n_contrib <= list length, image finite, bit-identical reruns."""
+    from diff_gaussian_rasterization import _C
+
+    cam = gs_scenes.identity_camera(1920, 1080)
+    sc = gs_scenes.random_gaussians(1_000_000, 3, cam=cam, seed=0).to(device)
+    s = gs_scenes.raster_settings_for(cam, 3, device=device)
+    e = torch.Tensor([])
+    args = (s.bg, sc.means3D, e, sc.opacities, sc.scales, sc.rotations, 1.0, e, s.viewmatrix, s.projmatrix,
+            s.tanfovx, s.tanfovy, 1080, 1920, sc.shs, 3, s.campos, False, False)
+    num, color, radii, geom, binb, imgb = _C.rasterize_gaussians(*args)
+    num2, color2, radii2, *_ = _C.rasterize_gaussians(*args)
+    assert num == num2 and torch.equal(color, color2) and torch.equal(radii, radii2)
+    ex = _C.debug_export(sc.P, 1920, 1080, num, geom, binb, imgb, device)
+    lst = ex["point_list"].long()
+    rng = ex["ranges"].long()
+    assert num == int(ex["tiles_touched"].sum())
+    # ranges partition [0, num) in tile order
+    nonempty = rng[:, 1] > rng[:, 0]
+    starts, ends = rng[nonempty, 0], rng[nonempty, 1]
+    assert starts[0] == 0 and ends[-1] == num and torch.all(starts[1:] == ends[:-1])
+    # inside each tile: (depth bits, gid) non-decreasing
+    depth_bits = ex["depth"].view(torch.int32).long()
+    tile_of = torch.repeat_interleave(torch.arange(rng.shape[0], device=device)[nonempty], ends - starts)
+    same = tile_of[1:] == tile_of[:-1]
+    d0, d1 = depth_bits[lst[:-1]], depth_bits[lst[1:]]
+    ordered = (d1 > d0) | ((d1 == d0) & (lst[1:] > lst[:-1]))
+    assert torch.all(ordered[same])
+    ncon = ex["n_contrib"].long()
+    assert torch.isfinite(color).all() and (color >= 0).all()
+    assert int(ncon.max()) <= int((ends - starts).max())

@@ -1,0 +1,127 @@
+"""Cross-check the CPU oracle's compositing core and analytic backward against an independent dense
+PyTorch restatement differentiated by autograd (tests/dense_ref.py).  This is what pins the
+render fwd/bwd + preprocess bwd of the oracle, since the reference has no test or fixture for them
+("parity unpinned" by the reference itself)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import dense_ref
+import gs_scenes
+
+
+def _scene(P, W, H, deg, seed, scale_range=(0.02, 0.15), z_range=(2.0, 6.0)):
+    cam = gs_scenes.identity_camera(W, H, fovy_deg=60.0)
+    sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=seed, scale_range=scale_range, z_range=z_range)
+    # keep centres well inside the frustum (the tx/tz clamp changes the gradient semantics)
+    sc.means3D[:, 0] *= 0.85
+    sc.means3D[:, 1] *= 0.85
+    sc.opacities.clamp_(max=0.95)
+    return cam, sc
+
+
+def _oracle_scene(oracle, cam, sc, bg, colors=None, cov3D=None, mod=1.0, deg=None):
+    deg = sc.sh_degree if deg is None else deg
+    return oracle.Scene(bg=bg, means3D=sc.means3D.numpy(), opacities=sc.opacities.numpy(), W=cam.image_width,
+                        H=cam.image_height, viewmatrix=cam.world_view_transform.numpy(),
+                        projmatrix=cam.full_proj_transform.numpy(), campos=cam.camera_center.numpy(),
+                        tanfovx=math.tan(cam.FoVx / 2), tanfovy=math.tan(cam.FoVy / 2),
+                        shs=None if colors is not None else sc.shs.numpy(), sh_degree=deg,
+                        colors_precomp=colors, scales=None if cov3D is not None else sc.scales.numpy(),
+                        rotations=None if cov3D is not None else sc.rotations.numpy(), cov3D_precomp=cov3D,
+                        scale_modifier=mod)
+
+
+def _close(a, b, rtol=2e-4, frac=2e-4, name=""):
+    """|a-b| <= rtol*|b| + frac*max|b| elementwise (fp32 oracle vs fp64 dense)."""
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    tol = rtol * np.abs(b) + frac * max(np.abs(b).max(), 1e-30)
+    bad = np.abs(a - b) > tol
+    assert not bad.any(), f"{name}: {bad.sum()} / {bad.size} off, max |d| {np.abs(a - b).max():.3e}, max|ref| {np.abs(b).max():.3e}"
+
+
+@pytest.mark.parametrize("deg,W,H,bgv", [(3, 70, 48, 0.0), (1, 64, 40, 0.3), (0, 33, 17, 1.0)])
+def test_oracle_forward_backward_vs_dense_autograd(oracle, deg, W, H, bgv):
+    cam, sc = _scene(40, W, H, deg, seed=deg + 11)
+    bg = np.full(3, bgv, np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg)
+    fw = oracle.forward(osc)
+    dpix = gs_scenes.dl_dimage(H, W, seed=3, scale=1.0).numpy()
+    gr = oracle.backward(osc, dpix)
+
+    d = torch.float64
+    m3 = sc.means3D.to(d).requires_grad_(True)
+    m2 = torch.zeros((40, 3), dtype=d, requires_grad=True)
+    op = sc.opacities.to(d).requires_grad_(True)
+    shs = sc.shs.to(d).requires_grad_(True)
+    scl = sc.scales.to(d).requires_grad_(True)
+    rot = sc.rotations.to(d).requires_grad_(True)
+    img, radii = dense_ref.render(m3, m2, op[:, 0], cam.world_view_transform.to(d), cam.full_proj_transform.to(d),
+                                  cam.camera_center.to(d), math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), W, H,
+                                  torch.tensor(bg, dtype=d), shs=shs, deg=deg, scales=scl, rots=rot)
+    assert fw["num_rendered"] > 0
+    np.testing.assert_array_equal(fw["radii"], radii.numpy())
+    _close(fw["color"], img.detach().numpy(), rtol=1e-5, frac=1e-5, name="image")
+    (img * torch.tensor(dpix, dtype=d)).sum().backward()
+    _close(gr["dmeans2D"][:, :2], m2.grad[:, :2].numpy(), name="dmeans2D")
+    assert np.all(gr["dmeans2D"][:, 2] == 0)
+    _close(gr["dopacity"], op.grad.numpy(), name="dopacity")
+    _close(gr["dsh"], shs.grad.numpy(), name="dsh")
+    _close(gr["dscales"], scl.grad.numpy(), name="dscales")
+    _close(gr["drotations"], rot.grad.numpy(), name="drotations")
+    _close(gr["dmeans3D"], m3.grad.numpy(), name="dmeans3D")
+
+
+def test_oracle_precomputed_colors_and_cov3d_vs_dense(oracle):
+    W, H = 48, 48
+    cam, sc = _scene(30, W, H, 0, seed=5)
+    g = torch.Generator().manual_seed(2)
+    colors = torch.rand((30, 3), generator=g)
+    cov = torch.tensor(oracle.cov3d(sc.scales.numpy(), 1.0, sc.rotations.numpy()))
+    bg = np.array([0.1, 0.2, 0.3], np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg, colors=colors.numpy(), cov3D=cov.numpy())
+    fw = oracle.forward(osc)
+    dpix = gs_scenes.dl_dimage(H, W, seed=4, scale=1.0).numpy()
+    gr = oracle.backward(osc, dpix)
+    d = torch.float64
+    m3 = sc.means3D.to(d).requires_grad_(True)
+    m2 = torch.zeros((30, 3), dtype=d, requires_grad=True)
+    op = sc.opacities.to(d).requires_grad_(True)
+    col = colors.to(d).requires_grad_(True)
+    cv = cov.to(d).requires_grad_(True)
+    img, radii = dense_ref.render(m3, m2, op[:, 0], cam.world_view_transform.to(d), cam.full_proj_transform.to(d),
+                                  cam.camera_center.to(d), math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), W, H,
+                                  torch.tensor(bg, dtype=d), colors=col, cov3D=cv)
+    np.testing.assert_array_equal(fw["radii"], radii.numpy())
+    _close(fw["color"], img.detach().numpy(), rtol=1e-5, frac=1e-5, name="image")
+    (img * torch.tensor(dpix, dtype=d)).sum().backward()
+    _close(gr["dcolors"], col.grad.numpy(), name="dcolors")
+    _close(gr["dcov3D"], cv.grad.numpy(), name="dcov3D")
+    _close(gr["dmeans3D"], m3.grad.numpy(), name="dmeans3D")
+    _close(gr["dopacity"], op.grad.numpy(), name="dopacity")
+
+
+def test_oracle_empty_scene_is_all_zero(oracle):
+    cam = gs_scenes.identity_camera(32, 32)
+    osc = oracle.Scene(bg=np.ones(3, np.float32), means3D=np.zeros((0, 3), np.float32),
+                       opacities=np.zeros((0, 1), np.float32), W=32, H=32,
+                       viewmatrix=cam.world_view_transform.numpy(), projmatrix=cam.full_proj_transform.numpy(),
+                       campos=cam.camera_center.numpy(), tanfovx=0.5, tanfovy=0.5,
+                       colors_precomp=np.zeros((0, 3), np.float32), cov3D_precomp=np.zeros((0, 6), np.float32))
+    fw = oracle.forward(osc)
+    assert fw["num_rendered"] == 0 and np.all(fw["color"] == 0)
+
+
+def test_oracle_sorted_list_is_tile_depth_index_ordered(oracle):
+    cam, sc = _scene(200, 96, 64, 0, seed=8)
+    osc = _oracle_scene(oracle, cam, sc, np.zeros(3, np.float32))
+    fw = oracle.forward(osc, intermediates=True)
+    lst, rng, depth = fw["point_list"], fw["ranges"], fw["depth"]
+    assert lst.shape[0] == fw["num_rendered"] == int(fw["tiles_touched"].sum())
+    for t in range(rng.shape[0]):
+        a, b = rng[t]
+        ids = lst[a:b]
+        keys = list(zip(depth[ids].view(np.uint32), ids))
+        assert keys == sorted(keys)
