@@ -2,8 +2,10 @@
 //
 // Restates the un-vendored upstream backward (spec SURVEY.md §8a a7-a8) without global atomics:
 //   k_render_bwd      one 256-lane workgroup per tile walks the tile's list back to front
-//                     (starting at the tile's max n_contrib -- later entries never contribute),
-//                     recovers T by division, computes the 9 per-(pixel, Gaussian) gradient terms,
+//                     (starting at the tile's max n_contrib -- later entries never contribute);
+//                     each wave64 owns an 8x8 quadrant and visits only the entries whose
+//                     conservative alpha box meets it (scalar walk over ballot masks),
+//                     recovers T with one reciprocal, computes the 9 per-(pixel, Gaussian) terms,
 //                     sums them over each wave64 with DPP (row_bcast:15/31 tree) into an LDS slab per
 //                     wave, then sums the 4 wave slabs in fixed order and STORES one 9-float record
 //                     per (Gaussian, tile) instance at the instance's depth-ordered slot.
@@ -30,13 +32,15 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_bwd(CameraArgs c, const uin
   __shared__ float4 s_co[GS_BLOCK];
   __shared__ float4 s_rgb[GS_BLOCK];
   __shared__ uint32_t s_slot[GS_BLOCK];
-  __shared__ float s_acc[4][GRAD_REC][GS_BLOCK];
+  __shared__ uint64_t s_mask[4][4];
+  __shared__ float s_acc[4][GS_BLOCK][ACC_STRIDE];  // per-wave partial records, 40-B rows
   const uint32_t tile = blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int px = tx * GS_TILE + (tid & 15), py = ty * GS_TILE + (tid >> 4);
-  const bool inside = px < c.W && py < c.H;
-  const float pfx = (float)px, pfy = (float)py;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const QuadPix q = quad_pixel(tx, ty, wid, lane);
+  const bool inside = q.px < c.W && q.py < c.H;
+  const float pfx = (float)q.px, pfy = (float)q.py;
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
   const uint32_t n_eff = min(tile_max[tile], n);
@@ -48,7 +52,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_bwd(CameraArgs c, const uin
     for (int k = 0; k < GRAD_REC; k++) r[k] = 0.0f;
   }
 
-  const size_t HW = (size_t)c.W * c.H, pix = inside ? (size_t)py * c.W + px : 0;
+  const size_t HW = (size_t)c.W * c.H, pix = inside ? (size_t)q.py * c.W + q.px : 0;
   const float T_final = inside ? final_T[pix] : 0.0f;
   float T = T_final;
   const uint32_t last_contributor = inside ? n_contrib[pix] : 0u;
@@ -60,11 +64,13 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_bwd(CameraArgs c, const uin
   float lc0 = 0.0f, lc1 = 0.0f, lc2 = 0.0f;  // last_color
   float last_alpha = 0.0f;
   const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
-  float* my_slab = &s_acc[wid][0][0];
+  // the wave's pixels are all finished once the walk is past their last contributors
+  const uint32_t wave_last = __builtin_amdgcn_readfirstlane(wave_max_u32(last_contributor));
 
   for (uint32_t base = 0; base < n_eff; base += GS_BLOCK) {
     const uint32_t cnt = min((uint32_t)GS_BLOCK, n_eff - base);
     __syncthreads();
+    uint32_t qmask = 0;
     if ((uint32_t)tid < cnt) {
       const uint32_t e = n_eff - 1 - (base + tid);
       const uint32_t slot = point_list[range.x + e];
@@ -74,66 +80,72 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_bwd(CameraArgs c, const uin
       s_co[tid] = make_float4(a.z, a.w, b.x, b.y);
       s_rgb[tid] = make_float4(b.z, b.w, d.x, 0.0f);
       s_slot[tid] = slot;
+      qmask = quadrant_mask(a.x, a.y, d.z, d.w, tx, ty);
     }
+    publish_masks(qmask, s_mask, tid);
     {
-      float4* z4 = reinterpret_cast<float4*>(my_slab);
+      float4* z4 = reinterpret_cast<float4*>(&s_acc[wid][0][0]);
 #pragma unroll
-      for (int k = 0; k < GRAD_REC * GS_BLOCK / 4 / 64; k++) z4[k * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < ACC_STRIDE * GS_BLOCK / 4 / 64; k++) z4[k * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
-    for (uint32_t j = 0; j < cnt; j++) {
-      const uint32_t e = n_eff - 1 - (base + j);
-      bool contrib = false;
-      float v[GRAD_REC];
-#pragma unroll
-      for (int k = 0; k < GRAD_REC; k++) v[k] = 0.0f;
-      if (inside && e < last_contributor) {
+#pragma unroll 1
+    for (int qq = 0; qq < 4; qq++) {
+      uint64_t m = uniform_u64(s_mask[qq][wid]);
+      while (m) {
+        const uint32_t j = (uint32_t)(qq * 64 + __builtin_ctzll(m));
+        m &= m - 1;
+        const uint32_t e = n_eff - 1 - (base + j);
+        if (e >= wave_last) continue;  // no pixel of this wave reaches entry e
         const float2 xy = s_xy[j];
         const float4 co = s_co[j];
         const float dx = xy.x - pfx, dy = xy.y - pfy;
         const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-        if (power <= 0.0f) {
-          const float G = gs_exp(power);
-          const float alpha = fminf(0.99f, co.w * G);
-          if (alpha >= 1.0f / 255.0f) {
-            contrib = true;
-            T = T / (1.f - alpha);
-            const float dchannel_dcolor = alpha * T;
-            const float4 rgb = s_rgb[j];
-            float dL_dalpha = 0.0f;
-            ar0 = last_alpha * lc0 + (1.f - last_alpha) * ar0;
-            lc0 = rgb.x;
-            dL_dalpha += (rgb.x - ar0) * dp0;
-            v[0] = dchannel_dcolor * dp0;
-            ar1 = last_alpha * lc1 + (1.f - last_alpha) * ar1;
-            lc1 = rgb.y;
-            dL_dalpha += (rgb.y - ar1) * dp1;
-            v[1] = dchannel_dcolor * dp1;
-            ar2 = last_alpha * lc2 + (1.f - last_alpha) * ar2;
-            lc2 = rgb.z;
-            dL_dalpha += (rgb.z - ar2) * dp2;
-            v[2] = dchannel_dcolor * dp2;
-            dL_dalpha *= T;
-            last_alpha = alpha;
-            dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-            const float dL_dG = co.w * dL_dalpha;
-            const float gdx = G * dx, gdy = G * dy;
-            const float dG_ddelx = -gdx * co.x - gdy * co.y;
-            const float dG_ddely = -gdy * co.z - gdx * co.y;
-            v[3] = dL_dG * dG_ddelx * ddelx_dx;
-            v[4] = dL_dG * dG_ddely * ddely_dy;
-            v[5] = -0.5f * gdx * dx * dL_dG;
-            v[6] = -0.5f * gdx * dy * dL_dG;
-            v[7] = -0.5f * gdy * dy * dL_dG;
-            v[8] = G * dL_dalpha;
-          }
-        }
-      }
-      if (__ballot(contrib) != 0) {
+        const float G = gs_exp(power);
+        const float alpha = fminf(0.99f, co.w * G);
+        const bool contrib = e < last_contributor && power <= 0.0f && alpha >= 1.0f / 255.0f;
+        float v[ACC_STRIDE];
 #pragma unroll
-        for (int k = 0; k < GRAD_REC; k++) {
-          const float sum = wave_sum_to_lane63(v[k]);
-          if (lane == 63) my_slab[k * GS_BLOCK + j] = sum;
+        for (int k = 0; k < ACC_STRIDE; k++) v[k] = 0.0f;
+        if (contrib) {
+          const float inv = 1.f / (1.f - alpha);
+          T = T * inv;
+          const float dchannel_dcolor = alpha * T;
+          const float4 rgb = s_rgb[j];
+          float dL_dalpha = 0.0f;
+          ar0 = last_alpha * lc0 + (1.f - last_alpha) * ar0;
+          lc0 = rgb.x;
+          dL_dalpha += (rgb.x - ar0) * dp0;
+          v[0] = dchannel_dcolor * dp0;
+          ar1 = last_alpha * lc1 + (1.f - last_alpha) * ar1;
+          lc1 = rgb.y;
+          dL_dalpha += (rgb.y - ar1) * dp1;
+          v[1] = dchannel_dcolor * dp1;
+          ar2 = last_alpha * lc2 + (1.f - last_alpha) * ar2;
+          lc2 = rgb.z;
+          dL_dalpha += (rgb.z - ar2) * dp2;
+          v[2] = dchannel_dcolor * dp2;
+          dL_dalpha *= T;
+          last_alpha = alpha;
+          dL_dalpha += (-T_final * inv) * bg_dot;
+          const float dL_dG = co.w * dL_dalpha;
+          const float gdx = G * dx, gdy = G * dy;
+          const float dG_ddelx = -gdx * co.x - gdy * co.y;
+          const float dG_ddely = -gdy * co.z - gdx * co.y;
+          v[3] = dL_dG * dG_ddelx * ddelx_dx;
+          v[4] = dL_dG * dG_ddely * ddely_dy;
+          v[5] = -0.5f * gdx * dx * dL_dG;
+          v[6] = -0.5f * gdx * dy * dL_dG;
+          v[7] = -0.5f * gdy * dy * dL_dG;
+          v[8] = G * dL_dalpha;
+        }
+        if (__ballot(contrib) != 0) {
+          wave_sum9_to_lane63(v);
+          if (lane == 63) {
+            float2* dst = reinterpret_cast<float2*>(&s_acc[wid][j][0]);
+#pragma unroll
+            for (int k = 0; k < ACC_STRIDE / 2; k++) dst[k] = make_float2(v[2 * k], v[2 * k + 1]);
+          }
         }
       }
     }
@@ -142,7 +154,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_bwd(CameraArgs c, const uin
       float* r = gradrec + (size_t)s_slot[tid] * GRAD_REC;
 #pragma unroll
       for (int k = 0; k < GRAD_REC; k++)
-        r[k] = s_acc[0][k][tid] + s_acc[1][k][tid] + s_acc[2][k][tid] + s_acc[3][k][tid];
+        r[k] = s_acc[0][tid][k] + s_acc[1][tid][k] + s_acc[2][tid][k] + s_acc[3][tid][k];
     }
   }
 }

@@ -39,9 +39,10 @@ constexpr float SH_C30 = -0.5900435899266435f, SH_C31 = 2.890611442640554f, SH_C
 
 // exp(x) of the splat falloff (x = power <= 0).  Cody-Waite reduction + degree-6 minimax
 // polynomial from correctly rounded IEEE ops only: 2 mul, 1 rndne, 8 fma, 1 add, 1 shift -- about
-// the issue cost of ocml's expf, and reproducible bit-for-bit by the CPU oracle.
+// the issue cost of ocml's expf, and reproducible bit-for-bit by the CPU oracle.  Branch-free:
+// x is clamped to [-87, 0] (below -87 the result, <= 1.7e-38, only ever meets `alpha < 1/255`).
 __device__ __forceinline__ float gs_exp(float x) {
-  if (!(x >= -87.0f)) return 0.0f;
+  x = fminf(fmaxf(x, -87.0f), 0.0f);
   float t = x * 1.44269504088896341f;
   float n = __builtin_rintf(t);
   float r = __builtin_fmaf(n, -0.693359375f, x);
@@ -201,8 +202,83 @@ __device__ __forceinline__ float wave_sum_to_lane63(float v) {
   return v;
 }
 
+// Nine independent 64-lane sums, interleaved step by step so consecutive DPP ops never read a
+// VGPR written by the instruction just before (no s_nop wait states); totals land in lane 63.
+template <int N>
+__device__ __forceinline__ void wave_sumN_to_lane63(float* v) {
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0xB1>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0x4E>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0x141>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0x140>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0x142, 0xA>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0x143, 0xC>(v[k]);
+}
+__device__ __forceinline__ void wave_sum9_to_lane63(float* v) { wave_sumN_to_lane63<9>(v); }
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
 __device__ __forceinline__ float readlane63(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// ------------------------------------------------------------------------------------------
+// render tiling: a 16x16 tile is 4 wave64 quadrants of 8x8 pixels (square regions meet fewer
+// splats than 4x16 strips).  Each staged batch entry carries a 4-bit quadrant mask from its
+// conservative alpha box; a wave walks only the entries of its quadrant (scalar bit loop).
+// ------------------------------------------------------------------------------------------
+struct QuadPix {
+  int px, py;
+};
+__device__ __forceinline__ QuadPix quad_pixel(int tx, int ty, int wid, int lane) {
+  QuadPix q;
+  q.px = tx * GS_TILE + 8 * (wid & 1) + (lane & 7);
+  q.py = ty * GS_TILE + 8 * (wid >> 1) + (lane >> 3);
+  return q;
+}
+
+// bit w set if the box [mx-ex, mx+ex] x [my-ey, my+ey] meets the pixel centres of quadrant w
+__device__ __forceinline__ uint32_t quadrant_mask(float mx, float my, float ex, float ey, int tx, int ty) {
+  if (!(ex >= 0.0f)) return 0u;
+  uint32_t m = 0;
+  const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const float qx0 = x0 + 8.0f * (w & 1), qy0 = y0 + 8.0f * (w >> 1);
+    const bool hit = (mx + ex >= qx0) && (mx - ex <= qx0 + 7.0f) && (my + ey >= qy0) && (my - ey <= qy0 + 7.0f);
+    m |= hit ? (1u << w) : 0u;
+  }
+  return m;
+}
+
+// each staging wave publishes, per quadrant, the 64-bit set of its entries meeting that quadrant
+__device__ __forceinline__ void publish_masks(uint32_t qmask, uint64_t (*s_mask)[4], int tid) {
+  const uint64_t b0 = __ballot(qmask & 1u), b1 = __ballot(qmask & 2u), b2 = __ballot(qmask & 4u),
+                 b3 = __ballot(qmask & 8u);
+  if ((tid & 63) == 0) {
+    s_mask[tid >> 6][0] = b0;
+    s_mask[tid >> 6][1] = b1;
+    s_mask[tid >> 6][2] = b2;
+    s_mask[tid >> 6][3] = b3;
+  }
+}
+
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
 }
 
 }  // namespace gs

@@ -129,9 +129,18 @@ __global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c
     float len = sqrtf(dx * dx + dy * dy + dz * dz);
     sh_to_rgb<(DEG < 0 ? 0 : DEG)>(g.shs + (size_t)i * g.M * 3, g.M, dx / len, dy / len, dz / len, rgb, cl);
   }
+  // conservative half extents of the {alpha >= 1/255} ellipse (render-side culling only; never
+  // changes a result): 0.5 d^T conic d <= ln(255 o)  ->  |dx| <= sqrt(2 ln(255 o) a), |dy| <= ...
+  const float op = g.opacities[i];
+  float ex = -1.0f, ey = -1.0f;
+  if (op >= 1.0f / 255.0f) {
+    const float t2 = 2.0f * fmaxf(logf(255.0f * op), 0.0f);
+    ex = sqrtf(t2 * cv.a) * 1.001f + 0.05f;
+    ey = sqrtf(t2 * cv.c) * 1.001f + 0.05f;
+  }
   splat[3 * i + 0] = make_float4(sx, sy, cxx, cxy);
-  splat[3 * i + 1] = make_float4(cyy, g.opacities[i], rgb[0], rgb[1]);
-  splat[3 * i + 2] = make_float4(rgb[2], pv.z, 0.0f, 0.0f);
+  splat[3 * i + 1] = make_float4(cyy, op, rgb[0], rgb[1]);
+  splat[3 * i + 2] = make_float4(rgb[2], pv.z, ex, ey);
   depth_key[i] = __float_as_uint(pv.z);
   radii[i] = radius;
   tiles[i] = (uint32_t)area;
@@ -255,54 +264,71 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   __shared__ float2 s_xy[GS_BLOCK];
   __shared__ float4 s_co[GS_BLOCK];
   __shared__ float4 s_rgb[GS_BLOCK];
+  __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
   __shared__ uint32_t s_max;
   const uint32_t tile = blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
-  const int tid = threadIdx.x;
-  const int px = tx * GS_TILE + (tid & 15), py = ty * GS_TILE + (tid >> 4);
-  const bool inside = px < c.W && py < c.H;
-  const float pfx = (float)px, pfy = (float)py;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const QuadPix q = quad_pixel(tx, ty, wid, lane);
+  const bool inside = q.px < c.W && q.py < c.H;
+  const float pfx = (float)q.px, pfy = (float)q.py;
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
   if (tid == 0) s_max = 0;
   float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
-  uint32_t contributor = 0, last = 0;
+  uint32_t last = 0;
   bool done = !inside;
   for (uint32_t base = 0; base < n; base += GS_BLOCK) {
     if (__syncthreads_and(done)) break;
-    if (base + tid < n) {
+    const uint32_t cnt = min((uint32_t)GS_BLOCK, n - base);
+    uint32_t qmask = 0;
+    if ((uint32_t)tid < cnt) {
       const uint32_t gid = presort_gid[point_list[range.x + base + tid]];
       const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
       s_xy[tid] = make_float2(a.x, a.y);
       s_co[tid] = make_float4(a.z, a.w, b.x, b.y);
       s_rgb[tid] = make_float4(b.z, b.w, d.x, 0.0f);
+      qmask = quadrant_mask(a.x, a.y, d.z, d.w, tx, ty);
     }
+    publish_masks(qmask, s_mask, tid);
     __syncthreads();
-    const uint32_t cnt = min((uint32_t)GS_BLOCK, n - base);
-    for (uint32_t j = 0; !done && j < cnt; j++) {
-      contributor++;
-      const float2 xy = s_xy[j];
-      const float4 co = s_co[j];
-      const float dx = xy.x - pfx, dy = xy.y - pfy;
-      const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-      if (power > 0.0f) continue;
-      const float alpha = fminf(0.99f, co.w * gs_exp(power));
-      if (alpha < 1.0f / 255.0f) continue;
-      const float test_T = T * (1.0f - alpha);
-      if (test_T < 0.0001f) {
-        done = true;
-        continue;
+    if (__ballot(!done) == 0) continue;
+#pragma unroll 1
+    for (int qq = 0; qq < 4; qq++) {
+      uint64_t m = uniform_u64(s_mask[qq][wid]);
+      while (m) {
+        const uint32_t j = (uint32_t)(qq * 64 + __builtin_ctzll(m));
+        m &= m - 1;
+        {
+          const float2 xy = s_xy[j];
+          const float4 co = s_co[j];
+          const float dx = xy.x - pfx, dy = xy.y - pfy;
+          const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+          const float alpha = fminf(0.99f, co.w * gs_exp(power));
+          if (!done && power <= 0.0f && alpha >= 1.0f / 255.0f) {
+            const float test_T = T * (1.0f - alpha);
+            if (test_T < 0.0001f) {
+              done = true;
+            } else {
+              const float4 rgb = s_rgb[j];
+              C0 += rgb.x * alpha * T;
+              C1 += rgb.y * alpha * T;
+              C2 += rgb.z * alpha * T;
+              T = test_T;
+              last = base + j + 1;
+            }
+          }
+        }
+        if (__ballot(!done) == 0) {
+          qq = 4;
+          break;
+        }
       }
-      const float4 rgb = s_rgb[j];
-      C0 += rgb.x * alpha * T;
-      C1 += rgb.y * alpha * T;
-      C2 += rgb.z * alpha * T;
-      T = test_T;
-      last = contributor;
     }
   }
   if (inside) {
-    const size_t pix = (size_t)py * c.W + px, HW = (size_t)c.W * c.H;
+    const size_t pix = (size_t)q.py * c.W + q.px, HW = (size_t)c.W * c.H;
     final_T[pix] = T;
     n_contrib[pix] = last;
     out[pix] = C0 + T * c.bg[0];

@@ -55,10 +55,11 @@ static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 static inline float f_as(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 static inline uint32_t u_as(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 
-/* exp(x) for the splat falloff; x <= 0 in practice.  Returns 0 below -87 (alpha would be far
- * below 1/255 for any opacity <= 1).  Identical op sequence in csrc/gs_common.h:gs_exp. */
+/* exp(x) for the splat falloff; x <= 0 in practice.  x is clamped to [-87, 0] (below -87 the
+ * result, <= 1.7e-38, only ever meets `alpha < 1/255`; above 0 the caller skips).  Identical op
+ * sequence in csrc/gs_common.h:gs_exp. */
 float oracle_exp(float x) {
-    if (!(x >= -87.0f)) return 0.0f;
+    x = fminf(fmaxf(x, -87.0f), 0.0f);
     float t = x * 1.44269504088896341f;
     float n = rintf(t);
     float r = fmaf(n, -0.693359375f, x);
@@ -644,7 +645,10 @@ long long oracle_backward(int P, int D, int M, const float* bg, int W, int H, co
                         float G = oracle_exp(power);
                         float alpha = fminf(0.99f, o->opacity * G);
                         if (alpha < 1.0f / 255.0f) continue;
-                        T = T / (1.f - alpha);
+                        /* T recovered with one correctly rounded reciprocal, reused for the background
+                         * term (upstream divides twice; identical up to one rounding) */
+                        float inv = 1.f / (1.f - alpha);
+                        T = T * inv;
                         float dchannel_dcolor = alpha * T;
                         float dL_dalpha = 0.0f;
                         double* a = iacc + (size_t)k * 9;
@@ -657,7 +661,7 @@ long long oracle_backward(int P, int D, int M, const float* bg, int W, int H, co
                         }
                         dL_dalpha *= T;
                         last_alpha = alpha;
-                        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+                        dL_dalpha += (-T_final * inv) * bg_dot;
                         float dL_dG = o->opacity * dL_dalpha;
                         float gdx = G * dx, gdy = G * dy;
                         float dG_ddelx = -gdx * o->conic[0] - gdy * o->conic[1];
