@@ -19,70 +19,86 @@
 
 namespace gs {
 
-__global__ __launch_bounds__(GS_BLOCK) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
-                                                         const uint32_t* __restrict__ point_list,
-                                                         const uint32_t* __restrict__ presort_gid,
-                                                         const float4* __restrict__ splat,
-                                                         const float* __restrict__ final_T,
-                                                         const uint32_t* __restrict__ n_contrib,
-                                                         const uint32_t* __restrict__ tile_max,
-                                                         const float* __restrict__ dL_dpix,
-                                                         float* __restrict__ gradrec) {
+constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x, y) and (x, y + 8)
+
+// Tile backward.  Wave w covers the 8x16 half [x0 + 8w, +8) x [y0, +16) of the tile; a lane holds
+// two vertically adjacent pixels so every per-pixel quantity is a 2-vector (v_pk_*_f32).  The
+// per-entry gradient terms of the two pixels are pre-summed in the lane, summed over each 16-lane
+// row with DPP, and the 4 row sums are added into the wave's LDS record with ds_add_f32.
+__global__ __launch_bounds__(BWD_THREADS) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
+                                                            const uint32_t* __restrict__ point_list,
+                                                            const uint32_t* __restrict__ presort_gid,
+                                                            const float4* __restrict__ splat,
+                                                            const float* __restrict__ final_T,
+                                                            const uint32_t* __restrict__ n_contrib,
+                                                            const uint32_t* __restrict__ tile_max,
+                                                            const float* __restrict__ dL_dpix,
+                                                            float* __restrict__ gradrec) {
   __shared__ float2 s_xy[GS_BLOCK];
   __shared__ float4 s_co[GS_BLOCK];
   __shared__ float4 s_rgb[GS_BLOCK];
   __shared__ uint32_t s_slot[GS_BLOCK];
-  __shared__ uint64_t s_mask[4][4];
-  __shared__ float s_acc[4][GS_BLOCK][ACC_STRIDE];  // per-wave partial records, 40-B rows
+  __shared__ uint64_t s_mask[4][2];  // [64-entry group][half]
+  __shared__ float s_acc[2][GS_BLOCK][ACC_STRIDE];
   const uint32_t tile = blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const QuadPix q = quad_pixel(tx, ty, wid, lane);
-  const bool inside = q.px < c.W && q.py < c.H;
-  const float pfx = (float)q.px, pfy = (float)q.py;
+  const int px = tx * GS_TILE + 8 * wid + (lane & 7);
+  const int pyA = ty * GS_TILE + (lane >> 3), pyB = pyA + 8;
+  const bool inA = px < c.W && pyA < c.H, inB = px < c.W && pyB < c.H;
+  const float pfx = (float)px;
+  const f2 pfy = {(float)pyA, (float)pyB};
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
   const uint32_t n_eff = min(tile_max[tile], n);
 
   // instances past the last contributor of every pixel get zero records
-  for (uint32_t e = n_eff + tid; e < n; e += GS_BLOCK) {
+  for (uint32_t e = n_eff + tid; e < n; e += BWD_THREADS) {
     float* r = gradrec + (size_t)point_list[range.x + e] * GRAD_REC;
 #pragma unroll
     for (int k = 0; k < GRAD_REC; k++) r[k] = 0.0f;
   }
 
-  const size_t HW = (size_t)c.W * c.H, pix = inside ? (size_t)q.py * c.W + q.px : 0;
-  const float T_final = inside ? final_T[pix] : 0.0f;
-  float T = T_final;
-  const uint32_t last_contributor = inside ? n_contrib[pix] : 0u;
-  const float dp0 = inside ? dL_dpix[pix] : 0.0f;
-  const float dp1 = inside ? dL_dpix[HW + pix] : 0.0f;
-  const float dp2 = inside ? dL_dpix[2 * HW + pix] : 0.0f;
-  const float bg_dot = c.bg[0] * dp0 + c.bg[1] * dp1 + c.bg[2] * dp2;
-  float ar0 = 0.0f, ar1 = 0.0f, ar2 = 0.0f;  // accum_rec
-  float lc0 = 0.0f, lc1 = 0.0f, lc2 = 0.0f;  // last_color
-  float last_alpha = 0.0f;
+  const size_t HW = (size_t)c.W * c.H;
+  const size_t pixA = inA ? (size_t)pyA * c.W + px : 0, pixB = inB ? (size_t)pyB * c.W + px : 0;
+  const f2 T_final = {inA ? final_T[pixA] : 0.0f, inB ? final_T[pixB] : 0.0f};
+  f2 T = T_final;
+  const uint32_t lastA = inA ? n_contrib[pixA] : 0u, lastB = inB ? n_contrib[pixB] : 0u;
+  const f2 dp0 = {inA ? dL_dpix[pixA] : 0.0f, inB ? dL_dpix[pixB] : 0.0f};
+  const f2 dp1 = {inA ? dL_dpix[HW + pixA] : 0.0f, inB ? dL_dpix[HW + pixB] : 0.0f};
+  const f2 dp2 = {inA ? dL_dpix[2 * HW + pixA] : 0.0f, inB ? dL_dpix[2 * HW + pixB] : 0.0f};
+  const f2 bg_dot = c.bg[0] * dp0 + c.bg[1] * dp1 + c.bg[2] * dp2;
+  f2 Aacc = 0.0f;  // sum_c accum_rec_c * dL/dpix_c
+  f2 Lc = 0.0f;    // sum_c last_color_c * dL/dpix_c
+  f2 last_alpha = 0.0f;
   const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
-  // the wave's pixels are all finished once the walk is past their last contributors
-  const uint32_t wave_last = __builtin_amdgcn_readfirstlane(wave_max_u32(last_contributor));
+  const uint32_t wave_last = __builtin_amdgcn_readfirstlane(wave_max_u32(max(lastA, lastB)));
 
   for (uint32_t base = 0; base < n_eff; base += GS_BLOCK) {
     const uint32_t cnt = min((uint32_t)GS_BLOCK, n_eff - base);
     __syncthreads();
-    uint32_t qmask = 0;
-    if ((uint32_t)tid < cnt) {
-      const uint32_t e = n_eff - 1 - (base + tid);
-      const uint32_t slot = point_list[range.x + e];
-      const uint32_t gid = presort_gid[slot];
-      const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
-      s_xy[tid] = make_float2(a.x, a.y);
-      s_co[tid] = make_float4(a.z, a.w, b.x, b.y);
-      s_rgb[tid] = make_float4(b.z, b.w, d.x, 0.0f);
-      s_slot[tid] = slot;
-      qmask = quadrant_mask(a.x, a.y, d.z, d.w, tx, ty);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int t = tid + BWD_THREADS * h;
+      uint32_t hm = 0;
+      if ((uint32_t)t < cnt) {
+        const uint32_t e = n_eff - 1 - (base + t);
+        const uint32_t slot = point_list[range.x + e];
+        const uint32_t gid = presort_gid[slot];
+        const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
+        s_xy[t] = make_float2(a.x, a.y);
+        s_co[t] = make_float4(a.z, a.w, b.x, b.y);
+        s_rgb[t] = make_float4(b.z, b.w, d.x, 0.0f);
+        s_slot[t] = slot;
+        hm = half_mask(a.x, a.y, d.z, d.w, tx, ty);
+      }
+      const uint64_t b0 = __ballot(hm & 1u), b1 = __ballot(hm & 2u);
+      if (lane == 0) {
+        s_mask[2 * h + wid][0] = b0;
+        s_mask[2 * h + wid][1] = b1;
+      }
     }
-    publish_masks(qmask, s_mask, tid);
     {
       float4* z4 = reinterpret_cast<float4*>(&s_acc[wid][0][0]);
 #pragma unroll
@@ -90,71 +106,91 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_bwd(CameraArgs c, const uin
     }
     __syncthreads();
 #pragma unroll 1
-    for (int qq = 0; qq < 4; qq++) {
-      uint64_t m = uniform_u64(s_mask[qq][wid]);
+    for (int g = 0; g < 4; g++) {
+      uint64_t m = uniform_u64(s_mask[g][wid]);
       while (m) {
-        const uint32_t j = (uint32_t)(qq * 64 + __builtin_ctzll(m));
+        const uint32_t j = (uint32_t)(g * 64 + __builtin_ctzll(m));
         m &= m - 1;
         const uint32_t e = n_eff - 1 - (base + j);
         if (e >= wave_last) continue;  // no pixel of this wave reaches entry e
         const float2 xy = s_xy[j];
         const float4 co = s_co[j];
-        const float dx = xy.x - pfx, dy = xy.y - pfy;
-        const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-        const float G = gs_exp(power);
-        const float alpha = fminf(0.99f, co.w * G);
-        const bool contrib = e < last_contributor && power <= 0.0f && alpha >= 1.0f / 255.0f;
-        float v[ACC_STRIDE];
+        const float dx = xy.x - pfx;
+        const f2 dy = xy.y - pfy;
+        const float t1 = co.x * dx * dx;
+        const f2 power = -0.5f * (t1 + co.z * dy * dy) - (co.y * dx) * dy;
+        const f2 G = gs_exp_pk(power);
+        const f2 oG = co.w * G;
+        const f2 alpha = {fminf(0.99f, oG.x), fminf(0.99f, oG.y)};
+        const bool cA = e < lastA && power.x <= 0.0f && alpha.x >= 1.0f / 255.0f;
+        const bool cB = e < lastB && power.y <= 0.0f && alpha.y >= 1.0f / 255.0f;
+        if (__ballot(cA || cB) == 0) continue;
+        // Reduced form of the upstream per-pair terms (same quantities, fewer ops per pixel):
+        //   w0..2 = alpha T dL/dpix_c;  q = dL/dG * G;  w3 = q dx, w4 = q dy;
+        //   w5 = q dx^2, w6 = q dx dy, w7 = q dy^2;  w8 = G dL/dalpha.
+        // The flush maps the pixel sums to the upstream record: dmean2D.x = -W/2 (cxx S3 + cxy S4),
+        // dmean2D.y = -H/2 (cyy S4 + cxy S3), dconic = -S5/2, -S6/2, -S7/2.
+        // accum_rec is carried as A = sum_c accum_rec_c dL/dpix_c and last_color as
+        // Lc = sum_c last_color_c dL/dpix_c, which is all dL/dalpha needs.
+        const float4 rgb = s_rgb[j];
+        const f2 omA = 1.f - alpha;
+        f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
+        inv = inv * (2.0f - omA * inv);  // one Newton step: ~0.5 ulp, like the IEEE divide
+        const f2 Tn = T * inv;
+        const f2 dch = alpha * Tn;
+        const f2 Cd = rgb.x * dp0 + rgb.y * dp1 + rgb.z * dp2;
+        const f2 An = last_alpha * Lc + (1.f - last_alpha) * Aacc;
+        const f2 dLa = (Cd - An) * Tn + (-T_final * inv) * bg_dot;
+        const f2 q = (co.w * dLa) * G;
+        const f2 w3 = q * dx, w4 = q * dy;
+        f2 vv[GRAD_REC];
+        vv[0] = dch * dp0;
+        vv[1] = dch * dp1;
+        vv[2] = dch * dp2;
+        vv[3] = w3;
+        vv[4] = w4;
+        vv[5] = w3 * dx;
+        vv[6] = w3 * dy;
+        vv[7] = w4 * dy;
+        vv[8] = G * dLa;
+        float w[GRAD_REC];
 #pragma unroll
-        for (int k = 0; k < ACC_STRIDE; k++) v[k] = 0.0f;
-        if (contrib) {
-          const float inv = 1.f / (1.f - alpha);
-          T = T * inv;
-          const float dchannel_dcolor = alpha * T;
-          const float4 rgb = s_rgb[j];
-          float dL_dalpha = 0.0f;
-          ar0 = last_alpha * lc0 + (1.f - last_alpha) * ar0;
-          lc0 = rgb.x;
-          dL_dalpha += (rgb.x - ar0) * dp0;
-          v[0] = dchannel_dcolor * dp0;
-          ar1 = last_alpha * lc1 + (1.f - last_alpha) * ar1;
-          lc1 = rgb.y;
-          dL_dalpha += (rgb.y - ar1) * dp1;
-          v[1] = dchannel_dcolor * dp1;
-          ar2 = last_alpha * lc2 + (1.f - last_alpha) * ar2;
-          lc2 = rgb.z;
-          dL_dalpha += (rgb.z - ar2) * dp2;
-          v[2] = dchannel_dcolor * dp2;
-          dL_dalpha *= T;
-          last_alpha = alpha;
-          dL_dalpha += (-T_final * inv) * bg_dot;
-          const float dL_dG = co.w * dL_dalpha;
-          const float gdx = G * dx, gdy = G * dy;
-          const float dG_ddelx = -gdx * co.x - gdy * co.y;
-          const float dG_ddely = -gdy * co.z - gdx * co.y;
-          v[3] = dL_dG * dG_ddelx * ddelx_dx;
-          v[4] = dL_dG * dG_ddely * ddely_dy;
-          v[5] = -0.5f * gdx * dx * dL_dG;
-          v[6] = -0.5f * gdx * dy * dL_dG;
-          v[7] = -0.5f * gdy * dy * dL_dG;
-          v[8] = G * dL_dalpha;
-        }
-        if (__ballot(contrib) != 0) {
-          wave_sum9_to_lane63(v);
-          if (lane == 63) {
-            float2* dst = reinterpret_cast<float2*>(&s_acc[wid][j][0]);
+        for (int k = 0; k < GRAD_REC; k++) w[k] = (cA ? vv[k].x : 0.0f) + (cB ? vv[k].y : 0.0f);
+        T.x = cA ? Tn.x : T.x;
+        T.y = cB ? Tn.y : T.y;
+        Aacc.x = cA ? An.x : Aacc.x;
+        Aacc.y = cB ? An.y : Aacc.y;
+        Lc.x = cA ? Cd.x : Lc.x;
+        Lc.y = cB ? Cd.y : Lc.y;
+        last_alpha.x = cA ? alpha.x : last_alpha.x;
+        last_alpha.y = cB ? alpha.y : last_alpha.y;
+        row_sumN<GRAD_REC>(w);
+        if ((lane & 15) == 15) {
 #pragma unroll
-            for (int k = 0; k < ACC_STRIDE / 2; k++) dst[k] = make_float2(v[2 * k], v[2 * k + 1]);
-          }
+          for (int k = 0; k < GRAD_REC; k++) atomicAdd(&s_acc[wid][j][k], w[k]);
         }
       }
     }
     __syncthreads();
-    if ((uint32_t)tid < cnt) {
-      float* r = gradrec + (size_t)s_slot[tid] * GRAD_REC;
 #pragma unroll
-      for (int k = 0; k < GRAD_REC; k++)
-        r[k] = s_acc[0][tid][k] + s_acc[1][tid][k] + s_acc[2][tid][k] + s_acc[3][tid][k];
+    for (int h = 0; h < 2; h++) {
+      const int t = tid + BWD_THREADS * h;
+      if ((uint32_t)t < cnt) {
+        float S[GRAD_REC];
+#pragma unroll
+        for (int k = 0; k < GRAD_REC; k++) S[k] = s_acc[0][t][k] + s_acc[1][t][k];
+        const float4 co = s_co[t];
+        float* r = gradrec + (size_t)s_slot[t] * GRAD_REC;
+        r[0] = S[0];
+        r[1] = S[1];
+        r[2] = S[2];
+        r[3] = -ddelx_dx * (co.x * S[3] + co.y * S[4]);
+        r[4] = -ddely_dy * (co.z * S[4] + co.y * S[3]);
+        r[5] = -0.5f * S[5];
+        r[6] = -0.5f * S[6];
+        r[7] = -0.5f * S[7];
+        r[8] = S[8];
+      }
     }
   }
 }
@@ -162,7 +198,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_bwd(CameraArgs c, const uin
 void bwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                 const float* dL_dpix, float* gradrec, hipStream_t st) {
   const int tiles = c.gx * c.gy;
-  GS_LAUNCH("render_bwd", k_render_bwd, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
+  GS_LAUNCH("render_bwd", k_render_bwd, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges, bin.point_list,
             bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, dL_dpix, gradrec);
 }
 

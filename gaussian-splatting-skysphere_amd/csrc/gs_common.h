@@ -60,6 +60,34 @@ __device__ __forceinline__ float gs_exp(float x) {
   return p * __uint_as_float((uint32_t)e << 23);
 }
 
+// Packed (two-pixel) form of gs_exp: identical op sequence per element, so each element is
+// bit-identical to gs_exp; mul/fma/add issue as v_pk_*_f32.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 gs_exp_pk(f2 x) {
+  x.x = fminf(fmaxf(x.x, -87.0f), 0.0f);
+  x.y = fminf(fmaxf(x.y, -87.0f), 0.0f);
+  f2 t = x * 1.44269504088896341f;
+  f2 n;
+  n.x = __builtin_rintf(t.x);
+  n.y = __builtin_rintf(t.y);
+  f2 r = pk_fma(n, (f2)(-0.693359375f), x);
+  r = pk_fma(n, (f2)(2.12194440e-4f), r);
+  f2 z = r * r;
+  f2 p = (f2)(1.9875691500e-4f);
+  p = pk_fma(p, r, (f2)(1.3981999507e-3f));
+  p = pk_fma(p, r, (f2)(8.3334519073e-3f));
+  p = pk_fma(p, r, (f2)(4.1665795894e-2f));
+  p = pk_fma(p, r, (f2)(1.6666665459e-1f));
+  p = pk_fma(p, r, (f2)(5.0000001201e-1f));
+  p = pk_fma(p, z, r);
+  p = p + 1.0f;
+  f2 s;
+  s.x = __uint_as_float((uint32_t)((int)n.x + 127) << 23);
+  s.y = __uint_as_float((uint32_t)((int)n.y + 127) << 23);
+  return p * s;
+}
+
 // m = 4x4 world_view_transform / full_proj_transform, row-major flattening of the torch tensor
 // (row-vector convention: translation in row 3; /root/reference/scene/cameras.py:54-56).
 struct float3v { float x, y, z; };
@@ -221,6 +249,19 @@ __device__ __forceinline__ void wave_sumN_to_lane63(float* v) {
 }
 __device__ __forceinline__ void wave_sum9_to_lane63(float* v) { wave_sumN_to_lane63<9>(v); }
 
+// Row (16-lane) sums of N values: after this every lane of a row holds its row's sum.
+template <int N>
+__device__ __forceinline__ void row_sumN(float* v) {
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0xB1>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0x4E>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0x141>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0x140>(v[k]);
+}
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
@@ -260,6 +301,17 @@ __device__ __forceinline__ uint32_t quadrant_mask(float mx, float my, float ex, 
     const bool hit = (mx + ex >= qx0) && (mx - ex <= qx0 + 7.0f) && (my + ey >= qy0) && (my - ey <= qy0 + 7.0f);
     m |= hit ? (1u << w) : 0u;
   }
+  return m;
+}
+
+// bit h set if the alpha box meets the pixel centres of the 8-wide column half h of the tile
+__device__ __forceinline__ uint32_t half_mask(float mx, float my, float ex, float ey, int tx, int ty) {
+  if (!(ex >= 0.0f)) return 0u;
+  const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
+  if (!(my + ey >= y0 && my - ey <= y0 + 15.0f)) return 0u;
+  uint32_t m = 0;
+  m |= (mx + ex >= x0 && mx - ex <= x0 + 7.0f) ? 1u : 0u;
+  m |= (mx + ex >= x0 + 8.0f && mx - ex <= x0 + 15.0f) ? 2u : 0u;
   return m;
 }
 
