@@ -91,7 +91,7 @@ __global__ __launch_bounds__(BWD_THREADS) void k_render_bwd(CameraArgs c, const 
         s_co[t] = make_float4(a.z, a.w, b.x, b.y);
         s_rgb[t] = make_float4(b.z, b.w, d.x, 0.0f);
         s_slot[t] = slot;
-        hm = half_mask(a.x, a.y, d.z, d.w, tx, ty);
+        hm = half_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
       }
       const uint64_t b0 = __ballot(hm & 1u), b1 = __ballot(hm & 2u);
       if (lane == 0) {

@@ -276,9 +276,9 @@ __device__ __forceinline__ float readlane63(float v) {
 }
 
 // ------------------------------------------------------------------------------------------
-// render tiling: a 16x16 tile is 4 wave64 quadrants of 8x8 pixels (square regions meet fewer
-// splats than 4x16 strips).  Each staged batch entry carries a 4-bit quadrant mask from its
-// conservative alpha box; a wave walks only the entries of its quadrant (scalar bit loop).
+// render tiling: a 16x16 tile is split into per-wave pixel rectangles (8x8 quadrants in the
+// forward, 8x16 halves in the backward).  Each staged batch entry carries a mask of the
+// rectangles its alpha >= 1/255 ellipse can reach; a wave walks only its entries (scalar loop).
 // ------------------------------------------------------------------------------------------
 struct QuadPix {
   int px, py;
@@ -290,28 +290,51 @@ __device__ __forceinline__ QuadPix quad_pixel(int tx, int ty, int wid, int lane)
   return q;
 }
 
-// bit w set if the box [mx-ex, mx+ex] x [my-ey, my+ey] meets the pixel centres of quadrant w
-__device__ __forceinline__ uint32_t quadrant_mask(float mx, float my, float ex, float ey, int tx, int ty) {
-  if (!(ex >= 0.0f)) return 0u;
-  uint32_t m = 0;
+// Conservative culling of (splat, pixel-rectangle) pairs.  A pixel p can only contribute if
+// alpha >= 1/255, i.e. q(p - m) <= 2 ln(255 o) with q(d) = cxx dx^2 + 2 cxy dx dy + cyy dy^2
+// (power = -q/2).  preprocess stores lim = 2 ln(255 o) (1 + 1e-3) + 1e-3 (or -1 when o < 1/255);
+// the minimum of q over the rectangle of pixel centres is found exactly (convex quadratic: at
+// the centre if inside, else on an edge) and compared with lim.  The margins absorb rounding,
+// so a culled pair never contributes: results are unchanged, only work is skipped.
+__device__ __forceinline__ float q_form(float cx, float cy, float cz, float dx, float dy) {
+  return cx * dx * dx + 2.0f * cy * dx * dy + cz * dy * dy;
+}
+__device__ __forceinline__ bool ellipse_meets_rect(float mx, float my, float cx, float cy, float cz, float lim,
+                                                   float x0, float x1, float y0, float y1) {
+  if (!(lim >= 0.0f)) return false;
+  const float dxl = x0 - mx, dxh = x1 - mx, dyl = y0 - my, dyh = y1 - my;
+  if (dxl <= 0.0f && dxh >= 0.0f && dyl <= 0.0f && dyh >= 0.0f) return true;
+  if (!(cx > 0.0f && cz > 0.0f)) return true;  // degenerate conic: do not cull
+  const float icx = 1.0f / cx, icz = 1.0f / cz;
+  float best = q_form(cx, cy, cz, dxl, fminf(fmaxf(-cy * dxl * icz, dyl), dyh));
+  best = fminf(best, q_form(cx, cy, cz, dxh, fminf(fmaxf(-cy * dxh * icz, dyl), dyh)));
+  best = fminf(best, q_form(cx, cy, cz, fminf(fmaxf(-cy * dyl * icx, dxl), dxh), dyl));
+  best = fminf(best, q_form(cx, cy, cz, fminf(fmaxf(-cy * dyh * icx, dxl), dxh), dyh));
+  return best <= lim;
+}
+
+// bit w set if the splat can contribute to a pixel of 8x8 quadrant w of tile (tx, ty)
+__device__ __forceinline__ uint32_t quadrant_mask(float mx, float my, float cx, float cy, float cz, float lim, int tx,
+                                                  int ty) {
+  if (!(lim >= 0.0f)) return 0u;
   const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
+  uint32_t m = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) {
-    const float qx0 = x0 + 8.0f * (w & 1), qy0 = y0 + 8.0f * (w >> 1);
-    const bool hit = (mx + ex >= qx0) && (mx - ex <= qx0 + 7.0f) && (my + ey >= qy0) && (my - ey <= qy0 + 7.0f);
-    m |= hit ? (1u << w) : 0u;
+    const float qx = x0 + 8.0f * (w & 1), qy = y0 + 8.0f * (w >> 1);
+    m |= ellipse_meets_rect(mx, my, cx, cy, cz, lim, qx, qx + 7.0f, qy, qy + 7.0f) ? (1u << w) : 0u;
   }
   return m;
 }
 
-// bit h set if the alpha box meets the pixel centres of the 8-wide column half h of the tile
-__device__ __forceinline__ uint32_t half_mask(float mx, float my, float ex, float ey, int tx, int ty) {
-  if (!(ex >= 0.0f)) return 0u;
+// bit h set if the splat can contribute to a pixel of the 8-wide column half h of the tile
+__device__ __forceinline__ uint32_t half_mask(float mx, float my, float cx, float cy, float cz, float lim, int tx,
+                                              int ty) {
+  if (!(lim >= 0.0f)) return 0u;
   const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
-  if (!(my + ey >= y0 && my - ey <= y0 + 15.0f)) return 0u;
   uint32_t m = 0;
-  m |= (mx + ex >= x0 && mx - ex <= x0 + 7.0f) ? 1u : 0u;
-  m |= (mx + ex >= x0 + 8.0f && mx - ex <= x0 + 15.0f) ? 2u : 0u;
+  m |= ellipse_meets_rect(mx, my, cx, cy, cz, lim, x0, x0 + 7.0f, y0, y0 + 15.0f) ? 1u : 0u;
+  m |= ellipse_meets_rect(mx, my, cx, cy, cz, lim, x0 + 8.0f, x0 + 15.0f, y0, y0 + 15.0f) ? 2u : 0u;
   return m;
 }
 

@@ -129,18 +129,13 @@ __global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c
     float len = sqrtf(dx * dx + dy * dy + dz * dz);
     sh_to_rgb<(DEG < 0 ? 0 : DEG)>(g.shs + (size_t)i * g.M * 3, g.M, dx / len, dy / len, dz / len, rgb, cl);
   }
-  // conservative half extents of the {alpha >= 1/255} ellipse (render-side culling only; never
-  // changes a result): 0.5 d^T conic d <= ln(255 o)  ->  |dx| <= sqrt(2 ln(255 o) a), |dy| <= ...
+  // culling limit of the {alpha >= 1/255} ellipse (render-side work skipping only; never
+  // changes a result, see ellipse_meets_rect): q(d) <= 2 ln(255 o), with safety margins
   const float op = g.opacities[i];
-  float ex = -1.0f, ey = -1.0f;
-  if (op >= 1.0f / 255.0f) {
-    const float t2 = 2.0f * fmaxf(logf(255.0f * op), 0.0f);
-    ex = sqrtf(t2 * cv.a) * 1.001f + 0.05f;
-    ey = sqrtf(t2 * cv.c) * 1.001f + 0.05f;
-  }
+  const float lim = op >= 1.0f / 255.0f ? 2.0f * fmaxf(logf(255.0f * op), 0.0f) * 1.001f + 1e-3f : -1.0f;
   splat[3 * i + 0] = make_float4(sx, sy, cxx, cxy);
   splat[3 * i + 1] = make_float4(cyy, op, rgb[0], rgb[1]);
-  splat[3 * i + 2] = make_float4(rgb[2], pv.z, ex, ey);
+  splat[3 * i + 2] = make_float4(rgb[2], pv.z, lim, 0.0f);
   depth_key[i] = __float_as_uint(pv.z);
   radii[i] = radius;
   tiles[i] = (uint32_t)area;
@@ -289,7 +284,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
       s_xy[tid] = make_float2(a.x, a.y);
       s_co[tid] = make_float4(a.z, a.w, b.x, b.y);
       s_rgb[tid] = make_float4(b.z, b.w, d.x, 0.0f);
-      qmask = quadrant_mask(a.x, a.y, d.z, d.w, tx, ty);
+      qmask = quadrant_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
     }
     publish_masks(qmask, s_mask, tid);
     __syncthreads();

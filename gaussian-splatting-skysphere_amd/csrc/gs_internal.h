@@ -46,7 +46,7 @@ struct CameraArgs {
 };
 
 struct GeomPtrs {
-  float4* splat;  // 3 per Gaussian: (x, y, cxx, cxy) (cyy, opacity, r, g) (b, depth, -, -)
+  float4* splat;  // 3 per Gaussian: (x, y, cxx, cxy) (cyy, opacity, r, g) (b, depth, cull_lim, -)
   uint32_t* depth_key;
   uint32_t* tiles;
   uint32_t* goff;  // first instance slot of each visible Gaussian (depth order)

@@ -157,11 +157,19 @@ struct DstArray {
 
 // ------------------------------------------------------------------------------------------
 // radix sort
+//
+// Stable LSD radix sort, 8-bit digits.  Per pass: k_radix_hist (per-block digit counts) ->
+// exclusive scan of the [digit][block] matrix -> k_radix_scatter.  A block walks its chunk in
+// tiles of 2048 keys (8 per lane): each wave ranks its 512 consecutive keys round by round with
+// ballot peer masks (stable), the 4 waves are combined per digit in LDS, the tile is reordered by
+// digit in LDS, and runs of equal digits are written out contiguously (coalesced stores).
 // ------------------------------------------------------------------------------------------
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;
 constexpr int SORT_THREADS = 256;
-constexpr int SORT_MAX_BLOCKS = 1024;
+constexpr int SORT_ITEMS = 8;
+constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;  // 2048 keys
+constexpr int SORT_MAX_BLOCKS = 512;
 
 struct SortPlan {
   uint32_t nb, chunk;
@@ -170,12 +178,12 @@ struct SortPlan {
 inline int radix_passes(int end_bit) { return (end_bit + RADIX_BITS - 1) / RADIX_BITS; }
 
 inline SortPlan sort_plan(uint64_t n_max) {
-  uint64_t tiles = (n_max + SORT_THREADS - 1) / SORT_THREADS;
+  uint64_t tiles = (n_max + SORT_TILE - 1) / SORT_TILE;
   if (tiles == 0) tiles = 1;
   uint64_t per = (tiles + SORT_MAX_BLOCKS - 1) / SORT_MAX_BLOCKS;
   SortPlan p;
   p.nb = (uint32_t)((tiles + per - 1) / per);
-  p.chunk = (uint32_t)(per * SORT_THREADS);
+  p.chunk = (uint32_t)(per * SORT_TILE);
   return p;
 }
 
@@ -184,6 +192,16 @@ inline size_t sort_scratch_words(uint64_t n_max) {
   SortPlan p = sort_plan(n_max);
   size_t hist = (size_t)RADIX * p.nb;
   return hist + scan_plan(hist).nb + 16;
+}
+
+// lanes of this wave whose `bits`-bit digit equals mine (valid lanes only)
+__device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits) {
+  uint64_t peers = __ballot(valid);
+  for (int b = 0; b < bits; b++) {
+    const uint64_t bb = __ballot((d >> b) & 1);
+    peers &= ((d >> b) & 1) ? bb : ~bb;
+  }
+  return peers;
 }
 
 static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys,
@@ -196,16 +214,21 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32
   __syncthreads();
   const uint64_t start = (uint64_t)blockIdx.x * chunk;
   const uint64_t end = start + chunk < n ? start + chunk : n;
-  for (uint64_t i = start + threadIdx.x; i < end; i += SORT_THREADS) {
-    uint32_t d = (keys[i] >> shift) & ((1u << bits) - 1u);
-    // wave-aggregated LDS increment: one atomic per distinct digit per wave
-    uint64_t peers = __ballot(1);
+  const uint32_t mask = (1u << bits) - 1u;
+  for (uint64_t t0 = start; t0 < end; t0 += SORT_TILE) {
+    uint32_t d[SORT_ITEMS];
+    bool v[SORT_ITEMS];
 #pragma unroll
-    for (int b = 0; b < RADIX_BITS; b++) {
-      uint64_t bb = __ballot((d >> b) & 1);
-      peers &= ((d >> b) & 1) ? bb : ~bb;
+    for (int k = 0; k < SORT_ITEMS; k++) {
+      const uint64_t i = t0 + (uint64_t)k * SORT_THREADS + threadIdx.x;
+      v[k] = i < end;
+      d[k] = v[k] ? (keys[i] >> shift) & mask : 0u;
     }
-    if ((peers & lanemask_lt()) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
+#pragma unroll
+    for (int k = 0; k < SORT_ITEMS; k++) {
+      const uint64_t peers = digit_peers(d[k], v[k], bits);
+      if (v[k] && (peers & lanemask_lt()) == 0) atomicAdd(&h[d[k]], (uint32_t)__popcll(peers));
+    }
   }
   __syncthreads();
   hist[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
@@ -215,48 +238,88 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, int bits, uint32_t chunk,
     uint32_t nb, const uint32_t* __restrict__ hist) {
-  __shared__ uint32_t base[RADIX];
-  __shared__ uint32_t wcnt[4][RADIX];
+  __shared__ uint32_t s_base[RADIX];      // global position of the next key of each digit
+  __shared__ uint32_t s_wcnt[4][RADIX];   // per-wave running counts -> per-wave exclusive prefix
+  __shared__ uint32_t s_loc[RADIX];       // digit offsets inside the tile (for the LDS reorder)
+  __shared__ uint32_t s_tot[RADIX];
+  __shared__ uint32_t s_scan[4];
+  __shared__ uint32_t s_key[SORT_TILE];
+  __shared__ uint32_t s_val[SORT_TILE];
   const uint32_t n = resolve_n(n_dev, n_max);
-  const uint32_t tid = threadIdx.x, wid = tid >> 6;
-  base[tid] = hist[(size_t)tid * nb + blockIdx.x];
+  const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  s_base[tid] = hist[(size_t)tid * nb + blockIdx.x];
   const uint64_t start = (uint64_t)blockIdx.x * chunk;
   const uint64_t end = start + chunk < n ? start + chunk : n;
   const uint32_t mask = (1u << bits) - 1u;
-  for (uint64_t t0 = start; t0 < end; t0 += SORT_THREADS) {
-    const uint64_t i = t0 + tid;
-    const bool valid = i < end;
-    const uint32_t key = valid ? keys_in[i] : 0u;
-    const uint32_t val = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
-    const uint32_t d = (key >> shift) & mask;
-    wcnt[0][tid] = 0;
-    wcnt[1][tid] = 0;
-    wcnt[2][tid] = 0;
-    wcnt[3][tid] = 0;
+  for (uint64_t t0 = start; t0 < end; t0 += SORT_TILE) {
+    s_wcnt[0][tid] = 0;
+    s_wcnt[1][tid] = 0;
+    s_wcnt[2][tid] = 0;
+    s_wcnt[3][tid] = 0;
     __syncthreads();
-    uint64_t peers = __ballot(valid);
-    for (int b = 0; b < bits; b++) {
-      uint64_t bb = __ballot((d >> b) & 1);
-      peers &= ((d >> b) & 1) ? bb : ~bb;
+    // wave wid ranks positions t0 + wid*512 + r*64 + lane, r = 0..7 (in order -> stable)
+    uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) {
+      const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
+      const bool v = i < end;
+      key[r] = v ? keys_in[i] : 0xFFFFFFFFu;
+      val[r] = v ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
     }
-    const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-    if (valid && rank == 0) wcnt[wid][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    // thread `tid` owns digit `tid`: exclusive prefix over the 4 waves, tile total
-    uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
-    __syncthreads();
-    wcnt[0][tid] = 0;
-    wcnt[1][tid] = c0;
-    wcnt[2][tid] = c0 + c1;
-    wcnt[3][tid] = c0 + c1 + c2;
-    __syncthreads();
-    if (valid) {
-      uint32_t pos = base[d] + wcnt[wid][d] + rank;
-      keys_out[pos] = key;
-      vals_out[pos] = val;
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) {
+      const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
+      const bool v = i < end;
+      const uint32_t d = (key[r] >> shift) & mask;
+      const uint64_t peers = digit_peers(d, v, bits);
+      const uint32_t before = (uint32_t)__popcll(peers & lanemask_lt());
+      const uint32_t run = v ? s_wcnt[wid][d] : 0u;
+      rank[r] = run + before;
+      // make sure every lane read the running count before the leader bumps it
+      __builtin_amdgcn_wave_barrier();
+      if (v && before == 0) s_wcnt[wid][d] = run + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    base[tid] += c0 + c1 + c2 + c3;
+    // digit tid: prefix over waves, tile total, then exclusive scan of totals over digits
+    const uint32_t c0 = s_wcnt[0][tid], c1 = s_wcnt[1][tid], c2 = s_wcnt[2][tid], c3 = s_wcnt[3][tid];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    uint32_t tot_all;
+    const uint32_t loc = block_excl_scan(tot, s_scan, &tot_all);
+    s_wcnt[0][tid] = 0;
+    s_wcnt[1][tid] = c0;
+    s_wcnt[2][tid] = c0 + c1;
+    s_wcnt[3][tid] = c0 + c1 + c2;
+    s_loc[tid] = loc;
+    s_tot[tid] = tot;
+    __syncthreads();
+    // reorder the tile by digit in LDS
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) {
+      const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
+      if (i < end) {
+        const uint32_t d = (key[r] >> shift) & mask;
+        const uint32_t slot = s_loc[d] + s_wcnt[wid][d] + rank[r];
+        s_key[slot] = key[r];
+        s_val[slot] = val[r];
+      }
+    }
+    __syncthreads();
+    // write runs of equal digits contiguously
+    const uint32_t ntile = (uint32_t)((end - t0) < (uint64_t)SORT_TILE ? (end - t0) : (uint64_t)SORT_TILE);
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) {
+      const uint32_t slot = (uint32_t)r * SORT_THREADS + tid;
+      if (slot < ntile) {
+        const uint32_t k = s_key[slot];
+        const uint32_t d = (k >> shift) & mask;
+        const uint32_t pos = s_base[d] + (slot - s_loc[d]);
+        keys_out[pos] = k;
+        vals_out[pos] = s_val[slot];
+      }
+    }
+    __syncthreads();
+    s_base[tid] += s_tot[tid];
   }
 }
 
