@@ -19,13 +19,47 @@
 
 namespace gs {
 
+// culling-side evaluation of one entry for a lane's two pixels (independent of the pixel state)
+struct Eval {
+  float4 co;
+  float dx;
+  f2 dy, G, alpha;
+  bool cA, cB;
+};
+__device__ __forceinline__ Eval eval_pair(float2 xy, float4 co, float pfx, f2 pfy, uint32_t e, uint32_t lastA,
+                                          uint32_t lastB) {
+  Eval v;
+  v.co = co;
+  v.dx = xy.x - pfx;
+  v.dy = xy.y - pfy;
+  const float t1 = co.x * v.dx * v.dx;
+  const f2 power = -0.5f * (t1 + co.z * v.dy * v.dy) - (co.y * v.dx) * v.dy;
+  v.G = gs_exp_pk(power);
+  const f2 oG = co.w * v.G;
+  v.alpha.x = fminf(0.99f, oG.x);
+  v.alpha.y = fminf(0.99f, oG.y);
+  v.cA = e < lastA && power.x <= 0.0f && v.alpha.x >= 1.0f / 255.0f;
+  v.cB = e < lastB && power.y <= 0.0f && v.alpha.y >= 1.0f / 255.0f;
+  return v;
+}
+
 constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x, y) and (x, y + 8)
+#ifndef GS_BWD_BATCH
+#define GS_BWD_BATCH 128
+#endif
+#ifndef GS_BWD_MINW
+#define GS_BWD_MINW 1
+#endif
+constexpr int BWD_BATCH = GS_BWD_BATCH;  // entries staged per round (128: LDS 16 KB/block -> 5 waves/SIMD)
+constexpr int BWD_GROUPS = BWD_BATCH / 64;
+constexpr int BWD_STAGE_ROUNDS = (BWD_BATCH + BWD_THREADS - 1) / BWD_THREADS;
+static_assert(BWD_BATCH % 64 == 0, "batch must be whole waves");
 
 // Tile backward.  Wave w covers the 8x16 half [x0 + 8w, +8) x [y0, +16) of the tile; a lane holds
 // two vertically adjacent pixels so every per-pixel quantity is a 2-vector (v_pk_*_f32).  The
 // per-entry gradient terms of the two pixels are pre-summed in the lane, summed over each 16-lane
 // row with DPP, and the 4 row sums are added into the wave's LDS record with ds_add_f32.
-__global__ __launch_bounds__(BWD_THREADS) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
+__global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ point_list,
                                                             const uint32_t* __restrict__ presort_gid,
                                                             const float4* __restrict__ splat,
@@ -34,12 +68,12 @@ __global__ __launch_bounds__(BWD_THREADS) void k_render_bwd(CameraArgs c, const 
                                                             const uint32_t* __restrict__ tile_max,
                                                             const float* __restrict__ dL_dpix,
                                                             float* __restrict__ gradrec) {
-  __shared__ float2 s_xy[GS_BLOCK];
-  __shared__ float4 s_co[GS_BLOCK];
-  __shared__ float4 s_rgb[GS_BLOCK];
-  __shared__ uint32_t s_slot[GS_BLOCK];
-  __shared__ uint64_t s_mask[4][2];  // [64-entry group][half]
-  __shared__ float s_acc[2][GS_BLOCK][ACC_STRIDE];
+  __shared__ float2 s_xy[BWD_BATCH];
+  __shared__ float4 s_co[BWD_BATCH];
+  __shared__ float4 s_rgb[BWD_BATCH];
+  __shared__ uint32_t s_slot[BWD_BATCH];
+  __shared__ uint64_t s_mask[BWD_GROUPS][2];  // [64-entry group][half]
+  __shared__ float s_acc[2][BWD_BATCH][ACC_STRIDE];
   const uint32_t tile = blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -75,12 +109,65 @@ __global__ __launch_bounds__(BWD_THREADS) void k_render_bwd(CameraArgs c, const 
   const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
   const uint32_t wave_last = __builtin_amdgcn_readfirstlane(wave_max_u32(max(lastA, lastB)));
 
-  for (uint32_t base = 0; base < n_eff; base += GS_BLOCK) {
-    const uint32_t cnt = min((uint32_t)GS_BLOCK, n_eff - base);
+  // gradient commit of entry j (walk order) for the lane's contributing pixels
+  auto apply = [&](uint32_t j, const Eval& v) {
+    const float4 co = v.co;
+    const f2 G = v.G, alpha = v.alpha, dy = v.dy;
+    const float dx = v.dx;
+    const bool cA = v.cA, cB = v.cB;
+    // Reduced form of the upstream per-pair terms (same quantities, fewer ops per pixel):
+    //   w0..2 = alpha T dL/dpix_c;  q = dL/dG * G;  w3 = q dx, w4 = q dy;
+    //   w5 = q dx^2, w6 = q dx dy, w7 = q dy^2;  w8 = G dL/dalpha.
+    // The flush maps the pixel sums to the upstream record: dmean2D.x = -W/2 (cxx S3 + cxy S4),
+    // dmean2D.y = -H/2 (cyy S4 + cxy S3), dconic = -S5/2, -S6/2, -S7/2.
+    // accum_rec is carried as A = sum_c accum_rec_c dL/dpix_c and last_color as
+    // Lc = sum_c last_color_c dL/dpix_c, which is all dL/dalpha needs.
+    const float4 rgb = s_rgb[j];
+    const f2 omA = 1.f - alpha;
+    f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
+    inv = inv * (2.0f - omA * inv);  // one Newton step: ~0.5 ulp, like the IEEE divide
+    const f2 Tn = T * inv;
+    const f2 dch = alpha * Tn;
+    const f2 Cd = rgb.x * dp0 + rgb.y * dp1 + rgb.z * dp2;
+    const f2 An = last_alpha * Lc + (1.f - last_alpha) * Aacc;
+    const f2 dLa = (Cd - An) * Tn + (-T_final * inv) * bg_dot;
+    const f2 q = (co.w * dLa) * G;
+    const f2 w3 = q * dx, w4 = q * dy;
+    f2 vv[GRAD_REC];
+    vv[0] = dch * dp0;
+    vv[1] = dch * dp1;
+    vv[2] = dch * dp2;
+    vv[3] = w3;
+    vv[4] = w4;
+    vv[5] = w3 * dx;
+    vv[6] = w3 * dy;
+    vv[7] = w4 * dy;
+    vv[8] = G * dLa;
+    float w[GRAD_REC];
+#pragma unroll
+    for (int k = 0; k < GRAD_REC; k++) w[k] = (cA ? vv[k].x : 0.0f) + (cB ? vv[k].y : 0.0f);
+    T.x = cA ? Tn.x : T.x;
+    T.y = cB ? Tn.y : T.y;
+    Aacc.x = cA ? An.x : Aacc.x;
+    Aacc.y = cB ? An.y : Aacc.y;
+    Lc.x = cA ? Cd.x : Lc.x;
+    Lc.y = cB ? Cd.y : Lc.y;
+    last_alpha.x = cA ? alpha.x : last_alpha.x;
+    last_alpha.y = cB ? alpha.y : last_alpha.y;
+    row_sumN<GRAD_REC>(w);
+    if ((lane & 15) == 15) {
+#pragma unroll
+      for (int k = 0; k < GRAD_REC; k++) atomicAdd(&s_acc[wid][j][k], w[k]);
+    }
+  };
+
+  for (uint32_t base = 0; base < n_eff; base += BWD_BATCH) {
+    const uint32_t cnt = min((uint32_t)BWD_BATCH, n_eff - base);
     __syncthreads();
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < BWD_STAGE_ROUNDS; h++) {
       const int t = tid + BWD_THREADS * h;
+      if (t >= BWD_BATCH) break;  // (wave-uniform)
       uint32_t hm = 0;
       if ((uint32_t)t < cnt) {
         const uint32_t e = n_eff - 1 - (base + t);
@@ -95,87 +182,34 @@ __global__ __launch_bounds__(BWD_THREADS) void k_render_bwd(CameraArgs c, const 
       }
       const uint64_t b0 = __ballot(hm & 1u), b1 = __ballot(hm & 2u);
       if (lane == 0) {
-        s_mask[2 * h + wid][0] = b0;
-        s_mask[2 * h + wid][1] = b1;
+        s_mask[t >> 6][0] = b0;
+        s_mask[t >> 6][1] = b1;
       }
     }
     {
       float4* z4 = reinterpret_cast<float4*>(&s_acc[wid][0][0]);
 #pragma unroll
-      for (int k = 0; k < ACC_STRIDE * GS_BLOCK / 4 / 64; k++) z4[k * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < (ACC_STRIDE * BWD_BATCH / 4 + 63) / 64; k++)
+        if (k * 64 + lane < ACC_STRIDE * BWD_BATCH / 4) z4[k * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
 #pragma unroll 1
-    for (int g = 0; g < 4; g++) {
+    for (int g = 0; g < BWD_GROUPS; g++) {
       uint64_t m = uniform_u64(s_mask[g][wid]);
       while (m) {
         const uint32_t j = (uint32_t)(g * 64 + __builtin_ctzll(m));
         m &= m - 1;
         const uint32_t e = n_eff - 1 - (base + j);
         if (e >= wave_last) continue;  // no pixel of this wave reaches entry e
-        const float2 xy = s_xy[j];
-        const float4 co = s_co[j];
-        const float dx = xy.x - pfx;
-        const f2 dy = xy.y - pfy;
-        const float t1 = co.x * dx * dx;
-        const f2 power = -0.5f * (t1 + co.z * dy * dy) - (co.y * dx) * dy;
-        const f2 G = gs_exp_pk(power);
-        const f2 oG = co.w * G;
-        const f2 alpha = {fminf(0.99f, oG.x), fminf(0.99f, oG.y)};
-        const bool cA = e < lastA && power.x <= 0.0f && alpha.x >= 1.0f / 255.0f;
-        const bool cB = e < lastB && power.y <= 0.0f && alpha.y >= 1.0f / 255.0f;
-        if (__ballot(cA || cB) == 0) continue;
-        // Reduced form of the upstream per-pair terms (same quantities, fewer ops per pixel):
-        //   w0..2 = alpha T dL/dpix_c;  q = dL/dG * G;  w3 = q dx, w4 = q dy;
-        //   w5 = q dx^2, w6 = q dx dy, w7 = q dy^2;  w8 = G dL/dalpha.
-        // The flush maps the pixel sums to the upstream record: dmean2D.x = -W/2 (cxx S3 + cxy S4),
-        // dmean2D.y = -H/2 (cyy S4 + cxy S3), dconic = -S5/2, -S6/2, -S7/2.
-        // accum_rec is carried as A = sum_c accum_rec_c dL/dpix_c and last_color as
-        // Lc = sum_c last_color_c dL/dpix_c, which is all dL/dalpha needs.
-        const float4 rgb = s_rgb[j];
-        const f2 omA = 1.f - alpha;
-        f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
-        inv = inv * (2.0f - omA * inv);  // one Newton step: ~0.5 ulp, like the IEEE divide
-        const f2 Tn = T * inv;
-        const f2 dch = alpha * Tn;
-        const f2 Cd = rgb.x * dp0 + rgb.y * dp1 + rgb.z * dp2;
-        const f2 An = last_alpha * Lc + (1.f - last_alpha) * Aacc;
-        const f2 dLa = (Cd - An) * Tn + (-T_final * inv) * bg_dot;
-        const f2 q = (co.w * dLa) * G;
-        const f2 w3 = q * dx, w4 = q * dy;
-        f2 vv[GRAD_REC];
-        vv[0] = dch * dp0;
-        vv[1] = dch * dp1;
-        vv[2] = dch * dp2;
-        vv[3] = w3;
-        vv[4] = w4;
-        vv[5] = w3 * dx;
-        vv[6] = w3 * dy;
-        vv[7] = w4 * dy;
-        vv[8] = G * dLa;
-        float w[GRAD_REC];
-#pragma unroll
-        for (int k = 0; k < GRAD_REC; k++) w[k] = (cA ? vv[k].x : 0.0f) + (cB ? vv[k].y : 0.0f);
-        T.x = cA ? Tn.x : T.x;
-        T.y = cB ? Tn.y : T.y;
-        Aacc.x = cA ? An.x : Aacc.x;
-        Aacc.y = cB ? An.y : Aacc.y;
-        Lc.x = cA ? Cd.x : Lc.x;
-        Lc.y = cB ? Cd.y : Lc.y;
-        last_alpha.x = cA ? alpha.x : last_alpha.x;
-        last_alpha.y = cB ? alpha.y : last_alpha.y;
-        row_sumN<GRAD_REC>(w);
-        if ((lane & 15) == 15) {
-#pragma unroll
-          for (int k = 0; k < GRAD_REC; k++) atomicAdd(&s_acc[wid][j][k], w[k]);
-        }
+        const Eval v = eval_pair(s_xy[j], s_co[j], pfx, pfy, e, lastA, lastB);
+        if (__ballot(v.cA || v.cB) != 0) apply(j, v);
       }
     }
     __syncthreads();
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < BWD_STAGE_ROUNDS; h++) {
       const int t = tid + BWD_THREADS * h;
-      if ((uint32_t)t < cnt) {
+      if (t < BWD_BATCH && (uint32_t)t < cnt) {
         float S[GRAD_REC];
 #pragma unroll
         for (int k = 0; k < GRAD_REC; k++) S[k] = s_acc[0][t][k] + s_acc[1][t][k];

@@ -292,27 +292,46 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
 #pragma unroll 1
     for (int qq = 0; qq < 4; qq++) {
       uint64_t m = uniform_u64(s_mask[qq][wid]);
+      // two entries per trip: their power / exp / alpha chains are independent (ILP); the
+      // compositing of the pair is then applied in order, exactly as one entry at a time
       while (m) {
-        const uint32_t j = (uint32_t)(qq * 64 + __builtin_ctzll(m));
+        const uint32_t j0 = (uint32_t)(qq * 64 + __builtin_ctzll(m));
         m &= m - 1;
-        {
-          const float2 xy = s_xy[j];
-          const float4 co = s_co[j];
-          const float dx = xy.x - pfx, dy = xy.y - pfy;
-          const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-          const float alpha = fminf(0.99f, co.w * gs_exp(power));
-          if (!done && power <= 0.0f && alpha >= 1.0f / 255.0f) {
-            const float test_T = T * (1.0f - alpha);
-            if (test_T < 0.0001f) {
-              done = true;
-            } else {
-              const float4 rgb = s_rgb[j];
-              C0 += rgb.x * alpha * T;
-              C1 += rgb.y * alpha * T;
-              C2 += rgb.z * alpha * T;
-              T = test_T;
-              last = base + j + 1;
-            }
+        const bool has1 = m != 0;
+        const uint32_t j1 = has1 ? (uint32_t)(qq * 64 + __builtin_ctzll(m)) : j0;
+        if (has1) m &= m - 1;
+        const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
+        const float4 co0 = s_co[j0], co1 = s_co[j1];
+        const float dx0 = xy0.x - pfx, dy0 = xy0.y - pfy;
+        const float dx1 = xy1.x - pfx, dy1 = xy1.y - pfy;
+        const float power0 = -0.5f * (co0.x * dx0 * dx0 + co0.z * dy0 * dy0) - co0.y * dx0 * dy0;
+        const float power1 = -0.5f * (co1.x * dx1 * dx1 + co1.z * dy1 * dy1) - co1.y * dx1 * dy1;
+        const float alpha0 = fminf(0.99f, co0.w * gs_exp(power0));
+        const float alpha1 = fminf(0.99f, co1.w * gs_exp(power1));
+        if (!done && power0 <= 0.0f && alpha0 >= 1.0f / 255.0f) {
+          const float test_T = T * (1.0f - alpha0);
+          if (test_T < 0.0001f) {
+            done = true;
+          } else {
+            const float4 rgb = s_rgb[j0];
+            C0 += rgb.x * alpha0 * T;
+            C1 += rgb.y * alpha0 * T;
+            C2 += rgb.z * alpha0 * T;
+            T = test_T;
+            last = base + j0 + 1;
+          }
+        }
+        if (has1 && !done && power1 <= 0.0f && alpha1 >= 1.0f / 255.0f) {
+          const float test_T = T * (1.0f - alpha1);
+          if (test_T < 0.0001f) {
+            done = true;
+          } else {
+            const float4 rgb = s_rgb[j1];
+            C0 += rgb.x * alpha1 * T;
+            C1 += rgb.y * alpha1 * T;
+            C2 += rgb.z * alpha1 * T;
+            T = test_T;
+            last = base + j1 + 1;
           }
         }
         if (__ballot(!done) == 0) {
