@@ -1,0 +1,79 @@
+"""View-parallel exchange (gs_view_parallel) on CPU with gloo, world_size 2: one flat bucket
+all-reduce of the 59-float/Gaussian gradient set, densify-statistics reduction, view sharding."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import gs_view_parallel as vp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, P, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(rank)
+        shapes = [(P, 3), (P, 1, 3), (P, 15, 3), (P, 1), (P, 3), (P, 4)]  # xyz f_dc f_rest opacity scaling rotation
+        params = [torch.zeros(s, requires_grad=True) for s in shapes]
+        for p in params:
+            p.grad = torch.randn(p.shape, generator=g)
+        local = [p.grad.clone() for p in params]
+        b = vp.GradBucket(params)
+        assert b.numel == 59 * P
+        b.allreduce()
+        acc = torch.zeros(P, 1) + rank
+        den = torch.ones(P, 1)
+        mr = torch.full((P,), float(rank + 1))
+        vp.reduce_densify_stats(acc, den, mr)
+        out_q.put((rank, [t.numpy() for t in local], [p.grad.numpy() for p in params], acc.numpy(), den.numpy(),
+                   mr.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucket_allreduce_and_densify_stats_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    P = 37
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, P, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, local, red, acc, den, mr = q.get(timeout=120)
+        res[r] = (local, red, acc, den, mr)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in range(6):
+        expect = res[0][0][k] + res[1][0][k]
+        for r in range(2):
+            torch.testing.assert_close(torch.tensor(res[r][1][k]), torch.tensor(expect))
+    for r in range(2):
+        assert (res[r][2] == 1).all() and (res[r][3] == 2).all() and (res[r][4] == 2).all()
+
+
+def test_shard_views_round_robin():
+    assert vp.shard_views(8, 0, 8) == [0]
+    assert vp.shard_views(8, 1, 2) == [1, 3, 5, 7]
+    views = sorted(v for r in range(3) for v in vp.shard_views(10, r, 3))
+    assert views == list(range(10))
+
+
+def test_single_process_allreduce_is_identity():
+    p = torch.zeros(5, 3, requires_grad=True)
+    p.grad = torch.arange(15.0).reshape(5, 3)
+    vp.allreduce_grads([p])
+    assert torch.equal(p.grad, torch.arange(15.0).reshape(5, 3))
