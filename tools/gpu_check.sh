@@ -14,4 +14,13 @@ if [ -n "$PROFILE" ]; then
   cd /tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof.log; exit 1; }
 fi
+if [ -n "$PMC" ]; then
+  cd /tmp
+  for pass in fetch:FETCH_SIZE write:WRITE_SIZE; do
+    name=${pass%%:*}; ctr=${pass#*:}
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctr -d $OUT/pmc_$name -o run --output-format csv -- python3 $R/tools/prof_step.py --workload c3 --steps 2 --warmup 1 > $OUT/pmc_$name.log 2>&1 || { echo "pmc $name failed"; tail -20 $OUT/pmc_$name.log; exit 1; }
+  done
+  cd $R
+  python tools/pmc_traffic.py $OUT c3 $OUT/pmc_traffic.json > $OUT/pmc_traffic.txt 2>&1 || { echo "pmc_traffic failed"; exit 1; }
+fi
 echo done
