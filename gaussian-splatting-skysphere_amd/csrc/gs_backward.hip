@@ -1,14 +1,15 @@
 // gs_backward.hip -- backward pass of the MI355X Gaussian rasterizer (gfx950).
 //
 // Restates the un-vendored upstream backward (spec SURVEY.md §8a a7-a8) without global atomics:
-//   k_render_bwd      one 256-lane workgroup per tile walks the tile's list back to front
+//   k_render_bwd      one 128-lane workgroup per tile walks the tile's list back to front
 //                     (starting at the tile's max n_contrib -- later entries never contribute);
-//                     each wave64 owns an 8x8 quadrant and visits only the entries whose
-//                     conservative alpha box meets it (scalar walk over ballot masks),
-//                     recovers T with one reciprocal, computes the 9 per-(pixel, Gaussian) terms,
-//                     sums them over each wave64 with DPP (row_bcast:15/31 tree) into an LDS slab per
-//                     wave, then sums the 4 wave slabs in fixed order and STORES one 9-float record
-//                     per (Gaussian, tile) instance at the instance's depth-ordered slot.
+//                     each wave64 owns an 8x16 half (two pixels per lane) and visits only the
+//                     entries whose exact alpha ellipse meets it (scalar walk over ballot masks),
+//                     recovers T with one reciprocal, forms the 9 per-entry sums of its lane's two
+//                     pixels, reduces them over the wave with permlane32/16 swaps (two values per
+//                     add) + DPP row sums, and stores them in an LDS record per wave; the flush adds
+//                     the two waves' records and STORES one 9-float record per (Gaussian, tile)
+//                     instance at the instance's depth-ordered slot.
 //   k_preprocess_bwd  one lane per Gaussian sums its contiguous instance records (fixed order:
 //                     deterministic, no float atomics) and runs conic -> cov2D -> cov3D / mean,
 //                     projection, SH and scale/rotation gradients in one pass.
@@ -57,8 +58,8 @@ static_assert(BWD_BATCH % 64 == 0, "batch must be whole waves");
 
 // Tile backward.  Wave w covers the 8x16 half [x0 + 8w, +8) x [y0, +16) of the tile; a lane holds
 // two vertically adjacent pixels so every per-pixel quantity is a 2-vector (v_pk_*_f32).  The
-// per-entry gradient terms of the two pixels are pre-summed in the lane, summed over each 16-lane
-// row with DPP, and the 4 row sums are added into the wave's LDS record with ds_add_f32.
+// per-entry gradient terms of the two pixels are pre-summed in the lane, summed over the wave
+// (wave_sum9_rows) and stored into the wave's LDS record by one lane per row.
 __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ point_list,
                                                             const uint32_t* __restrict__ presort_gid,
@@ -116,9 +117,11 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     const float dx = v.dx;
     const bool cA = v.cA, cB = v.cB;
     // Reduced form of the upstream per-pair terms (same quantities, fewer ops per pixel):
-    //   w0..2 = alpha T dL/dpix_c;  q = dL/dG * G;  w3 = q dx, w4 = q dy;
-    //   w5 = q dx^2, w6 = q dx dy, w7 = q dy^2;  w8 = G dL/dalpha.
-    // The flush maps the pixel sums to the upstream record: dmean2D.x = -W/2 (cxx S3 + cxy S4),
+    //   s0..2 = sum alpha T dL/dpix_c;  q = dL/dG * G;  s3 = sum q dx, s4 = sum q dy;
+    //   s5 = sum q dx^2, s6 = sum q dx dy, s7 = sum q dy^2;  s8 = sum G dL/dalpha,
+    // summed over the lane's two pixels (same column: dx is shared).  A pixel that does not
+    // contribute gets dL/dalpha = alpha T = 0, which zeroes all of its terms.
+    // The flush maps the wave sums to the upstream record: dmean2D.x = -W/2 (cxx S3 + cxy S4),
     // dmean2D.y = -H/2 (cyy S4 + cxy S3), dconic = -S5/2, -S6/2, -S7/2.
     // accum_rec is carried as A = sum_c accum_rec_c dL/dpix_c and last_color as
     // Lc = sum_c last_color_c dL/dpix_c, which is all dL/dalpha needs.
@@ -131,21 +134,20 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     const f2 Cd = rgb.x * dp0 + rgb.y * dp1 + rgb.z * dp2;
     const f2 An = last_alpha * Lc + (1.f - last_alpha) * Aacc;
     const f2 dLa = (Cd - An) * Tn + (-T_final * inv) * bg_dot;
-    const f2 q = (co.w * dLa) * G;
-    const f2 w3 = q * dx, w4 = q * dy;
-    f2 vv[GRAD_REC];
-    vv[0] = dch * dp0;
-    vv[1] = dch * dp1;
-    vv[2] = dch * dp2;
-    vv[3] = w3;
-    vv[4] = w4;
-    vv[5] = w3 * dx;
-    vv[6] = w3 * dy;
-    vv[7] = w4 * dy;
-    vv[8] = G * dLa;
-    float w[GRAD_REC];
-#pragma unroll
-    for (int k = 0; k < GRAD_REC; k++) w[k] = (cA ? vv[k].x : 0.0f) + (cB ? vv[k].y : 0.0f);
+    const f2 dLm = {cA ? dLa.x : 0.0f, cB ? dLa.y : 0.0f};
+    const f2 dcm = {cA ? dch.x : 0.0f, cB ? dch.y : 0.0f};
+    const f2 q = (co.w * dLm) * G;
+    const f2 w4 = q * dy;
+    float s[GRAD_REC];
+    s[0] = __builtin_fmaf(dcm.x, dp0.x, dcm.y * dp0.y);
+    s[1] = __builtin_fmaf(dcm.x, dp1.x, dcm.y * dp1.y);
+    s[2] = __builtin_fmaf(dcm.x, dp2.x, dcm.y * dp2.y);
+    s[3] = dx * (q.x + q.y);
+    s[4] = w4.x + w4.y;
+    s[5] = dx * s[3];
+    s[6] = dx * s[4];
+    s[7] = __builtin_fmaf(w4.x, dy.x, w4.y * dy.y);
+    s[8] = __builtin_fmaf(G.x, dLm.x, G.y * dLm.y);
     T.x = cA ? Tn.x : T.x;
     T.y = cB ? Tn.y : T.y;
     Aacc.x = cA ? An.x : Aacc.x;
@@ -154,10 +156,17 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     Lc.y = cB ? Cd.y : Lc.y;
     last_alpha.x = cA ? alpha.x : last_alpha.x;
     last_alpha.y = cB ? alpha.y : last_alpha.y;
-    row_sumN<GRAD_REC>(w);
-    if ((lane & 15) == 15) {
-#pragma unroll
-      for (int k = 0; k < GRAD_REC; k++) atomicAdd(&s_acc[wid][j][k], w[k]);
+    // wave sums: row r of d0 / d1 holds s[r] / s[4 + r]; every row of d8 a quarter of s[8]
+    float d0, d1, d8;
+    wave_sum9_rows(s, d0, d1, d8);
+    // materialise the sums with EXEC full: keeps the last DPP add out of the store branch, where
+    // it could not fold into v_add_f32_dpp
+    asm volatile("" ::"v"(d0), "v"(d1), "v"(d8));
+    if ((lane & 15) == 0) {
+      float* acc = &s_acc[wid][j][lane >> 4];
+      acc[0] = d0;
+      acc[4] = d1;
+      acc[8] = d8;
     }
   };
 
@@ -212,7 +221,9 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
       if (t < BWD_BATCH && (uint32_t)t < cnt) {
         float S[GRAD_REC];
 #pragma unroll
-        for (int k = 0; k < GRAD_REC; k++) S[k] = s_acc[0][t][k] + s_acc[1][t][k];
+        for (int k = 0; k < 8; k++) S[k] = s_acc[0][t][k] + s_acc[1][t][k];
+        S[8] = ((s_acc[0][t][8] + s_acc[0][t][9]) + (s_acc[0][t][10] + s_acc[0][t][11])) +
+               ((s_acc[1][t][8] + s_acc[1][t][9]) + (s_acc[1][t][10] + s_acc[1][t][11]));
         const float4 co = s_co[t];
         float* r = gradrec + (size_t)s_slot[t] * GRAD_REC;
         r[0] = S[0];

@@ -262,6 +262,31 @@ __device__ __forceinline__ void row_sumN(float* v) {
   for (int k = 0; k < N; k++) v[k] = v[k] + dpp_f<0x140>(v[k]);
 }
 
+// Wave sums of nine values with half-wave / row transposes: v_permlane32_swap and
+// v_permlane16_swap exchange halves of two registers so that one add halves the lane count of
+// two values at once.  On return row r (lanes 16r..16r+15) of d0 holds the 64-lane sum of s[r],
+// of d1 that of s[4 + r], and of d8 the sum of s[8] over row r only (the four row values add up
+// to the total of s[8]).  Every lane of a row holds its row's value.
+__device__ __forceinline__ float swap32_add(float a, float b) {
+  // lanes 0-31: a[l] + a[l + 32]; lanes 32-63: b[l - 32] + b[l]
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap16_add(float a, float b) {
+  // row pairs (0,1) and (2,3): rows 0 / 2 get a's, rows 1 / 3 get b's two-row sums
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void wave_sum9_rows(const float* s, float& d0, float& d1, float& d8) {
+  const float c0 = swap32_add(s[0], s[2]), c1 = swap32_add(s[1], s[3]);
+  const float c2 = swap32_add(s[4], s[6]), c3 = swap32_add(s[5], s[7]);
+  float v[3] = {swap16_add(c0, c1), swap16_add(c2, c3), s[8]};
+  row_sumN<3>(v);
+  d0 = v[0];
+  d1 = v[1];
+  d8 = v[2];
+}
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
