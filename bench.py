@@ -104,12 +104,6 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    lib = _native.load()
-    lib.gs_profile_reset()
-    lib.gs_profile_enable(1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -117,12 +111,22 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    lib.gs_profile_enable(0)
-    prof = _native.profile_stats()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # per-kernel durations: a second pass of the same K steps with HIP events around every launch
+    # (on the launch stream); kept out of the timed pass above because the event records add
+    # host work and small gaps between kernels
+    lib = _native.load()
+    lib.gs_profile_reset()
+    lib.gs_profile_enable(1)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    lib.gs_profile_enable(0)
+    prof = _native.profile_stats()
 
     # render-only (no_grad forward) throughput
     with torch.no_grad():

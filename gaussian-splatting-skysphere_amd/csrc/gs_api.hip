@@ -85,8 +85,9 @@ void trace_end(const char* name, hipStream_t st) {
   }
 }
 
-static void check_hip(hipError_t e, const char* what) {
+static bool check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) set_error("%s failed: %s", what, hipGetErrorString(e));
+  return e == hipSuccess;
 }
 
 static CameraArgs make_camera(const float* bg, int W, int H, const float* view, const float* proj, const float* campos,
@@ -177,6 +178,27 @@ size_t gs_grad_buffer_bytes(long long num_rendered) {
   return align_up((size_t)(num_rendered > 0 ? num_rendered : 1) * GRAD_REC * sizeof(float));
 }
 
+// Per-thread, per-device pinned readback word block + event (reused call after call: a call
+// waits on its event before returning, so the slot is free again when the next call starts).
+struct ReadbackSlot {
+  uint32_t* host = nullptr;
+  hipEvent_t ev = nullptr;
+};
+static ReadbackSlot* readback_slot() {
+  static thread_local ReadbackSlot slots[64];
+  int dev = 0;
+  if (!check_hip(hipGetDevice(&dev), "hipGetDevice")) return nullptr;
+  if (dev < 0 || dev >= 64) return set_error("device ordinal out of range"), nullptr;
+  ReadbackSlot& s = slots[dev];
+  if (!s.host) {
+    void* p = nullptr;
+    if (!check_hip(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc")) return nullptr;
+    if (!check_hip(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate")) return nullptr;
+    s.host = (uint32_t*)p;
+  }
+  return &s;
+}
+
 int gs_forward_preprocess(int P, int D, int M, const float* background, int W, int H, const float* means3D,
                           const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
                           float scale_modifier, const float* rotations, const float* cov3D_precomp,
@@ -195,14 +217,20 @@ int gs_forward_preprocess(int P, int D, int M, const float* background, int W, i
   geom_layout((size_t)P, &geo, (char*)geom_buffer);
   GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier};
   CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, prefiltered);
+  // num_rendered is the sum of the per-Gaussian tile counts, known when preprocess ends: read it
+  // back through pinned memory behind an event while the GPU goes on with compaction, the depth
+  // sort and the instance offsets, so the host round trip overlaps device work.
+  ReadbackSlot* rb = readback_slot();
+  if (!rb) return 1;
   fwd_preprocess(g, c, radii_out, geo, st);
+  check_hip(hipMemcpyAsync(rb->host, geo.counters, 16, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
+  check_hip(hipEventRecord(rb->ev, st), "hipEventRecord");
   fwd_order(P, geo, st);
-  uint32_t h[4] = {0, 0, 0, 0};
-  check_hip(hipMemcpyAsync(h, geo.counters, sizeof(h), hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
-  check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+  check_hip(hipEventSynchronize(rb->ev), "hipEventSynchronize");
   if (t_failed) return 1;
-  if (h[2] & 1u) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
-  *num_rendered_host = (long long)h[1];
+  const uint32_t err = rb->host[2], I = rb->host[3];
+  if (err & 1u) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
+  *num_rendered_host = (long long)I;
   return 0;
 }
 

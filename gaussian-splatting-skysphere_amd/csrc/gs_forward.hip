@@ -73,20 +73,19 @@ __device__ __forceinline__ void sh_to_rgb(const float* __restrict__ sh, int M, f
 }
 
 // DEG = -1: colours precomputed by the caller
+// One Gaussian; returns the number of tiles it touches (0 when culled).
 template <int DEG>
-__global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
-                                                    float4* __restrict__ splat, uint32_t* __restrict__ depth_key,
-                                                    uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
-                                                    uint32_t* __restrict__ counters) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= g.P) return;
+__device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g, const CameraArgs& c,
+                                                   int* __restrict__ radii, float4* __restrict__ splat,
+                                                   uint32_t* __restrict__ depth_key, uint32_t* __restrict__ tiles,
+                                                   uint8_t* __restrict__ clamped, uint32_t* __restrict__ counters) {
   radii[i] = 0;
   tiles[i] = 0;
   const float px = g.means3D[3 * i + 0], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
   const float3v pv = xf43(c.view, px, py, pz);
   if (pv.z <= 0.2f) {
     if (c.prefiltered) atomicOr(&counters[2], 1u);
-    return;
+    return 0;
   }
   const float* P = c.proj;
   const float hx = P[0] * px + P[4] * py + P[8] * pz + P[12];
@@ -105,7 +104,7 @@ __global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c
   }
   const Cov2D cv = cov2d(c.view, px, py, pz, cov3, c.fx, c.fy, c.tanfovx, c.tanfovy);
   const float det = cv.a * cv.c - cv.b * cv.b;
-  if (det == 0.0f) return;
+  if (det == 0.0f) return 0;
   const float det_inv = 1.f / det;
   const float cxx = cv.c * det_inv, cxy = -cv.b * det_inv, cyy = cv.a * det_inv;
   const float mid = 0.5f * (cv.a + cv.c);
@@ -116,7 +115,7 @@ __global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c
   int x0, y0, x1, y1;
   get_rect(sx, sy, radius, c.gx, c.gy, x0, y0, x1, y1);
   const int area = (x1 - x0) * (y1 - y0);
-  if (area == 0) return;
+  if (area == 0) return 0;
 
   float rgb[3];
   uint32_t cl = 0;
@@ -140,6 +139,28 @@ __global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c
   radii[i] = radius;
   tiles[i] = (uint32_t)area;
   clamped[i] = (uint8_t)cl;
+  return (uint32_t)area;
+}
+
+// The workgroup's tile total goes to counters[3] (= num_rendered, read back by the host as soon
+// as this kernel is done while the ordering kernels run).
+template <int DEG>
+__global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
+                                                    float4* __restrict__ splat, uint32_t* __restrict__ depth_key,
+                                                    uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
+                                                    uint32_t* __restrict__ counters) {
+  __shared__ uint32_t s_sum[4];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  uint32_t area = 0;
+  if (i < g.P) area = preprocess_one<DEG>(i, g, c, radii, splat, depth_key, tiles, clamped, counters);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) area += (uint32_t)__shfl_xor((int)area, d, 64);
+  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = area;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+    if (tot) atomicAdd(&counters[3], tot);
+  }
 }
 
 void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st) {

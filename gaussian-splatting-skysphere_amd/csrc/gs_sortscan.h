@@ -169,7 +169,7 @@ constexpr int RADIX = 1 << RADIX_BITS;
 constexpr int SORT_THREADS = 256;
 constexpr int SORT_ITEMS = 8;
 constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;  // 2048 keys
-constexpr int SORT_MAX_BLOCKS = 512;
+constexpr int SORT_MAX_BLOCKS = 4096;  // one 2048-key tile per workgroup up to 8M keys
 
 struct SortPlan {
   uint32_t nb, chunk;
