@@ -37,27 +37,27 @@ constexpr float SH_C30 = -0.5900435899266435f, SH_C31 = 2.890611442640554f, SH_C
                 SH_C33 = 0.3731763325901154f, SH_C34 = -0.4570457994644658f, SH_C35 = 1.445305721320277f,
                 SH_C36 = -0.5900435899266435f;
 
-// exp(x) of the splat falloff (x = power <= 0).  Cody-Waite reduction + degree-6 minimax
-// polynomial from correctly rounded IEEE ops only: 2 mul, 1 rndne, 8 fma, 1 add, 1 shift -- about
-// the issue cost of ocml's expf, and reproducible bit-for-bit by the CPU oracle.  Branch-free:
-// x is clamped to [-87, 0] (below -87 the result, <= 1.7e-38, only ever meets `alpha < 1/255`).
+// exp(x) of the splat falloff (x = power <= 0) as 2^t, t = x log2(e) rounded: rndne, one sub,
+// a degree-6 minimax polynomial for 2^(t - n) on [-0.5, 0.5] and v_ldexp_f32 -- correctly rounded
+// IEEE ops only, so the CPU oracle reproduces it bit-for-bit (oracle/gs_oracle.c:oracle_exp).
+// Relative error <= 5.1e-7 on [-8, 0].  Branch-free: x is clamped to [-80, 0] (below -80 the
+// result, <= 2e-35, only meets `alpha < 1/255` or a zero weight; results stay normal floats).
+// The hardware v_exp_f32 is not used: it is not correctly rounded (measured: 2.2 % of the floats
+// in [-126, 0] differ by 1 ulp from round(2^x); tools/probes/exp2_probe.hip), so no CPU
+// restatement could reproduce the threshold decisions that depend on it.
 __device__ __forceinline__ float gs_exp(float x) {
-  x = fminf(fmaxf(x, -87.0f), 0.0f);
-  float t = x * 1.44269504088896341f;
-  float n = __builtin_rintf(t);
-  float r = __builtin_fmaf(n, -0.693359375f, x);
-  r = __builtin_fmaf(n, 2.12194440e-4f, r);
-  float z = r * r;
-  float p = 1.9875691500e-4f;
-  p = __builtin_fmaf(p, r, 1.3981999507e-3f);
-  p = __builtin_fmaf(p, r, 8.3334519073e-3f);
-  p = __builtin_fmaf(p, r, 4.1665795894e-2f);
-  p = __builtin_fmaf(p, r, 1.6666665459e-1f);
-  p = __builtin_fmaf(p, r, 5.0000001201e-1f);
-  p = __builtin_fmaf(p, z, r);
-  p = p + 1.0f;
-  int e = (int)n + 127;
-  return p * __uint_as_float((uint32_t)e << 23);
+  x = fminf(fmaxf(x, -80.0f), 0.0f);
+  const float t = x * 1.44269504088896341f;
+  const float n = __builtin_rintf(t);
+  const float f = t - n;
+  float p = 1.5345810970757157e-4f;
+  p = __builtin_fmaf(p, f, 1.3399930903688073e-3f);
+  p = __builtin_fmaf(p, f, 9.618489071726799e-3f);
+  p = __builtin_fmaf(p, f, 5.550328642129898e-2f);
+  p = __builtin_fmaf(p, f, 2.4022646248340607e-1f);
+  p = __builtin_fmaf(p, f, 6.931471824645996e-1f);
+  p = __builtin_fmaf(p, f, 1.0f);
+  return __builtin_ldexpf(p, (int)n);
 }
 
 // Packed (two-pixel) form of gs_exp: identical op sequence per element, so each element is
@@ -65,27 +65,24 @@ __device__ __forceinline__ float gs_exp(float x) {
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 gs_exp_pk(f2 x) {
-  x.x = fminf(fmaxf(x.x, -87.0f), 0.0f);
-  x.y = fminf(fmaxf(x.y, -87.0f), 0.0f);
-  f2 t = x * 1.44269504088896341f;
+  x.x = fminf(fmaxf(x.x, -80.0f), 0.0f);
+  x.y = fminf(fmaxf(x.y, -80.0f), 0.0f);
+  const f2 t = x * 1.44269504088896341f;
   f2 n;
   n.x = __builtin_rintf(t.x);
   n.y = __builtin_rintf(t.y);
-  f2 r = pk_fma(n, (f2)(-0.693359375f), x);
-  r = pk_fma(n, (f2)(2.12194440e-4f), r);
-  f2 z = r * r;
-  f2 p = (f2)(1.9875691500e-4f);
-  p = pk_fma(p, r, (f2)(1.3981999507e-3f));
-  p = pk_fma(p, r, (f2)(8.3334519073e-3f));
-  p = pk_fma(p, r, (f2)(4.1665795894e-2f));
-  p = pk_fma(p, r, (f2)(1.6666665459e-1f));
-  p = pk_fma(p, r, (f2)(5.0000001201e-1f));
-  p = pk_fma(p, z, r);
-  p = p + 1.0f;
-  f2 s;
-  s.x = __uint_as_float((uint32_t)((int)n.x + 127) << 23);
-  s.y = __uint_as_float((uint32_t)((int)n.y + 127) << 23);
-  return p * s;
+  const f2 f = t - n;
+  f2 p = (f2)(1.5345810970757157e-4f);
+  p = pk_fma(p, f, (f2)(1.3399930903688073e-3f));
+  p = pk_fma(p, f, (f2)(9.618489071726799e-3f));
+  p = pk_fma(p, f, (f2)(5.550328642129898e-2f));
+  p = pk_fma(p, f, (f2)(2.4022646248340607e-1f));
+  p = pk_fma(p, f, (f2)(6.931471824645996e-1f));
+  p = pk_fma(p, f, (f2)(1.0f));
+  f2 r;
+  r.x = __builtin_ldexpf(p.x, (int)n.x);
+  r.y = __builtin_ldexpf(p.y, (int)n.y);
+  return r;
 }
 
 // m = 4x4 world_view_transform / full_proj_transform, row-major flattening of the torch tensor

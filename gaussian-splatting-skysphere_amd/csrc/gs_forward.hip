@@ -213,14 +213,28 @@ struct SrcTilesByRank {
   __device__ uint32_t operator()(uint32_t s) const { return tiles[sorted_gid[s]]; }
 };
 
+// instance offsets in depth order; also records, for every DUP_SLOTS-aligned slot, the depth rank
+// that owns it (the start of each load-balanced duplicate block)
+struct DstOffsets {
+  uint32_t* offsets;
+  uint32_t* first;
+  const uint32_t* counters;  // [0] V, [1] I (set by the scan's partial pass before this runs)
+  uint32_t P;
+  __device__ void operator()(uint32_t s, uint32_t ex, uint32_t v) const {
+    offsets[s] = ex;
+    if (!dup_balanced(counters[1], P)) return;
+    for (uint32_t m = (ex + DUP_SLOTS - 1) / DUP_SLOTS; m * DUP_SLOTS < ex + v; m++) first[m] = s;
+  }
+};
+
 void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
   const uint32_t n = (uint32_t)P;
   scan_exclusive(SrcVisible{geo.tiles}, DstCompact{geo.depth_key, geo.keys_a, geo.vals_a}, nullptr, n,
                  geo.scan_partial, &geo.counters[0], st);
   radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, false, &geo.counters[0], n, 32, geo.sort_scratch,
                    st);
-  scan_exclusive(SrcTilesByRank{geo.tiles, geo.sorted_gid}, DstArray{geo.offsets}, &geo.counters[0], n,
-                 geo.scan_partial, &geo.counters[1], st);
+  scan_exclusive(SrcTilesByRank{geo.tiles, geo.sorted_gid}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
+                 &geo.counters[0], n, geo.scan_partial, &geo.counters[1], st);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -248,24 +262,135 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* _
     }
 }
 
+// Load-balanced duplicate: workgroup b writes instance slots [b S, (b + 1) S), S = DUP_SLOTS.
+// The depth ranks owning those slots are [dup_first[b], dup_first[b + 1]] (at most S + 1 of
+// them); their offsets, ids and tile rectangles are staged in LDS, every slot finds its owner by
+// an inclusive max-scan over start marks, and keys / presort ids are written fully coalesced.
+// The workgroups also clear the tile ranges (k_ranges fills the non-empty ones).
+constexpr int DUP_THREADS = 256;
+constexpr int DUP_ITEMS = DUP_SLOTS / DUP_THREADS;
+__global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
+    uint32_t I, const uint32_t* __restrict__ counters, const uint32_t* __restrict__ dup_first,
+    const uint32_t* __restrict__ sorted_gid, const uint32_t* __restrict__ offsets, const int* __restrict__ radii,
+    const float4* __restrict__ splat, int gx, int gy, uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
+    uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges) {
+  __shared__ uint32_t s_off[DUP_SLOTS + 1];
+  __shared__ uint32_t s_gid[DUP_SLOTS + 1];
+  __shared__ uint32_t s_rect[DUP_SLOTS + 1];  // x0 | y0 << 8 | w << 16 (tile grid <= 255 x 255) -- see host check
+  __shared__ uint32_t s_own[DUP_SLOTS];
+  __shared__ uint32_t s_wmax[DUP_THREADS / 64];
+  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t tiles = (uint32_t)(gx * gy);
+  for (uint32_t t = b * DUP_THREADS + tid; t < tiles; t += gridDim.x * DUP_THREADS) ranges[t] = make_uint2(0u, 0u);
+  const uint32_t V = counters[0];
+  const uint32_t k0 = b * DUP_SLOTS;
+  const uint32_t k1 = min(k0 + DUP_SLOTS, I);
+  const uint32_t s_lo = dup_first[b];
+  const uint32_t s_hi = (k1 < I) ? dup_first[b + 1] : V - 1;
+  const uint32_t nG = s_hi - s_lo + 1;
+  for (uint32_t i = tid; i < DUP_SLOTS; i += DUP_THREADS) s_own[i] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < nG; i += DUP_THREADS) {
+    const uint32_t s = s_lo + i;
+    const uint32_t gid = sorted_gid[s];
+    const uint32_t off = offsets[s];
+    const float4 a = splat[3 * gid];
+    int x0, y0, x1, y1;
+    get_rect(a.x, a.y, radii[gid], gx, gy, x0, y0, x1, y1);
+    s_off[i] = off;
+    s_gid[i] = gid;
+    s_rect[i] = (uint32_t)x0 | ((uint32_t)y0 << 8) | ((uint32_t)(x1 - x0) << 16);
+    if (off >= k0) {
+      goff[gid] = off;
+      if (off < k1) s_own[off - k0] = i;
+    }
+  }
+  __syncthreads();
+  // inclusive max-scan of owner marks over the block's slots (consecutive DUP_ITEMS per thread)
+  uint32_t v[DUP_ITEMS];
+  uint32_t run = 0;
+#pragma unroll
+  for (int r = 0; r < DUP_ITEMS; r++) {
+    run = max(run, s_own[tid * DUP_ITEMS + r]);
+    v[r] = run;
+  }
+  uint32_t incl = run;
+  const uint32_t lane = tid & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
+    if (lane >= (uint32_t)d) incl = max(incl, o);
+  }
+  if (lane == 63) s_wmax[tid >> 6] = incl;
+  uint32_t excl = (uint32_t)__shfl_up((int)incl, 1, 64);
+  if (lane == 0) excl = 0;
+  __syncthreads();
+  for (uint32_t w = 0; w < (tid >> 6); w++) excl = max(excl, s_wmax[w]);
+#pragma unroll
+  for (int r = 0; r < DUP_ITEMS; r++) s_own[tid * DUP_ITEMS + r] = max(v[r], excl);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < DUP_ITEMS; r++) {
+    const uint32_t i = (uint32_t)r * DUP_THREADS + tid;
+    const uint32_t k = k0 + i;
+    if (k < k1) {
+      const uint32_t o = s_own[i];
+      const uint32_t j = k - s_off[o];
+      const uint32_t rc = s_rect[o];
+      const uint32_t w = rc >> 16;
+      const uint32_t q = j / w;
+      const uint32_t x = (rc & 255u) + (j - q * w), y = ((rc >> 8) & 255u) + q;
+      tile_keys[k] = y * (uint32_t)gx + x;
+      presort_gid[k] = s_gid[o];
+    }
+  }
+}
+
+// tile ranges over the sorted instance list, 4 instances per lane
 __global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __restrict__ tile, uint2* __restrict__ ranges) {
-  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= I) return;
-  const uint32_t t = tile[k];
-  if (k == 0 || tile[k - 1] != t) ranges[t].x = k;
-  if (k == I - 1 || tile[k + 1] != t) ranges[t].y = k + 1;
+  const uint32_t k0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (k0 >= I) return;
+  uint32_t t[6];
+  t[0] = k0 > 0 ? tile[k0 - 1] : 0xFFFFFFFFu;
+  if (k0 + 4 <= I && (k0 & 3) == 0) {
+    const uint4 q = *reinterpret_cast<const uint4*>(tile + k0);
+    t[1] = q.x;
+    t[2] = q.y;
+    t[3] = q.z;
+    t[4] = q.w;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; r++) t[1 + r] = k0 + r < I ? tile[k0 + r] : 0xFFFFFFFFu;
+  }
+  t[5] = k0 + 4 < I ? tile[k0 + 4] : 0xFFFFFFFFu;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint32_t k = k0 + r;
+    if (k >= I) break;
+    if (t[r + 1] != t[r]) ranges[t[r + 1]].x = k;
+    if (t[r + 2] != t[r + 1]) ranges[t[r + 1]].y = k + 1;
+  }
 }
 
 void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const GeomPtrs& geo, const BinPtrs& bin,
              const ImgPtrs& img, hipStream_t st) {
   const int tiles = c.gx * c.gy;
-  (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
-  if (I == 0) return;
-  GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
-            geo.sorted_gid, geo.offsets, radii, geo.splat, c.gx, c.gy, geo.goff, bin.keys_a, bin.presort_gid);
+  if (I == 0) {
+    (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
+    return;
+  }
+  if (dup_balanced(I, (uint32_t)P) && c.gx <= 255 && c.gy <= 255) {
+    GS_LAUNCH("duplicate", k_duplicate_lb, dim3((I + DUP_SLOTS - 1) / DUP_SLOTS), dim3(DUP_THREADS), 0, st, I,
+              geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, radii, geo.splat, c.gx, c.gy, geo.goff,
+              bin.keys_a, bin.presort_gid, img.ranges);
+  } else {
+    (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
+    GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
+              geo.sorted_gid, geo.offsets, radii, geo.splat, c.gx, c.gy, geo.goff, bin.keys_a, bin.presort_gid);
+  }
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tile_bits(tiles),
                    bin.sort_scratch, st);
-  GS_LAUNCH("ranges", k_ranges, dim3((I + 255) / 256), dim3(256), 0, st, I, bin.sorted_tile, img.ranges);
+  GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges);
 }
 
 // ------------------------------------------------------------------------------------------

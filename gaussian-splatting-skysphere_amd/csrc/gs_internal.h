@@ -23,6 +23,14 @@ constexpr int ACC_STRIDE = 12;  // LDS row of one per-wave partial record: s0..7
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Duplicate blocks: DUP_SLOTS consecutive instance slots per workgroup.  The owner table
+// dup_first has P + 1 entries, so the load-balanced duplicate runs while I <= DUP_SLOTS * P
+// (more than 2048 tiles per Gaussian on average falls back to the per-Gaussian kernel).
+constexpr uint32_t DUP_SLOTS = 2048;
+__host__ __device__ inline bool dup_balanced(uint32_t I, uint32_t P) {
+  return (uint64_t)I <= (uint64_t)DUP_SLOTS * (uint64_t)P;
+}
+
 struct GaussianArgs {
   int P, D, M;
   const float* means3D;
@@ -53,6 +61,7 @@ struct GeomPtrs {
   uint8_t* clamped;
   uint32_t *keys_a, *vals_a, *keys_b, *vals_b;
   uint32_t* offsets;  // per depth rank
+  uint32_t* dup_first;  // [P + 1] depth rank owning the first instance slot of each duplicate block
   uint32_t* scan_partial;
   uint32_t* sort_scratch;
   uint32_t* counters;  // [0] visible V, [1] instances I, [2] error flags
@@ -71,6 +80,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   size_t o_dkey = take(Pn * 4), o_tiles = take(Pn * 4), o_goff = take(Pn * 4), o_cl = take(Pn);
   size_t o_ka = take(Pn * 4), o_va = take(Pn * 4), o_kb = take(Pn * 4), o_vb = take(Pn * 4);
   size_t o_offs = take(Pn * 4);
+  size_t o_df = take((Pn + 1) * 4);
   size_t o_sp = take((size_t)scan_plan(Pn).nb * 4 + 64);
   size_t o_ss = take(sort_scratch_words(Pn) * 4);
   size_t o_cnt = take(64);
@@ -85,6 +95,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
     out->keys_b = (uint32_t*)(base + o_kb);
     out->vals_b = (uint32_t*)(base + o_vb);
     out->offsets = (uint32_t*)(base + o_offs);
+    out->dup_first = (uint32_t*)(base + o_df);
     out->scan_partial = (uint32_t*)(base + o_sp);
     out->sort_scratch = (uint32_t*)(base + o_ss);
     out->counters = (uint32_t*)(base + o_cnt);
