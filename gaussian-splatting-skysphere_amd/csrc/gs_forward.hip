@@ -454,32 +454,28 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
         const float power1 = -0.5f * (co1.x * dx1 * dx1 + co1.z * dy1 * dy1) - co1.y * dx1 * dy1;
         const float alpha0 = fminf(0.99f, co0.w * gs_exp(power0));
         const float alpha1 = fminf(0.99f, co1.w * gs_exp(power1));
-        if (!done && power0 <= 0.0f && alpha0 >= 1.0f / 255.0f) {
-          const float test_T = T * (1.0f - alpha0);
-          if (test_T < 0.0001f) {
-            done = true;
-          } else {
-            const float4 rgb = s_rgb[j0];
-            C0 += rgb.x * alpha0 * T;
-            C1 += rgb.y * alpha0 * T;
-            C2 += rgb.z * alpha0 * T;
-            T = test_T;
-            last = base + j0 + 1;
-          }
-        }
-        if (has1 && !done && power1 <= 0.0f && alpha1 >= 1.0f / 255.0f) {
-          const float test_T = T * (1.0f - alpha1);
-          if (test_T < 0.0001f) {
-            done = true;
-          } else {
-            const float4 rgb = s_rgb[j1];
-            C0 += rgb.x * alpha1 * T;
-            C1 += rgb.y * alpha1 * T;
-            C2 += rgb.z * alpha1 * T;
-            T = test_T;
-            last = base + j1 + 1;
-          }
-        }
+        const float4 rgb0 = s_rgb[j0], rgb1 = s_rgb[j1];
+        // branch-free compositing of the pair, in order (selects instead of divergent ifs)
+        bool c0 = !done && power0 <= 0.0f && alpha0 >= 1.0f / 255.0f;
+        const float tT0 = T * (1.0f - alpha0);
+        const bool s0 = c0 && tT0 < 0.0001f;  // T would drop below 1e-4: stop before entry 0
+        done = done || s0;
+        c0 = c0 && !s0;
+        C0 = c0 ? C0 + rgb0.x * alpha0 * T : C0;
+        C1 = c0 ? C1 + rgb0.y * alpha0 * T : C1;
+        C2 = c0 ? C2 + rgb0.z * alpha0 * T : C2;
+        T = c0 ? tT0 : T;
+        last = c0 ? base + j0 + 1 : last;
+        bool c1 = has1 && !done && power1 <= 0.0f && alpha1 >= 1.0f / 255.0f;
+        const float tT1 = T * (1.0f - alpha1);
+        const bool s1 = c1 && tT1 < 0.0001f;
+        done = done || s1;
+        c1 = c1 && !s1;
+        C0 = c1 ? C0 + rgb1.x * alpha1 * T : C0;
+        C1 = c1 ? C1 + rgb1.y * alpha1 * T : C1;
+        C2 = c1 ? C2 + rgb1.z * alpha1 * T : C2;
+        T = c1 ? tT1 : T;
+        last = c1 ? base + j1 + 1 : last;
         if (__ballot(!done) == 0) {
           qq = 4;
           break;
