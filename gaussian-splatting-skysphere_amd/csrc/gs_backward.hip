@@ -253,18 +253,15 @@ void bwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
 
 // SH backward for one Gaussian (order identical to oracle/gs_oracle.c sh_bwd_one).
 template <int DEG>
-__device__ __forceinline__ void sh_backward(const float* __restrict__ sh, int M, float vx, float vy, float vz,
-                                            uint32_t clamped, const float* dcol, float* __restrict__ dsh,
-                                            float* dmean) {
+// `row` is the Gaussian's SH row (3M floats) staged in LDS; on return it holds dL/dsh.
+__device__ __forceinline__ void sh_backward(float* row, int M, float vx, float vy, float vz,
+                                            uint32_t clamped, const float* dcol, float* dmean) {
   constexpr int K = (DEG + 1) * (DEG + 1);
   const float len = sqrtf(vx * vx + vy * vy + vz * vz);
   const float x = vx / len, y = vy / len, z = vz / len;
   float g[3];
 #pragma unroll
   for (int ch = 0; ch < 3; ch++) g[ch] = ((clamped >> ch) & 1) ? 0.0f : dcol[ch];
-  float s[K * 3];
-#pragma unroll
-  for (int k = 0; k < K * 3; k++) s[k] = sh[k];
   const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
   float b[16];
   b[0] = SH_C0;
@@ -289,15 +286,10 @@ __device__ __forceinline__ void sh_backward(const float* __restrict__ sh, int M,
     b[14] = (SH_C35 * z) * (xx - yy);
     b[15] = (SH_C36 * x) * (xx - 3.0f * yy);
   }
-#pragma unroll
-  for (int k = 0; k < K; k++)
-#pragma unroll
-    for (int ch = 0; ch < 3; ch++) dsh[3 * k + ch] = b[k] * g[ch];
-  for (int k = 3 * K; k < 3 * M; k++) dsh[k] = 0.0f;
   float ddx[3] = {0.f, 0.f, 0.f}, ddy[3] = {0.f, 0.f, 0.f}, ddz[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int ch = 0; ch < 3; ch++) {
-#define S(k) s[3 * (k) + ch]
+#define S(k) row[3 * (k) + ch]
     if (DEG > 0) {
       ddx[ch] = -SH_C1 * S(3);
       ddy[ch] = -SH_C1 * S(1);
@@ -323,6 +315,11 @@ __device__ __forceinline__ void sh_backward(const float* __restrict__ sh, int M,
     }
 #undef S
   }
+#pragma unroll
+  for (int k = 0; k < K; k++)
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) row[3 * k + ch] = b[k] * g[ch];
+  for (int k = 3 * K; k < 3 * M; k++) row[k] = 0.0f;
   const float d0 = ddx[0] * g[0] + ddx[1] * g[1] + ddx[2] * g[2];
   const float d1 = ddy[0] * g[0] + ddy[1] * g[1] + ddy[2] * g[2];
   const float d2 = ddz[0] * g[0] + ddz[1] * g[1] + ddz[2] * g[2];
@@ -375,14 +372,13 @@ __device__ __forceinline__ void cov3d_backward(float sx, float sy, float sz, flo
             4.f * z * (dR[0][0] + dR[1][1]);
 }
 
-template <int DEG>  // -1: colours precomputed (no SH gradient)
-__global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraArgs c,
-                                                        const uint32_t* __restrict__ tiles,
-                                                        const uint32_t* __restrict__ goff,
-                                                        const uint8_t* __restrict__ clamped,
-                                                        const float* __restrict__ gradrec, GradOut out) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= g.P) return;
+template <int DEG>
+__device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g, const CameraArgs& c,
+                                                   const uint32_t* __restrict__ tiles,
+                                                   const uint32_t* __restrict__ goff,
+                                                   const uint8_t* __restrict__ clamped,
+                                                   const float* __restrict__ gradrec, const GradOut& out,
+                                                   float* row) {
   const uint32_t cnt = tiles[i];
   if (cnt == 0) {
     // invisible: every gradient is zero (upstream: zero-initialised outputs, radii == 0 skipped)
@@ -400,8 +396,8 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
     out.dmean3D[3 * i + 2] = 0.f;
     if (out.dcov3D)
       for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
-    if (out.dsh)
-      for (int k = 0; k < 3 * g.M; k++) out.dsh[(size_t)i * 3 * g.M + k] = 0.f;
+    if (DEG >= 0)
+      for (int k = 0; k < 3 * g.M; k++) row[k] = 0.f;
     if (out.dscale)
       for (int k = 0; k < 3; k++) out.dscale[3 * i + k] = 0.f;
     if (out.drot)
@@ -501,8 +497,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
   if (DEG >= 0) {
     float shm[3];
     const float vx = px - c.campos[0], vy = py - c.campos[1], vz = pz - c.campos[2];
-    float* dsh = out.dsh + (size_t)i * 3 * g.M;
-    sh_backward<(DEG < 0 ? 0 : DEG)>(g.shs + (size_t)i * 3 * g.M, g.M, vx, vy, vz, clamped[i], dcol, dsh, shm);
+    sh_backward<(DEG < 0 ? 0 : DEG)>(row, g.M, vx, vy, vz, clamped[i], dcol, shm);
     dmean[0] = dmean[0] + shm[0];
     dmean[1] = dmean[1] + shm[1];
     dmean[2] = dmean[2] + shm[2];
@@ -524,11 +519,72 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
   }
 }
 
+// Block-wide copy of 256 consecutive SH rows (3M floats each) between global memory and an LDS
+// array with an odd row stride (3M + 1: conflict-free per-thread row access); dwordx4 global
+// accesses when rows are 16-B multiples and the base is aligned.
+__device__ __forceinline__ void rows_to_lds(const float* __restrict__ src, float* lds, int n, int rowf, int stride) {
+  const int total = n * rowf;
+  if ((rowf & 3) == 0 && (((uintptr_t)src) & 15) == 0) {
+    for (int q = threadIdx.x; q < (total >> 2); q += 256) {
+      const float4 v = reinterpret_cast<const float4*>(src)[q];
+      const int e = q << 2, t = e / rowf;
+      float* d = lds + t * stride + (e - t * rowf);
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+  } else {
+    for (int e = threadIdx.x; e < total; e += 256) {
+      const int t = e / rowf;
+      lds[t * stride + (e - t * rowf)] = src[e];
+    }
+  }
+}
+__device__ __forceinline__ void lds_to_rows(const float* lds, float* __restrict__ dst, int n, int rowf, int stride) {
+  const int total = n * rowf;
+  if ((rowf & 3) == 0 && (((uintptr_t)dst) & 15) == 0) {
+    for (int q = threadIdx.x; q < (total >> 2); q += 256) {
+      const int e = q << 2, t = e / rowf;
+      const float* d = lds + t * stride + (e - t * rowf);
+      reinterpret_cast<float4*>(dst)[q] = make_float4(d[0], d[1], d[2], d[3]);
+    }
+  } else {
+    for (int e = threadIdx.x; e < total; e += 256) {
+      const int t = e / rowf;
+      dst[e] = lds[t * stride + (e - t * rowf)];
+    }
+  }
+}
+
+template <int DEG>  // -1: colours precomputed (no SH gradient)
+__global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraArgs c,
+                                                        const uint32_t* __restrict__ tiles,
+                                                        const uint32_t* __restrict__ goff,
+                                                        const uint8_t* __restrict__ clamped,
+                                                        const float* __restrict__ gradrec, GradOut out) {
+  extern __shared__ float s_sh[];  // DEG >= 0: [256][3M + 1] SH rows, then dL/dsh rows
+  const int i0 = blockIdx.x * 256, i = i0 + (int)threadIdx.x;
+  const int nG = min(256, g.P - i0);
+  const int rowf = 3 * g.M, stride = rowf + 1;
+  float* row = s_sh + threadIdx.x * stride;
+  if (DEG >= 0) {
+    rows_to_lds(g.shs + (size_t)i0 * rowf, s_sh, nG, rowf, stride);
+    __syncthreads();
+  }
+  if (i < g.P) preprocess_bwd_one<DEG>(i, g, c, tiles, goff, clamped, gradrec, out, row);
+  if (DEG >= 0) {
+    __syncthreads();
+    lds_to_rows(s_sh, out.dsh + (size_t)i0 * rowf, nG, rowf, stride);
+  }
+}
+
 void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const float* gradrec,
                     const GradOut& out, hipStream_t st) {
   if (g.P <= 0) return;
   dim3 grid((g.P + 255) / 256), block(256);
   const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
+  const size_t lds = sh ? (size_t)256 * (3 * g.M + 1) * sizeof(float) : 0;
   if (!sh) {
     GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<-1>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
               gradrec, out);
@@ -536,19 +592,19 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
   }
   switch (g.D) {
     case 0:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<0>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<0>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
                 gradrec, out);
       break;
     case 1:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<1>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<1>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
                 gradrec, out);
       break;
     case 2:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<2>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<2>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
                 gradrec, out);
       break;
     default:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<3>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<3>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
                 gradrec, out);
       break;
   }
