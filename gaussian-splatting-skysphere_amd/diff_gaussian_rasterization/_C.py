@@ -100,11 +100,14 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     H, W = int(image_height), int(image_width)
     dev = x.device
     u8 = dict(dtype=torch.uint8, device=dev)
-    out_color = torch.zeros((3, H, W), dtype=torch.float32, device=dev)
-    radii = torch.zeros((x.P,), dtype=torch.int32, device=dev)
     if x.P == 0:
         # upstream: nothing is launched for an empty scene; the image stays all-zero (no background)
-        return 0, out_color, radii, torch.empty((0,), **u8), torch.empty((0,), **u8), torch.empty((0,), **u8)
+        return (0, torch.zeros((3, H, W), dtype=torch.float32, device=dev), torch.zeros((0,), dtype=torch.int32,
+                                                                                        device=dev),
+                torch.empty((0,), **u8), torch.empty((0,), **u8), torch.empty((0,), **u8))
+    # every pixel of the image and every radius is written by the kernels
+    out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+    radii = torch.empty((x.P,), dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
         st = _stream(dev)
         geom = torch.empty((_lib.gs_geom_buffer_bytes(x.P),), **u8)

@@ -75,13 +75,18 @@ class _RasterizeGaussians(torch.autograd.Function):
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                 raster_settings):
         s = raster_settings
+        # the camera matrices arrive transposed (cameras.py:54-56 world_view_transform is a
+        # .transpose(0, 1) view); make them contiguous once and reuse them in backward
+        view, proj = s.viewmatrix.contiguous(), s.projmatrix.contiguous()
         args = (s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
-                s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
+                view, proj, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
                 s.campos, s.prefiltered, s.debug)
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _run_with_snapshot(
             _C.rasterize_gaussians, args, s.debug, "snapshot_fw.dump", "forward")
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
+        ctx.matrices = (view, proj)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the (int) radii output
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii)
@@ -90,10 +95,13 @@ class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii):
         s = ctx.raster_settings
+        if grad_out_color is None:  # the colour output did not reach the loss
+            return (None,) * 9
         colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer, imgBuffer = (
             ctx.saved_tensors)
+        view, proj = ctx.matrices
         args = (s.bg, means3D, radii, colors_precomp, scales, rotations, s.scale_modifier, cov3Ds_precomp,
-                s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color.contiguous(), sh, s.sh_degree,
+                view, proj, s.tanfovx, s.tanfovy, grad_out_color.contiguous(), sh, s.sh_degree,
                 s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.debug)
 
         def _bwd(*a):
