@@ -46,12 +46,12 @@ __device__ __forceinline__ Eval eval_pair(float2 xy, float4 co, float pfx, f2 pf
 
 constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x, y) and (x, y + 8)
 #ifndef GS_BWD_BATCH
-#define GS_BWD_BATCH 128
+#define GS_BWD_BATCH 64
 #endif
 #ifndef GS_BWD_MINW
 #define GS_BWD_MINW 1
 #endif
-constexpr int BWD_BATCH = GS_BWD_BATCH;  // entries staged per round (128: LDS 16 KB/block -> 5 waves/SIMD)
+constexpr int BWD_BATCH = GS_BWD_BATCH;  // entries staged per round (64: 9 KB LDS/block -> 8 waves/SIMD)
 constexpr int BWD_GROUPS = BWD_BATCH / 64;
 constexpr int BWD_STAGE_ROUNDS = (BWD_BATCH + BWD_THREADS - 1) / BWD_THREADS;
 static_assert(BWD_BATCH % 64 == 0, "batch must be whole waves");
