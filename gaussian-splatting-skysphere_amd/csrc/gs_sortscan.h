@@ -4,7 +4,8 @@
 //
 // Scan: reduce -> single-workgroup partial scan -> down-sweep (3 launches).  Workgroup count is
 // capped at 1024 so the partial scan is one 1024-lane workgroup.
-// Radix sort: per pass (8-bit digit) upsweep histogram [digit][block] -> scan -> stable scatter.
+// Radix sort: per pass (8-bit digit) upsweep histogram [digit][block] -> per-digit row scan ->
+// stable scatter (3 launches per pass; the scatter adds the digit bases itself).
 // The scatter ranks keys inside a 256-key tile with wave64 ballots (per-bit peer masks, the
 // CDNA analogue of match_any), combines the 4 waves through LDS and keeps a running per-digit
 // base per workgroup, so equal digits keep input order (LSD stability).
@@ -159,7 +160,8 @@ struct DstArray {
 // radix sort
 //
 // Stable LSD radix sort, 8-bit digits.  Per pass: k_radix_hist (per-block digit counts) ->
-// exclusive scan of the [digit][block] matrix -> k_radix_scatter.  A block walks its chunk in
+// k_radix_rowscan (exclusive scan of each digit's row of the [digit][block] matrix + row totals)
+// -> k_radix_scatter (digit base = exclusive scan of the row totals, done per workgroup).  A block walks its chunk in
 // tiles of 2048 keys (8 per lane): each wave ranks its 512 consecutive keys round by round with
 // ballot peer masks (stable), the 4 waves are combined per digit in LDS, the tile is reordered by
 // digit in LDS, and runs of equal digits are written out contiguously (coalesced stores).
@@ -187,11 +189,11 @@ inline SortPlan sort_plan(uint64_t n_max) {
   return p;
 }
 
-// scratch words needed by radix_sort_pairs: histogram + its scan partials
+// scratch words needed by radix_sort_pairs: [digit][block] histogram + per-digit row totals
 inline size_t sort_scratch_words(uint64_t n_max) {
   SortPlan p = sort_plan(n_max);
   size_t hist = (size_t)RADIX * p.nb;
-  return hist + scan_plan(hist).nb + 16;
+  return hist + RADIX + 16;
 }
 
 // lanes of this wave whose `bits`-bit digit equals mine (valid lanes only)
@@ -234,10 +236,37 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32
   hist[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 
+// Row scan of the [digit][block] histogram: workgroup d turns row d into exclusive per-block
+// offsets (within digit d) and writes the row total; the scatter adds the digit base itself.
+static __global__ __launch_bounds__(SORT_THREADS) void k_radix_rowscan(uint32_t* __restrict__ hist, uint32_t nb,
+                                                                        uint32_t* __restrict__ row_total) {
+  __shared__ uint32_t sh[4];
+  uint32_t* row = hist + (size_t)blockIdx.x * nb;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < nb; base += SORT_THREADS * 4) {
+    const uint32_t i0 = base + threadIdx.x * 4;
+    uint32_t v[4], loc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      v[k] = i0 + k < nb ? row[i0 + k] : 0u;
+      loc += v[k];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(loc, sh, &tot) + carry;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (i0 + k < nb) row[i0 + k] = ex;
+      ex += v[k];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) row_total[blockIdx.x] = carry;
+}
+
 static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, int bits, uint32_t chunk,
-    uint32_t nb, const uint32_t* __restrict__ hist) {
+    uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ row_total) {
   __shared__ uint32_t s_base[RADIX];      // global position of the next key of each digit
   __shared__ uint32_t s_wcnt[4][RADIX];   // per-wave running counts -> per-wave exclusive prefix
   __shared__ uint32_t s_loc[RADIX];       // digit offsets inside the tile (for the LDS reorder)
@@ -247,7 +276,11 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   __shared__ uint32_t s_val[SORT_TILE];
   const uint32_t n = resolve_n(n_dev, n_max);
   const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  s_base[tid] = hist[(size_t)tid * nb + blockIdx.x];
+  {
+    uint32_t all;
+    const uint32_t digit_base = block_excl_scan(row_total[tid], s_scan, &all);
+    s_base[tid] = digit_base + hist[(size_t)tid * nb + blockIdx.x];
+  }
   const uint64_t start = (uint64_t)blockIdx.x * chunk;
   const uint64_t end = start + chunk < n ? start + chunk : n;
   const uint32_t mask = (1u << bits) - 1u;
@@ -329,17 +362,17 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
   SortPlan p = sort_plan(n_max);
   uint32_t* hist = scratch;
   const size_t hist_n = (size_t)RADIX * p.nb;
-  uint32_t* partial = scratch + hist_n;
+  uint32_t* row_total = scratch + hist_n;
   uint32_t *kin = keys_a, *vin = vals_a, *kout = keys_b, *vout = vals_b;
   bool in_b = false;
   for (int shift = 0; shift < end_bit; shift += RADIX_BITS) {
     int bits = end_bit - shift < RADIX_BITS ? end_bit - shift : RADIX_BITS;
     GS_LAUNCH("radix_hist", k_radix_hist, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, n_dev, n_max, shift, bits,
               p.chunk, p.nb, hist);
-    scan_exclusive(SrcArray{hist}, DstArray{hist}, nullptr, (uint32_t)hist_n, partial, nullptr, st);
+    GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX), dim3(SORT_THREADS), 0, st, hist, p.nb, row_total);
     const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
     GS_LAUNCH("radix_scatter", k_radix_scatter, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, vsrc, kout, vout, n_dev,
-              n_max, shift, bits, p.chunk, p.nb, hist);
+              n_max, shift, bits, p.chunk, p.nb, hist, row_total);
     uint32_t* t;
     t = kin; kin = kout; kout = t;
     t = vin; vin = vout; vout = t;
