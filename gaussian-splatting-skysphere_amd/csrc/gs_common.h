@@ -114,6 +114,86 @@ __device__ __forceinline__ void get_rect(float x, float y, int r, int gx, int gy
   y1 = min(gy, max(0, (int)((((y + fr) + 16.0f) - 1.0f) / 16.0f)));
 }
 
+// ln(x) for x >= 1 from correctly rounded IEEE ops only (frexp by bit fields, atanh series),
+// |error| < 2e-7 relative; the CPU oracle reproduces it bit-for-bit (oracle_log).  Used for the
+// culling limit, which must agree exactly between the binning here and in the oracle.
+__device__ __forceinline__ float gs_log(float x) {
+  const uint32_t u = __float_as_uint(x);
+  int e = (int)((u >> 23) & 255u) - 127;
+  float m = __uint_as_float((u & 0x7FFFFFu) | 0x3F800000u);
+  if (m > 1.41421356f) {
+    m = m * 0.5f;
+    e = e + 1;
+  }
+  const float f = m - 1.0f;
+  const float t = f / (2.0f + f);
+  const float t2 = t * t;
+  float p = 0.11111111f;
+  p = __builtin_fmaf(p, t2, 0.14285715f);
+  p = __builtin_fmaf(p, t2, 0.2f);
+  p = __builtin_fmaf(p, t2, 0.33333334f);
+  p = __builtin_fmaf(p, t2, 1.0f);
+  return __builtin_fmaf((float)e, 0.69314718f, (2.0f * t) * p);
+}
+// culling limit of the alpha >= 1/255 ellipse: q(d) <= lim (negative: never reaches 1/255)
+__device__ __forceinline__ float cull_lim(float op) {
+  return op >= 1.0f / 255.0f ? 2.0f * fmaxf(gs_log(255.0f * op), 0.0f) * 1.001f + 1e-3f : -1.0f;
+}
+
+// Tile-exact binning.  A splat is binned only into the tiles of its upstream rectangle whose
+// 16x16 pixel square can hold a pixel with alpha >= 1/255, i.e. q(d) <= lim for the conic q and the
+// culling limit lim (splat record).  Per tile row the x-extent of the ellipse over the row's pixel
+// band is closed-form (x_r(dy) is concave, x_l(dy) convex: their extrema over the band sit at the
+// clamp of the ellipse's extreme-x points), widened by margins, so the test is conservative: a
+// dropped (splat, tile) pair contributes alpha < 1/255 to every pixel of the tile and is skipped
+// by the compositing anyway.  Images and gradients are unchanged; the instance count drops
+// (C3: 6.58M -> 4.3M).  The op sequence is mirrored bit-for-bit by oracle/gs_oracle.c:row_span.
+struct SpanCtx {
+  float mx, my, A, B, det, R, dyr, AL;
+  int x0, x1, mode;  // mode 0: ellipse, 1: whole rectangle row (degenerate conic), 2: nothing
+};
+__device__ __forceinline__ SpanCtx span_ctx(float mx, float my, float A, float B, float C, float L, int x0, int x1) {
+  SpanCtx s;
+  s.mx = mx;
+  s.my = my;
+  s.A = A;
+  s.B = B;
+  s.x0 = x0;
+  s.x1 = x1;
+  s.det = A * C - B * B;
+  s.mode = !(L >= 0.0f) ? 2 : ((A > 0.0f && C > 0.0f && s.det > 0.0f) ? 0 : 1);
+  s.R = 0.0f;
+  s.dyr = 0.0f;
+  s.AL = 0.0f;
+  if (s.mode == 0) {
+    s.AL = A * L;
+    s.R = sqrtf(s.AL / s.det) * 1.0001f + 0.01f;
+    s.dyr = -B * sqrtf(L / (C * s.det));
+  }
+  return s;
+}
+// tiles [ta, tb) of tile row ty (empty: ta == tb)
+__device__ __forceinline__ void row_span(const SpanCtx& s, int ty, int& ta, int& tb) {
+  ta = tb = s.x0;
+  if (s.mode == 2) return;
+  if (s.mode == 1) {
+    tb = s.x1;
+    return;
+  }
+  const float lo = fmaxf((float)(GS_TILE * ty) - s.my, -s.R);
+  const float hi = fminf((float)(GS_TILE * ty + GS_TILE - 1) - s.my, s.R);
+  if (!(lo <= hi)) return;
+  const float d1 = fminf(fmaxf(s.dyr, lo), hi), d2 = fminf(fmaxf(-s.dyr, lo), hi);
+  const float xr = (-s.B * d1 + sqrtf(fmaxf(s.AL - s.det * d1 * d1, 0.0f))) / s.A;
+  const float xl = (-s.B * d2 - sqrtf(fmaxf(s.AL - s.det * d2 * d2, 0.0f))) / s.A;
+  const float X0 = fmaxf((s.mx + xl) - (0.05f + 0.001f * fabsf(xl)), -1.0e6f);
+  const float X1 = fminf((s.mx + xr) + (0.05f + 0.001f * fabsf(xr)), 1.0e6f);
+  const int a = max(s.x0, (int)ceilf((X0 - 15.0f) / 16.0f));
+  const int b = min(s.x1, (int)floorf(X1 / 16.0f) + 1);
+  ta = a;
+  tb = b > a ? b : a;
+}
+
 // rotation of the (w, x, y, z) quaternion, un-normalised (the caller normalises:
 // /root/reference/scene/gaussian_model.py:41,100-101)
 struct mat3 { float m[3][3]; };

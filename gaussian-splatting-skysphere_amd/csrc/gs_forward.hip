@@ -77,6 +77,7 @@ __device__ __forceinline__ void sh_to_rgb(const float* __restrict__ sh, int M, f
 template <int DEG>
 __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g, const CameraArgs& c,
                                                    int* __restrict__ radii, float4* __restrict__ splat,
+                                                   float4* __restrict__ binrec,
                                                    uint32_t* __restrict__ depth_key, uint32_t* __restrict__ tiles,
                                                    uint8_t* __restrict__ clamped, uint32_t* __restrict__ counters) {
   radii[i] = 0;
@@ -131,28 +132,40 @@ __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g,
   // culling limit of the {alpha >= 1/255} ellipse (render-side work skipping only; never
   // changes a result, see ellipse_meets_rect): q(d) <= 2 ln(255 o), with safety margins
   const float op = g.opacities[i];
-  const float lim = op >= 1.0f / 255.0f ? 2.0f * fmaxf(logf(255.0f * op), 0.0f) * 1.001f + 1e-3f : -1.0f;
+  const float lim = cull_lim(op);
   splat[3 * i + 0] = make_float4(sx, sy, cxx, cxy);
   splat[3 * i + 1] = make_float4(cyy, op, rgb[0], rgb[1]);
   splat[3 * i + 2] = make_float4(rgb[2], pv.z, lim, 0.0f);
   depth_key[i] = __float_as_uint(pv.z);
-  radii[i] = radius;
-  tiles[i] = (uint32_t)area;
+  radii[i] = radius;  // upstream visibility: the rectangle is non-empty
+  // tile-exact instance count (may be 0 for a visible splat whose alpha never reaches 1/255)
+  const SpanCtx sp = span_ctx(sx, sy, cxx, cxy, cyy, lim, x0, x1);
+  uint32_t count = 0;
+  for (int ty = y0; ty < y1; ty++) {
+    int ta, tb;
+    row_span(sp, ty, ta, tb);
+    count += (uint32_t)(tb - ta);
+  }
+  binrec[2 * i + 0] = make_float4(sx, sy, cxx, cxy);
+  binrec[2 * i + 1] = make_float4(cyy, lim, __uint_as_float((uint32_t)x0 | ((uint32_t)x1 << 16)),
+                                  __uint_as_float((uint32_t)y0 | ((uint32_t)y1 << 16)));
+  tiles[i] = count;
   clamped[i] = (uint8_t)cl;
-  return (uint32_t)area;
+  return count;
 }
 
 // The workgroup's tile total goes to counters[3] (= num_rendered, read back by the host as soon
 // as this kernel is done while the ordering kernels run).
 template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
-                                                    float4* __restrict__ splat, uint32_t* __restrict__ depth_key,
+                                                    float4* __restrict__ splat, float4* __restrict__ binrec,
+                                                    uint32_t* __restrict__ depth_key,
                                                     uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
                                                     uint32_t* __restrict__ counters) {
   __shared__ uint32_t s_sum[4];
   const int i = blockIdx.x * 256 + threadIdx.x;
   uint32_t area = 0;
-  if (i < g.P) area = preprocess_one<DEG>(i, g, c, radii, splat, depth_key, tiles, clamped, counters);
+  if (i < g.P) area = preprocess_one<DEG>(i, g, c, radii, splat, binrec, depth_key, tiles, clamped, counters);
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) area += (uint32_t)__shfl_xor((int)area, d, 64);
   if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = area;
@@ -167,25 +180,25 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
   (void)hipMemsetAsync(geo.counters, 0, 64, st);
   dim3 grid((g.P + 255) / 256), block(256);
   if (g.colors) {
-    GS_LAUNCH("preprocess", k_preprocess<-1>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+    GS_LAUNCH("preprocess", k_preprocess<-1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
               geo.clamped, geo.counters);
     return;
   }
   switch (g.D) {
     case 0:
-      GS_LAUNCH("preprocess", k_preprocess<0>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+      GS_LAUNCH("preprocess", k_preprocess<0>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
                 geo.clamped, geo.counters);
       break;
     case 1:
-      GS_LAUNCH("preprocess", k_preprocess<1>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+      GS_LAUNCH("preprocess", k_preprocess<1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
                 geo.clamped, geo.counters);
       break;
     case 2:
-      GS_LAUNCH("preprocess", k_preprocess<2>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+      GS_LAUNCH("preprocess", k_preprocess<2>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
                 geo.clamped, geo.counters);
       break;
     default:
-      GS_LAUNCH("preprocess", k_preprocess<3>, grid, block, 0, st, g, c, radii, geo.splat, geo.depth_key, geo.tiles,
+      GS_LAUNCH("preprocess", k_preprocess<3>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
                 geo.clamped, geo.counters);
       break;
   }
@@ -240,10 +253,18 @@ void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
 // ------------------------------------------------------------------------------------------
 // binning
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ SpanCtx span_of(const float4* __restrict__ binrec, uint32_t gid, int& y0, int& y1) {
+  const float4 a = binrec[2 * gid], b = binrec[2 * gid + 1];
+  const uint32_t xr = __float_as_uint(b.z), yr = __float_as_uint(b.w);
+  y0 = (int)(yr & 0xFFFFu);
+  y1 = (int)(yr >> 16);
+  return span_ctx(a.x, a.y, a.z, a.w, b.x, b.y, (int)(xr & 0xFFFFu), (int)(xr >> 16));
+}
+
 __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* __restrict__ counters,
                                                    const uint32_t* __restrict__ sorted_gid,
-                                                   const uint32_t* __restrict__ offsets, const int* __restrict__ radii,
-                                                   const float4* __restrict__ splat, int gx, int gy,
+                                                   const uint32_t* __restrict__ offsets,
+                                                   const float4* __restrict__ binrec, int gx,
                                                    uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
                                                    uint32_t* __restrict__ presort_gid) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
@@ -251,34 +272,38 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* _
   const uint32_t gid = sorted_gid[s];
   uint32_t off = offsets[s];
   goff[gid] = off;
-  const float4 a = splat[3 * gid];
-  int x0, y0, x1, y1;
-  get_rect(a.x, a.y, radii[gid], gx, gy, x0, y0, x1, y1);
-  for (int y = y0; y < y1; y++)
-    for (int x = x0; x < x1; x++) {
-      tile_keys[off] = (uint32_t)(y * gx + x);
+  int y0, y1;
+  const SpanCtx sp = span_of(binrec, gid, y0, y1);
+  for (int ty = y0; ty < y1; ty++) {
+    int ta, tb;
+    row_span(sp, ty, ta, tb);
+    for (int x = ta; x < tb; x++) {
+      tile_keys[off] = (uint32_t)(ty * gx + x);
       presort_gid[off] = gid;
       off++;
     }
+  }
 }
 
 // Load-balanced duplicate: workgroup b writes instance slots [b S, (b + 1) S), S = DUP_SLOTS.
 // The depth ranks owning those slots are [dup_first[b], dup_first[b + 1]] (at most S + 1 of
-// them); their offsets, ids and tile rectangles are staged in LDS, every slot finds its owner by
-// an inclusive max-scan over start marks, and keys / presort ids are written fully coalesced.
-// The workgroups also clear the tile ranges (k_ranges fills the non-empty ones).
+// them).  Each splat's instances are its tile-exact row spans (row_span), laid out row by row;
+// the row segments meeting the block are numbered with a workgroup scan, every slot finds its
+// segment by an inclusive max-scan over segment start marks, and keys / presort ids are written
+// fully coalesced.  The workgroups also clear the tile ranges (k_ranges fills the non-empty ones).
 constexpr int DUP_THREADS = 256;
 constexpr int DUP_ITEMS = DUP_SLOTS / DUP_THREADS;
 __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     uint32_t I, const uint32_t* __restrict__ counters, const uint32_t* __restrict__ dup_first,
-    const uint32_t* __restrict__ sorted_gid, const uint32_t* __restrict__ offsets, const int* __restrict__ radii,
-    const float4* __restrict__ splat, int gx, int gy, uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
+    const uint32_t* __restrict__ sorted_gid, const uint32_t* __restrict__ offsets,
+    const float4* __restrict__ binrec, int gx, int gy, uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
     uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges) {
-  __shared__ uint32_t s_off[DUP_SLOTS + 1];
-  __shared__ uint32_t s_gid[DUP_SLOTS + 1];
-  __shared__ uint32_t s_rect[DUP_SLOTS + 1];  // x0 | y0 << 8 | w << 16 (tile grid <= 255 x 255) -- see host check
   __shared__ uint32_t s_own[DUP_SLOTS];
+  __shared__ uint32_t s_seg_start[DUP_SLOTS];  // first slot of the row segment (may precede the block)
+  __shared__ uint32_t s_seg_tile[DUP_SLOTS];   // tile id of the segment's first slot
+  __shared__ uint32_t s_seg_gid[DUP_SLOTS];
   __shared__ uint32_t s_wmax[DUP_THREADS / 64];
+  __shared__ uint32_t s_scan[4];
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   const uint32_t tiles = (uint32_t)(gx * gy);
   for (uint32_t t = b * DUP_THREADS + tid; t < tiles; t += gridDim.x * DUP_THREADS) ranges[t] = make_uint2(0u, 0u);
@@ -288,25 +313,51 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   const uint32_t s_lo = dup_first[b];
   const uint32_t s_hi = (k1 < I) ? dup_first[b + 1] : V - 1;
   const uint32_t nG = s_hi - s_lo + 1;
+  const uint32_t G = (nG + DUP_THREADS - 1) / DUP_THREADS;  // consecutive ranks per thread (<= 9)
+  const uint32_t r0 = min(nG, tid * G), r1 = min(nG, r0 + G);
   for (uint32_t i = tid; i < DUP_SLOTS; i += DUP_THREADS) s_own[i] = 0;
-  __syncthreads();
-  for (uint32_t i = tid; i < nG; i += DUP_THREADS) {
-    const uint32_t s = s_lo + i;
-    const uint32_t gid = sorted_gid[s];
-    const uint32_t off = offsets[s];
-    const float4 a = splat[3 * gid];
-    int x0, y0, x1, y1;
-    get_rect(a.x, a.y, radii[gid], gx, gy, x0, y0, x1, y1);
-    s_off[i] = off;
-    s_gid[i] = gid;
-    s_rect[i] = (uint32_t)x0 | ((uint32_t)y0 << 8) | ((uint32_t)(x1 - x0) << 16);
-    if (off >= k0) {
-      goff[gid] = off;
-      if (off < k1) s_own[off - k0] = i;
+  // pass 1: count the row segments of my splats that meet [k0, k1)
+  uint32_t nseg = 0;
+  for (uint32_t r = r0; r < r1; r++) {
+    const uint32_t gid = sorted_gid[s_lo + r];
+    uint32_t pos = offsets[s_lo + r];
+    if (pos >= k0 && pos < k1) goff[gid] = pos;
+    if (pos >= k1) continue;
+    int y0, y1;
+    const SpanCtx sp = span_of(binrec, gid, y0, y1);
+    for (int ty = y0; ty < y1 && pos < k1; ty++) {
+      int ta, tb;
+      row_span(sp, ty, ta, tb);
+      const uint32_t w = (uint32_t)(tb - ta);
+      if (w && pos + w > k0) nseg++;
+      pos += w;
+    }
+  }
+  uint32_t total;
+  uint32_t seg = block_excl_scan(nseg, s_scan, &total);
+  // pass 2: write the segments and mark their first in-block slot
+  for (uint32_t r = r0; r < r1; r++) {
+    const uint32_t gid = sorted_gid[s_lo + r];
+    uint32_t pos = offsets[s_lo + r];
+    if (pos >= k1) continue;
+    int y0, y1;
+    const SpanCtx sp = span_of(binrec, gid, y0, y1);
+    for (int ty = y0; ty < y1 && pos < k1; ty++) {
+      int ta, tb;
+      row_span(sp, ty, ta, tb);
+      const uint32_t w = (uint32_t)(tb - ta);
+      if (w && pos + w > k0) {
+        s_seg_start[seg] = pos;
+        s_seg_tile[seg] = (uint32_t)(ty * gx + ta);
+        s_seg_gid[seg] = gid;
+        s_own[(pos > k0 ? pos : k0) - k0] = seg;
+        seg++;
+      }
+      pos += w;
     }
   }
   __syncthreads();
-  // inclusive max-scan of owner marks over the block's slots (consecutive DUP_ITEMS per thread)
+  // inclusive max-scan of segment marks over the block's slots (consecutive DUP_ITEMS per thread)
   uint32_t v[DUP_ITEMS];
   uint32_t run = 0;
 #pragma unroll
@@ -335,13 +386,8 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     const uint32_t k = k0 + i;
     if (k < k1) {
       const uint32_t o = s_own[i];
-      const uint32_t j = k - s_off[o];
-      const uint32_t rc = s_rect[o];
-      const uint32_t w = rc >> 16;
-      const uint32_t q = j / w;
-      const uint32_t x = (rc & 255u) + (j - q * w), y = ((rc >> 8) & 255u) + q;
-      tile_keys[k] = y * (uint32_t)gx + x;
-      presort_gid[k] = s_gid[o];
+      tile_keys[k] = s_seg_tile[o] + (k - s_seg_start[o]);
+      presort_gid[k] = s_seg_gid[o];
     }
   }
 }
@@ -379,14 +425,14 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
     (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
     return;
   }
-  if (dup_balanced(I, (uint32_t)P) && c.gx <= 255 && c.gy <= 255) {
+  if (dup_balanced(I, (uint32_t)P)) {
     GS_LAUNCH("duplicate", k_duplicate_lb, dim3((I + DUP_SLOTS - 1) / DUP_SLOTS), dim3(DUP_THREADS), 0, st, I,
-              geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, radii, geo.splat, c.gx, c.gy, geo.goff,
+              geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy, geo.goff,
               bin.keys_a, bin.presort_gid, img.ranges);
   } else {
     (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
     GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
-              geo.sorted_gid, geo.offsets, radii, geo.splat, c.gx, c.gy, geo.goff, bin.keys_a, bin.presort_gid);
+              geo.sorted_gid, geo.offsets, geo.binrec, c.gx, geo.goff, bin.keys_a, bin.presort_gid);
   }
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tile_bits(tiles),
                    bin.sort_scratch, st);

@@ -55,6 +55,7 @@ struct CameraArgs {
 
 struct GeomPtrs {
   float4* splat;  // 3 per Gaussian: (x, y, cxx, cxy) (cyy, opacity, r, g) (b, depth, cull_lim, -)
+  float4* binrec;  // 2 per Gaussian: (x, y, cxx, cxy) (cyy, cull_lim, x0 | x1 << 16, y0 | y1 << 16) for binning
   uint32_t* depth_key;
   uint32_t* tiles;
   uint32_t* goff;  // first instance slot of each visible Gaussian (depth order)
@@ -77,6 +78,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   };
   size_t Pn = P ? P : 1;
   size_t o_splat = take(Pn * 48);
+  size_t o_bin = take(Pn * 32);
   size_t o_dkey = take(Pn * 4), o_tiles = take(Pn * 4), o_goff = take(Pn * 4), o_cl = take(Pn);
   size_t o_ka = take(Pn * 4), o_va = take(Pn * 4), o_kb = take(Pn * 4), o_vb = take(Pn * 4);
   size_t o_offs = take(Pn * 4);
@@ -86,6 +88,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   size_t o_cnt = take(64);
   if (out && base) {
     out->splat = (float4*)(base + o_splat);
+    out->binrec = (float4*)(base + o_bin);
     out->depth_key = (uint32_t*)(base + o_dkey);
     out->tiles = (uint32_t*)(base + o_tiles);
     out->goff = (uint32_t*)(base + o_goff);

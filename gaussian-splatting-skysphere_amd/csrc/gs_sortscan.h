@@ -227,10 +227,8 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32
       d[k] = v[k] ? (keys[i] >> shift) & mask : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < SORT_ITEMS; k++) {
-      const uint64_t peers = digit_peers(d[k], v[k], bits);
-      if (v[k] && (peers & lanemask_lt()) == 0) atomicAdd(&h[d[k]], (uint32_t)__popcll(peers));
-    }
+    for (int k = 0; k < SORT_ITEMS; k++)
+      if (v[k]) atomicAdd(&h[d[k]], 1u);  // counts only: order-free, deterministic
   }
   __syncthreads();
   hist[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];

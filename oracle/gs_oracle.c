@@ -104,6 +104,69 @@ static inline void get_rect(float x, float y, int r, int gx, int gy, int* rmin, 
     rmax[1] = imin(gy, imax(0, (int)((((y + fr) + 16.0f) - 1.0f) / 16.0f)));
 }
 
+/* ln(x) for x >= 1 from correctly-rounded IEEE ops only (frexp by bit fields, atanh series):
+ * |error| < 2e-7 relative.  Identical op sequence in csrc/gs_common.h:gs_log. */
+float oracle_log(float x) {
+    uint32_t u = u_as(x);
+    int e = (int)((u >> 23) & 255u) - 127;
+    float m = f_as((u & 0x7FFFFFu) | 0x3F800000u);
+    if (m > 1.41421356f) { m = m * 0.5f; e = e + 1; }
+    float f = m - 1.0f;
+    float t = f / (2.0f + f);
+    float t2 = t * t;
+    float p = 0.11111111f;
+    p = fmaf(p, t2, 0.14285715f);
+    p = fmaf(p, t2, 0.2f);
+    p = fmaf(p, t2, 0.33333334f);
+    p = fmaf(p, t2, 1.0f);
+    return fmaf((float)e, 0.69314718f, (2.0f * t) * p);
+}
+
+/* culling limit of the alpha >= 1/255 ellipse, q(d) <= lim (negative: never reaches 1/255) */
+static inline float cull_lim(float op) {
+    return op >= 1.0f / 255.0f ? 2.0f * fmaxf(oracle_log(255.0f * op), 0.0f) * 1.001f + 1e-3f : -1.0f;
+}
+
+/* Tile-exact binning: tiles [ta, tb) of tile row ty whose pixel square can hold a pixel with
+ * q(d) <= lim.  Conservative (a dropped tile has alpha < 1/255 at all of its pixels), so images and
+ * gradients equal those of the full upstream rectangle (tested: oracle_set_exact_tiles(0) vs 1).
+ * Identical op sequence in csrc/gs_common.h:span_ctx / row_span. */
+static int g_exact_tiles = 1;
+void oracle_set_exact_tiles(int on) { g_exact_tiles = on; }
+
+typedef struct { float mx, my, A, B, det, R, dyr, AL; int x0, x1, mode; } SpanCtx;
+static SpanCtx span_ctx(float mx, float my, float A, float B, float C, float L, int x0, int x1) {
+    SpanCtx s;
+    s.mx = mx; s.my = my; s.A = A; s.B = B; s.x0 = x0; s.x1 = x1;
+    s.det = A * C - B * B;
+    s.mode = !(L >= 0.0f) ? 2 : ((A > 0.0f && C > 0.0f && s.det > 0.0f) ? 0 : 1);
+    if (!g_exact_tiles) s.mode = 1;
+    s.R = 0.0f; s.dyr = 0.0f; s.AL = 0.0f;
+    if (s.mode == 0) {
+        s.AL = A * L;
+        s.R = sqrtf(s.AL / s.det) * 1.0001f + 0.01f;
+        s.dyr = -B * sqrtf(L / (C * s.det));
+    }
+    return s;
+}
+static void row_span(const SpanCtx* s, int ty, int* ta, int* tb) {
+    *ta = *tb = s->x0;
+    if (s->mode == 2) return;
+    if (s->mode == 1) { *tb = s->x1; return; }
+    float lo = fmaxf((float)(TILE * ty) - s->my, -s->R);
+    float hi = fminf((float)(TILE * ty + TILE - 1) - s->my, s->R);
+    if (!(lo <= hi)) return;
+    float d1 = fminf(fmaxf(s->dyr, lo), hi), d2 = fminf(fmaxf(-s->dyr, lo), hi);
+    float xr = (-s->B * d1 + sqrtf(fmaxf(s->AL - s->det * d1 * d1, 0.0f))) / s->A;
+    float xl = (-s->B * d2 - sqrtf(fmaxf(s->AL - s->det * d2 * d2, 0.0f))) / s->A;
+    float X0 = fmaxf((s->mx + xl) - (0.05f + 0.001f * fabsf(xl)), -1.0e6f);
+    float X1 = fminf((s->mx + xr) + (0.05f + 0.001f * fabsf(xr)), 1.0e6f);
+    int a = imax(s->x0, (int)ceilf((X0 - 15.0f) / 16.0f));
+    int b = imin(s->x1, (int)floorf(X1 / 16.0f) + 1);
+    *ta = a;
+    *tb = b > a ? b : a;
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* cov3D  (ref: gaussian_model.py:27-31 + general_utils.py:78-110;  SURVEY §8a a4 step 4)        */
 /* ------------------------------------------------------------------------------------------ */
@@ -330,6 +393,8 @@ typedef struct {
     float depth;
     int radius;
     int rmin[2], rmax[2];
+    float lim;
+    uint32_t count; /* tile-exact instance count (row spans) */
     unsigned char clamped[3];
 } Splat;
 
@@ -415,6 +480,15 @@ static int preprocess_one(const Scene* s, int i, Splat* o) {
     o->depth = pv[2];
     o->radius = radius;
     o->rmin[0] = rmin[0]; o->rmin[1] = rmin[1]; o->rmax[0] = rmax[0]; o->rmax[1] = rmax[1];
+    o->lim = cull_lim(o->opacity);
+    SpanCtx sp = span_ctx(px, py, conic[0], conic[1], conic[2], o->lim, rmin[0], rmax[0]);
+    uint32_t count = 0;
+    for (int ty = rmin[1]; ty < rmax[1]; ty++) {
+        int ta, tb;
+        row_span(&sp, ty, &ta, &tb);
+        count += (uint32_t)(tb - ta);
+    }
+    o->count = count;
     return 1;
 }
 
@@ -444,21 +518,25 @@ static int bin_scene(const Scene* s, Binned* b) {
     long long I = 0;
 #pragma omp parallel for schedule(static) reduction(+ : I)
     for (int i = 0; i < s->P; i++)
-        if (preprocess_one(s, i, &b->sp[i]))
-            I += (long long)(b->sp[i].rmax[0] - b->sp[i].rmin[0]) * (b->sp[i].rmax[1] - b->sp[i].rmin[1]);
+        if (preprocess_one(s, i, &b->sp[i])) I += (long long)b->sp[i].count;
     b->I = I;
     b->inst = (Inst*)malloc((size_t)(I ? I : 1) * sizeof(Inst));
     long long k = 0;
     for (int i = 0; i < s->P; i++) {
         Splat* o = &b->sp[i];
         if (o->radius == 0) continue;
-        for (int y = o->rmin[1]; y < o->rmax[1]; y++)
-            for (int x = o->rmin[0]; x < o->rmax[0]; x++) {
+        SpanCtx sp = span_ctx(o->xy[0], o->xy[1], o->conic[0], o->conic[1], o->conic[2], o->lim, o->rmin[0],
+                              o->rmax[0]);
+        for (int y = o->rmin[1]; y < o->rmax[1]; y++) {
+            int ta, tb;
+            row_span(&sp, y, &ta, &tb);
+            for (int x = ta; x < tb; x++) {
                 b->inst[k].tile = (uint32_t)(y * s->gx + x);
                 b->inst[k].dkey = u_as(o->depth);
                 b->inst[k].gid = (uint32_t)i;
                 k++;
             }
+        }
     }
     qsort(b->inst, (size_t)I, sizeof(Inst), inst_cmp);
     int tiles = s->gx * s->gy;
@@ -565,7 +643,8 @@ long long oracle_forward(int P, int D, int M, const float* bg, int W, int H, con
         }
         if (out_rgb) for (int c = 0; c < 3; c++) out_rgb[3 * i + c] = o->rgb[c];
         if (out_depth) out_depth[i] = o->depth;
-        if (out_tiles) out_tiles[i] = o->radius > 0 ? (uint32_t)area : 0u;
+        if (out_tiles) out_tiles[i] = o->radius > 0 ? o->count : 0u;
+        (void)area;
         if (out_clamped) for (int c = 0; c < 3; c++) out_clamped[3 * i + c] = o->clamped[c];
     }
     render_fwd(&s, &b, out_color, out_finalT, out_ncontrib);

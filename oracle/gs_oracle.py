@@ -42,6 +42,8 @@ def lib():
         L = ctypes.CDLL(_LIB_PATH)
         L.oracle_exp.restype = ctypes.c_float
         L.oracle_exp.argtypes = [ctypes.c_float]
+        L.oracle_log.restype = ctypes.c_float
+        L.oracle_log.argtypes = [ctypes.c_float]
         L.oracle_forward.restype = ctypes.c_longlong
         L.oracle_backward.restype = ctypes.c_longlong
         _lib = L
@@ -155,6 +157,15 @@ def set_threads(n: int):
 
 def exp(x: float) -> float:
     return float(lib().oracle_exp(ctypes.c_float(x)))
+
+
+def log(x: float) -> float:
+    return float(lib().oracle_log(ctypes.c_float(x)))
+
+
+def set_exact_tiles(on: bool):
+    """Tile-exact binning (default, = the HIP path) or the full upstream tile rectangle."""
+    lib().oracle_set_exact_tiles(int(bool(on)))
 
 
 def sh_forward(deg, means, campos, shs):
