@@ -293,17 +293,21 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* _
 // fully coalesced.  The workgroups also clear the tile ranges (k_ranges fills the non-empty ones).
 constexpr int DUP_THREADS = 256;
 constexpr int DUP_ITEMS = DUP_SLOTS / DUP_THREADS;
+// LDS index of slot i in the owner array: one pad word per 8 slots keeps the per-thread runs of
+// 8 consecutive slots on distinct banks
+__device__ __forceinline__ uint32_t own_idx(uint32_t i) { return i + (i >> 3); }
+
 __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     uint32_t I, const uint32_t* __restrict__ counters, const uint32_t* __restrict__ dup_first,
     const uint32_t* __restrict__ sorted_gid, const uint32_t* __restrict__ offsets,
     const float4* __restrict__ binrec, int gx, int gy, uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
     uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges) {
-  __shared__ uint32_t s_own[DUP_SLOTS];
+  __shared__ uint32_t s_own[DUP_SLOTS + DUP_SLOTS / 8];  // (slot + 1) << 16 | segment at segment starts
   __shared__ uint32_t s_seg_start[DUP_SLOTS];  // first slot of the row segment (may precede the block)
   __shared__ uint32_t s_seg_tile[DUP_SLOTS];   // tile id of the segment's first slot
   __shared__ uint32_t s_seg_gid[DUP_SLOTS];
   __shared__ uint32_t s_wmax[DUP_THREADS / 64];
-  __shared__ uint32_t s_scan[4];
+  __shared__ uint32_t s_nseg;
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   const uint32_t tiles = (uint32_t)(gx * gy);
   for (uint32_t t = b * DUP_THREADS + tid; t < tiles; t += gridDim.x * DUP_THREADS) ranges[t] = make_uint2(0u, 0u);
@@ -313,12 +317,13 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   const uint32_t s_lo = dup_first[b];
   const uint32_t s_hi = (k1 < I) ? dup_first[b + 1] : V - 1;
   const uint32_t nG = s_hi - s_lo + 1;
-  const uint32_t G = (nG + DUP_THREADS - 1) / DUP_THREADS;  // consecutive ranks per thread (<= 9)
-  const uint32_t r0 = min(nG, tid * G), r1 = min(nG, r0 + G);
-  for (uint32_t i = tid; i < DUP_SLOTS; i += DUP_THREADS) s_own[i] = 0;
-  // pass 1: count the row segments of my splats that meet [k0, k1)
-  uint32_t nseg = 0;
-  for (uint32_t r = r0; r < r1; r++) {
+  for (uint32_t i = tid; i < DUP_SLOTS + DUP_SLOTS / 8; i += DUP_THREADS) s_own[i] = 0;
+  if (tid == 0) s_nseg = 0;
+  __syncthreads();
+  // row segments of the block's splats that meet [k0, k1): any segment numbering works, the
+  // marks carry their slot so the scan below picks the segment that starts last at or before
+  // each slot (deterministic output)
+  for (uint32_t r = tid; r < nG; r += DUP_THREADS) {
     const uint32_t gid = sorted_gid[s_lo + r];
     uint32_t pos = offsets[s_lo + r];
     if (pos >= k0 && pos < k1) goff[gid] = pos;
@@ -329,40 +334,24 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
       int ta, tb;
       row_span(sp, ty, ta, tb);
       const uint32_t w = (uint32_t)(tb - ta);
-      if (w && pos + w > k0) nseg++;
-      pos += w;
-    }
-  }
-  uint32_t total;
-  uint32_t seg = block_excl_scan(nseg, s_scan, &total);
-  // pass 2: write the segments and mark their first in-block slot
-  for (uint32_t r = r0; r < r1; r++) {
-    const uint32_t gid = sorted_gid[s_lo + r];
-    uint32_t pos = offsets[s_lo + r];
-    if (pos >= k1) continue;
-    int y0, y1;
-    const SpanCtx sp = span_of(binrec, gid, y0, y1);
-    for (int ty = y0; ty < y1 && pos < k1; ty++) {
-      int ta, tb;
-      row_span(sp, ty, ta, tb);
-      const uint32_t w = (uint32_t)(tb - ta);
       if (w && pos + w > k0) {
+        const uint32_t seg = atomicAdd(&s_nseg, 1u);
         s_seg_start[seg] = pos;
         s_seg_tile[seg] = (uint32_t)(ty * gx + ta);
         s_seg_gid[seg] = gid;
-        s_own[(pos > k0 ? pos : k0) - k0] = seg;
-        seg++;
+        const uint32_t at = (pos > k0 ? pos : k0) - k0;
+        s_own[own_idx(at)] = ((at + 1) << 16) | seg;
       }
       pos += w;
     }
   }
   __syncthreads();
-  // inclusive max-scan of segment marks over the block's slots (consecutive DUP_ITEMS per thread)
+  // inclusive max-scan of the marks over the block's slots (consecutive DUP_ITEMS per thread)
   uint32_t v[DUP_ITEMS];
   uint32_t run = 0;
 #pragma unroll
   for (int r = 0; r < DUP_ITEMS; r++) {
-    run = max(run, s_own[tid * DUP_ITEMS + r]);
+    run = max(run, s_own[own_idx(tid * DUP_ITEMS + r)]);
     v[r] = run;
   }
   uint32_t incl = run;
@@ -378,14 +367,14 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   __syncthreads();
   for (uint32_t w = 0; w < (tid >> 6); w++) excl = max(excl, s_wmax[w]);
 #pragma unroll
-  for (int r = 0; r < DUP_ITEMS; r++) s_own[tid * DUP_ITEMS + r] = max(v[r], excl);
+  for (int r = 0; r < DUP_ITEMS; r++) s_own[own_idx(tid * DUP_ITEMS + r)] = max(v[r], excl);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < DUP_ITEMS; r++) {
     const uint32_t i = (uint32_t)r * DUP_THREADS + tid;
     const uint32_t k = k0 + i;
     if (k < k1) {
-      const uint32_t o = s_own[i];
+      const uint32_t o = s_own[own_idx(i)] & 0xFFFFu;
       tile_keys[k] = s_seg_tile[o] + (k - s_seg_start[o]);
       presort_gid[k] = s_seg_gid[o];
     }
