@@ -159,6 +159,13 @@ def random_gaussians(P, sh_degree, cam: MiniCamera | None = None, seed=0, ball_r
     return GaussianScene(means.contiguous(), opac, scales, rots, shs, sh_degree)
 
 
+def concat_scenes(*scenes: GaussianScene) -> GaussianScene:
+    """Concatenate scenes of one SH degree (e.g. a skysphere-like mix of tiny and huge splats)."""
+    cat = lambda f: torch.cat([getattr(s, f) for s in scenes], 0).contiguous()  # noqa: E731
+    return GaussianScene(cat("means3D"), cat("opacities"), cat("scales"), cat("rotations"), cat("shs"),
+                         scenes[0].sh_degree)
+
+
 def raster_settings_for(cam: MiniCamera, sh_degree, bg=None, scale_modifier=1.0, debug=False, device="cuda"):
     """The settings the reference adapter builds (gaussian_renderer/__init__.py:33-49)."""
     from diff_gaussian_rasterization import GaussianRasterizationSettings

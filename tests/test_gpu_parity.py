@@ -144,6 +144,48 @@ def test_forward_bitexact_and_backward_vs_oracle(oracle, device, name, P, deg, W
     _check_backward(gr, leaves)
 
 
+def test_large_and_elongated_splats(oracle, device):
+    """Skysphere-like mix: many small splats plus large / very elongated ones spanning dozens of
+    tiles and several duplicate workgroups (row spans over many tile rows, segments crossing
+    workgroups, long per-Gaussian record runs)."""
+    W, H = 640, 360
+    cam = gs_scenes.identity_camera(W, H)
+    small = gs_scenes.random_gaussians(3000, 2, cam=cam, seed=21)
+    big = gs_scenes.random_gaussians(60, 2, cam=cam, seed=22, scale_range=(0.05, 1.5), z_range=(2.0, 4.0))
+    big.scales[::3, 0] *= 0.02  # needles
+    sc = gs_scenes.concat_scenes(small, big)
+    bg = np.array([0.1, 0.2, 0.3], np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg)
+    ofw = oracle.forward(osc, intermediates=True)
+    ofw["bg"] = bg
+    assert ofw["tiles_touched"].max() > 300
+    _check_forward_exact(ofw, cam, sc, device)
+    dpix = gs_scenes.dl_dimage(H, W, seed=23).numpy()
+    img, _, leaves = _gpu_run(cam, sc, device, bg, dpix)
+    np.testing.assert_array_equal(img.detach().cpu().numpy(), ofw["color"])
+    _check_backward(oracle.backward(osc, dpix), leaves)
+
+
+def test_few_huge_splats_use_per_splat_duplicate(oracle, device):
+    """More than 2048 instances per Gaussian on average: the binning falls back to the per-splat
+    duplicate kernel (DUP_SLOTS * P < num_rendered); results stay bit-exact."""
+    W, H = 1920, 1080
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(4, 0, cam=cam, seed=31, scale_range=(3.0, 6.0), z_range=(3.0, 5.0))
+    sc.means3D[:, :2] = 0.0
+    sc.opacities[:] = 0.9
+    bg = np.zeros(3, np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg)
+    ofw = oracle.forward(osc, intermediates=True)
+    ofw["bg"] = bg
+    assert ofw["num_rendered"] > 2048 * 4
+    _check_forward_exact(ofw, cam, sc, device)
+    dpix = gs_scenes.dl_dimage(H, W, seed=32).numpy()
+    img, _, leaves = _gpu_run(cam, sc, device, bg, dpix)
+    np.testing.assert_array_equal(img.detach().cpu().numpy(), ofw["color"])
+    _check_backward(oracle.backward(osc, dpix), leaves)
+
+
 def test_precomputed_colors_and_cov3d(oracle, device):
     W, H = 160, 96
     cam = gs_scenes.identity_camera(W, H)
