@@ -404,14 +404,19 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
       for (int k = 0; k < 4; k++) out.drot[4 * i + k] = 0.f;
     return;
   }
-  float a[GRAD_REC];
+  // per-tile records summed in fp64: a large splat's tile partials cancel (opposite sides pull
+  // its mean opposite ways), and an fp32 running sum over hundreds of tiles loses the difference
+  double acc[GRAD_REC];
 #pragma unroll
-  for (int k = 0; k < GRAD_REC; k++) a[k] = 0.0f;
+  for (int k = 0; k < GRAD_REC; k++) acc[k] = 0.0;
   const float* rec = gradrec + (size_t)goff[i] * GRAD_REC;
   for (uint32_t t = 0; t < cnt; t++) {
 #pragma unroll
-    for (int k = 0; k < GRAD_REC; k++) a[k] += rec[(size_t)t * GRAD_REC + k];
+    for (int k = 0; k < GRAD_REC; k++) acc[k] += (double)rec[(size_t)t * GRAD_REC + k];
   }
+  float a[GRAD_REC];
+#pragma unroll
+  for (int k = 0; k < GRAD_REC; k++) a[k] = (float)acc[k];
   const float dcol[3] = {a[0], a[1], a[2]};
   const float dm2x = a[3], dm2y = a[4];
   const float dcon0 = a[5], dcon1 = a[6], dcon2 = a[7];
