@@ -1,5 +1,9 @@
 """bench.py -- rasterizer forward+backward throughput on MI355X (BASELINE.json metric).
 
+Other BASELINE configs: --workload c1 / c2 (smaller), c4 (8 ring views of a 1M ball scene, one
+step = the 8 views sharded over the ranks + one all-reduce: strong scaling), c5 (5M Gaussians: HBM
+footprint in "hbm").
+
 Workload (N=1): BASELINE.json configs[2] "C3" -- 1M Gaussians, SH degree 3, 1920x1080, 16x16
 tiles, one view per step (synthetic scene per SURVEY.md §8d: frustum-uniform means, seed 0).
 One step = GaussianRasterizer forward + backward for one view (dL/dimage fixed, seed 1) through
@@ -35,6 +39,10 @@ WORKLOADS = {
     "c3": dict(P=1_000_000, deg=3, W=1920, H=1080, desc="C3: 1M Gaussians SH3 1920x1080, 16x16 tiles"),
     "c2": dict(P=100_000, deg=3, W=800, H=800, desc="C2: 100k Gaussians SH3 800x800"),
     "c1": dict(P=10_000, deg=0, W=256, H=256, desc="C1: 10k Gaussians SH0 256x256"),
+    # C4: one step = the 8 ring views (sharded over the ranks) + one gradient all-reduce
+    "c4": dict(P=1_000_000, deg=3, W=1920, H=1080, views=8,
+               desc="C4: 1M Gaussians SH3 1920x1080 in a ball, 8 ring views sharded over ranks"),
+    "c5": dict(P=5_000_000, deg=3, W=1920, H=1080, desc="C5: 5M Gaussians SH3 1920x1080 (HBM footprint)"),
 }
 
 
@@ -70,21 +78,31 @@ def main():
     dev = torch.device("cuda", local)
     wl = WORKLOADS[args.workload]
     P, deg, W, H = wl["P"], wl["deg"], wl["W"], wl["H"]
-    cam = gs_scenes.identity_camera(W, H)
-    sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=0)
+    n_views = wl.get("views", 0)
+    if n_views:  # C4: ball scene seen from a ring of cameras; this rank's share of the views
+        cams = gs_scenes.circle_cameras(n_views, 6.0, W, H)
+        my_views = vp.shard_views(n_views, rank, world)
+        sc = gs_scenes.random_gaussians(P, deg, seed=0, ball_radius=2.0)
+        cam = cams[my_views[0]]
+    else:
+        cam = gs_scenes.identity_camera(W, H)
+        cams, my_views = [cam], [0]
+        sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=0)
     settings = gs_scenes.raster_settings_for(cam, deg, device=dev)
     d = sc.to(dev)
     M = d.shs.shape[1]
     params = [t.clone().requires_grad_(True) for t in (d.means3D, d.shs, d.opacities, d.scales, d.rotations)]
     means2D = torch.zeros_like(params[0], requires_grad=True)
     dpix = gs_scenes.dl_dimage(H, W, seed=1).to(dev)
-    rast = GaussianRasterizer(settings)
+    rasts = [GaussianRasterizer(gs_scenes.raster_settings_for(cams[v], deg, device=dev)) for v in my_views]
+    rast = rasts[0]
     bucket = vp.GradBucket(params) if world > 1 else None
 
     def step():
-        img, _ = rast(means3D=params[0], means2D=means2D, opacities=params[2], shs=params[1], scales=params[3],
-                      rotations=params[4])
-        img.backward(dpix)
+        for r in rasts:  # gradients of this rank's views accumulate in .grad
+            img, _ = r(means3D=params[0], means2D=means2D, opacities=params[2], shs=params[1], scales=params[3],
+                       rotations=params[4])
+            img.backward(dpix)
         if world > 1:
             bucket.allreduce(unpack=False)  # one RCCL all-reduce of the 59-f32/Gaussian bucket
         for p in params:
@@ -102,6 +120,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -111,6 +130,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    peak_hbm = torch.cuda.max_memory_allocated(dev)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -143,7 +163,8 @@ def main():
         t_render = (time.perf_counter() - tr) / nr
 
     ms_per_step = 1e3 * elapsed / args.steps
-    value = world * args.steps / elapsed
+    # whole-job steps/s: weak scaling (C1-C3, C5) counts every rank's view; a C4 step is the 8-view batch
+    value = (1 if n_views else world) * args.steps / elapsed
 
     # per-kernel breakdown + roofline of the dominant kernel
     kernels = {}
@@ -184,17 +205,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if n_views else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded; SURVEY.md §8d distribution)",
         "config": {"workload": wl["desc"], "gaussians": P, "sh_degree": deg, "width": W, "height": H,
-                   "views_per_rank_per_step": 1, "parallelism": f"view-parallel dp{world}" +
+                   "views_per_rank_per_step": len(my_views), "views_per_step": n_views or world,
+                   "parallelism": f"view-parallel dp{world}" +
                    (" + RCCL all-reduce of 59 f32/Gaussian" if world > 1 else "")},
         "render_mpix_s": round(W * H / t_render / 1e6, 1),
         "render_ms": round(1e3 * t_render, 4),
         "num_rendered": int(num_rendered),
         "visible": visible,
+        "hbm": {"peak_allocated_GB": round(peak_hbm / 1e9, 3),
+                "scene_params_GB": round(sum(p.numel() for p in params) * 4 / 1e9, 3),
+                "geom_buffer_GB": round(lib.gs_geom_buffer_bytes(P) / 1e9, 3),
+                "binning_buffer_GB": round(lib.gs_binning_buffer_bytes(int(num_rendered), W, H) / 1e9, 3),
+                "image_buffer_GB": round(lib.gs_image_buffer_bytes(W, H) / 1e9, 3),
+                "grad_scratch_GB": round(lib.gs_grad_buffer_bytes(int(num_rendered)) / 1e9, 3)},
         "roofline": roofline,
         "step_algo_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
         "kernels": kernels,
