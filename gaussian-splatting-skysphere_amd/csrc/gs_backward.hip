@@ -248,6 +248,82 @@ void bwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
 }
 
 // ------------------------------------------------------------------------------------------
+// per-Gaussian record sums
+//
+// Each visible Gaussian owns the contiguous records [offsets[r], offsets[r + 1]) (r = its depth
+// rank).  A wave takes 64 consecutive ranks and sweeps their records 64 at a time (coalesced
+// loads, no per-Gaussian loop divergence): every lane finds its record's owner by a binary search
+// over the 64 offsets held in the lanes, a segmented inclusive wave scan sums the records of one
+// owner, and the segment's last lane adds the partial into the owner's fp64 LDS accumulator (a
+// large splat's tile partials cancel, so the cross-tile sum is kept in fp64).  The total goes
+// back into the owner's first record.  Fixed order throughout: deterministic.
+// ------------------------------------------------------------------------------------------
+constexpr int SUMREC_WAVES = 4;
+// one step of the segmented wave scan: v += (shifted v) when the shifted lane has the same owner
+// (owners are carried +1 so a lane without a source (0) never matches)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void seg_scan_step(float* v, uint32_t own1) {
+  const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own1, CTRL, ROW_MASK, 0xF, false);
+  const float f = o == own1 ? 1.0f : 0.0f;
+#pragma unroll
+  for (int c = 0; c < GRAD_REC; c++) v[c] = __builtin_fmaf(dpp_f<CTRL, ROW_MASK>(v[c]), f, v[c]);
+}
+
+__global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_t* __restrict__ counters,
+                                                                   const uint32_t* __restrict__ offsets,
+                                                                   float* __restrict__ gradrec) {
+  __shared__ double s_acc[SUMREC_WAVES][64][GRAD_REC];
+  __shared__ unsigned long long s_mark[SUMREC_WAVES];
+  const uint32_t V = counters[0], I = counters[1];
+  const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t r0 = (blockIdx.x * SUMREC_WAVES + wid) * 64;
+  if (r0 >= V) return;  // wave-uniform; the kernel has no workgroup barrier
+  const uint32_t nr = min(64u, V - r0);
+  const uint32_t my_off = lane < nr ? offsets[r0 + lane] : 0xFFFFFFFFu;
+  const uint32_t S0 = (uint32_t)__shfl((int)my_off, 0, 64);
+  const uint32_t S1 = (r0 + 64 < V) ? offsets[r0 + 64] : I;
+#pragma unroll
+  for (int c = 0; c < GRAD_REC; c++) s_acc[wid][lane][c] = 0.0;
+  const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  uint32_t jbase = 0xFFFFFFFFu;  // (number of owners starting before `base`) - 1
+  for (uint32_t base = S0; base < S1; base += 64) {
+    // slots of the chunk that start an owner -> bit mask -> owner of my slot by popcount
+    if (lane == 0) s_mark[wid] = 0ull;
+    __builtin_amdgcn_wave_barrier();
+    if (my_off >= base && my_off < base + 64) atomicOr(&s_mark[wid], 1ull << (my_off - base));
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long B = s_mark[wid];
+    const uint32_t own = jbase + (uint32_t)__popcll(B & le);
+    jbase += (uint32_t)__popcll(B);
+    const uint32_t k = base + lane;
+    const bool valid = k < S1;
+    const size_t kk = (size_t)(valid ? k : S1 - 1);
+    float v[GRAD_REC];
+#pragma unroll
+    for (int c = 0; c < GRAD_REC; c++) v[c] = gradrec[kk * GRAD_REC + c];
+#pragma unroll
+    for (int c = 0; c < GRAD_REC; c++) v[c] = valid ? v[c] : 0.0f;
+    const uint32_t own1 = valid ? own + 1 : 0;
+    seg_scan_step<0x111, 0xF>(v, own1);  // row_shr:1
+    seg_scan_step<0x112, 0xF>(v, own1);  // row_shr:2
+    seg_scan_step<0x114, 0xF>(v, own1);  // row_shr:4
+    seg_scan_step<0x118, 0xF>(v, own1);  // row_shr:8
+    seg_scan_step<0x142, 0xA>(v, own1);  // row_bcast:15 -> rows 1, 3
+    seg_scan_step<0x143, 0xC>(v, own1);  // row_bcast:31 -> rows 2, 3
+    const uint32_t next1 = (uint32_t)__shfl_down((int)own1, 1, 64);
+    if (valid && (lane == 63 || next1 != own1)) {
+#pragma unroll
+      for (int c = 0; c < GRAD_REC; c++) s_acc[wid][own][c] += (double)v[c];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane < nr) {
+#pragma unroll
+    for (int c = 0; c < GRAD_REC; c++) gradrec[(size_t)my_off * GRAD_REC + c] = (float)s_acc[wid][lane][c];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // preprocess backward
 // ------------------------------------------------------------------------------------------
 
@@ -404,19 +480,11 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
       for (int k = 0; k < 4; k++) out.drot[4 * i + k] = 0.f;
     return;
   }
-  // per-tile records summed in fp64: a large splat's tile partials cancel (opposite sides pull
-  // its mean opposite ways), and an fp32 running sum over hundreds of tiles loses the difference
-  double acc[GRAD_REC];
-#pragma unroll
-  for (int k = 0; k < GRAD_REC; k++) acc[k] = 0.0;
+  // the Gaussian's per-tile records were summed into its first record by k_sum_records
   const float* rec = gradrec + (size_t)goff[i] * GRAD_REC;
-  for (uint32_t t = 0; t < cnt; t++) {
-#pragma unroll
-    for (int k = 0; k < GRAD_REC; k++) acc[k] += (double)rec[(size_t)t * GRAD_REC + k];
-  }
   float a[GRAD_REC];
 #pragma unroll
-  for (int k = 0; k < GRAD_REC; k++) a[k] = (float)acc[k];
+  for (int k = 0; k < GRAD_REC; k++) a[k] = rec[k];
   const float dcol[3] = {a[0], a[1], a[2]};
   const float dm2x = a[3], dm2y = a[4];
   const float dcon0 = a[5], dcon1 = a[6], dcon2 = a[7];
@@ -584,9 +652,12 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
   }
 }
 
-void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const float* gradrec,
-                    const GradOut& out, hipStream_t st) {
+void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, float* gradrec,
+                    bool have_records, const GradOut& out, hipStream_t st) {
   if (g.P <= 0) return;
+  if (have_records)
+    GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
+              dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, gradrec);
   dim3 grid((g.P + 255) / 256), block(256);
   const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
   const size_t lds = sh ? (size_t)256 * (3 * g.M + 1) * sizeof(float) : 0;

@@ -195,8 +195,8 @@ struct GradOut {
   float* dscale;    // [P, 3] or null
   float* drot;      // [P, 4] or null
 };
-void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const float* gradrec,
-                    const GradOut& out, hipStream_t st);
+void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, float* gradrec,
+                    bool have_records, const GradOut& out, hipStream_t st);
 void knn_mean_dist2(int P, const float* pts, float* out, char* scratch, hipStream_t st);
 size_t knn_scratch_bytes(int P);
 
