@@ -51,11 +51,12 @@ def kernel_bytes(name, P, V, I, M, W, H, tiles):
     npix = W * H
     sh = 12 * M
     return {
-        "preprocess": P * (44 + sh + 8) + V * (36 + 4 + 1),
-        "render_fwd": I * (4 + 4 + 36) + npix * 20 + tiles * 12,
-        "render_bwd": I * (4 + 4 + 36 + 36) + npix * 20 + tiles * 12,
-        "preprocess_bwd": P * (8 + 44 + sh + 1 + 32 + 24 + sh) + I * 36,
-        "duplicate": V * 24 + I * 8,
+        "preprocess": P * (44 + sh + 4 + 4) + V * (48 + 32 + 4 + 1),
+        "render_fwd": I * (4 + 4 + 48) + npix * 20 + tiles * 12,
+        "render_bwd": I * (4 + 4 + 48 + 36) + npix * 20 + tiles * 12,
+        "sum_records": I * 36 + V * (4 + 36),
+        "preprocess_bwd": P * (8 + 44 + sh + 1 + 32 + 24 + sh) + V * 36,
+        "duplicate": V * (4 + 4 + 32 + 4) + I * 8,
         "ranges": I * 4 + tiles * 8,
     }.get(name)
 
@@ -190,7 +191,8 @@ def main():
                     algo_bytes_per_launch=dom_bytes)
     # whole-step algorithmic bytes (P*a_G + I*a_I + Npix*a_px)
     step_bytes = sum(kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles) or 0 for k in
-                     ("preprocess", "render_fwd", "render_bwd", "preprocess_bwd", "duplicate", "ranges"))
+                     ("preprocess", "render_fwd", "render_bwd", "sum_records", "preprocess_bwd", "duplicate",
+                      "ranges"))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
