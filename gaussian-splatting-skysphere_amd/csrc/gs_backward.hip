@@ -592,44 +592,6 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
   }
 }
 
-// Block-wide copy of 256 consecutive SH rows (3M floats each) between global memory and an LDS
-// array with an odd row stride (3M + 1: conflict-free per-thread row access); dwordx4 global
-// accesses when rows are 16-B multiples and the base is aligned.
-__device__ __forceinline__ void rows_to_lds(const float* __restrict__ src, float* lds, int n, int rowf, int stride) {
-  const int total = n * rowf;
-  if ((rowf & 3) == 0 && (((uintptr_t)src) & 15) == 0) {
-    for (int q = threadIdx.x; q < (total >> 2); q += 256) {
-      const float4 v = reinterpret_cast<const float4*>(src)[q];
-      const int e = q << 2, t = e / rowf;
-      float* d = lds + t * stride + (e - t * rowf);
-      d[0] = v.x;
-      d[1] = v.y;
-      d[2] = v.z;
-      d[3] = v.w;
-    }
-  } else {
-    for (int e = threadIdx.x; e < total; e += 256) {
-      const int t = e / rowf;
-      lds[t * stride + (e - t * rowf)] = src[e];
-    }
-  }
-}
-__device__ __forceinline__ void lds_to_rows(const float* lds, float* __restrict__ dst, int n, int rowf, int stride) {
-  const int total = n * rowf;
-  if ((rowf & 3) == 0 && (((uintptr_t)dst) & 15) == 0) {
-    for (int q = threadIdx.x; q < (total >> 2); q += 256) {
-      const int e = q << 2, t = e / rowf;
-      const float* d = lds + t * stride + (e - t * rowf);
-      reinterpret_cast<float4*>(dst)[q] = make_float4(d[0], d[1], d[2], d[3]);
-    }
-  } else {
-    for (int e = threadIdx.x; e < total; e += 256) {
-      const int t = e / rowf;
-      dst[e] = lds[t * stride + (e - t * rowf)];
-    }
-  }
-}
-
 template <int DEG>  // -1: colours precomputed (no SH gradient)
 __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraArgs c,
                                                         const uint32_t* __restrict__ tiles,
