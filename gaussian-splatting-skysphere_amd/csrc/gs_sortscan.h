@@ -363,8 +363,11 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
   uint32_t* row_total = scratch + hist_n;
   uint32_t *kin = keys_a, *vin = vals_a, *kout = keys_b, *vout = vals_b;
   bool in_b = false;
-  for (int shift = 0; shift < end_bit; shift += RADIX_BITS) {
-    int bits = end_bit - shift < RADIX_BITS ? end_bit - shift : RADIX_BITS;
+  // digits of (nearly) equal width: 13 bits -> 7 + 6, not 8 + 5 (longer runs in the first scatter)
+  const int npass = radix_passes(end_bit);
+  const int width = (end_bit + npass - 1) / npass;
+  for (int shift = 0; shift < end_bit; shift += width) {
+    int bits = end_bit - shift < width ? end_bit - shift : width;
     GS_LAUNCH("radix_hist", k_radix_hist, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, n_dev, n_max, shift, bits,
               p.chunk, p.nb, hist);
     GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX), dim3(SORT_THREADS), 0, st, hist, p.nb, row_total);
