@@ -34,6 +34,8 @@ import gs_view_parallel as vp  # noqa: E402
 from diff_gaussian_rasterization import GaussianRasterizer, _C, _native  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E
+# wave64 VALU issue peak: 256 CUs x 4 SIMD32 x 2.4 GHz / 2 cycles per wave64 instruction
+VALU_PEAK_IPS = 256 * 4 * 2.4e9 / 2
 
 WORKLOADS = {
     "c3": dict(P=1_000_000, deg=3, W=1920, H=1080, desc="C3: 1M Gaussians SH3 1920x1080, 16x16 tiles"),
@@ -189,6 +191,17 @@ def main():
     roofline = dict(bound="hbm", kernel=dom, achieved=round(achieved, 1) if achieved else None, peak=HBM_PEAK_GBS,
                     unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4) if achieved else None, traffic=traffic,
                     algo_bytes_per_launch=dom_bytes)
+    # the render kernels are VALU-issue bound, not HBM bound: report the issue-rate fraction too,
+    # from the committed PMC pass (SQ_INSTS_VALU per launch, device total) and the live duration
+    valu_path = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if os.path.exists(valu_path):
+        try:
+            vi = json.load(open(valu_path)).get(args.workload, {}).get(dom)
+        except Exception:
+            vi = None
+        if vi:
+            roofline["valu"] = dict(insts_per_launch=vi, peak_insts_per_s=VALU_PEAK_IPS,
+                                    frac=round(vi / (dom_avg_ms * 1e-3) / VALU_PEAK_IPS, 4))
     # whole-step algorithmic bytes (P*a_G + I*a_I + Npix*a_px)
     step_bytes = sum(kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles) or 0 for k in
                      ("preprocess", "render_fwd", "render_bwd", "sum_records", "preprocess_bwd", "duplicate",

@@ -16,7 +16,7 @@ if [ -n "$PROFILE" ]; then
 fi
 if [ -n "$PMC" ]; then
   cd /tmp
-  for pass in fetch:FETCH_SIZE write:WRITE_SIZE; do
+  for pass in fetch:FETCH_SIZE write:WRITE_SIZE sq2:SQ_INSTS_VALU; do
     name=${pass%%:*}; ctr=${pass#*:}
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctr -d $OUT/pmc_$name -o run --output-format csv -- python3 $R/tools/prof_step.py --workload c3 --steps 2 --warmup 1 > $OUT/pmc_$name.log 2>&1 || { echo "pmc $name failed"; tail -20 $OUT/pmc_$name.log; exit 1; }
   done

@@ -31,6 +31,7 @@ def per_kernel(counter, d):
             continue
         short = k.split("(")[0].replace("void ", "").split("<")[0].replace("gs::", "")
         short = short[2:] if short.startswith("k_") else short
+        short = {"duplicate_lb": "duplicate"}.get(short, short)  # profile names used by bench.py
         per_dispatch[row["Dispatch_Id"]] += float(row["Counter_Value"])
         names[row["Dispatch_Id"]] = short
     for disp, v in per_dispatch.items():
@@ -40,6 +41,12 @@ def per_kernel(counter, d):
 
 fetch = per_kernel("FETCH_SIZE", "pmc_fetch")
 write = per_kernel("WRITE_SIZE", "pmc_write")
+valu = per_kernel("SQ_INSTS_VALU", "pmc_sq2")
+if valu:  # wave-level VALU instructions per launch (device total), for the compute roofline
+    vpath = os.path.join(os.path.dirname(out_path), "pmc_valu.json")
+    vdata = json.load(open(vpath)) if os.path.exists(vpath) else {}
+    vdata[workload] = {k: int(round(v)) for k, v in sorted(valu.items())}
+    json.dump(vdata, open(vpath, "w"), indent=1, sort_keys=True)
 res = {}
 for k in sorted(set(fetch) & set(write)):
     res[k] = int(round((2 * fetch[k] + write[k]) * 1024))
