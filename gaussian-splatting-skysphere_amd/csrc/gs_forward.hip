@@ -441,6 +441,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   __shared__ float4 s_co[GS_BLOCK];
   __shared__ float4 s_rgb[GS_BLOCK];
   __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
+  __shared__ uint16_t s_qlist[4][GS_BLOCK];  // per quadrant wave: its batch entries in order
   __shared__ uint32_t s_max;
   const uint32_t tile = blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
@@ -470,52 +471,55 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
     publish_masks(qmask, s_mask, tid);
     __syncthreads();
     if (__ballot(!done) == 0) continue;
-#pragma unroll 1
-    for (int qq = 0; qq < 4; qq++) {
-      uint64_t m = uniform_u64(s_mask[qq][wid]);
-      // two entries per trip: their power / exp / alpha chains are independent (ILP); the
-      // compositing of the pair is then applied in order, exactly as one entry at a time
-      while (m) {
-        const uint32_t j0 = (uint32_t)(qq * 64 + __builtin_ctzll(m));
-        m &= m - 1;
-        const bool has1 = m != 0;
-        const uint32_t j1 = has1 ? (uint32_t)(qq * 64 + __builtin_ctzll(m)) : j0;
-        if (has1) m &= m - 1;
-        const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
-        const float4 co0 = s_co[j0], co1 = s_co[j1];
-        const float dx0 = xy0.x - pfx, dy0 = xy0.y - pfy;
-        const float dx1 = xy1.x - pfx, dy1 = xy1.y - pfy;
-        const float power0 = -0.5f * (co0.x * dx0 * dx0 + co0.z * dy0 * dy0) - co0.y * dx0 * dy0;
-        const float power1 = -0.5f * (co1.x * dx1 * dx1 + co1.z * dy1 * dy1) - co1.y * dx1 * dy1;
-        const float alpha0 = fminf(0.99f, co0.w * gs_exp(power0));
-        const float alpha1 = fminf(0.99f, co1.w * gs_exp(power1));
-        const float4 rgb0 = s_rgb[j0], rgb1 = s_rgb[j1];
-        // branch-free compositing of the pair, in order (selects instead of divergent ifs)
-        bool c0 = !done && power0 <= 0.0f && alpha0 >= 1.0f / 255.0f;
-        const float tT0 = T * (1.0f - alpha0);
-        const bool s0 = c0 && tT0 < 0.0001f;  // T would drop below 1e-4: stop before entry 0
-        done = done || s0;
-        c0 = c0 && !s0;
-        C0 = c0 ? C0 + rgb0.x * alpha0 * T : C0;
-        C1 = c0 ? C1 + rgb0.y * alpha0 * T : C1;
-        C2 = c0 ? C2 + rgb0.z * alpha0 * T : C2;
-        T = c0 ? tT0 : T;
-        last = c0 ? base + j0 + 1 : last;
-        bool c1 = has1 && !done && power1 <= 0.0f && alpha1 >= 1.0f / 255.0f;
-        const float tT1 = T * (1.0f - alpha1);
-        const bool s1 = c1 && tT1 < 0.0001f;
-        done = done || s1;
-        c1 = c1 && !s1;
-        C0 = c1 ? C0 + rgb1.x * alpha1 * T : C0;
-        C1 = c1 ? C1 + rgb1.y * alpha1 * T : C1;
-        C2 = c1 ? C2 + rgb1.z * alpha1 * T : C2;
-        T = c1 ? tT1 : T;
-        last = c1 ? base + j1 + 1 : last;
-        if (__ballot(!done) == 0) {
-          qq = 4;
-          break;
-        }
-      }
+    // dense, in-order list of this quadrant's entries, built by the wave itself (the per-entry
+    // walk then costs a uniform LDS read instead of a scalar bit-scan sequence)
+    uint32_t qcnt = 0;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const uint64_t m = uniform_u64(s_mask[g][wid]);
+      if ((m >> lane) & 1ull)
+        s_qlist[wid][qcnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+            (uint16_t)(g * 64 + lane);
+      qcnt += (uint32_t)__popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // two entries per trip: their power / exp / alpha chains are independent (ILP); the
+    // compositing of the pair is then applied in order, exactly as one entry at a time
+    for (uint32_t k = 0; k < qcnt; k += 2) {
+      const bool has1 = k + 1 < qcnt;
+      const uint32_t j0 = s_qlist[wid][k];
+      const uint32_t j1 = has1 ? (uint32_t)s_qlist[wid][k + 1] : j0;
+      const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
+      const float4 co0 = s_co[j0], co1 = s_co[j1];
+      const float dx0 = xy0.x - pfx, dy0 = xy0.y - pfy;
+      const float dx1 = xy1.x - pfx, dy1 = xy1.y - pfy;
+      const float power0 = -0.5f * (co0.x * dx0 * dx0 + co0.z * dy0 * dy0) - co0.y * dx0 * dy0;
+      const float power1 = -0.5f * (co1.x * dx1 * dx1 + co1.z * dy1 * dy1) - co1.y * dx1 * dy1;
+      const float alpha0 = fminf(0.99f, co0.w * gs_exp(power0));
+      const float alpha1 = fminf(0.99f, co1.w * gs_exp(power1));
+      const float4 rgb0 = s_rgb[j0], rgb1 = s_rgb[j1];
+      // branch-free compositing of the pair, in order (selects instead of divergent ifs)
+      bool c0 = !done && power0 <= 0.0f && alpha0 >= 1.0f / 255.0f;
+      const float tT0 = T * (1.0f - alpha0);
+      const bool s0 = c0 && tT0 < 0.0001f;  // T would drop below 1e-4: stop before entry 0
+      done = done || s0;
+      c0 = c0 && !s0;
+      C0 = c0 ? C0 + rgb0.x * alpha0 * T : C0;
+      C1 = c0 ? C1 + rgb0.y * alpha0 * T : C1;
+      C2 = c0 ? C2 + rgb0.z * alpha0 * T : C2;
+      T = c0 ? tT0 : T;
+      last = c0 ? base + j0 + 1 : last;
+      bool c1 = has1 && !done && power1 <= 0.0f && alpha1 >= 1.0f / 255.0f;
+      const float tT1 = T * (1.0f - alpha1);
+      const bool s1 = c1 && tT1 < 0.0001f;
+      done = done || s1;
+      c1 = c1 && !s1;
+      C0 = c1 ? C0 + rgb1.x * alpha1 * T : C0;
+      C1 = c1 ? C1 + rgb1.y * alpha1 * T : C1;
+      C2 = c1 ? C2 + rgb1.z * alpha1 * T : C2;
+      T = c1 ? tT1 : T;
+      last = c1 ? base + j1 + 1 : last;
+      if (__ballot(!done) == 0) break;
     }
   }
   if (inside) {
