@@ -33,9 +33,8 @@ __device__ __forceinline__ Eval eval_pair(float2 xy, float4 co, float pfx, f2 pf
   v.co = co;
   v.dx = xy.x - pfx;
   v.dy = xy.y - pfy;
-  const float t1 = co.x * v.dx * v.dx;
-  const f2 power = -0.5f * (t1 + co.z * v.dy * v.dy) - (co.y * v.dx) * v.dy;
-  v.G = gs_exp_pk(power);
+  const f2 power = falloff_log2_pk(co, v.dx, v.dy);  // log2(e) * power (co: fall_coefs)
+  v.G = gs_exp2_pk(power);
   const f2 oG = co.w * v.G;
   v.alpha.x = fminf(0.99f, oG.x);
   v.alpha.y = fminf(0.99f, oG.y);
@@ -70,7 +69,8 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
                                                             const float* __restrict__ dL_dpix,
                                                             float* __restrict__ gradrec) {
   __shared__ float2 s_xy[BWD_BATCH];
-  __shared__ float4 s_co[BWD_BATCH];
+  __shared__ float4 s_co[BWD_BATCH];  // falloff coefficients + opacity (fall_coefs)
+  __shared__ float4 s_cr[BWD_BATCH];  // raw conic (xx, xy, yy) for the record mapping
   __shared__ float4 s_rgb[BWD_BATCH];
   __shared__ uint32_t s_slot[BWD_BATCH];
   __shared__ uint64_t s_mask[BWD_GROUPS][2];  // [64-entry group][half]
@@ -184,7 +184,8 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         const uint32_t gid = presort_gid[slot];
         const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
         s_xy[t] = make_float2(a.x, a.y);
-        s_co[t] = make_float4(a.z, a.w, b.x, b.y);
+        s_co[t] = fall_coefs(a.z, a.w, b.x, b.y);
+        s_cr[t] = make_float4(a.z, a.w, b.x, 0.0f);
         s_rgb[t] = make_float4(b.z, b.w, d.x, 0.0f);
         s_slot[t] = slot;
         hm = half_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         for (int k = 0; k < 8; k++) S[k] = s_acc[0][t][k] + s_acc[1][t][k];
         S[8] = ((s_acc[0][t][8] + s_acc[0][t][9]) + (s_acc[0][t][10] + s_acc[0][t][11])) +
                ((s_acc[1][t][8] + s_acc[1][t][9]) + (s_acc[1][t][10] + s_acc[1][t][11]));
-        const float4 co = s_co[t];
+        const float4 co = s_cr[t];
         float* r = gradrec + (size_t)s_slot[t] * GRAD_REC;
         r[0] = S[0];
         r[1] = S[1];

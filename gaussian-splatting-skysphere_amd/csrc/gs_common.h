@@ -45,9 +45,8 @@ constexpr float SH_C30 = -0.5900435899266435f, SH_C31 = 2.890611442640554f, SH_C
 // The hardware v_exp_f32 is not used: it is not correctly rounded (measured: 2.2 % of the floats
 // in [-126, 0] differ by 1 ulp from round(2^x); tools/probes/exp2_probe.hip), so no CPU
 // restatement could reproduce the threshold decisions that depend on it.
-__device__ __forceinline__ float gs_exp(float x) {
-  x = fminf(fmaxf(x, -80.0f), 0.0f);
-  const float t = x * 1.44269504088896341f;
+__device__ __forceinline__ float gs_exp2(float t) {
+  t = fminf(fmaxf(t, -125.0f), 0.0f);
   const float n = __builtin_rintf(t);
   const float f = t - n;
   float p = 1.5345810970757157e-4f;
@@ -59,15 +58,15 @@ __device__ __forceinline__ float gs_exp(float x) {
   p = __builtin_fmaf(p, f, 1.0f);
   return __builtin_ldexpf(p, (int)n);
 }
+__device__ __forceinline__ float gs_exp(float x) { return gs_exp2(x * 1.44269504088896341f); }
 
-// Packed (two-pixel) form of gs_exp: identical op sequence per element, so each element is
-// bit-identical to gs_exp; mul/fma/add issue as v_pk_*_f32.
+// Packed (two-pixel) form of gs_exp2: identical op sequence per element, so each element is
+// bit-identical to gs_exp2; mul/fma/add issue as v_pk_*_f32.
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 gs_exp_pk(f2 x) {
-  x.x = fminf(fmaxf(x.x, -80.0f), 0.0f);
-  x.y = fminf(fmaxf(x.y, -80.0f), 0.0f);
-  const f2 t = x * 1.44269504088896341f;
+__device__ __forceinline__ f2 gs_exp2_pk(f2 t) {
+  t.x = fminf(fmaxf(t.x, -125.0f), 0.0f);
+  t.y = fminf(fmaxf(t.y, -125.0f), 0.0f);
   f2 n;
   n.x = __builtin_rintf(t.x);
   n.y = __builtin_rintf(t.y);
@@ -83,6 +82,29 @@ __device__ __forceinline__ f2 gs_exp_pk(f2 x) {
   r.x = __builtin_ldexpf(p.x, (int)n.x);
   r.y = __builtin_ldexpf(p.y, (int)n.y);
   return r;
+}
+
+// log2(e) * power of a splat at pixel offset (dx, dy) = mean - pixel.  The conic is scaled once
+// per staged splat (fall_coefs): A = cxx (-log2e / 2), B = cxy (-log2e), C = cyy (-log2e / 2), and
+// t = dx (A dx + B dy) + C dy^2 takes two FMAs + three multiplies per pixel.  Bit-identical to
+// oracle/gs_oracle.c:falloff_log2.
+constexpr float K_HALF_LOG2E = -0.72134752044448170f, K_LOG2E = -1.44269504088896341f;
+__device__ __forceinline__ float4 fall_coefs(float cxx, float cxy, float cyy, float opacity) {
+  return make_float4(cxx * K_HALF_LOG2E, cxy * K_LOG2E, cyy * K_HALF_LOG2E, opacity);
+}
+__device__ __forceinline__ float falloff_log2(float4 k, float dx, float dy) {
+  const float u = k.y * dy;
+  const float t = __builtin_fmaf(k.x, dx, u);
+  const float v = k.z * dy;
+  const float w = v * dy;
+  return __builtin_fmaf(dx, t, w);
+}
+__device__ __forceinline__ f2 falloff_log2_pk(float4 k, float dx, f2 dy) {
+  const f2 u = k.y * dy;
+  const f2 t = pk_fma((f2)(k.x), (f2)(dx), u);
+  const f2 v = k.z * dy;
+  const f2 w = v * dy;
+  return pk_fma((f2)(dx), t, w);
 }
 
 // m = 4x4 world_view_transform / full_proj_transform, row-major flattening of the torch tensor

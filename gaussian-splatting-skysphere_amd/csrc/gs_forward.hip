@@ -464,7 +464,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
       const uint32_t gid = presort_gid[point_list[range.x + base + tid]];
       const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
       s_xy[tid] = make_float2(a.x, a.y);
-      s_co[tid] = make_float4(a.z, a.w, b.x, b.y);
+      s_co[tid] = fall_coefs(a.z, a.w, b.x, b.y);
       s_rgb[tid] = make_float4(b.z, b.w, d.x, 0.0f);
       qmask = quadrant_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
     }
@@ -493,10 +493,10 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
       const float4 co0 = s_co[j0], co1 = s_co[j1];
       const float dx0 = xy0.x - pfx, dy0 = xy0.y - pfy;
       const float dx1 = xy1.x - pfx, dy1 = xy1.y - pfy;
-      const float power0 = -0.5f * (co0.x * dx0 * dx0 + co0.z * dy0 * dy0) - co0.y * dx0 * dy0;
-      const float power1 = -0.5f * (co1.x * dx1 * dx1 + co1.z * dy1 * dy1) - co1.y * dx1 * dy1;
-      const float alpha0 = fminf(0.99f, co0.w * gs_exp(power0));
-      const float alpha1 = fminf(0.99f, co1.w * gs_exp(power1));
+      const float power0 = falloff_log2(co0, dx0, dy0);  // log2(e) * power
+      const float power1 = falloff_log2(co1, dx1, dy1);
+      const float alpha0 = fminf(0.99f, co0.w * gs_exp2(power0));
+      const float alpha1 = fminf(0.99f, co1.w * gs_exp2(power1));
       const float4 rgb0 = s_rgb[j0], rgb1 = s_rgb[j1];
       // branch-free compositing of the pair, in order (selects instead of divergent ifs)
       bool c0 = !done && power0 <= 0.0f && alpha0 >= 1.0f / 255.0f;

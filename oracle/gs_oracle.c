@@ -24,9 +24,10 @@
  * Numerics contract (shared with the HIP kernels):
  *   - fp32 everywhere, IEEE round-to-nearest, NO contraction (build with -ffp-contract=off);
  *     every FMA is an explicit fmaf().  ndc->pixel is evaluated in double as upstream.
- *   - exp() of the Gaussian falloff is gs_exp(): exp2 of a rounded x log2(e), degree-6
- *     polynomial + ldexp, built only from correctly-rounded IEEE ops, so CPU and GPU agree
- *     bit-for-bit on every threshold decision (alpha < 1/255, T < 1e-4).
+ *   - the Gaussian falloff is 2^t with t = log2(e) * power from a conic pre-scaled by log2(e)
+ *     (falloff_log2, two FMAs) and exp2 by a degree-6 polynomial + ldexp (oracle_exp2), built
+ *     only from correctly-rounded IEEE ops, so CPU and GPU agree bit-for-bit on every threshold
+ *     decision (alpha < 1/255, T < 1e-4).
  *   - Operation order for every expression is fixed (left-to-right as written here).
  *   - Gradient sums over pixels / tiles are accumulated in double here (order-independent
  *     reference); the GPU sums in fp32 in its own order -> tolerance documented in tests.
@@ -55,15 +56,12 @@ static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 static inline float f_as(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 static inline uint32_t u_as(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 
-/* exp(x) for the splat falloff; x <= 0 in practice.  x is clamped to [-80, 0] (below -80 the
- * result, <= 2e-35, only ever meets `alpha < 1/255` or a zero weight; above 0 the caller skips;
- * the clamp keeps every result a normal float).  exp(x) = 2^t, t = x log2(e) rounded to float,
- * n = rint(t), 2^(t - n) by a degree-6 minimax polynomial on [-0.5, 0.5], scaled by ldexp.
- * Relative error <= 5.1e-7 on [-8, 0] (the rounding of t dominates).  Identical op sequence in
- * csrc/gs_common.h:gs_exp. */
-float oracle_exp(float x) {
-    x = fminf(fmaxf(x, -80.0f), 0.0f);
-    float t = x * 1.44269504088896341f;
+/* 2^t for the splat falloff, t <= 0 in practice: t is clamped to [-125, 0] (below, the result
+ * <= 2.4e-38 only ever meets `alpha < 1/255` or a zero weight; above 0 the caller skips; the clamp
+ * keeps every result a normal float); n = rint(t), 2^(t - n) by a degree-6 minimax polynomial on
+ * [-0.5, 0.5], scaled by ldexp.  Identical op sequence in csrc/gs_common.h:gs_exp2. */
+float oracle_exp2(float t) {
+    t = fminf(fmaxf(t, -125.0f), 0.0f);
     float n = rintf(t);
     float f = t - n;
     float p = 1.5345810970757157e-4f;
@@ -74,6 +72,24 @@ float oracle_exp(float x) {
     p = fmaf(p, f, 6.931471824645996e-1f);
     p = fmaf(p, f, 1.0f);
     return ldexpf(p, (int)n);
+}
+
+/* exp(x) = 2^(x log2 e), t rounded to float: relative error <= 5.1e-7 on [-8, 0] */
+float oracle_exp(float x) { return oracle_exp2(x * 1.44269504088896341f); }
+
+/* log2(e) * power of a splat at pixel offset (dx, dy) = mean - pixel, with the conic scaled once
+ * per splat: A = cxx (-log2e / 2), B = cxy (-log2e), C = cyy (-log2e / 2);
+ * t = dx (A dx + B dy) + C dy^2 as two FMAs.  Identical op sequence in the HIP render kernels
+ * (csrc/gs_common.h:falloff_log2). */
+#define K_HALF_LOG2E (-0.72134752044448170f)
+#define K_LOG2E (-1.44269504088896341f)
+static inline float falloff_log2(const float* conic, float dx, float dy) {
+    float A = conic[0] * K_HALF_LOG2E, B = conic[1] * K_LOG2E, C = conic[2] * K_HALF_LOG2E;
+    float u = B * dy;
+    float t = fmaf(A, dx, u);
+    float v = C * dy;
+    float w = v * dy;
+    return fmaf(dx, t, w);
 }
 
 /* world point -> view (transformPoint4x3).  m is the 4x4 `world_view_transform`
@@ -588,9 +604,9 @@ static void render_fwd(const Scene* s, const Binned* b, float* out, float* final
                         contributor++;
                         const Splat* o = &b->sp[b->inst[k].gid];
                         float dx = o->xy[0] - pfx, dy = o->xy[1] - pfy;
-                        float power = -0.5f * (o->conic[0] * dx * dx + o->conic[2] * dy * dy) - o->conic[1] * dx * dy;
-                        if (power > 0.0f) continue;
-                        float alpha = fminf(0.99f, o->opacity * oracle_exp(power));
+                        float power2 = falloff_log2(o->conic, dx, dy);
+                        if (power2 > 0.0f) continue;
+                        float alpha = fminf(0.99f, o->opacity * oracle_exp2(power2));
                         if (alpha < 1.0f / 255.0f) continue;
                         float test_T = T * (1.0f - alpha);
                         if (test_T < 0.0001f) break;
@@ -718,9 +734,9 @@ long long oracle_backward(int P, int D, int M, const float* bg, int W, int H, co
                         uint32_t gid = b.inst[k].gid;
                         const Splat* o = &b.sp[gid];
                         float dx = o->xy[0] - pfx, dy = o->xy[1] - pfy;
-                        float power = -0.5f * (o->conic[0] * dx * dx + o->conic[2] * dy * dy) - o->conic[1] * dx * dy;
-                        if (power > 0.0f) continue;
-                        float G = oracle_exp(power);
+                        float power2 = falloff_log2(o->conic, dx, dy);
+                        if (power2 > 0.0f) continue;
+                        float G = oracle_exp2(power2);
                         float alpha = fminf(0.99f, o->opacity * G);
                         if (alpha < 1.0f / 255.0f) continue;
                         /* T recovered with one correctly rounded reciprocal, reused for the background
