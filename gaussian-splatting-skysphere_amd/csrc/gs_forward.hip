@@ -431,6 +431,10 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
 // ------------------------------------------------------------------------------------------
 // render forward
 // ------------------------------------------------------------------------------------------
+#ifndef GS_FWD_ILP
+#define GS_FWD_ILP 3
+#endif
+constexpr int FWD_ILP = GS_FWD_ILP;
 __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                          const uint32_t* __restrict__ point_list,
                                                          const uint32_t* __restrict__ presort_gid,
@@ -483,42 +487,34 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
       qcnt += (uint32_t)__popcll(m);
     }
     __builtin_amdgcn_wave_barrier();
-    // two entries per trip: their power / exp / alpha chains are independent (ILP); the
-    // compositing of the pair is then applied in order, exactly as one entry at a time
-    for (uint32_t k = 0; k < qcnt; k += 2) {
-      const bool has1 = k + 1 < qcnt;
-      const uint32_t j0 = s_qlist[wid][k];
-      const uint32_t j1 = has1 ? (uint32_t)s_qlist[wid][k + 1] : j0;
-      const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
-      const float4 co0 = s_co[j0], co1 = s_co[j1];
-      const float dx0 = xy0.x - pfx, dy0 = xy0.y - pfy;
-      const float dx1 = xy1.x - pfx, dy1 = xy1.y - pfy;
-      const float power0 = falloff_log2(co0, dx0, dy0);  // log2(e) * power
-      const float power1 = falloff_log2(co1, dx1, dy1);
-      const float alpha0 = fminf(0.99f, co0.w * gs_exp2(power0));
-      const float alpha1 = fminf(0.99f, co1.w * gs_exp2(power1));
-      const float4 rgb0 = s_rgb[j0], rgb1 = s_rgb[j1];
-      // branch-free compositing of the pair, in order (selects instead of divergent ifs)
-      bool c0 = !done && power0 <= 0.0f && alpha0 >= 1.0f / 255.0f;
-      const float tT0 = T * (1.0f - alpha0);
-      const bool s0 = c0 && tT0 < 0.0001f;  // T would drop below 1e-4: stop before entry 0
-      done = done || s0;
-      c0 = c0 && !s0;
-      C0 = c0 ? C0 + rgb0.x * alpha0 * T : C0;
-      C1 = c0 ? C1 + rgb0.y * alpha0 * T : C1;
-      C2 = c0 ? C2 + rgb0.z * alpha0 * T : C2;
-      T = c0 ? tT0 : T;
-      last = c0 ? base + j0 + 1 : last;
-      bool c1 = has1 && !done && power1 <= 0.0f && alpha1 >= 1.0f / 255.0f;
-      const float tT1 = T * (1.0f - alpha1);
-      const bool s1 = c1 && tT1 < 0.0001f;
-      done = done || s1;
-      c1 = c1 && !s1;
-      C0 = c1 ? C0 + rgb1.x * alpha1 * T : C0;
-      C1 = c1 ? C1 + rgb1.y * alpha1 * T : C1;
-      C2 = c1 ? C2 + rgb1.z * alpha1 * T : C2;
-      T = c1 ? tT1 : T;
-      last = c1 ? base + j1 + 1 : last;
+    // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
+    // compositing is then applied entry by entry in list order, exactly as one at a time
+    for (uint32_t k = 0; k < qcnt; k += FWD_ILP) {
+      uint32_t j[FWD_ILP];
+      float pw[FWD_ILP], al[FWD_ILP];
+#pragma unroll
+      for (int u = 0; u < FWD_ILP; u++) {
+        j[u] = (k + u < qcnt) ? (uint32_t)s_qlist[wid][k + u] : (uint32_t)s_qlist[wid][k];
+        const float2 xy = s_xy[j[u]];
+        const float4 co = s_co[j[u]];
+        pw[u] = falloff_log2(co, xy.x - pfx, xy.y - pfy);  // log2(e) * power
+        al[u] = fminf(0.99f, co.w * gs_exp2(pw[u]));
+      }
+#pragma unroll
+      for (int u = 0; u < FWD_ILP; u++) {
+        const float4 rgb = s_rgb[j[u]];
+        // branch-free compositing (selects instead of divergent ifs)
+        bool cu = k + u < qcnt && !done && pw[u] <= 0.0f && al[u] >= 1.0f / 255.0f;
+        const float tT = T * (1.0f - al[u]);
+        const bool su = cu && tT < 0.0001f;  // T would drop below 1e-4: stop before this entry
+        done = done || su;
+        cu = cu && !su;
+        C0 = cu ? C0 + rgb.x * al[u] * T : C0;
+        C1 = cu ? C1 + rgb.y * al[u] * T : C1;
+        C2 = cu ? C2 + rgb.z * al[u] * T : C2;
+        T = cu ? tT : T;
+        last = cu ? base + j[u] + 1 : last;
+      }
       if (__ballot(!done) == 0) break;
     }
   }
