@@ -47,6 +47,9 @@ constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x
 #ifndef GS_BWD_BATCH
 #define GS_BWD_BATCH 64
 #endif
+#ifndef GS_BWD_ILP
+#define GS_BWD_ILP 1
+#endif
 #ifndef GS_BWD_MINW
 #define GS_BWD_MINW 1
 #endif
@@ -206,14 +209,32 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
 #pragma unroll 1
     for (int g = 0; g < BWD_GROUPS; g++) {
       uint64_t m = uniform_u64(s_mask[g][wid]);
+      // entries no pixel of this wave reaches (e >= wave_last) sit at the low bits: drop them
+      const int jmin = (int)n_eff - (int)wave_last - (int)base - g * 64;  // j - 64 g >= jmin
+      if (jmin > 0) m &= jmin >= 64 ? 0ull : ~((1ull << jmin) - 1ull);
+#if GS_BWD_ILP == 2
+      // two entries per trip: the two evaluations are independent (ILP); the commits stay in order
+      while (m) {
+        const uint32_t j0 = (uint32_t)(g * 64 + __builtin_ctzll(m));
+        m &= m - 1;
+        const bool has1 = m != 0;
+        const uint32_t j1 = has1 ? (uint32_t)(g * 64 + __builtin_ctzll(m)) : j0;
+        if (has1) m &= m - 1;
+        const Eval v0 = eval_pair(s_xy[j0], s_co[j0], pfx, pfy, n_eff - 1 - (base + j0), lastA, lastB);
+        Eval v1 = eval_pair(s_xy[j1], s_co[j1], pfx, pfy, n_eff - 1 - (base + j1), lastA, lastB);
+        v1.cA = v1.cA && has1;
+        v1.cB = v1.cB && has1;
+        if (__ballot(v0.cA || v0.cB) != 0) apply(j0, v0);
+        if (__ballot(v1.cA || v1.cB) != 0) apply(j1, v1);
+      }
+#else
       while (m) {
         const uint32_t j = (uint32_t)(g * 64 + __builtin_ctzll(m));
         m &= m - 1;
-        const uint32_t e = n_eff - 1 - (base + j);
-        if (e >= wave_last) continue;  // no pixel of this wave reaches entry e
-        const Eval v = eval_pair(s_xy[j], s_co[j], pfx, pfy, e, lastA, lastB);
+        const Eval v = eval_pair(s_xy[j], s_co[j], pfx, pfy, n_eff - 1 - (base + j), lastA, lastB);
         if (__ballot(v.cA || v.cB) != 0) apply(j, v);
       }
+#endif
     }
     __syncthreads();
 #pragma unroll
