@@ -293,7 +293,9 @@ __device__ __forceinline__ void seg_scan_step(float* v, uint32_t own1) {
 
 __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_t* __restrict__ counters,
                                                                    const uint32_t* __restrict__ offsets,
-                                                                   float* __restrict__ gradrec) {
+                                                                   const uint32_t* __restrict__ sorted_gid,
+                                                                   const float* __restrict__ gradrec,
+                                                                   float* __restrict__ gsum) {
   __shared__ double s_acc[SUMREC_WAVES][64][GRAD_REC];
   __shared__ unsigned long long s_mark[SUMREC_WAVES];
   const uint32_t V = counters[0], I = counters[1];
@@ -340,8 +342,9 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
     __builtin_amdgcn_wave_barrier();
   }
   if (lane < nr) {
+    const size_t gid = sorted_gid[r0 + lane];
 #pragma unroll
-    for (int c = 0; c < GRAD_REC; c++) gradrec[(size_t)my_off * GRAD_REC + c] = (float)s_acc[wid][lane][c];
+    for (int c = 0; c < GRAD_REC; c++) gsum[gid * GRAD_REC + c] = (float)s_acc[wid][lane][c];
   }
 }
 
@@ -475,7 +478,7 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
                                                    const uint32_t* __restrict__ tiles,
                                                    const uint32_t* __restrict__ goff,
                                                    const uint8_t* __restrict__ clamped,
-                                                   const float* __restrict__ gradrec, const GradOut& out,
+                                                   const float* __restrict__ gsum, const GradOut& out,
                                                    float* row) {
   const uint32_t cnt = tiles[i];
   if (cnt == 0) {
@@ -502,8 +505,8 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
       for (int k = 0; k < 4; k++) out.drot[4 * i + k] = 0.f;
     return;
   }
-  // the Gaussian's per-tile records were summed into its first record by k_sum_records
-  const float* rec = gradrec + (size_t)goff[i] * GRAD_REC;
+  // the Gaussian's per-tile records, summed by k_sum_records (index order: coalesced here)
+  const float* rec = gsum + (size_t)i * GRAD_REC;
   float a[GRAD_REC];
 #pragma unroll
   for (int k = 0; k < GRAD_REC; k++) a[k] = rec[k];
@@ -619,7 +622,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
                                                         const uint32_t* __restrict__ tiles,
                                                         const uint32_t* __restrict__ goff,
                                                         const uint8_t* __restrict__ clamped,
-                                                        const float* __restrict__ gradrec, GradOut out) {
+                                                        const float* __restrict__ gsum, GradOut out) {
   extern __shared__ float s_sh[];  // DEG >= 0: [256][3M + 1] SH rows, then dL/dsh rows
   const int i0 = blockIdx.x * 256, i = i0 + (int)threadIdx.x;
   const int nG = min(256, g.P - i0);
@@ -629,7 +632,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
     rows_to_lds(g.shs + (size_t)i0 * rowf, s_sh, nG, rowf, stride);
     __syncthreads();
   }
-  if (i < g.P) preprocess_bwd_one<DEG>(i, g, c, tiles, goff, clamped, gradrec, out, row);
+  if (i < g.P) preprocess_bwd_one<DEG>(i, g, c, tiles, goff, clamped, gsum, out, row);
   if (DEG >= 0) {
     __syncthreads();
     lds_to_rows(s_sh, out.dsh + (size_t)i0 * rowf, nG, rowf, stride);
@@ -641,31 +644,31 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
   if (g.P <= 0) return;
   if (have_records)
     GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
-              dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, gradrec);
+              dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, gradrec, geo.gsum);
   dim3 grid((g.P + 255) / 256), block(256);
   const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
   const size_t lds = sh ? (size_t)256 * (3 * g.M + 1) * sizeof(float) : 0;
   if (!sh) {
     GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<-1>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
-              gradrec, out);
+              geo.gsum, out);
     return;
   }
   switch (g.D) {
     case 0:
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<0>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
-                gradrec, out);
+                geo.gsum, out);
       break;
     case 1:
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<1>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
-                gradrec, out);
+                geo.gsum, out);
       break;
     case 2:
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<2>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
-                gradrec, out);
+                geo.gsum, out);
       break;
     default:
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<3>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
-                gradrec, out);
+                geo.gsum, out);
       break;
   }
 }

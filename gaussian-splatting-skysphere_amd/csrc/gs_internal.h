@@ -63,6 +63,7 @@ struct GeomPtrs {
   uint32_t *keys_a, *vals_a, *keys_b, *vals_b;
   uint32_t* offsets;  // per depth rank
   uint32_t* dup_first;  // [P + 1] depth rank owning the first instance slot of each duplicate block
+  float* gsum;  // [P][9] per-Gaussian sums of the backward records (k_sum_records -> k_preprocess_bwd)
   uint32_t* scan_partial;
   uint32_t* sort_scratch;
   uint32_t* counters;  // [0] visible V, [1] instances I, [2] error flags
@@ -83,6 +84,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   size_t o_ka = take(Pn * 4), o_va = take(Pn * 4), o_kb = take(Pn * 4), o_vb = take(Pn * 4);
   size_t o_offs = take(Pn * 4);
   size_t o_df = take((Pn + 1) * 4);
+  size_t o_gs = take(Pn * 4 * GRAD_REC);
   size_t o_sp = take((size_t)scan_plan(Pn).nb * 4 + 64);
   size_t o_ss = take(sort_scratch_words(Pn) * 4);
   size_t o_cnt = take(64);
@@ -99,6 +101,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
     out->vals_b = (uint32_t*)(base + o_vb);
     out->offsets = (uint32_t*)(base + o_offs);
     out->dup_first = (uint32_t*)(base + o_df);
+    out->gsum = (float*)(base + o_gs);
     out->scan_partial = (uint32_t*)(base + o_sp);
     out->sort_scratch = (uint32_t*)(base + o_ss);
     out->counters = (uint32_t*)(base + o_cnt);
