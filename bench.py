@@ -5,11 +5,13 @@ step = the 8 views sharded over the ranks + one all-reduce: strong scaling), c5 
 footprint in "hbm").
 
 Workload (N=1): BASELINE.json configs[2] "C3" -- 1M Gaussians, SH degree 3, 1920x1080, 16x16
-tiles, one view per step (synthetic scene per SURVEY.md §8d: frustum-uniform means, seed 0).
-One step = GaussianRasterizer forward + backward for one view (dL/dimage fixed, seed 1) through
-the drop-in package, i.e. exactly what train.py:86-93 runs on the rasterizer.  With --gpus N>1
-(torchrun, one rank per GPU, RCCL) every rank renders one view per step and the 59-float/Gaussian
-gradient bucket is all-reduced (view-parallel data parallelism, weak scaling).
+tiles (synthetic scene per SURVEY.md §8d: frustum-uniform means, seed 0).  One iteration = one
+view's GaussianRasterizer forward + backward (dL/dimage fixed, seed 1) through the drop-in
+package, i.e. exactly what train.py:86-93 runs on the rasterizer; `value` counts iterations
+(views) per second over the whole job.  A step = --views-per-rank views per rank (default 1 on
+one GPU, 4 with N > 1; gradients accumulated) followed, with --gpus N>1 (torchrun, one rank per
+GPU, RCCL), by one all-reduce of the 59-float/Gaussian gradient bucket (view-parallel data
+parallelism, weak scaling; DESIGN.md §7 on why the all-reduce is amortised over several views).
 
 Output: one JSON line (rank 0) with the metric, a per-kernel HIP-event breakdown, the roofline of
 the dominant kernel and the CPU oracle baseline timed on this host.
@@ -71,14 +73,25 @@ def main():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = all host cores, max 16)")
+    ap.add_argument("--views-per-rank", type=int, default=0,
+                    help="C1-C3/C5: views each rank renders (fwd+bwd, gradients accumulated) per step, "
+                         "i.e. per gradient all-reduce (DESIGN.md §7); value counts views. "
+                         "0 = 1 on one GPU, 4 with N > 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GS_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU (the
+    # driver's multi-GPU runs use RCCL, one rank per GPU)
+    backend = os.environ.get("GS_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     if world > 1:
-        vp.init_from_env("nccl")
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            vp.init_from_env("nccl")
+        else:
+            torch.cuda.set_device(dev)
+            dist.init_process_group(backend)
     wl = WORKLOADS[args.workload]
     P, deg, W, H = wl["P"], wl["deg"], wl["W"], wl["H"]
     n_views = wl.get("views", 0)
@@ -89,7 +102,8 @@ def main():
         cam = cams[my_views[0]]
     else:
         cam = gs_scenes.identity_camera(W, H)
-        cams, my_views = [cam], [0]
+        k_views = args.views_per_rank or (4 if world > 1 else 1)
+        cams, my_views = [cam], [0] * k_views
         sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=0)
     settings = gs_scenes.raster_settings_for(cam, deg, device=dev)
     d = sc.to(dev)
@@ -166,8 +180,10 @@ def main():
         t_render = (time.perf_counter() - tr) / nr
 
     ms_per_step = 1e3 * elapsed / args.steps
-    # whole-job steps/s: weak scaling (C1-C3, C5) counts every rank's view; a C4 step is the 8-view batch
-    value = (1 if n_views else world) * args.steps / elapsed
+    # whole-job views (= reference train iterations) per second: weak scaling (C1-C3, C5) counts
+    # every rank's views; a C4 step is the 8-view batch
+    views_per_step = n_views or world * len(my_views)
+    value = views_per_step * args.steps / elapsed
 
     # per-kernel breakdown + roofline of the dominant kernel
     kernels = {}
@@ -225,7 +241,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic (seeded; SURVEY.md §8d distribution)",
         "config": {"workload": wl["desc"], "gaussians": P, "sh_degree": deg, "width": W, "height": H,
-                   "views_per_rank_per_step": len(my_views), "views_per_step": n_views or world,
+                   "views_per_rank_per_step": len(my_views), "views_per_step": views_per_step,
                    "parallelism": f"view-parallel dp{world}" +
                    (" + RCCL all-reduce of 59 f32/Gaussian" if world > 1 else "")},
         "render_mpix_s": round(W * H / t_render / 1e6, 1),
@@ -239,7 +255,8 @@ def main():
                 "image_buffer_GB": round(lib.gs_image_buffer_bytes(W, H) / 1e9, 3),
                 "grad_scratch_GB": round(lib.gs_grad_buffer_bytes(int(num_rendered)) / 1e9, 3)},
         "roofline": roofline,
-        "step_algo_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+        "ms_per_view": round(ms_per_step / len(my_views), 4),
+        "step_algo_GBs": round(step_bytes / (ms_per_step / len(my_views) * 1e-3) / 1e9, 1),
         "kernels": kernels,
         "cpu_baseline": cpu,
     }
