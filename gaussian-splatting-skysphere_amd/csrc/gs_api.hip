@@ -342,6 +342,27 @@ int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, voi
   return t_failed ? 1 : 0;
 }
 
+/* ---- fused SSIM (utils/loss_utils.py:ssim) ---- */
+size_t gs_ssim_partial_count(int planes, int H, int W) { return ssim_partial_count(planes, H, W); }
+
+int gs_ssim_forward(int planes, int H, int W, const float* window11_host, const float* img1, const float* img2,
+                    float* dmaps, float* partial, float* plane_sum, void* stream) {
+  clear_error(0);
+  if (planes <= 0 || H <= 0 || W <= 0) return set_error("ssim: empty image"), 1;
+  if (!window11_host || !img1 || !img2 || !dmaps || !partial || !plane_sum) return set_error("ssim: missing pointer"), 1;
+  ssim_forward(planes, H, W, window11_host, img1, img2, dmaps, partial, plane_sum, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
+int gs_ssim_backward(int planes, int channels, int H, int W, const float* window11_host, const float* img1,
+                     const float* img2, const float* dmaps, const float* scale, float* dimg1, void* stream) {
+  clear_error(0);
+  if (planes <= 0 || H <= 0 || W <= 0 || channels <= 0 || planes % channels) return set_error("ssim: bad shape"), 1;
+  if (!window11_host || !img1 || !img2 || !dmaps || !scale || !dimg1) return set_error("ssim: missing pointer"), 1;
+  ssim_backward(planes, channels, H, W, window11_host, img1, img2, dmaps, scale, dimg1, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
 int gs_debug_export(int P, int W, int H, long long num_rendered, const void* geom_buffer, const void* binning_buffer,
                     const void* image_buffer, uint32_t* point_list, uint32_t* ranges, float* xy, float* conic_opacity,
                     float* rgb, float* depth, uint32_t* tiles_touched, float* final_T, uint32_t* n_contrib,

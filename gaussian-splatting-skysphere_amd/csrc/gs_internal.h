@@ -201,6 +201,11 @@ struct GradOut {
 void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, float* gradrec,
                     bool have_records, const GradOut& out, hipStream_t st);
 void knn_mean_dist2(int P, const float* pts, float* out, char* scratch, hipStream_t st);
+void ssim_forward(int planes, int H, int W, const float* win11, const float* img1, const float* img2, float* dmaps,
+                  float* partial, float* plane_sum, hipStream_t st);
+void ssim_backward(int planes, int C, int H, int W, const float* win11, const float* img1, const float* img2,
+                   const float* dmaps, const float* scale, float* dimg1, hipStream_t st);
+size_t ssim_partial_count(int planes, int H, int W);
 size_t knn_scratch_bytes(int P);
 
 }  // namespace gs

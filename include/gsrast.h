@@ -16,6 +16,9 @@
  *   gs_mark_visible                            <-  _C.mark_visible(...)
  *   gs_knn_mean_dist2                          <-  simple_knn._C.distCUDA2(points)
  *                                                  (/root/reference/scene/gaussian_model.py:20,134)
+ *   gs_ssim_forward / gs_ssim_backward         <-  utils.loss_utils.ssim(img1, img2)
+ *                                                  (/root/reference/utils/loss_utils.py:33-60,
+ *                                                   called at train.py:92)
  *
  * Conventions
  *   - Every pointer argument is a DEVICE pointer (HBM of the current HIP device) unless its name
@@ -109,6 +112,18 @@ int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const 
 /* ---- simple-knn: mean squared distance to the 3 nearest other points ---- */
 size_t gs_knn_scratch_bytes(int P);
 int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, void* stream);
+
+/* ---- fused SSIM of the photometric loss  <-  utils/loss_utils.py:ssim (train.py:91-92) ----
+ * img1, img2: [planes, H, W] fp32 (planes = images x channels), window11_host: the 11 float32
+ * weights of loss_utils.gaussian(11, 1.5) (host memory).  Forward writes per-plane sums of the
+ * SSIM map to plane_sum[planes] and the three per-pixel partials to dmaps[3, planes, H, W]
+ * (kept for backward); partial has gs_ssim_partial_count(planes, H, W) floats.  Backward writes
+ * dimg1 = scale[plane / channels] * dSSIM-sum/dimg1 (scale: device, one per image). */
+size_t gs_ssim_partial_count(int planes, int H, int W);
+int gs_ssim_forward(int planes, int H, int W, const float* window11_host, const float* img1, const float* img2,
+                    float* dmaps, float* partial, float* plane_sum, void* stream);
+int gs_ssim_backward(int planes, int channels, int H, int W, const float* window11_host, const float* img1,
+                     const float* img2, const float* dmaps, const float* scale, float* dimg1, void* stream);
 
 /* ---- debug export of forward intermediates (tests) ----
  * Copies (device -> device) whichever outputs are non-NULL: point_list[num_rendered] (Gaussian ids

@@ -12,6 +12,7 @@ Reference functions exercised (all on CPU):
                                        module itself needs plyfile/simple_knn, absent here)
   - utils/graphics_utils.py:38-71      getWorld2View2, getProjectionMatrix
   - gaussian_renderer/__init__.py:73-78  convert_SHs_python colour path (+0.5, clamp_min 0)
+  - utils/loss_utils.py:17-60          l1_loss, gaussian / create_window, ssim (+ autograd grads)
 """
 import os
 import sys
@@ -113,9 +114,40 @@ def camera_vectors(gfx):
     np.savez_compressed(os.path.join(OUT, "camera_golden.npz"), **out)
 
 
+def loss_vectors():
+    import utils.loss_utils as lu  # noqa
+
+    g = torch.Generator().manual_seed(77)
+    out = {"window1d": lu.gaussian(11, 1.5).numpy()}
+    cases = {"chw": (3, 37, 45), "bchw": (2, 3, 20, 27), "tiny": (1, 7, 9)}
+    for name, shape in cases.items():
+        a = torch.rand(shape, generator=g)
+        b = (a + 0.15 * torch.randn(shape, generator=g)).clamp(0, 1)
+        a = a.requires_grad_(True)
+        s = lu.ssim(a, b)
+        s.backward()
+        out[f"{name}_img1"] = a.detach().numpy()
+        out[f"{name}_img2"] = b.numpy()
+        out[f"{name}_ssim"] = np.array(s.item(), np.float64)
+        out[f"{name}_grad"] = a.grad.numpy()
+        a2 = a.detach().clone().requires_grad_(True)
+        l1 = lu.l1_loss(a2, b)
+        l1.backward()
+        out[f"{name}_l1"] = np.array(l1.item(), np.float64)
+        out[f"{name}_l1grad"] = a2.grad.numpy()
+        if len(shape) == 4:  # size_average=False: per-image SSIM
+            a3 = a.detach().clone().requires_grad_(True)
+            s3 = lu.ssim(a3, b, size_average=False)
+            s3.sum().backward()
+            out[f"{name}_ssim_per_image"] = s3.detach().numpy()
+            out[f"{name}_grad_per_image_sum"] = a3.grad.numpy()
+    np.savez_compressed(os.path.join(OUT, "loss_golden.npz"), **out)
+
+
 if __name__ == "__main__":
     sh_utils, gu, gfx = _import_ref()
     sh_vectors(sh_utils)
     cov_vectors(gu)
     camera_vectors(gfx)
+    loss_vectors()
     print("wrote", sorted(f for f in os.listdir(OUT) if f.endswith(".npz")))
