@@ -363,6 +363,72 @@ int gs_ssim_backward(int planes, int channels, int H, int W, const float* window
   return t_failed ? 1 : 0;
 }
 
+/* ---- fused optimizer step and densification statistics (train.py:114-124) ---- */
+int gs_adam_step(int count, float* const* params_host, const float* const* grads_host, float* const* exp_avg_host,
+                 float* const* exp_avg_sq_host, const long long* numel_host, const double* lr_host,
+                 const long long* step_host, const double* weight_decay_host, double beta1, double beta2, double eps,
+                 int maximize, void* stream) {
+  clear_error(0);
+  if (count < 0) return set_error("adam: count must be >= 0"), 1;
+  if (count == 0) return 0;
+  if (!params_host || !grads_host || !exp_avg_host || !exp_avg_sq_host || !numel_host || !lr_host || !step_host)
+    return set_error("adam: missing pointer"), 1;
+  for (int k = 0; k < count; k++) {
+    if (numel_host[k] > 0 && (!params_host[k] || !grads_host[k] || !exp_avg_host[k] || !exp_avg_sq_host[k]))
+      return set_error("adam: missing tensor pointer"), 1;
+    if (step_host[k] < 1) return set_error("adam: step must be >= 1"), 1;
+  }
+  adam_step(count, params_host, grads_host, exp_avg_host, exp_avg_sq_host, numel_host, lr_host, step_host,
+            weight_decay_host, beta1, beta2, eps, maximize != 0, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
+int gs_activate_forward(int P, int sh_rest, const float* features_dc, const float* features_rest,
+                        const float* opacity_raw, const float* scaling_raw, const float* rotation_raw, float* shs,
+                        float* opacity, float* scales, float* rotations, void* stream) {
+  clear_error(0);
+  if (P < 0 || sh_rest < 0) return set_error("activate: P and sh_rest must be >= 0"), 1;
+  if (P == 0) return 0;
+  if (!features_dc || (sh_rest && !features_rest) || !opacity_raw || !scaling_raw || !rotation_raw || !shs ||
+      !opacity || !scales || !rotations)
+    return set_error("activate: missing pointer"), 1;
+  if (((uintptr_t)rotation_raw | (uintptr_t)rotations | (uintptr_t)shs) & 15)
+    return set_error("activate: rotation / shs buffers must be 16-byte aligned"), 1;
+  activate_forward(P, sh_rest, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw, shs, opacity,
+                   scales, rotations, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
+int gs_activate_backward(int P, int sh_rest, const float* dL_dshs, const float* dL_dopacity, const float* dL_dscales,
+                         const float* dL_drotations, const float* opacity, const float* scales,
+                         const float* rotation_raw, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
+                         float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw, void* stream) {
+  clear_error(0);
+  if (P < 0 || sh_rest < 0) return set_error("activate: P and sh_rest must be >= 0"), 1;
+  if (P == 0) return 0;
+  if ((dL_dshs && (!dL_dfeatures_dc || (sh_rest && !dL_dfeatures_rest))) ||
+      (dL_dopacity && (!opacity || !dL_dopacity_raw)) || (dL_dscales && (!scales || !dL_dscaling_raw)) ||
+      (dL_drotations && (!rotation_raw || !dL_drotation_raw)))
+    return set_error("activate: missing pointer"), 1;
+  if (((uintptr_t)dL_dshs | (uintptr_t)dL_drotations | (uintptr_t)rotation_raw | (uintptr_t)dL_drotation_raw) & 15)
+    return set_error("activate: rotation / shs buffers must be 16-byte aligned"), 1;
+  activate_backward(P, sh_rest, dL_dshs, dL_dopacity, dL_dscales, dL_drotations, opacity, scales, rotation_raw,
+                    dL_dfeatures_dc, dL_dfeatures_rest, dL_dopacity_raw, dL_dscaling_raw, dL_drotation_raw,
+                    (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
+int gs_densify_stats(int P, const int* radii, const float* grad2d, int grad_stride, float* max_radii2D,
+                     float* grad_accum, float* denom, void* stream) {
+  clear_error(0);
+  if (P < 0) return set_error("densify_stats: P must be >= 0"), 1;
+  if (P == 0) return 0;
+  if (grad_stride < 2) return set_error("densify_stats: grad_stride must be >= 2"), 1;
+  if (!radii || !grad2d || !max_radii2D || !grad_accum || !denom) return set_error("densify_stats: missing pointer"), 1;
+  densify_stats(P, radii, grad2d, grad_stride, max_radii2D, grad_accum, denom, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
 int gs_debug_export(int P, int W, int H, long long num_rendered, const void* geom_buffer, const void* binning_buffer,
                     const void* image_buffer, uint32_t* point_list, uint32_t* ranges, float* xy, float* conic_opacity,
                     float* rgb, float* depth, uint32_t* tiles_touched, float* final_T, uint32_t* n_contrib,

@@ -206,6 +206,18 @@ void ssim_forward(int planes, int H, int W, const float* win11, const float* img
 void ssim_backward(int planes, int C, int H, int W, const float* win11, const float* img1, const float* img2,
                    const float* dmaps, const float* scale, float* dimg1, hipStream_t st);
 size_t ssim_partial_count(int planes, int H, int W);
+constexpr int ADAM_MAX_TENSORS = 16;  // parameter tensors per Adam launch
+void adam_step(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+               float* const* exp_avg_sq, const long long* numel, const double* lr, const long long* step,
+               const double* weight_decay, double beta1, double beta2, double eps, bool maximize, hipStream_t st);
+void activate_forward(int P, int rest_w, const float* f_dc, const float* f_rest, const float* o_raw,
+                      const float* s_raw, const float* q_raw, float* shs, float* opac, float* scales, float* rots,
+                      hipStream_t st);
+void activate_backward(int P, int rest_w, const float* dshs, const float* dopac, const float* dscales,
+                       const float* drots, const float* opac, const float* scales, const float* q_raw, float* d_dc,
+                       float* d_rest, float* d_o, float* d_s, float* d_q, hipStream_t st);
+void densify_stats(int P, const int* radii, const float* grad2d, int grad_stride, float* max_radii2D,
+                   float* grad_accum, float* denom, hipStream_t st);
 size_t knn_scratch_bytes(int P);
 
 }  // namespace gs

@@ -1,0 +1,251 @@
+// gs_train.hip -- fused per-iteration training updates around the rasterizer.
+//
+//   k_adam              one launch for all parameter groups of GaussianModel's optimizer
+//                       (/root/reference/scene/gaussian_model.py:154-163: torch.optim.Adam, six
+//                       groups, eps 1e-15): m, v, p updated in one pass, 16-B accesses.  Same update
+//                       as torch's Adam (amsgrad off, no weight decay):
+//                         m = m + (1 - b1) (g - m);  v = b2 v + (1 - b2) g^2
+//                         p = p - (lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+//                       in torch's operation order (see adam_one).
+//   k_densify_stats     train.py:114-115 + gaussian_model.py:405-407 in one pass:
+//                         vis = radii > 0; max_r[vis] = max(max_r, radii)
+//                         accum[vis] += |grad2D[vis, :2]|;  denom[vis] += 1
+//   k_activate_fwd/bwd  the render() inputs of GaussianModel's properties (gaussian_model.py:95-115,
+//                       read at gaussian_renderer/__init__.py:53-80) in one launch each way:
+//                         shs = cat(f_dc, f_rest, 1)   opacity = sigmoid(o)   scales = exp(s)
+//                         rotations = q / max(|q|, 1e-12)      (F.normalize, p = 2, dim = 1)
+//                       and their adjoints.  Blocks [0, feat_blocks) move the SH rows, 4 floats per
+//                       thread (a Gaussian's 16x3 row is 12 float4); the rest do the per-Gaussian
+//                       activations.
+#include <cmath>
+
+#include "gs_internal.h"
+
+namespace gs {
+
+// One launch updates up to ADAM_MAX_TENSORS parameter tensors; a thread owns 4 consecutive
+// elements of one tensor (16-B loads/stores of p, g, m, v when aligned, scalar tail otherwise).
+struct AdamLaunch {
+  float* p[ADAM_MAX_TENSORS];
+  const float* g[ADAM_MAX_TENSORS];
+  float* m[ADAM_MAX_TENSORS];
+  float* v[ADAM_MAX_TENSORS];
+  uint64_t end[ADAM_MAX_TENSORS];  // inclusive-scan end of each tensor, in 4-element chunks
+  uint64_t n[ADAM_MAX_TENSORS];    // elements
+  float neg_step_size[ADAM_MAX_TENSORS];  // -lr / (1 - b1^t)
+  float bc2_sqrt[ADAM_MAX_TENSORS];       // sqrt(1 - b2^t)
+  float wd[ADAM_MAX_TENSORS];
+  int count, maximize;
+  float w1, w2, b2, eps;  // 1 - b1, 1 - b2, b2, eps
+};
+
+// Operation order of torch's foreach Adam on the device (torch/optim/adam.py _multi_tensor_adam,
+// ATen lerp / addcmul / addcdiv functors, compiled with FMA contraction): scalars rounded to float
+// from the Python doubles, each tensor op rounded to float.
+__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamLaunch& a, float nss,
+                                         float bc2s, float wd) {
+  if (a.maximize) g = -g;
+  if (wd != 0.0f) g = __builtin_fmaf(wd, p, g);  // grad.add(param, alpha=weight_decay)
+  m = __builtin_fmaf(a.w1, g - m, m);             // exp_avg.lerp_(grad, 1 - beta1), weight < 0.5 branch
+  v = __builtin_fmaf(a.w2 * g, g, v * a.b2);      // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+  const float denom = sqrtf(v) / bc2s + a.eps;    // (sqrt(v) / sqrt(bc2)) + eps
+  p = __builtin_fmaf(nss, m / denom, p);          // param.addcdiv_(m, denom, -lr / bc1)
+}
+
+__global__ __launch_bounds__(256) void k_adam(AdamLaunch a, uint64_t total_chunks) {
+  const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= total_chunks) return;
+  int k = 0;
+  while (k + 1 < a.count && c >= a.end[k]) k++;
+  const uint64_t i = (c - (k ? a.end[k - 1] : 0)) * 4;
+  const uint64_t n = a.n[k];
+  float *p = a.p[k] + i, *m = a.m[k] + i, *v = a.v[k] + i;
+  const float* g = a.g[k] + i;
+  const float ss = a.neg_step_size[k], ib = a.bc2_sqrt[k], wd = a.wd[k];
+  const bool vec = i + 4 <= n && (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
+  if (vec) {
+    float4 P = *reinterpret_cast<float4*>(p), G = *reinterpret_cast<const float4*>(g);
+    float4 M = *reinterpret_cast<float4*>(m), V = *reinterpret_cast<float4*>(v);
+    adam_one(P.x, G.x, M.x, V.x, a, ss, ib, wd);
+    adam_one(P.y, G.y, M.y, V.y, a, ss, ib, wd);
+    adam_one(P.z, G.z, M.z, V.z, a, ss, ib, wd);
+    adam_one(P.w, G.w, M.w, V.w, a, ss, ib, wd);
+    *reinterpret_cast<float4*>(p) = P;
+    *reinterpret_cast<float4*>(m) = M;
+    *reinterpret_cast<float4*>(v) = V;
+  } else {
+    const int cnt = (int)(n - i < 4 ? n - i : 4);
+    for (int j = 0; j < cnt; j++) adam_one(p[j], g[j], m[j], v[j], a, ss, ib, wd);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_densify_stats(int P, const int* __restrict__ radii,
+                                                       const float* __restrict__ grad2d, int gstride, float* __restrict__ max_r,
+                                                       float* __restrict__ accum, float* __restrict__ denom) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= P) return;
+  const int r = radii[i];
+  if (r <= 0) return;
+  max_r[i] = fmaxf(max_r[i], (float)r);
+  const float gx = grad2d[(size_t)gstride * i], gy = grad2d[(size_t)gstride * i + 1];
+  accum[i] += sqrtf(gx * gx + gy * gy);
+  denom[i] += 1.0f;
+}
+
+void adam_step(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+               float* const* exp_avg_sq, const long long* numel, const double* lr, const long long* step,
+               const double* weight_decay, double beta1, double beta2, double eps, bool maximize, hipStream_t st) {
+  for (int base = 0; base < count; base += ADAM_MAX_TENSORS) {
+    AdamLaunch a{};
+    uint64_t chunks = 0;
+    for (int k = base; k < count && k < base + ADAM_MAX_TENSORS; k++) {
+      if (numel[k] <= 0) continue;
+      const int j = a.count++;
+      a.p[j] = params[k];
+      a.g[j] = grads[k];
+      a.m[j] = exp_avg[k];
+      a.v[j] = exp_avg_sq[k];
+      a.n[j] = (uint64_t)numel[k];
+      chunks += (a.n[j] + 3) / 4;
+      a.end[j] = chunks;
+      // bias corrections in double on the host, as torch's Adam forms them from the Python step
+      const double t = (double)step[k];
+      const double bc1 = 1.0 - std::pow(beta1, t), bc2 = 1.0 - std::pow(beta2, t);
+      a.neg_step_size[j] = (float)(-(lr[k] / bc1));
+      a.bc2_sqrt[j] = (float)std::sqrt(bc2);
+      a.wd[j] = weight_decay ? (float)weight_decay[k] : 0.0f;
+    }
+    if (!a.count) continue;
+    a.w1 = (float)(1.0 - beta1);
+    a.w2 = (float)(1.0 - beta2);
+    a.b2 = (float)beta2;
+    a.eps = (float)eps;
+    a.maximize = maximize ? 1 : 0;
+    GS_LAUNCH("adam", k_adam, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, st, a, chunks);
+  }
+}
+
+void densify_stats(int P, const int* radii, const float* grad2d, int grad_stride, float* max_radii2D,
+                   float* grad_accum, float* denom, hipStream_t st) {
+  GS_LAUNCH("densify_stats", k_densify_stats, dim3((P + 255) / 256), dim3(256), 0, st, P, radii, grad2d,
+            grad_stride, max_radii2D, grad_accum, denom);
+}
+
+
+__global__ __launch_bounds__(256) void k_activate_fwd(int P, int feat_blocks, int rest_w,
+                                                      const float* __restrict__ f_dc, const float* __restrict__ f_rest,
+                                                      const float* __restrict__ o_raw, const float* __restrict__ s_raw,
+                                                      const float* __restrict__ q_raw, float* __restrict__ shs,
+                                                      float* __restrict__ opac, float* __restrict__ scales,
+                                                      float* __restrict__ rots) {
+  const int row = 3 + rest_w;
+  if ((int)blockIdx.x < feat_blocks) {
+    const uint64_t e = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (e >= (uint64_t)P * row) return;
+    const uint64_t gi = e / row;
+    const int k = (int)(e - gi * row);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int kk = k + j;
+      // rows of 3 + rest_w floats: a float4 may straddle two Gaussians when row % 4 != 0
+      const uint64_t g2 = kk < row ? gi : gi + 1;
+      const int k2 = kk < row ? kk : kk - row;
+      v[j] = (g2 >= (uint64_t)P) ? 0.f : (k2 < 3 ? f_dc[g2 * 3 + k2] : f_rest[g2 * rest_w + (k2 - 3)]);
+    }
+    if (row % 4 == 0) {
+      *reinterpret_cast<float4*>(shs + e) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      for (int j = 0; j < 4 && e + j < (uint64_t)P * row; j++) shs[e + j] = v[j];
+    }
+    return;
+  }
+  const int i = (blockIdx.x - feat_blocks) * 256 + threadIdx.x;
+  if (i >= P) return;
+  opac[i] = 1.0f / (1.0f + expf(-o_raw[i]));
+#pragma unroll
+  for (int j = 0; j < 3; j++) scales[3 * i + j] = expf(s_raw[3 * i + j]);
+  const float4 q = *reinterpret_cast<const float4*>(q_raw + 4 * i);
+  const float n = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
+  *reinterpret_cast<float4*>(rots + 4 * i) = make_float4(q.x / n, q.y / n, q.z / n, q.w / n);
+}
+
+// Adjoint.  opacity: dL/do = g * (1 - y) * y (y = sigmoid(o), saved); scales: dL/ds = g * exp(s)
+// (saved output); rotation: y = q / n, n = max(|q|, 1e-12):
+//   dL/dq = g / n - q * <g, q> / (n^2 |q|) * [|q| > 1e-12]  (div, clamp_min and norm adjoints)
+__global__ __launch_bounds__(256) void k_activate_bwd(int P, int feat_blocks, int rest_w,
+                                                      const float* __restrict__ dshs, const float* __restrict__ dopac,
+                                                      const float* __restrict__ dscales, const float* __restrict__ drots,
+                                                      const float* __restrict__ opac, const float* __restrict__ scales,
+                                                      const float* __restrict__ q_raw, float* __restrict__ d_dc,
+                                                      float* __restrict__ d_rest, float* __restrict__ d_o,
+                                                      float* __restrict__ d_s, float* __restrict__ d_q) {
+  const int row = 3 + rest_w;
+  if ((int)blockIdx.x < feat_blocks) {
+    const uint64_t e = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    const uint64_t tot = (uint64_t)P * row;
+    if (e >= tot) return;
+    float v[4];
+    if (row % 4 == 0) {
+      const float4 t = *reinterpret_cast<const float4*>(dshs + e);
+      v[0] = t.x, v[1] = t.y, v[2] = t.z, v[3] = t.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = e + j < tot ? dshs[e + j] : 0.f;
+    }
+    const uint64_t gi = e / row;
+    const int k = (int)(e - gi * row);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (e + j >= tot) break;
+      const int kk = k + j;
+      const uint64_t g2 = kk < row ? gi : gi + 1;
+      const int k2 = kk < row ? kk : kk - row;
+      if (k2 < 3)
+        d_dc[g2 * 3 + k2] = v[j];
+      else
+        d_rest[g2 * rest_w + (k2 - 3)] = v[j];
+    }
+    return;
+  }
+  const int i = (blockIdx.x - feat_blocks) * 256 + threadIdx.x;
+  if (i >= P) return;
+  if (dopac) {
+    const float y = opac[i];
+    d_o[i] = dopac[i] * (1.0f - y) * y;
+  }
+  if (dscales) {
+#pragma unroll
+    for (int j = 0; j < 3; j++) d_s[3 * i + j] = dscales[3 * i + j] * scales[3 * i + j];
+  }
+  if (drots) {
+    const float4 q = *reinterpret_cast<const float4*>(q_raw + 4 * i);
+    const float4 g = *reinterpret_cast<const float4*>(drots + 4 * i);
+    const float len = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    const float n = fmaxf(len, 1e-12f);
+    const float dot = g.x * q.x + g.y * q.y + g.z * q.z + g.w * q.w;
+    const float c = len > 1e-12f ? dot / (n * n) / len : 0.0f;
+    *reinterpret_cast<float4*>(d_q + 4 * i) =
+        make_float4(g.x / n - c * q.x, g.y / n - c * q.y, g.z / n - c * q.z, g.w / n - c * q.w);
+  }
+}
+
+void activate_forward(int P, int rest_w, const float* f_dc, const float* f_rest, const float* o_raw,
+                      const float* s_raw, const float* q_raw, float* shs, float* opac, float* scales, float* rots,
+                      hipStream_t st) {
+  const uint64_t fe = ((uint64_t)P * (3 + rest_w) + 3) / 4;
+  const int fb = (int)((fe + 255) / 256), gb = (P + 255) / 256;
+  GS_LAUNCH("activate_fwd", k_activate_fwd, dim3(fb + gb), dim3(256), 0, st, P, fb, rest_w, f_dc, f_rest, o_raw,
+            s_raw, q_raw, shs, opac, scales, rots);
+}
+
+void activate_backward(int P, int rest_w, const float* dshs, const float* dopac, const float* dscales,
+                       const float* drots, const float* opac, const float* scales, const float* q_raw, float* d_dc,
+                       float* d_rest, float* d_o, float* d_s, float* d_q, hipStream_t st) {
+  const uint64_t fe = dshs ? ((uint64_t)P * (3 + rest_w) + 3) / 4 : 0;
+  const int fb = (int)((fe + 255) / 256), gb = (P + 255) / 256;
+  GS_LAUNCH("activate_bwd", k_activate_bwd, dim3(fb + gb), dim3(256), 0, st, P, fb, rest_w, dshs, dopac, dscales,
+            drots, opac, scales, q_raw, d_dc, d_rest, d_o, d_s, d_q);
+}
+
+}  // namespace gs

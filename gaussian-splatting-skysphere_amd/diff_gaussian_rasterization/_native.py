@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("GSRAST_LIB", os.path.join(_PKG_ROOT, "build", "libgsr
 
 _c_p = ctypes.c_void_p
 _c_i = ctypes.c_int
+_c_d = ctypes.c_double
 _c_f = ctypes.c_float
 _c_ll = ctypes.c_longlong
 _c_sz = ctypes.c_size_t
@@ -52,6 +53,10 @@ SIGNATURES = {
     "gs_ssim_partial_count": (_c_sz, [_c_i, _c_i, _c_i]),
     "gs_ssim_forward": (_c_i, [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_ssim_backward": (_c_i, [_c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "gs_adam_step": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_d, _c_d, _c_d, _c_i, _c_p]),
+    "gs_activate_forward": (_c_i, [_c_i, _c_i] + [_c_p] * 9 + [_c_p]),
+    "gs_activate_backward": (_c_i, [_c_i, _c_i] + [_c_p] * 12 + [_c_p]),
+    "gs_densify_stats": (_c_i, [_c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_p]),
     "gs_debug_export": (
         _c_i,
         [_c_i, _c_i, _c_i, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p],

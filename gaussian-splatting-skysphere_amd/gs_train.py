@@ -1,0 +1,254 @@
+"""Per-iteration training updates of train.py on MI355X, around the rasterizer.
+
+`FusedAdam` is a drop-in for the `torch.optim.Adam` that GaussianModel.training_setup builds
+(/root/reference/scene/gaussian_model.py:154-163: six param groups, one tensor each, per-group lr
+from the schedulers, eps 1e-15) and that train.py steps every iteration (train.py:123-124).  All
+parameter tensors are updated by ONE HIP launch (csrc/gs_train.hip k_adam: p, grad, exp_avg,
+exp_avg_sq in one pass, 16-B accesses) instead of torch's foreach chain of eight kernels per
+tensor list.  It keeps torch's optimizer state exactly: `state[p]` holds 'step' (CPU float32
+tensor), 'exp_avg', 'exp_avg_sq', so GaussianModel's densification code that concatenates / masks
+/ replaces those entries (gaussian_model.py:286-300, 317-340) and `state_dict()` /
+`load_state_dict()` checkpoints work unchanged, in both directions with torch.optim.Adam.
+
+`activate` / `render_inputs` produce the rasterizer inputs from GaussianModel's raw parameters
+(get_features / get_opacity / get_scaling / get_rotation, gaussian_model.py:95-115, read by
+gaussian_renderer/__init__.py:53-80) with one HIP launch forward and one backward, in place of
+torch's cat + sigmoid + exp + normalize chains and their autograd graph.
+
+`add_densification_stats` folds train.py:115-116 (max_radii2D update + GaussianModel.
+add_densification_stats, gaussian_model.py:405-407) into one HIP pass over the Gaussians.
+
+Use:  in GaussianModel.training_setup, `self.optimizer = FusedAdam(l, lr=0.0, eps=1e-15)`;
+in render(), `means3D, shs, opacity, scales, rotations = render_inputs(pc)`;
+in train.py, `add_densification_stats(gaussians, viewspace_point_tensor, radii)`.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from diff_gaussian_rasterization import _native
+
+_lib = _native.load()
+
+_MAX_TENSORS = 64  # per C call (the library splits into launches of 16 tensors)
+
+
+def _check_f32_dense(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"{what}: MI355X/HIP path needs device tensors; there is no CPU path")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{what}: expected float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: must be contiguous")
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad=False) with one fused HIP launch per step.
+
+    Update per element, as torch's Adam:  g <- -g if maximize; g <- g + weight_decay * p;
+    m <- m + (1 - b1)(g - m);  v <- b2 v + (1 - b2) g^2;
+    p <- p - lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps).
+    """
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False, *,
+                 maximize=False, foreach=None, capturable=False, differentiable=False, fused=None,
+                 decoupled_weight_decay=False):
+        if not 0.0 <= float(lr):
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameters: {betas}")
+        if not 0.0 <= weight_decay:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        if amsgrad:
+            raise NotImplementedError("FusedAdam: amsgrad is not supported (the reference never sets it)")
+        if decoupled_weight_decay:
+            raise NotImplementedError("FusedAdam: decoupled weight decay (AdamW) is not supported")
+        if capturable or differentiable:
+            raise NotImplementedError("FusedAdam: capturable / differentiable modes are not supported")
+        # same defaults keys as torch.optim.Adam so state_dicts move between the two
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad, maximize=maximize,
+                        foreach=foreach, capturable=capturable, differentiable=differentiable, fused=fused,
+                        decoupled_weight_decay=decoupled_weight_decay)
+        super().__init__(params, defaults)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        batches: dict = {}
+        for group in self.param_groups:
+            if group.get("amsgrad", False) or group.get("decoupled_weight_decay", False):
+                raise NotImplementedError("FusedAdam: amsgrad / decoupled weight decay are not supported")
+            b1, b2 = group["betas"]
+            key_h = (float(b1), float(b2), float(group["eps"]), bool(group.get("maximize", False)))
+            lr = float(group["lr"])
+            wd = float(group.get("weight_decay", 0.0))
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                grad = p.grad
+                if grad.is_sparse:
+                    raise RuntimeError("FusedAdam does not support sparse gradients")
+                _check_f32_dense(p, "FusedAdam param")
+                if grad.shape != p.shape:
+                    raise ValueError(f"FusedAdam: grad shape {tuple(grad.shape)} != param {tuple(p.shape)}")
+                if grad.dtype != torch.float32 or grad.device != p.device:
+                    raise TypeError("FusedAdam: grad must be float32 on the parameter's device")
+                if not grad.is_contiguous():
+                    grad = grad.contiguous()
+                state = self.state[p]
+                if len(state) == 0:
+                    state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                m, v = state["exp_avg"], state["exp_avg_sq"]
+                _check_f32_dense(m, "FusedAdam exp_avg")
+                _check_f32_dense(v, "FusedAdam exp_avg_sq")
+                if m.numel() != p.numel() or v.numel() != p.numel():
+                    raise ValueError("FusedAdam: optimizer state does not match the parameter size")
+                step_t = state["step"]
+                if torch.is_tensor(step_t):
+                    step_t += 1
+                    t = int(step_t.item())
+                else:
+                    t = int(step_t) + 1
+                    state["step"] = torch.tensor(float(t), dtype=torch.float32)
+                batches.setdefault((p.device, key_h), []).append((p, grad, m, v, lr, t, wd))
+        for (dev, (b1, b2, eps, maximize)), items in batches.items():
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            for s in range(0, len(items), _MAX_TENSORS):
+                self._launch(items[s:s + _MAX_TENSORS], b1, b2, eps, maximize, dev, st)
+        return loss
+
+    @staticmethod
+    def _launch(items, b1, b2, eps, maximize, dev, st):
+        n = len(items)
+        ptrs = ctypes.c_void_p * n
+        P, G, M, V = (ptrs(*[ctypes.c_void_p(it[j].data_ptr()) for it in items]) for j in range(4))
+        numel = (ctypes.c_longlong * n)(*[it[0].numel() for it in items])
+        lr = (ctypes.c_double * n)(*[it[4] for it in items])
+        steps = (ctypes.c_longlong * n)(*[it[5] for it in items])
+        wd = (ctypes.c_double * n)(*[it[6] for it in items])
+        cast = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+        with torch.cuda.device(dev):
+            _native.check(_lib.gs_adam_step(n, cast(P), cast(G), cast(M), cast(V), cast(numel), cast(lr),
+                                            cast(steps), cast(wd), b1, b2, eps, int(maximize), st), "adam step")
+
+
+def densify_stats(max_radii2D: torch.Tensor, grad_accum: torch.Tensor, denom: torch.Tensor, radii: torch.Tensor,
+                  viewspace_grad: torch.Tensor) -> None:
+    """In place, for every i with radii[i] > 0 (train.py:115, gaussian_model.py:405-407):
+    max_radii2D[i] = max(max_radii2D[i], radii[i]); grad_accum[i] += ||viewspace_grad[i, :2]||;
+    denom[i] += 1."""
+    P = radii.shape[0]
+    for t, name in ((max_radii2D, "max_radii2D"), (grad_accum, "xyz_gradient_accum"), (denom, "denom")):
+        _check_f32_dense(t, name)
+        if t.numel() != P:
+            raise ValueError(f"{name}: expected {P} entries, got {t.numel()}")
+    _check_f32_dense(viewspace_grad, "viewspace grad")
+    if viewspace_grad.dim() != 2 or viewspace_grad.shape[0] != P or viewspace_grad.shape[1] < 2:
+        raise ValueError(f"viewspace grad: expected [{P}, >=2], got {tuple(viewspace_grad.shape)}")
+    if radii.dtype != torch.int32 or not radii.is_cuda or not radii.is_contiguous():
+        raise TypeError("radii: expected a contiguous int32 device tensor (the rasterizer's output)")
+    if P == 0:
+        return
+    dev = radii.device
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    with torch.cuda.device(dev):
+        _native.check(_lib.gs_densify_stats(P, ctypes.c_void_p(radii.data_ptr()),
+                                            ctypes.c_void_p(viewspace_grad.data_ptr()), viewspace_grad.shape[1],
+                                            ctypes.c_void_p(max_radii2D.data_ptr()),
+                                            ctypes.c_void_p(grad_accum.data_ptr()),
+                                            ctypes.c_void_p(denom.data_ptr()), st), "densify stats")
+
+
+def add_densification_stats(gaussians, viewspace_point_tensor: torch.Tensor, radii: torch.Tensor) -> None:
+    """train.py:115-116 in one launch: updates gaussians.max_radii2D, .xyz_gradient_accum, .denom
+    for the visible Gaussians (radii > 0, the reference's visibility_filter)."""
+    if viewspace_point_tensor.grad is None:
+        raise RuntimeError("add_densification_stats: viewspace_point_tensor has no gradient (call backward first)")
+    densify_stats(gaussians.max_radii2D, gaussians.xyz_gradient_accum, gaussians.denom, radii,
+                  viewspace_point_tensor.grad)
+
+
+def _aligned(t: torch.Tensor) -> torch.Tensor:
+    """contiguous with a 16-byte aligned base (the float4 paths of the activation kernels)"""
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class _Activate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f_dc, f_rest, opacity_raw, scaling_raw, rotation_raw):
+        P = f_dc.shape[0]
+        if f_dc.shape[1:] != (1, 3) or f_rest.dim() != 3 or f_rest.shape[0] != P or f_rest.shape[2] != 3:
+            raise ValueError(f"activate: expected features_dc [P,1,3] and features_rest [P,K,3], got "
+                             f"{tuple(f_dc.shape)} / {tuple(f_rest.shape)}")
+        if opacity_raw.numel() != P or scaling_raw.shape != (P, 3) or rotation_raw.shape != (P, 4):
+            raise ValueError("activate: expected opacity [P,1], scaling [P,3], rotation [P,4]")
+        ins = [_aligned(t.detach()) for t in (f_dc, f_rest, opacity_raw, scaling_raw, rotation_raw)]
+        for t, name in zip(ins, ("features_dc", "features_rest", "opacity", "scaling", "rotation")):
+            _check_f32_dense(t, name)
+        dc, rest, o, s, q = ins
+        K = rest.shape[1]
+        dev = dc.device
+        shs = torch.empty((P, 1 + K, 3), dtype=torch.float32, device=dev)
+        opac = torch.empty(tuple(opacity_raw.shape), dtype=torch.float32, device=dev)
+        scales = torch.empty((P, 3), dtype=torch.float32, device=dev)
+        rots = torch.empty((P, 4), dtype=torch.float32, device=dev)
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        with torch.cuda.device(dev):
+            _native.check(_lib.gs_activate_forward(P, 3 * K, _ptr(dc), _ptr(rest), _ptr(o), _ptr(s), _ptr(q),
+                                                   _ptr(shs), _ptr(opac), _ptr(scales), _ptr(rots), st), "activate")
+        ctx.P, ctx.K = P, K
+        ctx.shapes = (tuple(f_dc.shape), tuple(f_rest.shape), tuple(opacity_raw.shape))
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(opac, scales, q)
+        return shs, opac, scales, rots
+
+    @staticmethod
+    def backward(ctx, dshs, dopac, dscales, drots):
+        opac, scales, q = ctx.saved_tensors
+        P, K = ctx.P, ctx.K
+        dev = q.device
+        need = ctx.needs_input_grad
+        dshs = _aligned(dshs) if dshs is not None and (need[0] or need[1]) else None
+        dopac = dopac.contiguous() if dopac is not None and need[2] else None
+        dscales = dscales.contiguous() if dscales is not None and need[3] else None
+        drots = _aligned(drots) if drots is not None and need[4] else None
+        g_dc = torch.empty(ctx.shapes[0], dtype=torch.float32, device=dev) if dshs is not None else None
+        g_rest = torch.empty(ctx.shapes[1], dtype=torch.float32, device=dev) if dshs is not None else None
+        g_o = torch.empty(ctx.shapes[2], dtype=torch.float32, device=dev) if dopac is not None else None
+        g_s = torch.empty((P, 3), dtype=torch.float32, device=dev) if dscales is not None else None
+        g_q = torch.empty((P, 4), dtype=torch.float32, device=dev) if drots is not None else None
+        if any(t is not None for t in (dshs, dopac, dscales, drots)):
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            with torch.cuda.device(dev):
+                _native.check(_lib.gs_activate_backward(P, 3 * K, _ptr(dshs), _ptr(dopac), _ptr(dscales),
+                                                        _ptr(drots), _ptr(opac), _ptr(scales), _ptr(q), _ptr(g_dc),
+                                                        _ptr(g_rest), _ptr(g_o), _ptr(g_s), _ptr(g_q), st),
+                              "activate backward")
+        return g_dc, g_rest, g_o, g_s, g_q
+
+
+def activate(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw):
+    """(shs, opacity, scales, rotations) = (cat(dc, rest, 1), sigmoid(o), exp(s), normalize(q)),
+    differentiable; one HIP launch each way (csrc/gs_train.hip k_activate_fwd / k_activate_bwd)."""
+    return _Activate.apply(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw)
+
+
+def render_inputs(pc):
+    """The tensors gaussian_renderer.render() reads from a GaussianModel (__init__.py:53-80):
+    (means3D, shs, opacity, scales, rotations)."""
+    shs, opac, scales, rots = activate(pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation)
+    return pc._xyz, shs, opac, scales, rots

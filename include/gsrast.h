@@ -19,6 +19,11 @@
  *   gs_ssim_forward / gs_ssim_backward         <-  utils.loss_utils.ssim(img1, img2)
  *                                                  (/root/reference/utils/loss_utils.py:33-60,
  *                                                   called at train.py:92)
+ *   gs_adam_step                               <-  torch.optim.Adam.step() of GaussianModel
+ *                                                  (/root/reference/scene/gaussian_model.py:163)
+ *   gs_densify_stats                           <-  train.py:115-116 / gaussian_model.py:405-407
+ *   gs_activate_forward / gs_activate_backward <-  GaussianModel.get_features / get_opacity /
+ *                                                  get_scaling / get_rotation (gaussian_model.py:95-115)
  *
  * Conventions
  *   - Every pointer argument is a DEVICE pointer (HBM of the current HIP device) unless its name
@@ -124,6 +129,44 @@ int gs_ssim_forward(int planes, int H, int W, const float* window11_host, const 
                     float* dmaps, float* partial, float* plane_sum, void* stream);
 int gs_ssim_backward(int planes, int channels, int H, int W, const float* window11_host, const float* img1,
                      const float* img2, const float* dmaps, const float* scale, float* dimg1, void* stream);
+
+/* ---- fused Adam step  <-  torch.optim.Adam.step() of GaussianModel's optimizer
+ *      (/root/reference/scene/gaussian_model.py:154-163, stepped at train.py:123-124) ----
+ * count parameter tensors, each with its own lr / step (the reference has one tensor per param
+ * group, per-group lr from the schedulers).  The pointer/size arrays are HOST arrays of DEVICE
+ * pointers; each tensor is dense fp32 with numel elements and p, grad, exp_avg, exp_avg_sq of equal
+ * size.  step[k] >= 1 is the step count AFTER this update (torch increments before updating).
+ * lr / weight_decay / betas / eps are the Python doubles of the param groups (rounded to float on the
+ * way to the device exactly where torch rounds them).  weight_decay_host may be NULL (all zero).
+ * amsgrad is not supported (the reference never sets it). */
+int gs_adam_step(int count, float* const* params_host, const float* const* grads_host, float* const* exp_avg_host,
+                 float* const* exp_avg_sq_host, const long long* numel_host, const double* lr_host,
+                 const long long* step_host, const double* weight_decay_host, double beta1, double beta2, double eps,
+                 int maximize, void* stream);
+
+/* ---- render() inputs from GaussianModel's raw parameters  <-  get_features / get_opacity /
+ *      get_scaling / get_rotation (/root/reference/scene/gaussian_model.py:95-115, read at
+ *      gaussian_renderer/__init__.py:53-80) ----
+ * Forward: shs[P, 1 + sh_rest/3, 3] = cat(features_dc[P,1,3], features_rest[P,sh_rest/3,3]);
+ * opacity[P] = sigmoid(opacity_raw); scales[P,3] = exp(scaling_raw);
+ * rotations[P,4] = rotation_raw / max(|rotation_raw|, 1e-12).
+ * Backward: the adjoints (any of the four dL_d* inputs may be NULL: its outputs are not written);
+ * opacity / scales are the forward OUTPUTS, rotation_raw the forward input.  Rotation and shs
+ * buffers must be 16-byte aligned. */
+int gs_activate_forward(int P, int sh_rest, const float* features_dc, const float* features_rest,
+                        const float* opacity_raw, const float* scaling_raw, const float* rotation_raw, float* shs,
+                        float* opacity, float* scales, float* rotations, void* stream);
+int gs_activate_backward(int P, int sh_rest, const float* dL_dshs, const float* dL_dopacity, const float* dL_dscales,
+                         const float* dL_drotations, const float* opacity, const float* scales,
+                         const float* rotation_raw, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
+                         float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw, void* stream);
+
+/* ---- densification statistics  <-  train.py:115-116 + GaussianModel.add_densification_stats
+ *      (/root/reference/scene/gaussian_model.py:405-407) ----
+ * For every i with radii[i] > 0:  max_radii2D[i] = max(max_radii2D[i], radii[i]);
+ * grad_accum[i] += |grad2d[i * grad_stride + 0..1]|_2;  denom[i] += 1.  (grad_accum, denom: [P, 1]) */
+int gs_densify_stats(int P, const int* radii, const float* grad2d, int grad_stride, float* max_radii2D,
+                     float* grad_accum, float* denom, void* stream);
 
 /* ---- debug export of forward intermediates (tests) ----
  * Copies (device -> device) whichever outputs are non-NULL: point_list[num_rendered] (Gaussian ids
