@@ -418,6 +418,80 @@ int gs_activate_backward(int P, int sh_rest, const float* dL_dshs, const float* 
   return t_failed ? 1 : 0;
 }
 
+/* ---- densify_and_prune (gaussian_model.py:391-403) ---- */
+static DensifyParams make_dens_params(double grad_threshold, double pd_extent, double min_opacity, double big_extent,
+                                      int has_screen, double max_screen, int N) {
+  DensifyParams dp;
+  dp.thr = (float)grad_threshold;
+  dp.pd_ext = (float)pd_extent;
+  dp.min_op = (float)min_opacity;
+  dp.big_ext = (float)big_extent;
+  dp.max_screen = (float)max_screen;
+  dp.inv_split = 1.0f / (float)(0.8 * N);
+  dp.screen = has_screen ? 1 : 0;
+  return dp;
+}
+
+size_t gs_densify_block_count(int P) { return P > 0 ? (size_t)((P + 255) / 256) : 0; }
+
+int gs_densify_classify(int P, const float* grad_accum, const float* denom, const float* opacity_raw,
+                        const float* scaling_raw, double grad_threshold, double pd_extent, double min_opacity,
+                        double big_extent, int has_screen, double max_screen, int N, uint8_t* flags,
+                        uint32_t* block_counts, uint32_t* totals, void* stream) {
+  clear_error(0);
+  if (P <= 0 || N < 1) return set_error("densify: P must be > 0 and N >= 1"), 1;
+  if (!grad_accum || !denom || !opacity_raw || !scaling_raw || !flags || !block_counts || !totals)
+    return set_error("densify: missing pointer"), 1;
+  const DensifyParams dp = make_dens_params(grad_threshold, pd_extent, min_opacity, big_extent, has_screen,
+                                            max_screen, N);
+  densify_classify(P, dp, grad_accum, denom, opacity_raw, scaling_raw, flags, block_counts, totals,
+                   (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
+int gs_densify_split_stds(int P, int N, const uint32_t* totals_host, const uint8_t* flags,
+                          const uint32_t* block_counts, const float* scaling_raw, float* stds, void* stream) {
+  clear_error(0);
+  if (P <= 0 || N < 1 || !totals_host) return set_error("densify: bad arguments"), 1;
+  if (totals_host[2] == 0) return 0;
+  if (!flags || !block_counts || !scaling_raw || !stds) return set_error("densify: missing pointer"), 1;
+  densify_stds(P, N, totals_host[2], flags, block_counts, scaling_raw, stds, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
+int gs_densify_emit(int P, int N, const uint32_t* totals_host, const uint8_t* flags, const uint32_t* block_counts,
+                    const float* samples, const float* const* params_host, const float* const* exp_avg_host,
+                    const float* const* exp_avg_sq_host, float* const* out_params_host,
+                    float* const* out_exp_avg_host, float* const* out_exp_avg_sq_host, const int* widths_host,
+                    void* stream) {
+  clear_error(0);
+  if (P <= 0 || N < 1 || !totals_host || !flags || !block_counts || !params_host || !out_params_host || !widths_host)
+    return set_error("densify: missing argument"), 1;
+  if (totals_host[2] && !samples) return set_error("densify: split samples missing"), 1;
+  if (widths_host[DT_XYZ] != 3 || widths_host[DT_FDC] != 3 || widths_host[DT_OPACITY] != 1 ||
+      widths_host[DT_SCALING] != 3 || widths_host[DT_ROT] != 4 || widths_host[DT_FREST] < 0)
+    return set_error("densify: row widths must be xyz 3, f_dc 3, f_rest 3K, opacity 1, scaling 3, rotation 4"), 1;
+  DensTensors t;
+  for (int q = 0; q < DENS_TENSORS; q++) {
+    t.src[q] = params_host[q];
+    t.dst[q] = out_params_host[q];
+    t.width[q] = widths_host[q];
+    const bool has_m = exp_avg_host && exp_avg_host[q];
+    if (has_m && (!exp_avg_sq_host || !exp_avg_sq_host[q] || !out_exp_avg_host || !out_exp_avg_host[q] ||
+                  !out_exp_avg_sq_host || !out_exp_avg_sq_host[q]))
+      return set_error("densify: incomplete optimizer state pointers"), 1;
+    t.m_src[q] = has_m ? exp_avg_host[q] : nullptr;
+    t.v_src[q] = has_m ? exp_avg_sq_host[q] : nullptr;
+    t.m_dst[q] = has_m ? out_exp_avg_host[q] : nullptr;
+    t.v_dst[q] = has_m ? out_exp_avg_sq_host[q] : nullptr;
+    if ((!t.src[q] || !t.dst[q]) && t.width[q] > 0) return set_error("densify: missing parameter pointer"), 1;
+  }
+  DensCounts n{totals_host[0], totals_host[1], totals_host[2], totals_host[3]};
+  const DensifyParams dp = make_dens_params(0, 0, 0, 0, 0, 0, N);
+  densify_emit(P, N, dp, n, flags, block_counts, samples, t, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
 int gs_densify_stats(int P, const int* radii, const float* grad2d, int grad_stride, float* max_radii2D,
                      float* grad_accum, float* denom, void* stream) {
   clear_error(0);

@@ -216,6 +216,33 @@ void activate_forward(int P, int rest_w, const float* f_dc, const float* f_rest,
 void activate_backward(int P, int rest_w, const float* dshs, const float* dopac, const float* dscales,
                        const float* drots, const float* opac, const float* scales, const float* q_raw, float* d_dc,
                        float* d_rest, float* d_o, float* d_s, float* d_q, hipStream_t st);
+// densify_and_prune (csrc/gs_densify.hip)
+struct DensifyParams {
+  // scalars rounded to float as torch compares them; a tensor divided by a Python scalar is
+  // multiplied by the float reciprocal on the device (ATen div_true with a CPU scalar), hence inv_split
+  float thr, pd_ext, min_op, big_ext, max_screen, inv_split;
+  int screen;                                                  // `if max_screen_size:`
+};
+struct DensCounts {
+  uint32_t keep_a, keep_b, split, keep_c;
+};
+constexpr int DENS_TENSORS = 6;
+enum { DT_XYZ = 0, DT_FDC = 1, DT_FREST = 2, DT_OPACITY = 3, DT_SCALING = 4, DT_ROT = 5 };
+struct DensTensors {
+  const float* src[DENS_TENSORS];
+  const float* m_src[DENS_TENSORS];  // Adam exp_avg (NULL: the group has no state yet)
+  const float* v_src[DENS_TENSORS];
+  float* dst[DENS_TENSORS];
+  float* m_dst[DENS_TENSORS];
+  float* v_dst[DENS_TENSORS];
+  int width[DENS_TENSORS];
+};
+void densify_classify(int P, const DensifyParams& dp, const float* accum, const float* denom, const float* opacity,
+                      const float* scaling, uint8_t* flags, uint32_t* counts, uint32_t* totals, hipStream_t st);
+void densify_stds(int P, int N, uint32_t n_split, const uint8_t* flags, const uint32_t* bases, const float* scaling,
+                  float* stds, hipStream_t st);
+void densify_emit(int P, int N, const DensifyParams& dp, const DensCounts& n, const uint8_t* flags,
+                  const uint32_t* bases, const float* samples, const DensTensors& t, hipStream_t st);
 void densify_stats(int P, const int* radii, const float* grad2d, int grad_stride, float* max_radii2D,
                    float* grad_accum, float* denom, hipStream_t st);
 size_t knn_scratch_bytes(int P);

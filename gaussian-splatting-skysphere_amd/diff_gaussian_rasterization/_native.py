@@ -56,6 +56,11 @@ SIGNATURES = {
     "gs_adam_step": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_d, _c_d, _c_d, _c_i, _c_p]),
     "gs_activate_forward": (_c_i, [_c_i, _c_i] + [_c_p] * 9 + [_c_p]),
     "gs_activate_backward": (_c_i, [_c_i, _c_i] + [_c_p] * 12 + [_c_p]),
+    "gs_densify_block_count": (_c_sz, [_c_i]),
+    "gs_densify_classify": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_d, _c_d, _c_d, _c_d, _c_i, _c_d, _c_i, _c_p, _c_p,
+                                   _c_p, _c_p]),
+    "gs_densify_split_stds": (_c_i, [_c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "gs_densify_emit": (_c_i, [_c_i, _c_i] + [_c_p] * 12),
     "gs_densify_stats": (_c_i, [_c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_p]),
     "gs_debug_export": (
         _c_i,

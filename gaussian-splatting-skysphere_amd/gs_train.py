@@ -252,3 +252,101 @@ def render_inputs(pc):
     (means3D, shs, opacity, scales, rotations)."""
     shs, opac, scales, rots = activate(pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation)
     return pc._xyz, shs, opac, scales, rots
+
+
+_DENS_NAMES = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
+_DENS_ATTRS = ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
+
+
+def densify_and_prune(gaussians, max_grad, min_opacity, extent, max_screen_size, N: int = 2) -> None:
+    """GaussianModel.densify_and_prune (gaussian_model.py:391-403) in three HIP passes.
+
+    Same effect on `gaussians` as the reference: the six parameters become new nn.Parameters of
+    the final size in the reference's order (kept originals, kept clones, kept split children), the
+    Adam moments follow them (zeros for new rows, 'step' kept), the densification stats are re-zeroed,
+    and the split draws come from torch.normal with the reference's shapes and order (same RNG
+    stream).  Every parameter and moment is rewritten once instead of four times
+    (csrc/gs_densify.hip)."""
+    params = [getattr(gaussians, a) for a in _DENS_ATTRS]
+    xyz = params[0]
+    P = xyz.shape[0]
+    if P == 0:
+        return
+    dev = xyz.device
+    src = [p.detach() for p in params]
+    for t, n in zip(src, _DENS_NAMES):
+        _check_f32_dense(t, n)
+        if t.shape[0] != P:
+            raise ValueError(f"densify: {n} has {t.shape[0]} rows, xyz has {P}")
+    accum = gaussians.xyz_gradient_accum.contiguous()
+    denom = gaussians.denom.contiguous()
+    for t, n in ((accum, "xyz_gradient_accum"), (denom, "denom")):
+        _check_f32_dense(t, n)
+        if t.numel() != P:
+            raise ValueError(f"densify: {n} must have {P} entries")
+    widths = [int(t[0].numel()) for t in src]
+    flags = torch.empty((P,), dtype=torch.uint8, device=dev)
+    counts = torch.empty((4 * _lib.gs_densify_block_count(P),), dtype=torch.int32, device=dev)
+    totals = torch.empty((4,), dtype=torch.int32, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    with torch.cuda.device(dev):
+        _native.check(_lib.gs_densify_classify(
+            P, _ptr(accum), _ptr(denom), _ptr(src[3]), _ptr(src[4]), float(max_grad),
+            float(gaussians.percent_dense * extent), float(min_opacity), float(0.1 * extent),
+            1 if max_screen_size else 0, float(max_screen_size) if max_screen_size else 0.0, int(N),
+            _ptr(flags), _ptr(counts), _ptr(totals), st), "densify classify")
+        tot = [int(v) for v in totals.cpu()]  # the one host read: sizes of the new tensors
+        tot_h = (ctypes.c_uint32 * 4)(*tot)
+        n_split = tot[2]
+        stds = torch.empty((N * n_split, 3), dtype=torch.float32, device=dev)
+        _native.check(_lib.gs_densify_split_stds(P, N, tot_h, _ptr(flags), _ptr(counts), _ptr(src[4]),
+                                                 _ptr(stds) if n_split else None, st), "densify stds")
+        # the reference's draw (gaussian_model.py:359-360): same shapes, same generator stream
+        samples = torch.normal(mean=torch.zeros((stds.size(0), 3), device=dev), std=stds).contiguous()
+        Pn = tot[0] + tot[1] + N * tot[3]
+        groups = {g["name"]: g for g in gaussians.optimizer.param_groups}
+        states, outs, m_in, v_in, m_out, v_out = [], [], [], [], [], []
+        for n, t in zip(_DENS_NAMES, src):
+            grp = groups[n]
+            if len(grp["params"]) != 1 or grp["params"][0] is not params[_DENS_NAMES.index(n)]:
+                raise ValueError(f"densify: optimizer group '{n}' must hold exactly the model's tensor")
+            stt = gaussians.optimizer.state.get(grp["params"][0], None)
+            states.append(stt)
+            outs.append(torch.empty((Pn,) + tuple(t.shape[1:]), dtype=torch.float32, device=dev))
+            if stt is not None:
+                m, v = stt["exp_avg"].contiguous(), stt["exp_avg_sq"].contiguous()
+                _check_f32_dense(m, f"{n} exp_avg")
+                if m.shape != t.shape or v.shape != t.shape:
+                    raise ValueError(f"densify: optimizer state of '{n}' does not match the parameter")
+                m_in.append(m)
+                v_in.append(v)
+                m_out.append(torch.empty_like(outs[-1]))
+                v_out.append(torch.empty_like(outs[-1]))
+            else:
+                m_in.append(None)
+                v_in.append(None)
+                m_out.append(None)
+                v_out.append(None)
+        arr = lambda ts: (ctypes.c_void_p * 6)(*[_ptr(x) for x in ts])  # noqa: E731
+        _native.check(_lib.gs_densify_emit(
+            P, N, tot_h, _ptr(flags), _ptr(counts), _ptr(samples) if n_split else None,
+            ctypes.cast(arr(src), ctypes.c_void_p), ctypes.cast(arr(m_in), ctypes.c_void_p),
+            ctypes.cast(arr(v_in), ctypes.c_void_p), ctypes.cast(arr(outs), ctypes.c_void_p),
+            ctypes.cast(arr(m_out), ctypes.c_void_p), ctypes.cast(arr(v_out), ctypes.c_void_p),
+            ctypes.cast((ctypes.c_int * 6)(*widths), ctypes.c_void_p), st), "densify emit")
+    # optimizer surgery as cat_tensors_to_optimizer / _prune_optimizer do it
+    for i, n in enumerate(_DENS_NAMES):
+        grp = groups[n]
+        old = grp["params"][0]
+        newp = torch.nn.Parameter(outs[i].requires_grad_(True))
+        stt = states[i]
+        if stt is not None:
+            stt["exp_avg"], stt["exp_avg_sq"] = m_out[i], v_out[i]
+            del gaussians.optimizer.state[old]
+            gaussians.optimizer.state[newp] = stt
+        grp["params"][0] = newp
+        setattr(gaussians, _DENS_ATTRS[i], newp)
+    gaussians.xyz_gradient_accum = torch.zeros((Pn, 1), device=dev)
+    gaussians.denom = torch.zeros((Pn, 1), device=dev)
+    gaussians.max_radii2D = torch.zeros((Pn,), device=dev)
+    torch.cuda.empty_cache()

@@ -22,6 +22,8 @@
  *   gs_adam_step                               <-  torch.optim.Adam.step() of GaussianModel
  *                                                  (/root/reference/scene/gaussian_model.py:163)
  *   gs_densify_stats                           <-  train.py:115-116 / gaussian_model.py:405-407
+ *   gs_densify_classify / _split_stds / _emit  <-  GaussianModel.densify_and_prune
+ *                                                  (gaussian_model.py:391-403)
  *   gs_activate_forward / gs_activate_backward <-  GaussianModel.get_features / get_opacity /
  *                                                  get_scaling / get_rotation (gaussian_model.py:95-115)
  *
@@ -160,6 +162,34 @@ int gs_activate_backward(int P, int sh_rest, const float* dL_dshs, const float* 
                          const float* dL_drotations, const float* opacity, const float* scales,
                          const float* rotation_raw, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
                          float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw, void* stream);
+
+/* ---- densify_and_prune  <-  GaussianModel.densify_and_prune (/root/reference/scene/
+ *      gaussian_model.py:391-403 with densify_and_clone :375-389, densify_and_split :348-373,
+ *      prune_points :289-305, cat_tensors_to_optimizer :307-326), called at train.py:118-120 ----
+ * Three steps with one host read in between (the caller allocates the new tensors):
+ *  1. gs_densify_classify: per Gaussian flags[P] (u8) and per-block counts
+ *     (block_counts: 4 * gs_densify_block_count(P) u32, scanned in place to block bases);
+ *     totals[4] (device) = {kept originals, kept clones, split parents, kept split parents}.
+ *     Scalars are the Python values of the reference call (grad_threshold = max_grad,
+ *     pd_extent = percent_dense * extent, big_extent = 0.1 * extent, has_screen = bool(max_screen_size)).
+ *  2. gs_densify_split_stds (totals copied to the host): stds[N * totals[2], 3] = exp(scaling) of the
+ *     split parents in the reference's repeat order; the caller draws
+ *     samples = torch.normal(mean=zeros, std=stds) exactly as gaussian_model.py:358-360 does.
+ *  3. gs_densify_emit: writes the final rows (P' = totals[0] + totals[1] + N * totals[3]) of the six
+ *     parameter tensors in order xyz, f_dc, f_rest, opacity, scaling, rotation (row widths
+ *     3, 3, 3K, 1, 3, 4) and of their Adam moments (NULL entries: group without state). */
+size_t gs_densify_block_count(int P);
+int gs_densify_classify(int P, const float* grad_accum, const float* denom, const float* opacity_raw,
+                        const float* scaling_raw, double grad_threshold, double pd_extent, double min_opacity,
+                        double big_extent, int has_screen, double max_screen, int N, uint8_t* flags,
+                        uint32_t* block_counts, uint32_t* totals, void* stream);
+int gs_densify_split_stds(int P, int N, const uint32_t* totals_host, const uint8_t* flags,
+                          const uint32_t* block_counts, const float* scaling_raw, float* stds, void* stream);
+int gs_densify_emit(int P, int N, const uint32_t* totals_host, const uint8_t* flags, const uint32_t* block_counts,
+                    const float* samples, const float* const* params_host, const float* const* exp_avg_host,
+                    const float* const* exp_avg_sq_host, float* const* out_params_host,
+                    float* const* out_exp_avg_host, float* const* out_exp_avg_sq_host, const int* widths_host,
+                    void* stream);
 
 /* ---- densification statistics  <-  train.py:115-116 + GaussianModel.add_densification_stats
  *      (/root/reference/scene/gaussian_model.py:405-407) ----

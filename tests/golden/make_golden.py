@@ -13,7 +13,12 @@ Reference functions exercised (all on CPU):
   - utils/graphics_utils.py:38-71      getWorld2View2, getProjectionMatrix
   - gaussian_renderer/__init__.py:73-78  convert_SHs_python colour path (+0.5, clamp_min 0)
   - utils/loss_utils.py:17-60          l1_loss, gaussian / create_window, ssim (+ autograd grads)
+  - scene/gaussian_model.py:258-403    GaussianModel.densify_and_prune with its optimizer surgery, run
+                                       on CPU: the module is loaded with empty stand-ins for the two
+                                       imports it does not use on this path (plyfile, simple_knn._C) and
+                                       the same device="cuda"-dropping torch proxy
 """
+import math
 import os
 import sys
 import types
@@ -144,10 +149,104 @@ def loss_vectors():
     np.savez_compressed(os.path.join(OUT, "loss_golden.npz"), **out)
 
 
+def _ref_gaussian_model():
+    """scene/gaussian_model.py imported on CPU (its plyfile / simple_knn imports are unused here)."""
+    for name, attrs in (("plyfile", ("PlyData", "PlyElement")), ("simple_knn", ()), ("simple_knn._C", ("distCUDA2",))):
+        if name not in sys.modules:
+            m = types.ModuleType(name)
+            for a in attrs:
+                setattr(m, a, None)
+            sys.modules[name] = m
+    import scene.gaussian_model as gm  # noqa
+
+    gm.torch = _TORCH_CPU
+    return gm
+
+
+class _TorchCPUProxy(types.ModuleType):
+    """torch proxy whose zeros() ignores device= (the reference hard-codes cuda)."""
+
+    def __getattr__(self, k):
+        return getattr(torch, k)
+
+    @staticmethod
+    def zeros(*a, **kw):
+        kw.pop("device", None)
+        return torch.zeros(*a, **kw)
+
+
+_TORCH_CPU = _TorchCPUProxy("torch")
+
+DENSIFY_LRS = [1.6e-4, 2.5e-3, 1.25e-4, 5e-2, 5e-3, 1e-3]
+DENSIFY_NAMES = ["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"]
+
+
+def densify_inputs(P, seed):
+    """Parameters / stats that exercise clone, split (kept and pruned children), NaN grads, opacity
+    and world-size pruning with percent_dense 0.01, extent 2 (pd_extent 0.02, big 0.2), thr 2e-4."""
+    g = torch.Generator().manual_seed(seed)
+    d = {
+        "xyz": torch.randn((P, 3), generator=g),
+        "f_dc": torch.randn((P, 1, 3), generator=g),
+        "f_rest": torch.randn((P, 15, 3), generator=g) * 0.1,
+        "opacity": torch.randn((P, 1), generator=g) * 3.0,
+        "scaling": math.log(0.003) + torch.rand((P, 3), generator=g) * (math.log(0.5) - math.log(0.003)),
+        "rotation": torch.randn((P, 4), generator=g),
+    }
+    denom = torch.randint(0, 6, (P, 1), generator=g).float()
+    accum = torch.rand((P, 1), generator=g) * 4e-4 * denom
+    accum[denom == 0] = 0.0
+    radii = torch.randint(0, 30, (P,), generator=g).float()
+    grads = {k: torch.randn(v.shape, generator=g) for k, v in d.items()}
+    return d, accum, denom, radii, grads
+
+
+def densify_vectors(gm_mod):
+    out = {}
+    for case, (P, seed, screen) in {"a": (400, 11, 20), "b": (300, 12, None)}.items():
+        d, accum, denom, radii, grads = densify_inputs(P, seed)
+        m = gm_mod.GaussianModel(3)
+        for n, attr in zip(DENSIFY_NAMES, ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling",
+                                           "_rotation")):
+            setattr(m, attr, torch.nn.Parameter(d[n].clone().requires_grad_(True)))
+        m.percent_dense = 0.01
+        groups = [{"params": [getattr(m, a)], "lr": lr, "name": n} for n, a, lr in
+                  zip(DENSIFY_NAMES, ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"),
+                      DENSIFY_LRS)]
+        m.optimizer = torch.optim.Adam(groups, lr=0.0, eps=1e-15)
+        for _ in range(2):  # non-trivial Adam moments
+            for grp in m.optimizer.param_groups:
+                grp["params"][0].grad = grads[grp["name"]].clone()
+            m.optimizer.step()
+        for grp in m.optimizer.param_groups:
+            n = grp["name"]
+            out[f"{case}_in_{n}"] = grp["params"][0].detach().numpy().copy()
+            st = m.optimizer.state[grp["params"][0]]
+            out[f"{case}_in_{n}_exp_avg"] = st["exp_avg"].numpy().copy()
+            out[f"{case}_in_{n}_exp_avg_sq"] = st["exp_avg_sq"].numpy().copy()
+            m.optimizer.state[grp["params"][0]] = st
+        m.xyz_gradient_accum, m.denom, m.max_radii2D = accum.clone(), denom.clone(), radii.clone()
+        out[f"{case}_in_accum"], out[f"{case}_in_denom"], out[f"{case}_in_max_radii2D"] = (
+            accum.numpy(), denom.numpy(), radii.numpy())
+        out[f"{case}_args"] = np.array([2e-4, 0.005, 2.0, -1.0 if screen is None else screen, seed], np.float64)
+        torch.manual_seed(seed)
+        m.densify_and_prune(2e-4, 0.005, 2.0, screen)
+        for grp in m.optimizer.param_groups:
+            n = grp["name"]
+            out[f"{case}_out_{n}"] = grp["params"][0].detach().numpy()
+            st = m.optimizer.state[grp["params"][0]]
+            out[f"{case}_out_{n}_exp_avg"] = st["exp_avg"].numpy()
+            out[f"{case}_out_{n}_exp_avg_sq"] = st["exp_avg_sq"].numpy()
+            out[f"{case}_out_{n}_step"] = np.array(float(st["step"]))
+        out[f"{case}_out_sizes"] = np.array([m.xyz_gradient_accum.shape[0], m.denom.shape[0], m.max_radii2D.shape[0]])
+    np.savez_compressed(os.path.join(OUT, "densify_golden.npz"), **out)
+
+
 if __name__ == "__main__":
     sh_utils, gu, gfx = _import_ref()
     sh_vectors(sh_utils)
     cov_vectors(gu)
     camera_vectors(gfx)
     loss_vectors()
+    densify_vectors(_ref_gaussian_model())
     print("wrote", sorted(f for f in os.listdir(OUT) if f.endswith(".npz")))
