@@ -242,6 +242,8 @@ def main():
         "data": "synthetic (seeded; SURVEY.md §8d distribution)",
         "config": {"workload": wl["desc"], "gaussians": P, "sh_degree": deg, "width": W, "height": H,
                    "views_per_rank_per_step": len(my_views), "views_per_step": views_per_step,
+                   "render_exp2": "exact-polynomial" if os.environ.get("GSRAST_EXACT_EXP", "0") not in ("", "0")
+                   else "hardware v_exp_f32",
                    "parallelism": f"view-parallel dp{world}" +
                    (" + RCCL all-reduce of 59 f32/Gaussian" if world > 1 else "")},
         "render_mpix_s": round(W * H / t_render / 1e6, 1),

@@ -1,3 +1,5 @@
+#include <atomic>
+#include <cstdlib>
 // gs_api.hip -- C ABI (include/gsrast.h): argument validation, buffer layout, stage orchestration,
 // error capture, debug synchronisation and per-kernel HIP-event timing.
 #include <stdarg.h>
@@ -162,6 +164,19 @@ __global__ void k_export_splat(int P, const float4* splat, float* xy, float* co,
 }  // namespace gs
 
 using namespace gs;
+
+namespace gs {
+static std::atomic<int> g_exact_exp{-1};  // -1: not yet read from GSRAST_EXACT_EXP
+bool exact_exp() {
+  int v = g_exact_exp.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("GSRAST_EXACT_EXP");
+    v = (e && e[0] && e[0] != '0') ? 1 : 0;
+    g_exact_exp.store(v, std::memory_order_relaxed);
+  }
+  return v != 0;
+}
+}  // namespace gs
 
 extern "C" {
 
@@ -340,6 +355,13 @@ int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, voi
   if (!points || !out || !scratch) return set_error("missing pointer"), 1;
   knn_mean_dist2(P, points, out, (char*)scratch, (hipStream_t)stream);
   return t_failed ? 1 : 0;
+}
+
+/* ---- numerics mode of the render loops ---- */
+int gs_set_exact_exp(int exact) {
+  const int prev = exact_exp() ? 1 : 0;
+  gs::g_exact_exp.store(exact ? 1 : 0, std::memory_order_relaxed);
+  return prev;
 }
 
 /* ---- fused SSIM (utils/loss_utils.py:ssim) ---- */

@@ -27,6 +27,7 @@ struct Eval {
   f2 dy, G, alpha;
   bool cA, cB;
 };
+template <bool EXACT>
 __device__ __forceinline__ Eval eval_pair(float2 xy, float4 co, float pfx, f2 pfy, uint32_t e, uint32_t lastA,
                                           uint32_t lastB) {
   Eval v;
@@ -34,7 +35,7 @@ __device__ __forceinline__ Eval eval_pair(float2 xy, float4 co, float pfx, f2 pf
   v.dx = xy.x - pfx;
   v.dy = xy.y - pfy;
   const f2 power = falloff_log2_pk(co, v.dx, v.dy);  // log2(e) * power (co: fall_coefs)
-  v.G = gs_exp2_pk(power);
+  v.G = exp2_pk_m<EXACT>(power);
   const f2 oG = co.w * v.G;
   v.alpha.x = fminf(0.99f, oG.x);
   v.alpha.y = fminf(0.99f, oG.y);
@@ -62,6 +63,7 @@ static_assert(BWD_BATCH % 64 == 0, "batch must be whole waves");
 // two vertically adjacent pixels so every per-pixel quantity is a 2-vector (v_pk_*_f32).  The
 // per-entry gradient terms of the two pixels are pre-summed in the lane, summed over the wave
 // (wave_sum9_rows) and stored into the wave's LDS record by one lane per row.
+template <bool EXACT>
 __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ point_list,
                                                             const uint32_t* __restrict__ presort_gid,
@@ -220,8 +222,8 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         const bool has1 = m != 0;
         const uint32_t j1 = has1 ? (uint32_t)(g * 64 + __builtin_ctzll(m)) : j0;
         if (has1) m &= m - 1;
-        const Eval v0 = eval_pair(s_xy[j0], s_co[j0], pfx, pfy, n_eff - 1 - (base + j0), lastA, lastB);
-        Eval v1 = eval_pair(s_xy[j1], s_co[j1], pfx, pfy, n_eff - 1 - (base + j1), lastA, lastB);
+        const Eval v0 = eval_pair<EXACT>(s_xy[j0], s_co[j0], pfx, pfy, n_eff - 1 - (base + j0), lastA, lastB);
+        Eval v1 = eval_pair<EXACT>(s_xy[j1], s_co[j1], pfx, pfy, n_eff - 1 - (base + j1), lastA, lastB);
         v1.cA = v1.cA && has1;
         v1.cB = v1.cB && has1;
         if (__ballot(v0.cA || v0.cB) != 0) apply(j0, v0);
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
       while (m) {
         const uint32_t j = (uint32_t)(g * 64 + __builtin_ctzll(m));
         m &= m - 1;
-        const Eval v = eval_pair(s_xy[j], s_co[j], pfx, pfy, n_eff - 1 - (base + j), lastA, lastB);
+        const Eval v = eval_pair<EXACT>(s_xy[j], s_co[j], pfx, pfy, n_eff - 1 - (base + j), lastA, lastB);
         if (__ballot(v.cA || v.cB) != 0) apply(j, v);
       }
 #endif
@@ -265,8 +267,12 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
 void bwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                 const float* dL_dpix, float* gradrec, hipStream_t st) {
   const int tiles = c.gx * c.gy;
-  GS_LAUNCH("render_bwd", k_render_bwd, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges, bin.point_list,
-            bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, dL_dpix, gradrec);
+  if (exact_exp())
+    GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,
+              bin.point_list, bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, dL_dpix, gradrec);
+  else
+    GS_LAUNCH("render_bwd", k_render_bwd<false>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,
+              bin.point_list, bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, dL_dpix, gradrec);
 }
 
 // ------------------------------------------------------------------------------------------

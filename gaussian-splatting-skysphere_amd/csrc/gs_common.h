@@ -84,6 +84,25 @@ __device__ __forceinline__ f2 gs_exp2_pk(f2 t) {
   return r;
 }
 
+// Render-loop exp2 by numerics mode (gs_set_exact_exp): EXACT = the deterministic polynomial above,
+// mirrored by the CPU oracle (bit-exact forward); otherwise the hardware v_exp_f32 (<= 1 ulp, not
+// reproducible on the CPU), 11 -> 1 VALU ops per evaluation.  Same clamp to [-125, 0] in both.
+template <bool EXACT>
+__device__ __forceinline__ float exp2_m(float t) {
+  if constexpr (EXACT) return gs_exp2(t);
+  else return __builtin_amdgcn_exp2f(fminf(fmaxf(t, -125.0f), 0.0f));
+}
+template <bool EXACT>
+__device__ __forceinline__ f2 exp2_pk_m(f2 t) {
+  if constexpr (EXACT) return gs_exp2_pk(t);
+  else {
+    f2 r;
+    r.x = exp2_m<false>(t.x);
+    r.y = exp2_m<false>(t.y);
+    return r;
+  }
+}
+
 // log2(e) * power of a splat at pixel offset (dx, dy) = mean - pixel.  The conic is scaled once
 // per staged splat (fall_coefs): A = cxx (-log2e / 2), B = cxy (-log2e), C = cyy (-log2e / 2), and
 // t = dx (A dx + B dy) + C dy^2 takes two FMAs + three multiplies per pixel.  Bit-identical to

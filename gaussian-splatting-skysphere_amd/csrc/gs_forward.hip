@@ -435,6 +435,7 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
 #define GS_FWD_ILP 3
 #endif
 constexpr int FWD_ILP = GS_FWD_ILP;
+template <bool EXACT>
 __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                          const uint32_t* __restrict__ point_list,
                                                          const uint32_t* __restrict__ presort_gid,
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
         const float2 xy = s_xy[j[u]];
         const float4 co = s_co[j[u]];
         pw[u] = falloff_log2(co, xy.x - pfx, xy.y - pfy);  // log2(e) * power
-        al[u] = fminf(0.99f, co.w * gs_exp2(pw[u]));
+        al[u] = fminf(0.99f, co.w * exp2_m<EXACT>(pw[u]));
       }
 #pragma unroll
       for (int u = 0; u < FWD_ILP; u++) {
@@ -535,8 +536,12 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
 void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
                 hipStream_t st) {
   const int tiles = c.gx * c.gy;
-  GS_LAUNCH("render_fwd", k_render_fwd, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-            bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
+  if (exact_exp())
+    GS_LAUNCH("render_fwd", k_render_fwd<true>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
+              bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
+  else
+    GS_LAUNCH("render_fwd", k_render_fwd<false>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
+              bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
 }
 
 // ------------------------------------------------------------------------------------------

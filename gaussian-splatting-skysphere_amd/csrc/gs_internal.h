@@ -18,6 +18,10 @@
 
 namespace gs {
 
+// Numerics mode of the render loops (gs_set_exact_exp): true = deterministic exp2 (bit-exact with
+// the CPU oracle), false = hardware v_exp_f32 (default).  Process-wide, read at launch time.
+bool exact_exp();
+
 constexpr int GRAD_REC = 9;    // dcolor(3), dmean2D(2), dconic(xx, xy, yy), dopacity
 constexpr int ACC_STRIDE = 12;  // LDS row of one per-wave partial record: s0..7 + 4 partials of s8
 

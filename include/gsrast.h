@@ -120,6 +120,15 @@ int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const 
 size_t gs_knn_scratch_bytes(int P);
 int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, void* stream);
 
+/* ---- numerics mode of the render loops (process-wide) ----
+ * exact != 0: the render kernels evaluate exp2 with a deterministic polynomial that the CPU oracle
+ * mirrors, so the whole forward is bit-identical to the oracle.  exact == 0 (default): the
+ * hardware v_exp_f32 (<= 1 ulp); forward images / final_T then match the oracle within float
+ * tolerance, with identical integer outputs except near the alpha / T thresholds (tests/
+ * test_gpu_parity.py, fast-mode cases).  The initial mode comes from GSRAST_EXACT_EXP=1.
+ * Returns the previous mode.  Set it between steps, not while a step is in flight. */
+int gs_set_exact_exp(int exact);
+
 /* ---- fused SSIM of the photometric loss  <-  utils/loss_utils.py:ssim (train.py:91-92) ----
  * img1, img2: [planes, H, W] fp32 (planes = images x channels), window11_host: the 11 float32
  * weights of loss_utils.gaussian(11, 1.5) (host memory).  Forward writes per-plane sums of the

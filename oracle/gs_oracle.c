@@ -584,6 +584,14 @@ static void init_scene(Scene* s, int P, int D, int M, const float* bg, int W, in
 /* render forward                                                              */
 /* ------------------------------------------------------------------------------------------ */
 
+/* Optional per-pixel flags for the device's fast numerics mode (hardware exp2, <= 1 ulp): a pixel
+ * is marked when one of its discrete decisions sits so close to its threshold that a 1-ulp exp2
+ * or the drift of T it causes could flip it -- alpha within 1e-6 (relative) of 1/255, or a tested
+ * T(1 - alpha) within 2e-5 (relative) of 1e-4.  Side output only: the oracle's arithmetic is the
+ * same with or without it. */
+static unsigned char* g_near = NULL;
+void oracle_set_near_flags(unsigned char* flags) { g_near = flags; }
+
 static void render_fwd(const Scene* s, const Binned* b, float* out, float* finalT, uint32_t* ncontrib) {
     int W = s->W, H = s->H;
     int ntiles = s->gx * s->gy;
@@ -600,21 +608,26 @@ static void render_fwd(const Scene* s, const Binned* b, float* out, float* final
                     float pfx = (float)px, pfy = (float)py;
                     float T = 1.0f, C[3] = {0, 0, 0};
                     uint32_t contributor = 0, last = 0;
+                    int near = 0;
                     for (uint32_t k = r0; k < r1; k++) {
                         contributor++;
                         const Splat* o = &b->sp[b->inst[k].gid];
                         float dx = o->xy[0] - pfx, dy = o->xy[1] - pfy;
                         float power2 = falloff_log2(o->conic, dx, dy);
                         if (power2 > 0.0f) continue;
-                        float alpha = fminf(0.99f, o->opacity * oracle_exp2(power2));
+                        float a_raw = o->opacity * oracle_exp2(power2);
+                        if (g_near && fabs((double)a_raw * 255.0 - 1.0) < 1e-6) near = 1;
+                        float alpha = fminf(0.99f, a_raw);
                         if (alpha < 1.0f / 255.0f) continue;
                         float test_T = T * (1.0f - alpha);
+                        if (g_near && fabs((double)test_T * 1e4 - 1.0) < 2e-5) near = 1;
                         if (test_T < 0.0001f) break;
                         for (int c = 0; c < 3; c++) C[c] += o->rgb[c] * alpha * T;
                         T = test_T;
                         last = contributor;
                     }
                     size_t pix = (size_t)py * W + px;
+                    if (g_near) g_near[pix] = (unsigned char)near;
                     if (finalT) finalT[pix] = T;
                     if (ncontrib) ncontrib[pix] = last;
                     for (int c = 0; c < 3; c++) out[(size_t)c * H * W + pix] = C[c] + T * s->bg[c];

@@ -44,6 +44,7 @@ def lib():
         L.oracle_exp.argtypes = [ctypes.c_float]
         L.oracle_log.restype = ctypes.c_float
         L.oracle_log.argtypes = [ctypes.c_float]
+        L.oracle_set_near_flags.argtypes = [ctypes.c_void_p]
         L.oracle_forward.restype = ctypes.c_longlong
         L.oracle_backward.restype = ctypes.c_longlong
         _lib = L
@@ -95,9 +96,20 @@ class Scene:
                 ctypes.c_float(self.tanfovx), ctypes.c_float(self.tanfovy))
 
 
-def forward(sc: Scene, intermediates: bool = False):
-    """Returns dict(color[3,H,W], radii[P], num_rendered, and intermediates if asked)."""
+def forward(sc: Scene, intermediates: bool = False, near: bool = False):
+    """Returns dict(color[3,H,W], radii[P], num_rendered, and intermediates if asked).
+    near=True adds near[H,W] (uint8): pixels with a decision close to the alpha / T thresholds
+    (see oracle_set_near_flags in gs_oracle.c), for comparisons with the device's fast exp2."""
     L = lib()
+    if near:
+        flags = np.zeros((sc.H, sc.W), np.uint8)
+        L.oracle_set_near_flags(flags.ctypes.data_as(ctypes.c_void_p))
+        try:
+            out = forward(sc, intermediates)
+        finally:
+            L.oracle_set_near_flags(None)
+        out["near"] = flags
+        return out
     P, W, H = sc.P, sc.W, sc.H
     gx, gy = (W + 15) // 16, (H + 15) // 16
     color = np.zeros((3, H, W), np.float32)

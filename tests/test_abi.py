@@ -55,3 +55,19 @@ def test_knn_and_validation_errors_without_gpu():
     rc = lib.gs_forward_preprocess(0, 0, 1, None, 0, 16, None, None, None, None, None, 1.0, None, None, None,
                                    None, None, 0.5, 0.5, 0, None, None, ctypes.byref(nr), 0, None)
     assert rc != 0 and "image size" in _native.last_error()
+
+
+def test_numerics_mode_default_and_env():
+    """Fast exp2 is the default; GSRAST_EXACT_EXP=1 selects the bit-exact mode (fresh processes)."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, %r); from diff_gaussian_rasterization import _native; "
+            "L = _native.load(); print(L.gs_set_exact_exp(0), L.gs_set_exact_exp(1))") % os.path.join(
+                ROOT, "gaussian-splatting-skysphere_amd")
+    env = {k: v for k, v in os.environ.items() if k != "GSRAST_EXACT_EXP"}
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["0", "0"]
+    env["GSRAST_EXACT_EXP"] = "1"
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["1", "0"]
