@@ -24,7 +24,7 @@ namespace gs {
 struct Eval {
   float4 co;
   float dx;
-  f2 dy, G, alpha;
+  f2 dy, G, oG, alpha;
   bool cA, cB;
 };
 template <bool EXACT>
@@ -36,9 +36,9 @@ __device__ __forceinline__ Eval eval_pair(float2 xy, float4 co, float pfx, f2 pf
   v.dy = xy.y - pfy;
   const f2 power = falloff_log2_pk(co, v.dx, v.dy);  // log2(e) * power (co: fall_coefs)
   v.G = exp2_pk_m<EXACT>(power);
-  const f2 oG = co.w * v.G;
-  v.alpha.x = fminf(0.99f, oG.x);
-  v.alpha.y = fminf(0.99f, oG.y);
+  v.oG = co.w * v.G;
+  v.alpha.x = fminf(0.99f, v.oG.x);
+  v.alpha.y = fminf(0.99f, v.oG.y);
   v.cA = e < lastA && power.x <= 0.0f && v.alpha.x >= 1.0f / 255.0f;
   v.cB = e < lastB && power.y <= 0.0f && v.alpha.y >= 1.0f / 255.0f;
   return v;
@@ -109,6 +109,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   const f2 dp1 = {inA ? dL_dpix[HW + pixA] : 0.0f, inB ? dL_dpix[HW + pixB] : 0.0f};
   const f2 dp2 = {inA ? dL_dpix[2 * HW + pixA] : 0.0f, inB ? dL_dpix[2 * HW + pixB] : 0.0f};
   const f2 bg_dot = c.bg[0] * dp0 + c.bg[1] * dp1 + c.bg[2] * dp2;
+  const f2 tbg = -T_final * bg_dot;  // d(T_final bg . dL/dpix)/dalpha = tbg / (1 - alpha)
   f2 Aacc = 0.0f;  // sum_c accum_rec_c * dL/dpix_c
   f2 Lc = 0.0f;    // sum_c last_color_c * dL/dpix_c
   f2 last_alpha = 0.0f;
@@ -117,7 +118,6 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
 
   // gradient commit of entry j (walk order) for the lane's contributing pixels
   auto apply = [&](uint32_t j, const Eval& v) {
-    const float4 co = v.co;
     const f2 G = v.G, alpha = v.alpha, dy = v.dy;
     const float dx = v.dx;
     const bool cA = v.cA, cB = v.cB;
@@ -133,15 +133,15 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     const float4 rgb = s_rgb[j];
     const f2 omA = 1.f - alpha;
     f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
-    inv = inv * (2.0f - omA * inv);  // one Newton step: ~0.5 ulp, like the IEEE divide
+    inv = pk_fma(inv, pk_fma(-omA, inv, (f2)(1.0f)), inv);  // one Newton step: ~0.5 ulp, like the IEEE divide
     const f2 Tn = T * inv;
     const f2 dch = alpha * Tn;
-    const f2 Cd = rgb.x * dp0 + rgb.y * dp1 + rgb.z * dp2;
-    const f2 An = last_alpha * Lc + (1.f - last_alpha) * Aacc;
-    const f2 dLa = (Cd - An) * Tn + (-T_final * inv) * bg_dot;
+    const f2 Cd = pk_fma((f2)(rgb.z), dp2, pk_fma((f2)(rgb.y), dp1, rgb.x * dp0));
+    const f2 An = pk_fma(last_alpha, Lc - Aacc, Aacc);  // last_alpha Lc + (1 - last_alpha) Aacc
+    const f2 dLa = pk_fma(Cd - An, Tn, tbg * inv);
     const f2 dLm = {cA ? dLa.x : 0.0f, cB ? dLa.y : 0.0f};
     const f2 dcm = {cA ? dch.x : 0.0f, cB ? dch.y : 0.0f};
-    const f2 q = (co.w * dLm) * G;
+    const f2 q = v.oG * dLm;  // dL/dG G = o G dL/dalpha (not gated by the 0.99 clamp)
     const f2 w4 = q * dy;
     float s[GRAD_REC];
     s[0] = __builtin_fmaf(dcm.x, dp0.x, dcm.y * dp0.y);
