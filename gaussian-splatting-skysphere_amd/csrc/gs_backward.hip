@@ -131,36 +131,35 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     // accum_rec is carried as A = sum_c accum_rec_c dL/dpix_c and last_color as
     // Lc = sum_c last_color_c dL/dpix_c, which is all dL/dalpha needs.
     const float4 rgb = s_rgb[j];
-    const f2 omA = 1.f - alpha;
+    // A pixel that does not contribute is run as an alpha = 0 entry: T, accum_rec and last_alpha
+    // then pass through unchanged bit for bit (1 / (1 - 0) = 1, fma(0, x, A) = A) and its colour
+    // terms vanish, so only dL/dalpha needs a mask.
+    const f2 ae = {cA ? alpha.x : 0.0f, cB ? alpha.y : 0.0f};
+    const f2 omA = 1.f - ae;
     f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
     inv = pk_fma(inv, pk_fma(-omA, inv, (f2)(1.0f)), inv);  // one Newton step: ~0.5 ulp, like the IEEE divide
     const f2 Tn = T * inv;
-    const f2 dch = alpha * Tn;
+    const f2 dch = ae * Tn;
     const f2 Cd = pk_fma((f2)(rgb.z), dp2, pk_fma((f2)(rgb.y), dp1, rgb.x * dp0));
     const f2 An = pk_fma(last_alpha, Lc - Aacc, Aacc);  // last_alpha Lc + (1 - last_alpha) Aacc
     const f2 dLa = pk_fma(Cd - An, Tn, tbg * inv);
     const f2 dLm = {cA ? dLa.x : 0.0f, cB ? dLa.y : 0.0f};
-    const f2 dcm = {cA ? dch.x : 0.0f, cB ? dch.y : 0.0f};
     const f2 q = v.oG * dLm;  // dL/dG G = o G dL/dalpha (not gated by the 0.99 clamp)
     const f2 w4 = q * dy;
     float s[GRAD_REC];
-    s[0] = __builtin_fmaf(dcm.x, dp0.x, dcm.y * dp0.y);
-    s[1] = __builtin_fmaf(dcm.x, dp1.x, dcm.y * dp1.y);
-    s[2] = __builtin_fmaf(dcm.x, dp2.x, dcm.y * dp2.y);
+    s[0] = __builtin_fmaf(dch.x, dp0.x, dch.y * dp0.y);
+    s[1] = __builtin_fmaf(dch.x, dp1.x, dch.y * dp1.y);
+    s[2] = __builtin_fmaf(dch.x, dp2.x, dch.y * dp2.y);
     s[3] = dx * (q.x + q.y);
     s[4] = w4.x + w4.y;
     s[5] = dx * s[3];
     s[6] = dx * s[4];
     s[7] = __builtin_fmaf(w4.x, dy.x, w4.y * dy.y);
     s[8] = __builtin_fmaf(G.x, dLm.x, G.y * dLm.y);
-    T.x = cA ? Tn.x : T.x;
-    T.y = cB ? Tn.y : T.y;
-    Aacc.x = cA ? An.x : Aacc.x;
-    Aacc.y = cB ? An.y : Aacc.y;
-    Lc.x = cA ? Cd.x : Lc.x;
-    Lc.y = cB ? Cd.y : Lc.y;
-    last_alpha.x = cA ? alpha.x : last_alpha.x;
-    last_alpha.y = cB ? alpha.y : last_alpha.y;
+    T = Tn;
+    Aacc = An;
+    Lc = Cd;
+    last_alpha = ae;
     // wave sums: row r of d0 / d1 holds s[r] / s[4 + r]; every row of d8 a quarter of s[8]
     float d0, d1, d8;
     wave_sum9_rows(s, d0, d1, d8);
