@@ -510,9 +510,16 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
         const bool su = cu && tT < 0.0001f;  // T would drop below 1e-4: stop before this entry
         done = done || su;
         cu = cu && !su;
-        C0 = cu ? C0 + rgb.x * al[u] * T : C0;
-        C1 = cu ? C1 + rgb.y * al[u] * T : C1;
-        C2 = cu ? C2 + rgb.z * al[u] * T : C2;
+        if constexpr (EXACT) {  // upstream's order, (rgb alpha) T, mirrored by the oracle
+          C0 = cu ? C0 + rgb.x * al[u] * T : C0;
+          C1 = cu ? C1 + rgb.y * al[u] * T : C1;
+          C2 = cu ? C2 + rgb.z * al[u] * T : C2;
+        } else {  // one weight, three FMAs; a skipped entry adds rgb * 0 (C unchanged)
+          const float w = cu ? al[u] * T : 0.0f;
+          C0 = __builtin_fmaf(rgb.x, w, C0);
+          C1 = __builtin_fmaf(rgb.y, w, C1);
+          C2 = __builtin_fmaf(rgb.z, w, C2);
+        }
         T = cu ? tT : T;
         last = cu ? base + j[u] + 1 : last;
       }
