@@ -178,6 +178,13 @@ bool exact_exp() {
 }
 }  // namespace gs
 
+namespace gs {
+uint32_t next_scan_epoch() {
+  static std::atomic<uint32_t> e{0};
+  return (e.fetch_add(1, std::memory_order_relaxed) % ((1u << 30) - 1u)) + 1u;
+}
+}  // namespace gs
+
 extern "C" {
 
 int gs_abi_version(void) { return GSRAST_ABI_VERSION; }
@@ -269,6 +276,12 @@ int gs_forward_render(int P, const float* background, int W, int H, const float*
   img_layout(W, H, &img, (char*)image_buffer);
   fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
   fwd_render(c, geo, bin, img, out_color, st);
+  if (debug && !t_failed) {  // debug: surface a look-back wait that ran out (never expected)
+    uint32_t err = 0;
+    if (check_hip(hipMemcpyAsync(&err, &geo.counters[2], 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(err)") &&
+        check_hip(hipStreamSynchronize(st), "hipStreamSynchronize") && (err & 4u))
+      return set_error("ordering scan: look-back wait timed out"), 1;
+  }
   return t_failed ? 1 : 0;
 }
 

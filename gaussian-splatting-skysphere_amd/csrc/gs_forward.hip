@@ -231,23 +231,24 @@ struct SrcTilesByRank {
 struct DstOffsets {
   uint32_t* offsets;
   uint32_t* first;
-  const uint32_t* counters;  // [0] V, [1] I (set by the scan's partial pass before this runs)
+  const uint32_t* counters;  // [3] I (summed by preprocess, complete before this scan runs)
   uint32_t P;
   __device__ void operator()(uint32_t s, uint32_t ex, uint32_t v) const {
     offsets[s] = ex;
-    if (!dup_balanced(counters[1], P)) return;
+    if (!dup_balanced(counters[3], P)) return;
     for (uint32_t m = (ex + DUP_SLOTS - 1) / DUP_SLOTS; m * DUP_SLOTS < ex + v; m++) first[m] = s;
   }
 };
 
 void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
   const uint32_t n = (uint32_t)P;
-  scan_exclusive(SrcVisible{geo.tiles}, DstCompact{geo.depth_key, geo.keys_a, geo.vals_a}, nullptr, n,
-                 geo.scan_partial, &geo.counters[0], st);
+  scan_exclusive_lb(SrcVisible{geo.tiles}, DstCompact{geo.depth_key, geo.keys_a, geo.vals_a}, nullptr, n,
+                    geo.lb_status, &geo.counters[8], &geo.counters[0], &geo.counters[2], st);
   radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, false, &geo.counters[0], n, 32, geo.sort_scratch,
                    st);
-  scan_exclusive(SrcTilesByRank{geo.tiles, geo.sorted_gid}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
-                 &geo.counters[0], n, geo.scan_partial, &geo.counters[1], st);
+  scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid},
+                    DstOffsets{geo.offsets, geo.dup_first, geo.counters, n}, &geo.counters[0], n, geo.lb_status,
+                    &geo.counters[9], &geo.counters[1], &geo.counters[2], st);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -69,8 +69,11 @@ struct GeomPtrs {
   uint32_t* dup_first;  // [P + 1] depth rank owning the first instance slot of each duplicate block
   float* gsum;  // [P][9] per-Gaussian sums of the backward records (k_sum_records -> k_preprocess_bwd)
   uint32_t* scan_partial;
+  uint64_t* lb_status;  // look-back scan status words (lb_tiles(P))
   uint32_t* sort_scratch;
-  uint32_t* counters;  // [0] visible V, [1] instances I, [2] error flags
+  // [0] visible V, [1] instances I, [2] error flags (1 prefiltered cull, 4 look-back timeout),
+  // [3] num_rendered from preprocess, [8] / [9] look-back tile counters (compaction / offsets)
+  uint32_t* counters;
   uint32_t* sorted_gid;  // = vals_a or vals_b after the depth sort
 };
 
@@ -90,6 +93,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   size_t o_df = take((Pn + 1) * 4);
   size_t o_gs = take(Pn * 4 * GRAD_REC);
   size_t o_sp = take((size_t)scan_plan(Pn).nb * 4 + 64);
+  size_t o_lb = take((size_t)lb_tiles(Pn) * 8);
   size_t o_ss = take(sort_scratch_words(Pn) * 4);
   size_t o_cnt = take(64);
   if (out && base) {
@@ -107,6 +111,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
     out->dup_first = (uint32_t*)(base + o_df);
     out->gsum = (float*)(base + o_gs);
     out->scan_partial = (uint32_t*)(base + o_sp);
+    out->lb_status = (uint64_t*)(base + o_lb);
     out->sort_scratch = (uint32_t*)(base + o_ss);
     out->counters = (uint32_t*)(base + o_cnt);
     out->sorted_gid = (radix_passes(32) % 2 == 0) ? out->vals_a : out->vals_b;

@@ -146,6 +146,136 @@ inline void scan_exclusive(Src src, Dst dst, const uint32_t* n_dev, uint32_t n_m
             p.chunk, partial);
 }
 
+// ------------------------------------------------------------------------------------------
+// Single-pass exclusive scan with decoupled look-back (1 launch instead of reduce / partials /
+// down-sweep).  Each workgroup takes the next tile id from a counter (ids follow start order, so
+// a workgroup only ever waits for workgroups that are already running), scans its 2048-element
+// tile, publishes its aggregate, then one wave looks back 64 predecessors at a time until it
+// finds an inclusive prefix, and publishes its own.  A status word is one 64-bit atomic:
+// [63:34] epoch (per call, so stale words from earlier calls never match), [33:32] state
+// (1 aggregate, 2 inclusive prefix), [31:0] value.  The counter must be 0 at launch (the forward
+// zeroes its counters before preprocessing).  Waits are bounded: a word that never arrives sets
+// err_flag bit 2 and the scan finishes (with a wrong result) instead of hanging the device.
+// ------------------------------------------------------------------------------------------
+constexpr int LB_THREADS = 256;
+constexpr int LB_ITEMS = 8;
+constexpr int LB_TILE = LB_THREADS * LB_ITEMS;  // 2048 elements
+constexpr uint64_t LB_AGG = 1, LB_PREFIX = 2;
+constexpr uint32_t LB_SPIN_LIMIT = 1u << 22;
+constexpr uint32_t LB_STATIC_MAX = 512;
+
+inline uint32_t lb_tiles(uint64_t n_max) { return (uint32_t)((n_max + LB_TILE - 1) / LB_TILE) + (n_max == 0); }
+
+__device__ __forceinline__ uint64_t lb_word(uint32_t epoch, uint64_t state, uint32_t v) {
+  return ((uint64_t)epoch << 34) | (state << 32) | v;
+}
+__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t w) {
+  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class Src, class Dst>
+__global__ __launch_bounds__(LB_THREADS) void k_scan_lb(Src src, Dst dst, const uint32_t* n_dev, uint32_t n_max,
+                                                        uint64_t* __restrict__ status, uint32_t* tile_counter,
+                                                        uint32_t epoch, uint32_t* total_out, uint32_t* err_flag) {
+  __shared__ uint32_t sh[4];
+  __shared__ uint32_t s_tile, s_excl;
+  // Tile ids: with a grid every CU can hold at once (LB_STATIC_MAX workgroups, a quarter of the
+  // residency of this small kernel) all workgroups run concurrently and blockIdx is safe;
+  // larger grids take ids in start order from the counter (one same-address atomic per workgroup).
+  uint32_t tile = blockIdx.x;
+  if (gridDim.x > LB_STATIC_MAX) {
+    if (threadIdx.x == 0) s_tile = atomicAdd(tile_counter, 1u);
+    __syncthreads();
+    tile = s_tile;
+  }
+  const uint32_t n = resolve_n(n_dev, n_max);
+  const uint64_t i0 = (uint64_t)tile * LB_TILE + (uint64_t)threadIdx.x * LB_ITEMS;
+  uint32_t v[LB_ITEMS], loc = 0;
+#pragma unroll
+  for (int k = 0; k < LB_ITEMS; k++) {
+    v[k] = (i0 + k < n) ? src((uint32_t)(i0 + k)) : 0u;
+    loc += v[k];
+  }
+  uint32_t agg;
+  uint32_t ex = block_excl_scan(loc, sh, &agg);
+  if (threadIdx.x < 64) {
+    const uint32_t lane = threadIdx.x;
+    if (lane == 0) lb_store(&status[tile], lb_word(epoch, tile == 0 ? LB_PREFIX : LB_AGG, agg));
+    // look back LB_WIN predecessors per round: lane l holds tiles t - 4l .. t - 4l - 3
+    uint32_t excl = 0;
+    int64_t t = (int64_t)tile - 1;
+    while (t >= 0) {
+      uint64_t w[4];
+      bool ready = true;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int64_t idx = t - 4 * (int64_t)lane - k;
+        w[k] = idx >= 0 ? lb_load(&status[idx]) : lb_word(epoch, LB_PREFIX, 0);
+        ready = ready && (uint32_t)(w[k] >> 34) == epoch;
+      }
+      uint32_t spins = 0;
+      while (__ballot(!ready) != 0) {  // wait until every word of the window has been published
+        __builtin_amdgcn_s_sleep(1);
+        ready = true;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int64_t idx = t - 4 * (int64_t)lane - k;
+          if ((uint32_t)(w[k] >> 34) != epoch) w[k] = lb_load(&status[idx]);
+          ready = ready && (uint32_t)(w[k] >> 34) == epoch;
+        }
+        if (++spins > LB_SPIN_LIMIT) {
+          if (lane == 0) atomicOr(err_flag, 4u);
+#pragma unroll
+          for (int k = 0; k < 4; k++) w[k] = lb_word(epoch, LB_PREFIX, 0);
+          ready = true;
+        }
+      }
+      // nearest inclusive prefix: first (lane, k) in window order
+      int kf = 4;
+#pragma unroll
+      for (int k = 3; k >= 0; k--)
+        if (((w[k] >> 32) & 3u) == LB_PREFIX) kf = k;
+      const uint64_t pm = __ballot(kf < 4);
+      const uint32_t stop = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
+      uint32_t c = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (lane < stop || (lane == stop && k <= kf)) c += (uint32_t)w[k];
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d, 64);
+      excl += c;
+      if (pm) break;
+      t -= 256;
+    }
+    if (lane == 0) {
+      if (tile > 0) lb_store(&status[tile], lb_word(epoch, LB_PREFIX, excl + agg));
+      s_excl = excl;
+      if (tile == gridDim.x - 1 && total_out) *total_out = excl + agg;
+    }
+  }
+  __syncthreads();
+  ex += s_excl;
+#pragma unroll
+  for (int k = 0; k < LB_ITEMS; k++) {
+    if (i0 + k < n) dst((uint32_t)(i0 + k), ex, v[k]);
+    ex += v[k];
+  }
+}
+
+uint32_t next_scan_epoch();  // host: a fresh non-zero epoch per call (gs_api.hip)
+
+// host: one-launch scan.  status needs lb_tiles(n_max) u64; *tile_counter must be 0.
+template <class Src, class Dst>
+inline void scan_exclusive_lb(Src src, Dst dst, const uint32_t* n_dev, uint32_t n_max, uint64_t* status,
+                              uint32_t* tile_counter, uint32_t* total_out, uint32_t* err_flag, hipStream_t st) {
+  const uint32_t tiles = lb_tiles(n_max);
+  GS_LAUNCH("scan_lb", (k_scan_lb<Src, Dst>), dim3(tiles), dim3(LB_THREADS), 0, st, src, dst, n_dev, n_max, status,
+            tile_counter, next_scan_epoch(), total_out, err_flag);
+}
+
 // simple functors
 struct SrcArray {
   const uint32_t* a;
