@@ -245,12 +245,12 @@ int gs_forward_preprocess(int P, int D, int M, const float* background, int W, i
   ReadbackSlot* rb = readback_slot();
   if (!rb) return 1;
   fwd_preprocess(g, c, radii_out, geo, st);
-  check_hip(hipMemcpyAsync(rb->host, geo.counters, 16, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
+  check_hip(hipMemcpyAsync(rb->host, geo.counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
   check_hip(hipEventRecord(rb->ev, st), "hipEventRecord");
   fwd_order(P, geo, st);
   check_hip(hipEventSynchronize(rb->ev), "hipEventSynchronize");
   if (t_failed) return 1;
-  const uint32_t err = rb->host[2], I = rb->host[3];
+  const uint32_t err = rb->host[CNT_ERR], I = rb->host[CNT_NREND];
   if (err & 1u) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
   *num_rendered_host = (long long)I;
   return 0;
@@ -278,7 +278,7 @@ int gs_forward_render(int P, const float* background, int W, int H, const float*
   fwd_render(c, geo, bin, img, out_color, st);
   if (debug && !t_failed) {  // debug: surface a look-back wait that ran out (never expected)
     uint32_t err = 0;
-    if (check_hip(hipMemcpyAsync(&err, &geo.counters[2], 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(err)") &&
+    if (check_hip(hipMemcpyAsync(&err, &geo.counters[CNT_ERR], 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(err)") &&
         check_hip(hipStreamSynchronize(st), "hipStreamSynchronize") && (err & 4u))
       return set_error("ordering scan: look-back wait timed out"), 1;
   }

@@ -303,7 +303,7 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
                                                                    float* __restrict__ gsum) {
   __shared__ double s_acc[SUMREC_WAVES][64][GRAD_REC];
   __shared__ unsigned long long s_mark[SUMREC_WAVES];
-  const uint32_t V = counters[0], I = counters[1];
+  const uint32_t V = counters[CNT_V], I = counters[CNT_I];
   const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t r0 = (blockIdx.x * SUMREC_WAVES + wid) * 64;
   if (r0 >= V) return;  // wave-uniform; the kernel has no workgroup barrier
@@ -315,7 +315,22 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
   for (int c = 0; c < GRAD_REC; c++) s_acc[wid][lane][c] = 0.0;
   const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
   uint32_t jbase = 0xFFFFFFFFu;  // (number of owners starting before `base`) - 1
+  // records of the next chunk are loaded one chunk ahead (their HBM latency overlaps this chunk)
+  float vn[GRAD_REC];
+  {
+    const size_t kk = (size_t)min(S0 + lane, S1 - 1);
+#pragma unroll
+    for (int c = 0; c < GRAD_REC; c++) vn[c] = S0 < S1 ? gradrec[kk * GRAD_REC + c] : 0.0f;
+  }
   for (uint32_t base = S0; base < S1; base += 64) {
+    float v[GRAD_REC];
+#pragma unroll
+    for (int c = 0; c < GRAD_REC; c++) v[c] = vn[c];
+    if (base + 64 < S1) {
+      const size_t kn = (size_t)min(base + 64 + lane, S1 - 1);
+#pragma unroll
+      for (int c = 0; c < GRAD_REC; c++) vn[c] = gradrec[kn * GRAD_REC + c];
+    }
     // slots of the chunk that start an owner -> bit mask -> owner of my slot by popcount
     if (lane == 0) s_mark[wid] = 0ull;
     __builtin_amdgcn_wave_barrier();
@@ -326,10 +341,6 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
     jbase += (uint32_t)__popcll(B);
     const uint32_t k = base + lane;
     const bool valid = k < S1;
-    const size_t kk = (size_t)(valid ? k : S1 - 1);
-    float v[GRAD_REC];
-#pragma unroll
-    for (int c = 0; c < GRAD_REC; c++) v[c] = gradrec[kk * GRAD_REC + c];
 #pragma unroll
     for (int c = 0; c < GRAD_REC; c++) v[c] = valid ? v[c] : 0.0f;
     const uint32_t own1 = valid ? own + 1 : 0;

@@ -4,8 +4,9 @@
 // /root/reference/.gitmodules:4-6; spec SURVEY.md §8a a4-a6) as:
 //   k_preprocess   one lane per Gaussian: cull, project, cov3D -> EWA cov2D -> conic, radius,
 //                  tile rectangle, SH -> RGB; writes the 48-B splat record used by render.
-//   fwd_order      visibility compaction (scan), stable 32-bit depth radix sort of the visible
-//                  Gaussians, exclusive scan of their tile counts in depth order.
+//   fwd_order      stable 32-bit depth radix sort of the Gaussians with instances (the first
+//                  pass drops the others: compaction), exclusive scan of their tile counts in
+//                  depth order.
 //   k_duplicate    one lane per depth-ranked Gaussian writes its (tile, slot) instances; slots of
 //                  a Gaussian are contiguous and in depth order.
 //   tile sort      stable radix sort of the instances by tile id only: because the input is
@@ -77,15 +78,15 @@ __device__ __forceinline__ void sh_to_rgb(const float* __restrict__ sh, int M, f
 template <int DEG>
 __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g, const CameraArgs& c,
                                                    int* __restrict__ radii, float4* __restrict__ splat,
-                                                   float4* __restrict__ binrec,
-                                                   uint32_t* __restrict__ depth_key, uint32_t* __restrict__ tiles,
-                                                   uint8_t* __restrict__ clamped, uint32_t* __restrict__ counters) {
+                                                   float4* __restrict__ binrec, uint32_t& dbits,
+                                                   uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
+                                                   uint32_t* __restrict__ counters) {
   radii[i] = 0;
   tiles[i] = 0;
   const float px = g.means3D[3 * i + 0], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
   const float3v pv = xf43(c.view, px, py, pz);
   if (pv.z <= 0.2f) {
-    if (c.prefiltered) atomicOr(&counters[2], 1u);
+    if (c.prefiltered) atomicOr(&counters[CNT_ERR], 1u);
     return 0;
   }
   const float* P = c.proj;
@@ -136,7 +137,7 @@ __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g,
   splat[3 * i + 0] = make_float4(sx, sy, cxx, cxy);
   splat[3 * i + 1] = make_float4(cyy, op, rgb[0], rgb[1]);
   splat[3 * i + 2] = make_float4(rgb[2], pv.z, lim, 0.0f);
-  depth_key[i] = __float_as_uint(pv.z);
+  dbits = __float_as_uint(pv.z);
   radii[i] = radius;  // upstream visibility: the rectangle is non-empty
   // tile-exact instance count (may be 0 for a visible splat whose alpha never reaches 1/255)
   const SpanCtx sp = span_ctx(sx, sy, cxx, cxy, cyy, lim, x0, x1);
@@ -154,25 +155,38 @@ __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g,
   return count;
 }
 
-// The workgroup's tile total goes to counters[3] (= num_rendered, read back by the host as soon
-// as this kernel is done while the ordering kernels run).
+// The workgroup's tile total (num_rendered, read back by the host as soon as this kernel is done
+// while the ordering kernels run) and its count of Gaussians with instances (V) go to
+// counters[CNT_NREND] / [CNT_V] by one 64-bit atomic add.  depth_key[i] is the depth's bits for those and DEPTH_DROP for every other
+// Gaussian: the first depth-sort pass drops them, which is the visibility compaction.
 template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
                                                     float4* __restrict__ splat, float4* __restrict__ binrec,
                                                     uint32_t* __restrict__ depth_key,
                                                     uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
                                                     uint32_t* __restrict__ counters) {
-  __shared__ uint32_t s_sum[4];
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  uint32_t area = 0;
-  if (i < g.P) area = preprocess_one<DEG>(i, g, c, radii, splat, binrec, depth_key, tiles, clamped, counters);
+  __shared__ uint32_t s_sum[4], s_vis[4];
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  uint32_t area = 0, dbits = 0;
+  if (i < g.P) {
+    area = preprocess_one<DEG>(i, g, c, radii, splat, binrec, dbits, tiles, clamped, counters);
+    depth_key[i] = area ? dbits : DEPTH_DROP;
+  }
+  uint32_t vis = area ? 1u : 0u;
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) area += (uint32_t)__shfl_xor((int)area, d, 64);
-  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = area;
+  for (int d = 32; d >= 1; d >>= 1) {
+    area += (uint32_t)__shfl_xor((int)area, d, 64);
+    vis += (uint32_t)__shfl_xor((int)vis, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_sum[threadIdx.x >> 6] = area;
+    s_vis[threadIdx.x >> 6] = vis;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-    if (tot) atomicAdd(&counters[3], tot);
+    const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
+    if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(&counters[CNT_NREND]), ((unsigned long long)nv << 32) | tot);
   }
 }
 
@@ -180,25 +194,25 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
   (void)hipMemsetAsync(geo.counters, 0, 64, st);
   dim3 grid((g.P + 255) / 256), block(256);
   if (g.colors) {
-    GS_LAUNCH("preprocess", k_preprocess<-1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
+    GS_LAUNCH("preprocess", k_preprocess<-1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
               geo.clamped, geo.counters);
     return;
   }
   switch (g.D) {
     case 0:
-      GS_LAUNCH("preprocess", k_preprocess<0>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
+      GS_LAUNCH("preprocess", k_preprocess<0>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
                 geo.clamped, geo.counters);
       break;
     case 1:
-      GS_LAUNCH("preprocess", k_preprocess<1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
+      GS_LAUNCH("preprocess", k_preprocess<1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
                 geo.clamped, geo.counters);
       break;
     case 2:
-      GS_LAUNCH("preprocess", k_preprocess<2>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
+      GS_LAUNCH("preprocess", k_preprocess<2>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
                 geo.clamped, geo.counters);
       break;
     default:
-      GS_LAUNCH("preprocess", k_preprocess<3>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.depth_key, geo.tiles,
+      GS_LAUNCH("preprocess", k_preprocess<3>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
                 geo.clamped, geo.counters);
       break;
   }
@@ -207,20 +221,6 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
 // ------------------------------------------------------------------------------------------
 // ordering: compaction -> depth sort -> instance offsets
 // ------------------------------------------------------------------------------------------
-struct SrcVisible {
-  const uint32_t* tiles;
-  __device__ uint32_t operator()(uint32_t i) const { return tiles[i] > 0 ? 1u : 0u; }
-};
-struct DstCompact {
-  const uint32_t* depth_key;
-  uint32_t *keys, *vals;
-  __device__ void operator()(uint32_t i, uint32_t ex, uint32_t v) const {
-    if (v) {
-      keys[ex] = depth_key[i];
-      vals[ex] = i;
-    }
-  }
-};
 struct SrcTilesByRank {
   const uint32_t *tiles, *sorted_gid;
   __device__ uint32_t operator()(uint32_t s) const { return tiles[sorted_gid[s]]; }
@@ -231,24 +231,24 @@ struct SrcTilesByRank {
 struct DstOffsets {
   uint32_t* offsets;
   uint32_t* first;
-  const uint32_t* counters;  // [3] I (summed by preprocess, complete before this scan runs)
+  const uint32_t* counters;  // [CNT_NREND] I (summed by preprocess, complete before this scan runs)
   uint32_t P;
   __device__ void operator()(uint32_t s, uint32_t ex, uint32_t v) const {
     offsets[s] = ex;
-    if (!dup_balanced(counters[3], P)) return;
+    if (!dup_balanced(counters[CNT_NREND], P)) return;
     for (uint32_t m = (ex + DUP_SLOTS - 1) / DUP_SLOTS; m * DUP_SLOTS < ex + v; m++) first[m] = s;
   }
 };
 
 void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
   const uint32_t n = (uint32_t)P;
-  scan_exclusive_lb(SrcVisible{geo.tiles}, DstCompact{geo.depth_key, geo.keys_a, geo.vals_a}, nullptr, n,
-                    geo.lb_status, &geo.counters[8], &geo.counters[0], &geo.counters[2], st);
-  radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, false, &geo.counters[0], n, 32, geo.sort_scratch,
-                   st);
+  // depth sort of the Gaussians with instances: the first pass reads all P keys in index order
+  // and drops the DEPTH_DROP ones (compaction), the later passes sort the V survivors
+  radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32, geo.sort_scratch,
+                   st, /*drop_first=*/true);
   scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid},
-                    DstOffsets{geo.offsets, geo.dup_first, geo.counters, n}, &geo.counters[0], n, geo.lb_status,
-                    &geo.counters[9], &geo.counters[1], &geo.counters[2], st);
+                    DstOffsets{geo.offsets, geo.dup_first, geo.counters, n}, &geo.counters[CNT_V], n, geo.lb_status,
+                    &geo.counters[CNT_LB_TILE], &geo.counters[CNT_I], &geo.counters[CNT_ERR], st);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* _
                                                    uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
                                                    uint32_t* __restrict__ presort_gid) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-  if (s >= P || s >= counters[0]) return;
+  if (s >= P || s >= counters[CNT_V]) return;
   const uint32_t gid = sorted_gid[s];
   uint32_t off = offsets[s];
   goff[gid] = off;
@@ -302,17 +302,19 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     uint32_t I, const uint32_t* __restrict__ counters, const uint32_t* __restrict__ dup_first,
     const uint32_t* __restrict__ sorted_gid, const uint32_t* __restrict__ offsets,
     const float4* __restrict__ binrec, int gx, int gy, uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
-    uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges) {
+    uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges, uint32_t* __restrict__ hist0, uint32_t mask0) {
   __shared__ uint32_t s_own[DUP_SLOTS + DUP_SLOTS / 8];  // (slot + 1) << 16 | segment at segment starts
   __shared__ uint32_t s_seg_start[DUP_SLOTS];  // first slot of the row segment (may precede the block)
   __shared__ uint32_t s_seg_tile[DUP_SLOTS];   // tile id of the segment's first slot
   __shared__ uint32_t s_seg_gid[DUP_SLOTS];
   __shared__ uint32_t s_wmax[DUP_THREADS / 64];
   __shared__ uint32_t s_nseg;
+  __shared__ uint32_t s_hist[RADIX];
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  s_hist[tid] = 0;
   const uint32_t tiles = (uint32_t)(gx * gy);
   for (uint32_t t = b * DUP_THREADS + tid; t < tiles; t += gridDim.x * DUP_THREADS) ranges[t] = make_uint2(0u, 0u);
-  const uint32_t V = counters[0];
+  const uint32_t V = counters[CNT_V];
   const uint32_t k0 = b * DUP_SLOTS;
   const uint32_t k1 = min(k0 + DUP_SLOTS, I);
   const uint32_t s_lo = dup_first[b];
@@ -376,9 +378,17 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     const uint32_t k = k0 + i;
     if (k < k1) {
       const uint32_t o = s_own[own_idx(i)] & 0xFFFFu;
-      tile_keys[k] = s_seg_tile[o] + (k - s_seg_start[o]);
+      const uint32_t key = s_seg_tile[o] + (k - s_seg_start[o]);
+      tile_keys[k] = key;
       presort_gid[k] = s_seg_gid[o];
+      if (hist0) atomicAdd(&s_hist[key & mask0], 1u);  // counts only: order-free
     }
+  }
+  // the tile sort's first-pass digit counts of this block's slots (its sort tile is the same 2048
+  // slots): the sort skips that pass's counting launch
+  if (hist0) {
+    __syncthreads();
+    hist0[(size_t)tid * gridDim.x + b] = s_hist[tid];
   }
 }
 
@@ -415,17 +425,22 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
     (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
     return;
   }
+  const int tbits = tile_bits(tiles);
+  bool hist0 = false;
   if (dup_balanced(I, (uint32_t)P)) {
+    // one duplicate block per sort tile: the duplicate also counts the first sort pass's digits
+    hist0 = sort_plan(I).chunk == DUP_SLOTS;
     GS_LAUNCH("duplicate", k_duplicate_lb, dim3((I + DUP_SLOTS - 1) / DUP_SLOTS), dim3(DUP_THREADS), 0, st, I,
               geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy, geo.goff,
-              bin.keys_a, bin.presort_gid, img.ranges);
+              bin.keys_a, bin.presort_gid, img.ranges, hist0 ? bin.sort_scratch : nullptr,
+              (1u << radix_first_bits(tbits)) - 1u);
   } else {
     (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
     GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
               geo.sorted_gid, geo.offsets, geo.binrec, c.gx, geo.goff, bin.keys_a, bin.presort_gid);
   }
-  radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tile_bits(tiles),
-                   bin.sort_scratch, st);
+  radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tbits, bin.sort_scratch, st,
+                   false, hist0);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges);
 }
 

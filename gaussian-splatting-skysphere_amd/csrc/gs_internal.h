@@ -3,8 +3,9 @@
 // upstream's geomBuffer / binningBuffer / imgBuffer).
 //
 // Layout (all arrays 256-B aligned, structure-of-arrays except the 48-B splat record):
-//   geometry  (per Gaussian, P)      splat float4x3 | depth_key u32 | tiles u32 | goff u32 |
-//                                    clamped u8 | depth-sort keys/vals x2 u32 | offsets u32 |
+//   geometry  (per Gaussian, P)      splat float4x3 | binrec float4x2 | tiles u32 | goff u32 |
+//                                    clamped u8 | depth-sort keys/vals x2 u32 (keys_a: depth keys
+//                                    written by preprocess) | offsets u32 |
 //                                    scan partials | sort scratch | counters
 //   binning   (per instance, I)      tile keys/vals x2 u32 | presort_gid u32 | sort scratch
 //   image     (per pixel / tile)     ranges uint2 | final_T f32 | n_contrib u32 | tile_max u32
@@ -57,10 +58,11 @@ struct CameraArgs {
   int prefiltered;
 };
 
+constexpr int CNT_I = 1, CNT_ERR = 2, CNT_NREND = 4, CNT_V = 5, CNT_LB_TILE = 9;
+
 struct GeomPtrs {
   float4* splat;  // 3 per Gaussian: (x, y, cxx, cxy) (cyy, opacity, r, g) (b, depth, cull_lim, -)
   float4* binrec;  // 2 per Gaussian: (x, y, cxx, cxy) (cyy, cull_lim, x0 | x1 << 16, y0 | y1 << 16) for binning
-  uint32_t* depth_key;
   uint32_t* tiles;
   uint32_t* goff;  // first instance slot of each visible Gaussian (depth order)
   uint8_t* clamped;
@@ -71,8 +73,9 @@ struct GeomPtrs {
   uint32_t* scan_partial;
   uint64_t* lb_status;  // look-back scan status words (lb_tiles(P))
   uint32_t* sort_scratch;
-  // [0] visible V, [1] instances I, [2] error flags (1 prefiltered cull, 4 look-back timeout),
-  // [3] num_rendered from preprocess, [8] / [9] look-back tile counters (compaction / offsets)
+  // [1] instances I (offsets scan), [2] error flags (1 prefiltered cull, 4 look-back timeout),
+  // [4] / [5] num_rendered / V (Gaussians with instances) summed by preprocess as ONE 64-bit
+  // word (one same-address atomic per workgroup), [9] look-back tile counter (offsets scan)
   uint32_t* counters;
   uint32_t* sorted_gid;  // = vals_a or vals_b after the depth sort
 };
@@ -87,7 +90,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   size_t Pn = P ? P : 1;
   size_t o_splat = take(Pn * 48);
   size_t o_bin = take(Pn * 32);
-  size_t o_dkey = take(Pn * 4), o_tiles = take(Pn * 4), o_goff = take(Pn * 4), o_cl = take(Pn);
+  size_t o_tiles = take(Pn * 4), o_goff = take(Pn * 4), o_cl = take(Pn);
   size_t o_ka = take(Pn * 4), o_va = take(Pn * 4), o_kb = take(Pn * 4), o_vb = take(Pn * 4);
   size_t o_offs = take(Pn * 4);
   size_t o_df = take((Pn + 1) * 4);
@@ -99,7 +102,6 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   if (out && base) {
     out->splat = (float4*)(base + o_splat);
     out->binrec = (float4*)(base + o_bin);
-    out->depth_key = (uint32_t*)(base + o_dkey);
     out->tiles = (uint32_t*)(base + o_tiles);
     out->goff = (uint32_t*)(base + o_goff);
     out->clamped = (uint8_t*)(base + o_cl);

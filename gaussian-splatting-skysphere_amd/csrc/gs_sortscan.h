@@ -296,6 +296,7 @@ struct DstArray {
 // ballot peer masks (stable), the 4 waves are combined per digit in LDS, the tile is reordered by
 // digit in LDS, and runs of equal digits are written out contiguously (coalesced stores).
 // ------------------------------------------------------------------------------------------
+constexpr uint32_t DEPTH_DROP = 0xFFFFFFFFu;  // key of a Gaussian without instances (dropped)
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;
 constexpr int SORT_THREADS = 256;
@@ -308,6 +309,12 @@ struct SortPlan {
 };
 
 inline int radix_passes(int end_bit) { return (end_bit + RADIX_BITS - 1) / RADIX_BITS; }
+// digit width of every pass (the last may be narrower): equal widths, 13 bits -> 7 + 6
+inline int radix_width(int end_bit) {
+  const int np = radix_passes(end_bit);
+  return (end_bit + np - 1) / np;
+}
+inline int radix_first_bits(int end_bit) { return end_bit < radix_width(end_bit) ? end_bit : radix_width(end_bit); }
 
 inline SortPlan sort_plan(uint64_t n_max) {
   uint64_t tiles = (n_max + SORT_TILE - 1) / SORT_TILE;
@@ -339,7 +346,8 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits
 static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys,
                                                                      const uint32_t* n_dev, uint32_t n_max,
                                                                      int shift, int bits, uint32_t chunk,
-                                                                     uint32_t nb, uint32_t* __restrict__ hist) {
+                                                                     uint32_t nb, uint32_t* __restrict__ hist,
+                                                                     bool drop) {
   __shared__ uint32_t h[RADIX];
   const uint32_t n = resolve_n(n_dev, n_max);
   h[threadIdx.x] = 0;
@@ -353,8 +361,9 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32
 #pragma unroll
     for (int k = 0; k < SORT_ITEMS; k++) {
       const uint64_t i = t0 + (uint64_t)k * SORT_THREADS + threadIdx.x;
-      v[k] = i < end;
-      d[k] = v[k] ? (keys[i] >> shift) & mask : 0u;
+      const uint32_t key = i < end ? keys[i] : DEPTH_DROP;
+      v[k] = i < end && !(drop && key == DEPTH_DROP);
+      d[k] = (key >> shift) & mask;
     }
 #pragma unroll
     for (int k = 0; k < SORT_ITEMS; k++)
@@ -394,7 +403,7 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_rowscan(uint32_t*
 static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, int bits, uint32_t chunk,
-    uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ row_total) {
+    uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ row_total, bool drop) {
   __shared__ uint32_t s_base[RADIX];      // global position of the next key of each digit
   __shared__ uint32_t s_wcnt[4][RADIX];   // per-wave running counts -> per-wave exclusive prefix
   __shared__ uint32_t s_loc[RADIX];       // digit offsets inside the tile (for the LDS reorder)
@@ -430,7 +439,7 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
       const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
-      const bool v = i < end;
+      const bool v = i < end && !(drop && key[r] == DEPTH_DROP);
       const uint32_t d = (key[r] >> shift) & mask;
       const uint64_t peers = digit_peers(d, v, bits);
       const uint32_t before = (uint32_t)__popcll(peers & lanemask_lt());
@@ -458,7 +467,7 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
       const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
-      if (i < end) {
+      if (i < end && !(drop && key[r] == DEPTH_DROP)) {
         const uint32_t d = (key[r] >> shift) & mask;
         const uint32_t slot = s_loc[d] + s_wcnt[wid][d] + rank[r];
         s_key[slot] = key[r];
@@ -467,7 +476,7 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     }
     __syncthreads();
     // write runs of equal digits contiguously
-    const uint32_t ntile = (uint32_t)((end - t0) < (uint64_t)SORT_TILE ? (end - t0) : (uint64_t)SORT_TILE);
+    const uint32_t ntile = tot_all;  // keys kept in this tile
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
       const uint32_t slot = (uint32_t)r * SORT_THREADS + tid;
@@ -484,9 +493,13 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   }
 }
 
+// hist0_ready: the caller already wrote the first pass's [digit][block] counts into scratch.
+// drop_first: the first pass reads n_max keys (host count) and drops those equal to DEPTH_DROP;
+// the later passes then sort the *n_dev survivors.  Otherwise every pass sorts n (n_dev / n_max).
 static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b,
                                     bool vals_identity, const uint32_t* n_dev, uint32_t n_max, int end_bit,
-                                    uint32_t* scratch, hipStream_t st) {
+                                    uint32_t* scratch, hipStream_t st, bool drop_first = false,
+                                    bool hist0_ready = false) {
   SortPlan p = sort_plan(n_max);
   uint32_t* hist = scratch;
   const size_t hist_n = (size_t)RADIX * p.nb;
@@ -494,16 +507,18 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
   uint32_t *kin = keys_a, *vin = vals_a, *kout = keys_b, *vout = vals_b;
   bool in_b = false;
   // digits of (nearly) equal width: 13 bits -> 7 + 6, not 8 + 5 (longer runs in the first scatter)
-  const int npass = radix_passes(end_bit);
-  const int width = (end_bit + npass - 1) / npass;
+  const int width = radix_width(end_bit);
   for (int shift = 0; shift < end_bit; shift += width) {
     int bits = end_bit - shift < width ? end_bit - shift : width;
-    GS_LAUNCH("radix_hist", k_radix_hist, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, n_dev, n_max, shift, bits,
-              p.chunk, p.nb, hist);
+    const bool drop = drop_first && shift == 0;
+    const uint32_t* nd = drop ? nullptr : n_dev;
+    if (!(hist0_ready && shift == 0))
+      GS_LAUNCH("radix_hist", k_radix_hist, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, nd, n_max, shift, bits,
+                p.chunk, p.nb, hist, drop);
     GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX), dim3(SORT_THREADS), 0, st, hist, p.nb, row_total);
     const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
-    GS_LAUNCH("radix_scatter", k_radix_scatter, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, vsrc, kout, vout, n_dev,
-              n_max, shift, bits, p.chunk, p.nb, hist, row_total);
+    GS_LAUNCH("radix_scatter", k_radix_scatter, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, vsrc, kout, vout, nd,
+              n_max, shift, bits, p.chunk, p.nb, hist, row_total, drop);
     uint32_t* t;
     t = kin; kin = kout; kout = t;
     t = vin; vin = vout; vout = t;

@@ -390,6 +390,24 @@ def test_all_culled_scene_is_background(oracle, device):
         assert torch.all(v.grad == 0), k
 
 
+def test_interleaved_culled_gaussians(oracle, device):
+    """Culled Gaussians scattered through the index order (behind the camera, every third one):
+    the first depth-sort pass drops them inside every sort tile (the visibility compaction)."""
+    W, H = 160, 120
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(9000, 2, cam=cam, seed=12)
+    sc.means3D[::3, 2] = -sc.means3D[::3, 2]
+    bg = np.zeros(3, np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg)
+    ofw = oracle.forward(osc, intermediates=True)
+    ofw["bg"] = bg
+    _check_forward_exact(ofw, cam, sc, device)
+    dpix = gs_scenes.dl_dimage(H, W, seed=13).numpy()
+    _, radii, leaves = _gpu_run(cam, sc, device, bg, dpix)
+    assert torch.all(radii[::3] == 0) and int((radii > 0).sum()) > 3000
+    _check_backward(oracle.backward(osc, dpix), leaves)
+
+
 def test_multi_view_circle_cameras(oracle, device):
     """C4-style cameras (look-at, non-identity view) exercise the full view / projection path."""
     cams = gs_scenes.circle_cameras(3, 6.0, 200, 150)
