@@ -447,10 +447,11 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
 // ------------------------------------------------------------------------------------------
 // render forward
 // ------------------------------------------------------------------------------------------
-#ifndef GS_FWD_ILP
-#define GS_FWD_ILP 3
-#endif
-constexpr int FWD_ILP = GS_FWD_ILP;
+// Entries are staged as three 16-B LDS records at one byte offset o (o, o + 4 KB, o + 8 KB):
+//   (x, y, r, g) | falloff coefficients + opacity | (b, bits(entry index + 1), -, -)
+// and each quadrant wave's dense list holds the offsets (u16), read FWD_ILP = 4 at a time with one
+// 8-B LDS read: a list entry costs no address arithmetic and no dependent list read per entry.
+constexpr int FWD_ILP = 4;
 template <bool EXACT>
 __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                          const uint32_t* __restrict__ point_list,
@@ -458,11 +459,9 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
                                                          const float4* __restrict__ splat, float* __restrict__ out,
                                                          float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                          uint32_t* __restrict__ tile_max) {
-  __shared__ float2 s_xy[GS_BLOCK];
-  __shared__ float4 s_co[GS_BLOCK];
-  __shared__ float4 s_rgb[GS_BLOCK];
+  __shared__ float4 s_ent[3 * GS_BLOCK];
   __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
-  __shared__ uint16_t s_qlist[4][GS_BLOCK];  // per quadrant wave: its batch entries in order
+  __shared__ __attribute__((aligned(8))) uint16_t s_qlist[4][GS_BLOCK + FWD_ILP];  // per quadrant wave: byte offsets
   __shared__ uint32_t s_max;
   const uint32_t tile = blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
@@ -473,6 +472,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   const float pfx = (float)q.px, pfy = (float)q.py;
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
+  const char* ent = reinterpret_cast<const char*>(s_ent);
   if (tid == 0) s_max = 0;
   float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
   uint32_t last = 0;
@@ -484,42 +484,44 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
     if ((uint32_t)tid < cnt) {
       const uint32_t gid = presort_gid[point_list[range.x + base + tid]];
       const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
-      s_xy[tid] = make_float2(a.x, a.y);
-      s_co[tid] = fall_coefs(a.z, a.w, b.x, b.y);
-      s_rgb[tid] = make_float4(b.z, b.w, d.x, 0.0f);
+      s_ent[tid] = make_float4(a.x, a.y, b.z, b.w);
+      s_ent[GS_BLOCK + tid] = fall_coefs(a.z, a.w, b.x, b.y);
+      s_ent[2 * GS_BLOCK + tid] = make_float4(d.x, __uint_as_float(base + tid + 1), 0.0f, 0.0f);
       qmask = quadrant_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
     }
     publish_masks(qmask, s_mask, tid);
     __syncthreads();
     if (__ballot(!done) == 0) continue;
-    // dense, in-order list of this quadrant's entries, built by the wave itself (the per-entry
-    // walk then costs a uniform LDS read instead of a scalar bit-scan sequence)
+    // dense, in-order list of this quadrant's entries (as LDS byte offsets), built by the wave
     uint32_t qcnt = 0;
 #pragma unroll
     for (int g = 0; g < 4; g++) {
       const uint64_t m = uniform_u64(s_mask[g][wid]);
       if ((m >> lane) & 1ull)
         s_qlist[wid][qcnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-            (uint16_t)(g * 64 + lane);
+            (uint16_t)(16 * (g * 64 + lane));
       qcnt += (uint32_t)__popcll(m);
     }
+    if (lane < FWD_ILP) s_qlist[wid][qcnt + lane] = 0;  // pad the last group (masked below)
     __builtin_amdgcn_wave_barrier();
     // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
     // compositing is then applied entry by entry in list order, exactly as one at a time
     for (uint32_t k = 0; k < qcnt; k += FWD_ILP) {
-      uint32_t j[FWD_ILP];
+      const uint2 w = *reinterpret_cast<const uint2*>(&s_qlist[wid][k]);
+      const uint32_t o[FWD_ILP] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
       float pw[FWD_ILP], al[FWD_ILP];
 #pragma unroll
       for (int u = 0; u < FWD_ILP; u++) {
-        j[u] = (k + u < qcnt) ? (uint32_t)s_qlist[wid][k + u] : (uint32_t)s_qlist[wid][k];
-        const float2 xy = s_xy[j[u]];
-        const float4 co = s_co[j[u]];
-        pw[u] = falloff_log2(co, xy.x - pfx, xy.y - pfy);  // log2(e) * power
+        const float4 xr = *reinterpret_cast<const float4*>(ent + o[u]);
+        const float4 co = *reinterpret_cast<const float4*>(ent + o[u] + 16 * GS_BLOCK);
+        pw[u] = falloff_log2(co, xr.x - pfx, xr.y - pfy);  // log2(e) * power
         al[u] = fminf(0.99f, co.w * exp2_m<EXACT>(pw[u]));
       }
 #pragma unroll
       for (int u = 0; u < FWD_ILP; u++) {
-        const float4 rgb = s_rgb[j[u]];
+        const float4 xr = *reinterpret_cast<const float4*>(ent + o[u]);
+        const float2 bl = *reinterpret_cast<const float2*>(ent + o[u] + 32 * GS_BLOCK);
+        const float rr = xr.z, rg = xr.w, rb = bl.x;
         // branch-free compositing (selects instead of divergent ifs)
         bool cu = k + u < qcnt && !done && pw[u] <= 0.0f && al[u] >= 1.0f / 255.0f;
         const float tT = T * (1.0f - al[u]);
@@ -527,17 +529,17 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
         done = done || su;
         cu = cu && !su;
         if constexpr (EXACT) {  // upstream's order, (rgb alpha) T, mirrored by the oracle
-          C0 = cu ? C0 + rgb.x * al[u] * T : C0;
-          C1 = cu ? C1 + rgb.y * al[u] * T : C1;
-          C2 = cu ? C2 + rgb.z * al[u] * T : C2;
+          C0 = cu ? C0 + rr * al[u] * T : C0;
+          C1 = cu ? C1 + rg * al[u] * T : C1;
+          C2 = cu ? C2 + rb * al[u] * T : C2;
         } else {  // one weight, three FMAs; a skipped entry adds rgb * 0 (C unchanged)
-          const float w = cu ? al[u] * T : 0.0f;
-          C0 = __builtin_fmaf(rgb.x, w, C0);
-          C1 = __builtin_fmaf(rgb.y, w, C1);
-          C2 = __builtin_fmaf(rgb.z, w, C2);
+          const float wgt = cu ? al[u] * T : 0.0f;
+          C0 = __builtin_fmaf(rr, wgt, C0);
+          C1 = __builtin_fmaf(rg, wgt, C1);
+          C2 = __builtin_fmaf(rb, wgt, C2);
         }
         T = cu ? tT : T;
-        last = cu ? base + j[u] + 1 : last;
+        last = cu ? __float_as_uint(bl.y) : last;
       }
       if (__ballot(!done) == 0) break;
     }
