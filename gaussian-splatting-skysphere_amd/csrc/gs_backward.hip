@@ -117,7 +117,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   const uint32_t wave_last = __builtin_amdgcn_readfirstlane(wave_max_u32(max(lastA, lastB)));
 
   // gradient commit of entry j (walk order) for the lane's contributing pixels
-  auto apply = [&](uint32_t j, const Eval& v) {
+  auto apply = [&](uint32_t j, const Eval& v, const float4 rgb) {
     const f2 G = v.G, alpha = v.alpha, dy = v.dy;
     const float dx = v.dx;
     const bool cA = v.cA, cB = v.cB;
@@ -130,7 +130,6 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     // dmean2D.y = -H/2 (cyy S4 + cxy S3), dconic = -S5/2, -S6/2, -S7/2.
     // accum_rec is carried as A = sum_c accum_rec_c dL/dpix_c and last_color as
     // Lc = sum_c last_color_c dL/dpix_c, which is all dL/dalpha needs.
-    const float4 rgb = s_rgb[j];
     // A pixel that does not contribute is run as an alpha = 0 entry: T, accum_rec and last_alpha
     // then pass through unchanged bit for bit (1 / (1 - 0) = 1, fma(0, x, A) = A) and its colour
     // terms vanish, so only dL/dalpha needs a mask.
@@ -225,15 +224,15 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         Eval v1 = eval_pair<EXACT>(s_xy[j1], s_co[j1], pfx, pfy, n_eff - 1 - (base + j1), lastA, lastB);
         v1.cA = v1.cA && has1;
         v1.cB = v1.cB && has1;
-        if (__ballot(v0.cA || v0.cB) != 0) apply(j0, v0);
-        if (__ballot(v1.cA || v1.cB) != 0) apply(j1, v1);
+        if (__ballot(v0.cA || v0.cB) != 0) apply(j0, v0, s_rgb[j0]);
+        if (__ballot(v1.cA || v1.cB) != 0) apply(j1, v1, s_rgb[j1]);
       }
 #else
       while (m) {
         const uint32_t j = (uint32_t)(g * 64 + __builtin_ctzll(m));
         m &= m - 1;
         const Eval v = eval_pair<EXACT>(s_xy[j], s_co[j], pfx, pfy, n_eff - 1 - (base + j), lastA, lastB);
-        if (__ballot(v.cA || v.cB) != 0) apply(j, v);
+        if (__ballot(v.cA || v.cB) != 0) apply(j, v, s_rgb[j]);
       }
 #endif
     }
