@@ -28,7 +28,7 @@ struct Eval {
   bool cA, cB;
 };
 template <bool EXACT>
-__device__ __forceinline__ Eval eval_pair(float2 xy, float4 co, float pfx, f2 pfy, uint32_t e, uint32_t lastA,
+__device__ __forceinline__ Eval eval_pair(float4 xy, float4 co, float pfx, f2 pfy, uint32_t e, uint32_t lastA,
                                           uint32_t lastB) {
   Eval v;
   v.co = co;
@@ -73,10 +73,10 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
                                                             const uint32_t* __restrict__ tile_max,
                                                             const float* __restrict__ dL_dpix,
                                                             float* __restrict__ gradrec) {
-  __shared__ float2 s_xy[BWD_BATCH];
-  __shared__ float4 s_co[BWD_BATCH];  // falloff coefficients + opacity (fall_coefs)
+  // entry j: three 16-B records at one LDS byte offset 16 j (one address register per entry):
+  //   (x, y, r, g) | falloff coefficients + opacity (fall_coefs) | (b, -, -, -)
+  __shared__ float4 s_ent[3 * BWD_BATCH];
   __shared__ float4 s_cr[BWD_BATCH];  // raw conic (xx, xy, yy) for the record mapping
-  __shared__ float4 s_rgb[BWD_BATCH];
   __shared__ uint32_t s_slot[BWD_BATCH];
   __shared__ uint64_t s_mask[BWD_GROUPS][2];  // [64-entry group][half]
   __shared__ float s_acc[2][BWD_BATCH][ACC_STRIDE];
@@ -116,8 +116,13 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
   const uint32_t wave_last = __builtin_amdgcn_readfirstlane(wave_max_u32(max(lastA, lastB)));
 
+  // this lane's row slot of entry 0's record, as an LDS (32-bit) pointer: the per-entry address
+  // is then one 32-bit add instead of a 64-bit multiply-add on a generic pointer
+  using lds_float = __attribute__((address_space(3))) float;
+  lds_float* const acc_lane = (lds_float*)(&s_acc[wid][0][lane >> 4]);
   // gradient commit of entry j (walk order) for the lane's contributing pixels
-  auto apply = [&](uint32_t j, const Eval& v, const float4 rgb) {
+  auto apply = [&](uint32_t j, const Eval& v, const float4 xr) {
+    const float4 rgb = make_float4(xr.z, xr.w, s_ent[2 * BWD_BATCH + j].x, 0.0f);
     const f2 G = v.G, alpha = v.alpha, dy = v.dy;
     const float dx = v.dx;
     const bool cA = v.cA, cB = v.cB;
@@ -166,7 +171,10 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     // it could not fold into v_add_f32_dpp
     asm volatile("" ::"v"(d0), "v"(d1), "v"(d8));
     if ((lane & 15) == 0) {
-      float* acc = &s_acc[wid][j][lane >> 4];
+      // scalar entry offset, kept out of a 64-bit multiply-add (the asm pins it in an SGPR)
+      uint32_t eo = j * ACC_STRIDE;
+      asm volatile("" : "+s"(eo));
+      lds_float* acc = acc_lane + eo;
       acc[0] = d0;
       acc[4] = d1;
       acc[8] = d8;
@@ -186,10 +194,10 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         const uint32_t slot = point_list[range.x + e];
         const uint32_t gid = presort_gid[slot];
         const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
-        s_xy[t] = make_float2(a.x, a.y);
-        s_co[t] = fall_coefs(a.z, a.w, b.x, b.y);
+        s_ent[t] = make_float4(a.x, a.y, b.z, b.w);
+        s_ent[BWD_BATCH + t] = fall_coefs(a.z, a.w, b.x, b.y);
+        s_ent[2 * BWD_BATCH + t] = make_float4(d.x, 0.0f, 0.0f, 0.0f);
         s_cr[t] = make_float4(a.z, a.w, b.x, 0.0f);
-        s_rgb[t] = make_float4(b.z, b.w, d.x, 0.0f);
         s_slot[t] = slot;
         hm = half_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
       }
@@ -220,19 +228,21 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         const bool has1 = m != 0;
         const uint32_t j1 = has1 ? (uint32_t)(g * 64 + __builtin_ctzll(m)) : j0;
         if (has1) m &= m - 1;
-        const Eval v0 = eval_pair<EXACT>(s_xy[j0], s_co[j0], pfx, pfy, n_eff - 1 - (base + j0), lastA, lastB);
-        Eval v1 = eval_pair<EXACT>(s_xy[j1], s_co[j1], pfx, pfy, n_eff - 1 - (base + j1), lastA, lastB);
+        const float4 x0 = s_ent[j0], x1 = s_ent[j1];
+        const Eval v0 = eval_pair<EXACT>(x0, s_ent[BWD_BATCH + j0], pfx, pfy, n_eff - 1 - (base + j0), lastA, lastB);
+        Eval v1 = eval_pair<EXACT>(x1, s_ent[BWD_BATCH + j1], pfx, pfy, n_eff - 1 - (base + j1), lastA, lastB);
         v1.cA = v1.cA && has1;
         v1.cB = v1.cB && has1;
-        if (__ballot(v0.cA || v0.cB) != 0) apply(j0, v0, s_rgb[j0]);
-        if (__ballot(v1.cA || v1.cB) != 0) apply(j1, v1, s_rgb[j1]);
+        if (__ballot(v0.cA || v0.cB) != 0) apply(j0, v0, x0);
+        if (__ballot(v1.cA || v1.cB) != 0) apply(j1, v1, x1);
       }
 #else
       while (m) {
         const uint32_t j = (uint32_t)(g * 64 + __builtin_ctzll(m));
         m &= m - 1;
-        const Eval v = eval_pair<EXACT>(s_xy[j], s_co[j], pfx, pfy, n_eff - 1 - (base + j), lastA, lastB);
-        if (__ballot(v.cA || v.cB) != 0) apply(j, v, s_rgb[j]);
+        const float4 xr = s_ent[j];
+        const Eval v = eval_pair<EXACT>(xr, s_ent[BWD_BATCH + j], pfx, pfy, n_eff - 1 - (base + j), lastA, lastB);
+        if (__ballot(v.cA || v.cB) != 0) apply(j, v, xr);
       }
 #endif
     }
