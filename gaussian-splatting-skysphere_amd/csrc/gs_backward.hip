@@ -141,7 +141,10 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     const f2 ae = {cA ? alpha.x : 0.0f, cB ? alpha.y : 0.0f};
     const f2 omA = 1.f - ae;
     f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
-    inv = pk_fma(inv, pk_fma(-omA, inv, (f2)(1.0f)), inv);  // one Newton step: ~0.5 ulp, like the IEEE divide
+    // exact mode: one Newton step (~0.5 ulp, like the IEEE divide).  Fast mode: the hardware
+    // reciprocal alone (<= 1 ulp; the T recovered over ~200 entries drifts ~1e-6 relative at
+    // most, and 1 / (1 - 0) = 1 exactly, so non-contributing pixels still pass T through)
+    if constexpr (EXACT) inv = pk_fma(inv, pk_fma(-omA, inv, (f2)(1.0f)), inv);
     const f2 Tn = T * inv;
     const f2 dch = ae * Tn;
     const f2 Cd = pk_fma((f2)(rgb.z), dp2, pk_fma((f2)(rgb.y), dp1, rgb.x * dp0));

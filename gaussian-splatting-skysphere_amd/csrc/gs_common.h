@@ -90,7 +90,10 @@ __device__ __forceinline__ f2 gs_exp2_pk(f2 t) {
 template <bool EXACT>
 __device__ __forceinline__ float exp2_m(float t) {
   if constexpr (EXACT) return gs_exp2(t);
-  else return __builtin_amdgcn_exp2f(fminf(fmaxf(t, -125.0f), 0.0f));
+  // fast mode: the hardware exp2 without the exact mode's clamp to [-125, 0] (t > 0 only occurs
+  // by rounding next to a splat centre and such an entry is skipped (power > 0); below -125 the
+  // result only ever meets alpha < 1/255)
+  else return __builtin_amdgcn_exp2f(t);
 }
 template <bool EXACT>
 __device__ __forceinline__ f2 exp2_pk_m(f2 t) {
@@ -105,25 +108,24 @@ __device__ __forceinline__ f2 exp2_pk_m(f2 t) {
 
 // log2(e) * power of a splat at pixel offset (dx, dy) = mean - pixel.  The conic is scaled once
 // per staged splat (fall_coefs): A = cxx (-log2e / 2), B = cxy (-log2e), C = cyy (-log2e / 2), and
-// t = dx (A dx + B dy) + C dy^2 takes two FMAs + three multiplies per pixel.  Bit-identical to
-// oracle/gs_oracle.c:falloff_log2.
+// t = (A dx) dx + dy (B dx + C dy): three multiplies + two FMAs per pixel, and for the backward's
+// two pixels of one column (same dx) the three multiplies are shared, so the pair costs two
+// packed FMAs.  Bit-identical to oracle/gs_oracle.c:falloff_log2.
 constexpr float K_HALF_LOG2E = -0.72134752044448170f, K_LOG2E = -1.44269504088896341f;
 __device__ __forceinline__ float4 fall_coefs(float cxx, float cxy, float cyy, float opacity) {
   return make_float4(cxx * K_HALF_LOG2E, cxy * K_LOG2E, cyy * K_HALF_LOG2E, opacity);
 }
 __device__ __forceinline__ float falloff_log2(float4 k, float dx, float dy) {
-  const float u = k.y * dy;
-  const float t = __builtin_fmaf(k.x, dx, u);
-  const float v = k.z * dy;
-  const float w = v * dy;
-  return __builtin_fmaf(dx, t, w);
+  const float a2 = (k.x * dx) * dx;
+  const float b = k.y * dx;
+  const float t = __builtin_fmaf(k.z, dy, b);
+  return __builtin_fmaf(dy, t, a2);
 }
 __device__ __forceinline__ f2 falloff_log2_pk(float4 k, float dx, f2 dy) {
-  const f2 u = k.y * dy;
-  const f2 t = pk_fma((f2)(k.x), (f2)(dx), u);
-  const f2 v = k.z * dy;
-  const f2 w = v * dy;
-  return pk_fma((f2)(dx), t, w);
+  const float a2 = (k.x * dx) * dx;
+  const float b = k.y * dx;
+  const f2 t = pk_fma((f2)(k.z), dy, (f2)(b));
+  return pk_fma(dy, t, (f2)(a2));
 }
 
 // m = 4x4 world_view_transform / full_proj_transform, row-major flattening of the torch tensor

@@ -79,17 +79,17 @@ float oracle_exp(float x) { return oracle_exp2(x * 1.44269504088896341f); }
 
 /* log2(e) * power of a splat at pixel offset (dx, dy) = mean - pixel, with the conic scaled once
  * per splat: A = cxx (-log2e / 2), B = cxy (-log2e), C = cyy (-log2e / 2);
- * t = dx (A dx + B dy) + C dy^2 as two FMAs.  Identical op sequence in the HIP render kernels
- * (csrc/gs_common.h:falloff_log2). */
+ * t = (A dx) dx + dy (B dx + C dy): three multiplies, two FMAs.  Identical op sequence in the HIP
+ * render kernels (csrc/gs_common.h:falloff_log2); upstream's power = -0.5 (cxx dx^2 + cyy dy^2)
+ * - cxy dx dy times log2(e), up to rounding. */
 #define K_HALF_LOG2E (-0.72134752044448170f)
 #define K_LOG2E (-1.44269504088896341f)
 static inline float falloff_log2(const float* conic, float dx, float dy) {
     float A = conic[0] * K_HALF_LOG2E, B = conic[1] * K_LOG2E, C = conic[2] * K_HALF_LOG2E;
-    float u = B * dy;
-    float t = fmaf(A, dx, u);
-    float v = C * dy;
-    float w = v * dy;
-    return fmaf(dx, t, w);
+    float a2 = (A * dx) * dx;
+    float b = B * dx;
+    float t = fmaf(C, dy, b);
+    return fmaf(dy, t, a2);
 }
 
 /* world point -> view (transformPoint4x3).  m is the 4x4 `world_view_transform`
