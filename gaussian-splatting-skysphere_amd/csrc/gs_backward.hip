@@ -123,7 +123,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   // gradient commit of entry j (walk order) for the lane's contributing pixels
   auto apply = [&](uint32_t j, const Eval& v, const float4 xr) {
     const float4 rgb = make_float4(xr.z, xr.w, s_ent[2 * BWD_BATCH + j].x, 0.0f);
-    const f2 G = v.G, alpha = v.alpha, dy = v.dy;
+    const f2 alpha = v.alpha, dy = v.dy;
     const float dx = v.dx;
     const bool cA = v.cA, cB = v.cB;
     // Reduced form of the upstream per-pair terms (same quantities, fewer ops per pixel):
@@ -157,12 +157,12 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     s[0] = __builtin_fmaf(dch.x, dp0.x, dch.y * dp0.y);
     s[1] = __builtin_fmaf(dch.x, dp1.x, dch.y * dp1.y);
     s[2] = __builtin_fmaf(dch.x, dp2.x, dch.y * dp2.y);
-    s[3] = dx * (q.x + q.y);
+    s[8] = q.x + q.y;  // sum_px o G dL/dalpha: dL/dopacity = S8 / o at the flush
+    s[3] = dx * s[8];
     s[4] = w4.x + w4.y;
     s[5] = dx * s[3];
     s[6] = dx * s[4];
     s[7] = __builtin_fmaf(w4.x, dy.x, w4.y * dy.y);
-    s[8] = __builtin_fmaf(G.x, dLm.x, G.y * dLm.y);
     T = Tn;
     Aacc = An;
     Lc = Cd;
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         s_ent[t] = make_float4(a.x, a.y, b.z, b.w);
         s_ent[BWD_BATCH + t] = fall_coefs(a.z, a.w, b.x, b.y);
         s_ent[2 * BWD_BATCH + t] = make_float4(d.x, 0.0f, 0.0f, 0.0f);
-        s_cr[t] = make_float4(a.z, a.w, b.x, 0.0f);
+        s_cr[t] = make_float4(a.z, a.w, b.x, b.y);  // raw conic + opacity
         s_slot[t] = slot;
         hm = half_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
       }
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         r[5] = -0.5f * S[5];
         r[6] = -0.5f * S[6];
         r[7] = -0.5f * S[7];
-        r[8] = S[8];
+        r[8] = S[8] != 0.0f ? S[8] / co.w : 0.0f;  // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
       }
     }
   }
