@@ -44,12 +44,27 @@ __device__ __forceinline__ Eval eval_pair(float4 xy, float4 co, float pfx, f2 pf
   return v;
 }
 
+// a 36-B gradient record as three 12-B stores (global_store_dwordx3; 4-B alignment is enough)
+struct __attribute__((aligned(4))) Rec3 {
+  float a, b, c;
+};
+
+// the 36-B record read as three 12-B pieces (merged into 16-B loads; 4-B alignment is enough)
+__device__ __forceinline__ void load_rec(const float* p, float* v) {
+  const Rec3* r = reinterpret_cast<const Rec3*>(p);
+  const Rec3 a = r[0], b = r[1], c = r[2];
+  v[0] = a.a, v[1] = a.b, v[2] = a.c, v[3] = b.a, v[4] = b.b, v[5] = b.c, v[6] = c.a, v[7] = c.b, v[8] = c.c;
+}
+
 constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x, y) and (x, y + 8)
 #ifndef GS_BWD_BATCH
 #define GS_BWD_BATCH 64
 #endif
 #ifndef GS_BWD_ILP
 #define GS_BWD_ILP 1
+#endif
+#ifndef GS_BWD_NOZERO
+#define GS_BWD_NOZERO 0  // timing experiments only (wrong gradients)
 #endif
 #ifndef GS_BWD_MINW
 #define GS_BWD_MINW 1
@@ -94,10 +109,11 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   const uint32_t n_eff = min(tile_max[tile], n);
 
   // instances past the last contributor of every pixel get zero records
-  for (uint32_t e = n_eff + tid; e < n; e += BWD_THREADS) {
-    float* r = gradrec + (size_t)point_list[range.x + e] * GRAD_REC;
-#pragma unroll
-    for (int k = 0; k < GRAD_REC; k++) r[k] = 0.0f;
+  for (uint32_t e = n_eff + tid; e < (GS_BWD_NOZERO ? 0u : n); e += BWD_THREADS) {
+    Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)point_list[range.x + e] * GRAD_REC);
+    r[0] = Rec3{0.0f, 0.0f, 0.0f};
+    r[1] = Rec3{0.0f, 0.0f, 0.0f};
+    r[2] = Rec3{0.0f, 0.0f, 0.0f};
   }
 
   const size_t HW = (size_t)c.W * c.H;
@@ -260,16 +276,11 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         S[8] = ((s_acc[0][t][8] + s_acc[0][t][9]) + (s_acc[0][t][10] + s_acc[0][t][11])) +
                ((s_acc[1][t][8] + s_acc[1][t][9]) + (s_acc[1][t][10] + s_acc[1][t][11]));
         const float4 co = s_cr[t];
-        float* r = gradrec + (size_t)s_slot[t] * GRAD_REC;
-        r[0] = S[0];
-        r[1] = S[1];
-        r[2] = S[2];
-        r[3] = -ddelx_dx * (co.x * S[3] + co.y * S[4]);
-        r[4] = -ddely_dy * (co.z * S[4] + co.y * S[3]);
-        r[5] = -0.5f * S[5];
-        r[6] = -0.5f * S[6];
-        r[7] = -0.5f * S[7];
-        r[8] = S[8] != 0.0f ? S[8] / co.w : 0.0f;  // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
+        Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)s_slot[t] * GRAD_REC);
+        r[0] = Rec3{S[0], S[1], S[2]};
+        r[1] = Rec3{-ddelx_dx * (co.x * S[3] + co.y * S[4]), -ddely_dy * (co.z * S[4] + co.y * S[3]), -0.5f * S[5]};
+        // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
+        r[2] = Rec3{-0.5f * S[6], -0.5f * S[7], S[8] != 0.0f ? S[8] / co.w : 0.0f};
       }
     }
   }
@@ -332,7 +343,8 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
   {
     const size_t kk = (size_t)min(S0 + lane, S1 - 1);
 #pragma unroll
-    for (int c = 0; c < GRAD_REC; c++) vn[c] = S0 < S1 ? gradrec[kk * GRAD_REC + c] : 0.0f;
+    for (int c = 0; c < GRAD_REC; c++) vn[c] = 0.0f;
+    if (S0 < S1) load_rec(gradrec + kk * GRAD_REC, vn);
   }
   for (uint32_t base = S0; base < S1; base += 64) {
     float v[GRAD_REC];
@@ -340,8 +352,7 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
     for (int c = 0; c < GRAD_REC; c++) v[c] = vn[c];
     if (base + 64 < S1) {
       const size_t kn = (size_t)min(base + 64 + lane, S1 - 1);
-#pragma unroll
-      for (int c = 0; c < GRAD_REC; c++) vn[c] = gradrec[kn * GRAD_REC + c];
+      load_rec(gradrec + kn * GRAD_REC, vn);
     }
     // slots of the chunk that start an owner -> bit mask -> owner of my slot by popcount
     if (lane == 0) s_mark[wid] = 0ull;
