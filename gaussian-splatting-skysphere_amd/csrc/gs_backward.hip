@@ -108,14 +108,6 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   const uint32_t n = range.y - range.x;
   const uint32_t n_eff = min(tile_max[tile], n);
 
-  // instances past the last contributor of every pixel get zero records
-  for (uint32_t e = n_eff + tid; e < (GS_BWD_NOZERO ? 0u : n); e += BWD_THREADS) {
-    Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)point_list[range.x + e] * GRAD_REC);
-    r[0] = Rec3{0.0f, 0.0f, 0.0f};
-    r[1] = Rec3{0.0f, 0.0f, 0.0f};
-    r[2] = Rec3{0.0f, 0.0f, 0.0f};
-  }
-
   const size_t HW = (size_t)c.W * c.H;
   const size_t pixA = inA ? (size_t)pyA * c.W + px : 0, pixB = inB ? (size_t)pyB * c.W + px : 0;
   const f2 T_final = {inA ? final_T[pixA] : 0.0f, inB ? final_T[pixB] : 0.0f};
@@ -284,6 +276,16 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
       }
     }
   }
+
+  // instances past the last contributor of every pixel get zero records (at the end: the
+  // walk's VALU work starts without waiting on these loads)
+  for (uint32_t e = n_eff + tid; e < (GS_BWD_NOZERO ? 0u : n); e += BWD_THREADS) {
+    Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)point_list[range.x + e] * GRAD_REC);
+    r[0] = Rec3{0.0f, 0.0f, 0.0f};
+    r[1] = Rec3{0.0f, 0.0f, 0.0f};
+    r[2] = Rec3{0.0f, 0.0f, 0.0f};
+  }
+
 }
 
 void bwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
