@@ -461,7 +461,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
                                                          uint32_t* __restrict__ tile_max) {
   __shared__ float4 s_ent[3 * GS_BLOCK];
   __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
-  __shared__ __attribute__((aligned(8))) uint16_t s_qlist[4][GS_BLOCK + FWD_ILP];  // per quadrant wave: byte offsets
+  __shared__ __attribute__((aligned(8))) uint16_t s_qlist[4][GS_BLOCK + 2 * FWD_ILP];  // per quadrant wave: byte offsets
   __shared__ uint32_t s_max;
   const uint32_t tile = blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
@@ -502,12 +502,15 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
             (uint16_t)(16 * (g * 64 + lane));
       qcnt += (uint32_t)__popcll(m);
     }
-    if (lane < FWD_ILP) s_qlist[wid][qcnt + lane] = 0;  // pad the last group (masked below)
+    if (lane < 2 * FWD_ILP) s_qlist[wid][qcnt + lane] = 0;  // pad the last group and the prefetch (masked below)
     __builtin_amdgcn_wave_barrier();
     // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
     // compositing is then applied entry by entry in list order, exactly as one at a time
+    // the next group's offsets are read one trip ahead (one dependent LDS round trip per trip)
+    uint2 wn = *reinterpret_cast<const uint2*>(&s_qlist[wid][0]);
     for (uint32_t k = 0; k < qcnt; k += FWD_ILP) {
-      const uint2 w = *reinterpret_cast<const uint2*>(&s_qlist[wid][k]);
+      const uint2 w = wn;
+      wn = *reinterpret_cast<const uint2*>(&s_qlist[wid][k + FWD_ILP]);
       const uint32_t o[FWD_ILP] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
       float pw[FWD_ILP], al[FWD_ILP];
 #pragma unroll
