@@ -221,6 +221,7 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
 // ------------------------------------------------------------------------------------------
 // ordering: compaction -> depth sort -> instance offsets
 // ------------------------------------------------------------------------------------------
+
 struct SrcTilesByRank {
   const uint32_t *tiles, *sorted_gid;
   __device__ uint32_t operator()(uint32_t s) const { return tiles[sorted_gid[s]]; }
@@ -243,12 +244,25 @@ struct DstOffsets {
 void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
   const uint32_t n = (uint32_t)P;
   // depth sort of the Gaussians with instances: the first pass reads all P keys in index order
-  // and drops the DEPTH_DROP ones (compaction), the later passes sort the V survivors
-  radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32, geo.sort_scratch,
-                   st, /*drop_first=*/true);
-  scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid},
-                    DstOffsets{geo.offsets, geo.dup_first, geo.counters, n}, &geo.counters[CNT_V], n, geo.lb_status,
-                    &geo.counters[CNT_LB_TILE], &geo.counters[CNT_I], &geo.counters[CNT_ERR], st);
+  // and drops the DEPTH_DROP ones (compaction), the later passes sort the V survivors.
+  if (lb_tiles(n) <= LB_STATIC_MAX) {
+    // up to 1M Gaussians: the offsets scan is one look-back launch whose grid is resident (static
+    // tile ids); it gathers each rank's tile count (the gather is cheaper here than carrying the
+    // counts through the four sort passes)
+    radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
+                     geo.sort_scratch, st, /*drop_first=*/true);
+    scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
+                      &geo.counters[CNT_V], n, geo.lb_status, &geo.counters[CNT_LB_TILE], &geo.counters[CNT_I],
+                      &geo.counters[CNT_ERR], st);
+  } else {
+    // larger scenes: the tile counts travel with the keys through the sort (read in index order by
+    // the first pass), and the 3-launch scan reads them in depth order, coalesced (C5, 5M: the
+    // per-rank gather and the ticketed look-back took 197 us)
+    radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
+                     geo.sort_scratch, st, /*drop_first=*/true, false, geo.tiles, geo.rtiles_a, geo.rtiles_b);
+    scan_exclusive(SrcArray{geo.tiles_by_rank}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
+                   &geo.counters[CNT_V], n, geo.scan_partial, &geo.counters[CNT_I], st);
+  }
 }
 
 // ------------------------------------------------------------------------------------------

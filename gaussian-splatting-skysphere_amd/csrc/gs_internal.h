@@ -68,6 +68,8 @@ struct GeomPtrs {
   uint8_t* clamped;
   uint32_t *keys_a, *vals_a, *keys_b, *vals_b;
   uint32_t* offsets;  // per depth rank
+  uint32_t *rtiles_a, *rtiles_b;  // tile counts carried through the depth sort (aux stream)
+  uint32_t* tiles_by_rank;        // = rtiles_a or rtiles_b after the depth sort
   uint32_t* dup_first;  // [P + 1] depth rank owning the first instance slot of each duplicate block
   float* gsum;  // [P][9] per-Gaussian sums of the backward records (k_sum_records -> k_preprocess_bwd)
   uint32_t* scan_partial;
@@ -93,6 +95,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   size_t o_tiles = take(Pn * 4), o_goff = take(Pn * 4), o_cl = take(Pn);
   size_t o_ka = take(Pn * 4), o_va = take(Pn * 4), o_kb = take(Pn * 4), o_vb = take(Pn * 4);
   size_t o_offs = take(Pn * 4);
+  size_t o_rta = take(Pn * 4), o_rtb = take(Pn * 4);
   size_t o_df = take((Pn + 1) * 4);
   size_t o_gs = take(Pn * 4 * GRAD_REC);
   size_t o_sp = take((size_t)scan_plan(Pn).nb * 4 + 64);
@@ -110,6 +113,9 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
     out->keys_b = (uint32_t*)(base + o_kb);
     out->vals_b = (uint32_t*)(base + o_vb);
     out->offsets = (uint32_t*)(base + o_offs);
+    out->rtiles_a = (uint32_t*)(base + o_rta);
+    out->rtiles_b = (uint32_t*)(base + o_rtb);
+    out->tiles_by_rank = (radix_passes(32) % 2 == 0) ? out->rtiles_b : out->rtiles_a;
     out->dup_first = (uint32_t*)(base + o_df);
     out->gsum = (float*)(base + o_gs);
     out->scan_partial = (uint32_t*)(base + o_sp);

@@ -400,10 +400,13 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_rowscan(uint32_t*
   if (threadIdx.x == 0) row_total[blockIdx.x] = carry;
 }
 
-static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
+// AUX: a second value stream travels with the keys (aux_in[i] -> aux_out[pos])
+template <bool AUX>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, int bits, uint32_t chunk,
-    uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ row_total, bool drop) {
+    uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ row_total, bool drop,
+    const uint32_t* __restrict__ aux_in, uint32_t* __restrict__ aux_out) {
   __shared__ uint32_t s_base[RADIX];      // global position of the next key of each digit
   __shared__ uint32_t s_wcnt[4][RADIX];   // per-wave running counts -> per-wave exclusive prefix
   __shared__ uint32_t s_loc[RADIX];       // digit offsets inside the tile (for the LDS reorder)
@@ -411,6 +414,7 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   __shared__ uint32_t s_scan[4];
   __shared__ uint32_t s_key[SORT_TILE];
   __shared__ uint32_t s_val[SORT_TILE];
+  __shared__ uint32_t s_aux[AUX ? SORT_TILE : 1];
   const uint32_t n = resolve_n(n_dev, n_max);
   const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   {
@@ -428,13 +432,14 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     s_wcnt[3][tid] = 0;
     __syncthreads();
     // wave wid ranks positions t0 + wid*512 + r*64 + lane, r = 0..7 (in order -> stable)
-    uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
+    uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS], aux[AUX ? SORT_ITEMS : 1];
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
       const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
       const bool v = i < end;
       key[r] = v ? keys_in[i] : 0xFFFFFFFFu;
       val[r] = v ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
+      if constexpr (AUX) aux[r] = v ? aux_in[i] : 0u;
     }
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
@@ -472,6 +477,7 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
         const uint32_t slot = s_loc[d] + s_wcnt[wid][d] + rank[r];
         s_key[slot] = key[r];
         s_val[slot] = val[r];
+        if constexpr (AUX) s_aux[slot] = aux[r];
       }
     }
     __syncthreads();
@@ -486,6 +492,7 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
         const uint32_t pos = s_base[d] + (slot - s_loc[d]);
         keys_out[pos] = k;
         vals_out[pos] = s_val[slot];
+        if constexpr (AUX) aux_out[pos] = s_aux[slot];
       }
     }
     __syncthreads();
@@ -493,19 +500,25 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   }
 }
 
+// aux0 / aux_a / aux_b (optional): a second value stream in input order (aux0) that travels with
+// the keys; pass p writes aux_a (p even) or aux_b (p odd), so the result is in aux_b after an even
+// number of passes and in aux_a after an odd one.
 // hist0_ready: the caller already wrote the first pass's [digit][block] counts into scratch.
 // drop_first: the first pass reads n_max keys (host count) and drops those equal to DEPTH_DROP;
 // the later passes then sort the *n_dev survivors.  Otherwise every pass sorts n (n_dev / n_max).
 static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b,
                                     bool vals_identity, const uint32_t* n_dev, uint32_t n_max, int end_bit,
                                     uint32_t* scratch, hipStream_t st, bool drop_first = false,
-                                    bool hist0_ready = false) {
+                                    bool hist0_ready = false, const uint32_t* aux0 = nullptr,
+                                    uint32_t* aux_a = nullptr, uint32_t* aux_b = nullptr) {
   SortPlan p = sort_plan(n_max);
   uint32_t* hist = scratch;
   const size_t hist_n = (size_t)RADIX * p.nb;
   uint32_t* row_total = scratch + hist_n;
   uint32_t *kin = keys_a, *vin = vals_a, *kout = keys_b, *vout = vals_b;
   bool in_b = false;
+  const uint32_t* ain = aux0;
+  uint32_t* aout = aux_a;
   // digits of (nearly) equal width: 13 bits -> 7 + 6, not 8 + 5 (longer runs in the first scatter)
   const int width = radix_width(end_bit);
   for (int shift = 0; shift < end_bit; shift += width) {
@@ -517,8 +530,15 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
                 p.chunk, p.nb, hist, drop);
     GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX), dim3(SORT_THREADS), 0, st, hist, p.nb, row_total);
     const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
-    GS_LAUNCH("radix_scatter", k_radix_scatter, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, vsrc, kout, vout, nd,
-              n_max, shift, bits, p.chunk, p.nb, hist, row_total, drop);
+    if (aux0) {
+      GS_LAUNCH("radix_scatter", k_radix_scatter<true>, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, vsrc, kout, vout,
+                nd, n_max, shift, bits, p.chunk, p.nb, hist, row_total, drop, ain, aout);
+      ain = aout;
+      aout = aout == aux_a ? aux_b : aux_a;
+    } else {
+      GS_LAUNCH("radix_scatter", k_radix_scatter<false>, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, vsrc, kout,
+                vout, nd, n_max, shift, bits, p.chunk, p.nb, hist, row_total, drop, nullptr, nullptr);
+    }
     uint32_t* t;
     t = kin; kin = kout; kout = t;
     t = vin; vin = vout; vout = t;

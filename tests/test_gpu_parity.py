@@ -515,3 +515,21 @@ def test_large_c3_properties(device):
     ncon = ex["n_contrib"].long()
     assert torch.isfinite(color).all() and (color >= 0).all()
     assert int(ncon.max()) <= int((ends - starts).max())
+
+
+def test_large_scene_sort_path_vs_oracle(oracle, device):
+    """More than 1,048,576 Gaussians take the large-scene ordering path (tile counts carried
+    through the depth sort, 3-launch offsets scan; gs_forward.hip fwd_order).  A small image keeps
+    the oracle quick; a third of the Gaussians sit behind the camera (dropped by the first pass)."""
+    W, H = 320, 240
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(1_100_000, 1, cam=cam, seed=21)
+    sc.means3D[::3, 2] = -sc.means3D[::3, 2]
+    bg = np.zeros(3, np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg)
+    ofw = oracle.forward(osc, intermediates=True)
+    ofw["bg"] = bg
+    _check_forward_exact(ofw, cam, sc, device)
+    dpix = gs_scenes.dl_dimage(H, W, seed=22).numpy()
+    _, _, leaves = _gpu_run(cam, sc, device, bg, dpix)
+    _check_backward(oracle.backward(osc, dpix), leaves)
