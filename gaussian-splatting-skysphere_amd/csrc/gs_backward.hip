@@ -378,7 +378,7 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
     const uint32_t next1 = (uint32_t)__shfl_down((int)own1, 1, 64);
     if (valid && (lane == 63 || next1 != own1)) {
 #pragma unroll
-      for (int c = 0; c < GRAD_REC; c++) s_acc[wid][own][c] += (double)v[c];
+      for (int c = 0; c < GRAD_REC; c++) atomicAdd(&s_acc[wid][own][c], (double)v[c]);  // ds_add_f64: one lane per owner, fixed order
     }
     __builtin_amdgcn_wave_barrier();
   }
