@@ -541,21 +541,28 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
         const float rr = xr.z, rg = xr.w, rb = bl.x;
         // branch-free compositing (selects instead of divergent ifs)
         bool cu = k + u < qcnt && !done && pw[u] <= 0.0f && al[u] >= 1.0f / 255.0f;
-        const float tT = T * (1.0f - al[u]);
-        const bool su = cu && tT < 0.0001f;  // T would drop below 1e-4: stop before this entry
-        done = done || su;
-        cu = cu && !su;
-        if constexpr (EXACT) {  // upstream's order, (rgb alpha) T, mirrored by the oracle
+        if constexpr (EXACT) {  // upstream's order, T (1 - alpha) and (rgb alpha) T, mirrored by the oracle
+          const float tT = T * (1.0f - al[u]);
+          const bool su = cu && tT < 0.0001f;  // T would drop below 1e-4: stop before this entry
+          done = done || su;
+          cu = cu && !su;
           C0 = cu ? C0 + rr * al[u] * T : C0;
           C1 = cu ? C1 + rg * al[u] * T : C1;
           C2 = cu ? C2 + rb * al[u] * T : C2;
-        } else {  // one weight, three FMAs; a skipped entry adds rgb * 0 (C unchanged)
+          T = cu ? tT : T;
+        } else {
+          // T - alpha T as one FMA (one rounding of T (1 - alpha)); one weight, three FMAs (a
+          // skipped entry adds rgb * 0); `keep` as a >= test so both masks come from one compare
+          const float tT = __builtin_fmaf(-al[u], T, T);
+          const bool keep = tT >= 0.0001f;
+          done = done || (cu && !keep);
+          cu = cu && keep;
           const float wgt = cu ? al[u] * T : 0.0f;
           C0 = __builtin_fmaf(rr, wgt, C0);
           C1 = __builtin_fmaf(rg, wgt, C1);
           C2 = __builtin_fmaf(rb, wgt, C2);
+          T = cu ? tT : T;
         }
-        T = cu ? tT : T;
         last = cu ? __float_as_uint(bl.y) : last;
       }
       if (__ballot(!done) == 0) break;
