@@ -482,14 +482,17 @@ def test_knn_matches_oracle(oracle, device, P):
     np.testing.assert_allclose(got, ref, rtol=1e-6, atol=0)
 
 
-def test_large_c3_properties(device):
-    """C3 size (1M Gaussians SH3, 1920x1080) -- size-independent properties instead of the oracle:
-    the tile-sorted list is ordered by (tile, depth, index), ranges tile the list exactly,
-    n_contrib <= list length, image finite, bit-identical reruns."""
+@pytest.mark.parametrize("P", [1_000_000, 5_000_000], ids=["C3_1M", "C5_5M"])
+def test_large_c3_properties(device, P):
+    """C3 / C5 sizes (1M / 5M Gaussians SH3, 1920x1080) -- size-independent properties instead of
+    the oracle: the tile-sorted list is ordered by (tile, depth, index), ranges tile the list
+    exactly, n_contrib <= list length, image finite, bit-identical reruns.  C5 (I = 21.6M) also
+    covers the sort chunks of several 2048-key tiles per workgroup (I > 8.4M: no first-pass
+    counts from the duplicate) and the large-scene ordering path."""
     from diff_gaussian_rasterization import _C
 
     cam = gs_scenes.identity_camera(1920, 1080)
-    sc = gs_scenes.random_gaussians(1_000_000, 3, cam=cam, seed=0).to(device)
+    sc = gs_scenes.random_gaussians(P, 3, cam=cam, seed=0).to(device)
     s = gs_scenes.raster_settings_for(cam, 3, device=device)
     e = torch.Tensor([])
     args = (s.bg, sc.means3D, e, sc.opacities, sc.scales, sc.rotations, 1.0, e, s.viewmatrix, s.projmatrix,
@@ -498,6 +501,8 @@ def test_large_c3_properties(device):
     num2, color2, radii2, *_ = _C.rasterize_gaussians(*args)
     assert num == num2 and torch.equal(color, color2) and torch.equal(radii, radii2)
     ex = _C.debug_export(sc.P, 1920, 1080, num, geom, binb, imgb, device)
+    if P > 1_000_000:
+        assert num > 8_400_000  # the multi-tile sort chunks are exercised
     lst = ex["point_list"].long()
     rng = ex["ranges"].long()
     assert num == int(ex["tiles_touched"].sum())
