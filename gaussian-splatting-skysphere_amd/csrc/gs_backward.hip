@@ -517,7 +517,6 @@ __device__ __forceinline__ void cov3d_backward(float sx, float sy, float sz, flo
 template <int DEG>
 __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g, const CameraArgs& c,
                                                    const uint32_t* __restrict__ tiles,
-                                                   const uint32_t* __restrict__ goff,
                                                    const uint8_t* __restrict__ clamped,
                                                    const float* __restrict__ gsum, const GradOut& out,
                                                    float* row) {
@@ -661,8 +660,7 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
 template <int DEG>  // -1: colours precomputed (no SH gradient)
 __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraArgs c,
                                                         const uint32_t* __restrict__ tiles,
-                                                        const uint32_t* __restrict__ goff,
-                                                        const uint8_t* __restrict__ clamped,
+                                                             const uint8_t* __restrict__ clamped,
                                                         const float* __restrict__ gsum, GradOut out) {
   extern __shared__ float s_sh[];  // DEG >= 0: [256][3M + 1] SH rows, then dL/dsh rows
   const int i0 = blockIdx.x * 256, i = i0 + (int)threadIdx.x;
@@ -673,7 +671,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
     rows_to_lds(g.shs + (size_t)i0 * rowf, s_sh, nG, rowf, stride);
     __syncthreads();
   }
-  if (i < g.P) preprocess_bwd_one<DEG>(i, g, c, tiles, goff, clamped, gsum, out, row);
+  if (i < g.P) preprocess_bwd_one<DEG>(i, g, c, tiles, clamped, gsum, out, row);
   if (DEG >= 0) {
     __syncthreads();
     lds_to_rows(s_sh, out.dsh + (size_t)i0 * rowf, nG, rowf, stride);
@@ -690,25 +688,25 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
   const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
   const size_t lds = sh ? (size_t)256 * (3 * g.M + 1) * sizeof(float) : 0;
   if (!sh) {
-    GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<-1>, grid, block, 0, st, g, c, geo.tiles, geo.goff, geo.clamped,
+    GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<-1>, grid, block, 0, st, g, c, geo.tiles, geo.clamped,
               geo.gsum, out);
     return;
   }
   switch (g.D) {
     case 0:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<0>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<0>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,
                 geo.gsum, out);
       break;
     case 1:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<1>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<1>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,
                 geo.gsum, out);
       break;
     case 2:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<2>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<2>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,
                 geo.gsum, out);
       break;
     default:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<3>, grid, block, lds, st, g, c, geo.tiles, geo.goff, geo.clamped,
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<3>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,
                 geo.gsum, out);
       break;
   }

@@ -280,13 +280,12 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* _
                                                    const uint32_t* __restrict__ sorted_gid,
                                                    const uint32_t* __restrict__ offsets,
                                                    const float4* __restrict__ binrec, int gx,
-                                                   uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
+                                                   uint32_t* __restrict__ tile_keys,
                                                    uint32_t* __restrict__ presort_gid) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
   if (s >= P || s >= counters[CNT_V]) return;
   const uint32_t gid = sorted_gid[s];
   uint32_t off = offsets[s];
-  goff[gid] = off;
   int y0, y1;
   const SpanCtx sp = span_of(binrec, gid, y0, y1);
   for (int ty = y0; ty < y1; ty++) {
@@ -315,7 +314,7 @@ __device__ __forceinline__ uint32_t own_idx(uint32_t i) { return i + (i >> 3); }
 __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     uint32_t I, const uint32_t* __restrict__ counters, const uint32_t* __restrict__ dup_first,
     const uint32_t* __restrict__ sorted_gid, const uint32_t* __restrict__ offsets,
-    const float4* __restrict__ binrec, int gx, int gy, uint32_t* __restrict__ goff, uint32_t* __restrict__ tile_keys,
+    const float4* __restrict__ binrec, int gx, int gy, uint32_t* __restrict__ tile_keys,
     uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges, uint32_t* __restrict__ hist0, uint32_t mask0) {
   __shared__ uint32_t s_own[DUP_SLOTS + DUP_SLOTS / 8];  // (slot + 1) << 16 | segment at segment starts
   __shared__ uint32_t s_seg_start[DUP_SLOTS];  // first slot of the row segment (may precede the block)
@@ -343,7 +342,6 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   for (uint32_t r = tid; r < nG; r += DUP_THREADS) {
     const uint32_t gid = sorted_gid[s_lo + r];
     uint32_t pos = offsets[s_lo + r];
-    if (pos >= k0 && pos < k1) goff[gid] = pos;
     if (pos >= k1) continue;
     int y0, y1;
     const SpanCtx sp = span_of(binrec, gid, y0, y1);
@@ -445,13 +443,13 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
     // one duplicate block per sort tile: the duplicate also counts the first sort pass's digits
     hist0 = sort_plan(I).chunk == DUP_SLOTS;
     GS_LAUNCH("duplicate", k_duplicate_lb, dim3((I + DUP_SLOTS - 1) / DUP_SLOTS), dim3(DUP_THREADS), 0, st, I,
-              geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy, geo.goff,
+              geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy,
               bin.keys_a, bin.presort_gid, img.ranges, hist0 ? bin.sort_scratch : nullptr,
               (1u << radix_first_bits(tbits)) - 1u);
   } else {
     (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
     GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
-              geo.sorted_gid, geo.offsets, geo.binrec, c.gx, geo.goff, bin.keys_a, bin.presort_gid);
+              geo.sorted_gid, geo.offsets, geo.binrec, c.gx, bin.keys_a, bin.presort_gid);
   }
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tbits, bin.sort_scratch, st,
                    false, hist0);

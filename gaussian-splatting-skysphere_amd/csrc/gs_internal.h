@@ -3,7 +3,7 @@
 // upstream's geomBuffer / binningBuffer / imgBuffer).
 //
 // Layout (all arrays 256-B aligned, structure-of-arrays except the 48-B splat record):
-//   geometry  (per Gaussian, P)      splat float4x3 | binrec float4x2 | tiles u32 | goff u32 |
+//   geometry  (per Gaussian, P)      splat float4x3 | binrec float4x2 | tiles u32 |
 //                                    clamped u8 | depth-sort keys/vals x2 u32 (keys_a: depth keys
 //                                    written by preprocess) | offsets u32 |
 //                                    scan partials | sort scratch | counters
@@ -64,7 +64,6 @@ struct GeomPtrs {
   float4* splat;  // 3 per Gaussian: (x, y, cxx, cxy) (cyy, opacity, r, g) (b, depth, cull_lim, -)
   float4* binrec;  // 2 per Gaussian: (x, y, cxx, cxy) (cyy, cull_lim, x0 | x1 << 16, y0 | y1 << 16) for binning
   uint32_t* tiles;
-  uint32_t* goff;  // first instance slot of each visible Gaussian (depth order)
   uint8_t* clamped;
   uint32_t *keys_a, *vals_a, *keys_b, *vals_b;
   uint32_t* offsets;  // per depth rank
@@ -92,7 +91,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   size_t Pn = P ? P : 1;
   size_t o_splat = take(Pn * 48);
   size_t o_bin = take(Pn * 32);
-  size_t o_tiles = take(Pn * 4), o_goff = take(Pn * 4), o_cl = take(Pn);
+  size_t o_tiles = take(Pn * 4), o_cl = take(Pn);
   size_t o_ka = take(Pn * 4), o_va = take(Pn * 4), o_kb = take(Pn * 4), o_vb = take(Pn * 4);
   size_t o_offs = take(Pn * 4);
   size_t o_rta = take(Pn * 4), o_rtb = take(Pn * 4);
@@ -106,7 +105,6 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
     out->splat = (float4*)(base + o_splat);
     out->binrec = (float4*)(base + o_bin);
     out->tiles = (uint32_t*)(base + o_tiles);
-    out->goff = (uint32_t*)(base + o_goff);
     out->clamped = (uint8_t*)(base + o_cl);
     out->keys_a = (uint32_t*)(base + o_ka);
     out->vals_a = (uint32_t*)(base + o_va);
