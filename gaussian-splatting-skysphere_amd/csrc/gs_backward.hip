@@ -39,8 +39,9 @@ __device__ __forceinline__ Eval eval_pair(float4 xy, float4 co, float pfx, f2 pf
   v.oG = co.w * v.G;
   v.alpha.x = fminf(0.99f, v.oG.x);
   v.alpha.y = fminf(0.99f, v.oG.y);
-  v.cA = e < lastA && power.x <= 0.0f && v.alpha.x >= 1.0f / 255.0f;
-  v.cB = e < lastB && power.y <= 0.0f && v.alpha.y >= 1.0f / 255.0f;
+  // fast mode drops upstream's `power > 0` skip exactly as the forward does (k_render_fwd)
+  v.cA = e < lastA && (!EXACT || power.x <= 0.0f) && v.alpha.x >= 1.0f / 255.0f;
+  v.cB = e < lastB && (!EXACT || power.y <= 0.0f) && v.alpha.y >= 1.0f / 255.0f;
   return v;
 }
 

@@ -538,7 +538,10 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
         const float2 bl = *reinterpret_cast<const float2*>(ent + o[u] + 32 * GS_BLOCK);
         const float rr = xr.z, rg = xr.w, rb = bl.x;
         // branch-free compositing (selects instead of divergent ifs)
-        bool cu = k + u < qcnt && !done && pw[u] <= 0.0f && al[u] >= 1.0f / 255.0f;
+        // upstream skips power > 0; with a positive-definite conic that only happens by rounding
+        // within ~1e-3 px of a splat centre, so the fast mode leaves the test out (the backward
+        // matches it entry for entry)
+        bool cu = k + u < qcnt && !done && (!EXACT || pw[u] <= 0.0f) && al[u] >= 1.0f / 255.0f;
         if constexpr (EXACT) {  // upstream's order, T (1 - alpha) and (rgb alpha) T, mirrored by the oracle
           const float tT = T * (1.0f - al[u]);
           const bool su = cu && tT < 0.0001f;  // T would drop below 1e-4: stop before this entry
