@@ -336,6 +336,7 @@ inline size_t sort_scratch_words(uint64_t n_max) {
 // lanes of this wave whose `bits`-bit digit equals mine (valid lanes only)
 __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits) {
   uint64_t peers = __ballot(valid);
+#pragma unroll
   for (int b = 0; b < bits; b++) {
     const uint64_t bb = __ballot((d >> b) & 1);
     peers &= ((d >> b) & 1) ? bb : ~bb;
@@ -400,11 +401,12 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_rowscan(uint32_t*
   if (threadIdx.x == 0) row_total[blockIdx.x] = carry;
 }
 
-// AUX: a second value stream travels with the keys (aux_in[i] -> aux_out[pos])
-template <bool AUX>
+// AUX: a second value stream travels with the keys (aux_in[i] -> aux_out[pos]).  BITS: the digit
+// width, a template parameter so the ballot ranking unrolls.
+template <bool AUX, int BITS>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
-    uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, int bits, uint32_t chunk,
+    uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, uint32_t chunk,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ row_total, bool drop,
     const uint32_t* __restrict__ aux_in, uint32_t* __restrict__ aux_out) {
   __shared__ uint32_t s_base[RADIX];      // global position of the next key of each digit
@@ -424,7 +426,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   }
   const uint64_t start = (uint64_t)blockIdx.x * chunk;
   const uint64_t end = start + chunk < n ? start + chunk : n;
-  const uint32_t mask = (1u << bits) - 1u;
+  constexpr uint32_t mask = (1u << BITS) - 1u;
   for (uint64_t t0 = start; t0 < end; t0 += SORT_TILE) {
     s_wcnt[0][tid] = 0;
     s_wcnt[1][tid] = 0;
@@ -446,7 +448,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
       const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
       const bool v = i < end && !(drop && key[r] == DEPTH_DROP);
       const uint32_t d = (key[r] >> shift) & mask;
-      const uint64_t peers = digit_peers(d, v, bits);
+      const uint64_t peers = digit_peers(d, v, BITS);
       const uint32_t before = (uint32_t)__popcll(peers & lanemask_lt());
       const uint32_t run = v ? s_wcnt[wid][d] : 0u;
       rank[r] = run + before;
@@ -500,6 +502,27 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   }
 }
 
+template <bool AUX>
+static inline void launch_scatter(int bits, uint32_t nb, hipStream_t st, const uint32_t* kin, const uint32_t* vin,
+                                  uint32_t* kout, uint32_t* vout, const uint32_t* nd, uint32_t n_max, int shift,
+                                  uint32_t chunk, const uint32_t* hist, const uint32_t* row_total, bool drop,
+                                  const uint32_t* ain, uint32_t* aout) {
+#define GS_SCATTER(B)                                                                                             \
+  GS_LAUNCH("radix_scatter", (k_radix_scatter<AUX, B>), dim3(nb), dim3(SORT_THREADS), 0, st, kin, vin, kout, vout, \
+            nd, n_max, shift, chunk, nb, hist, row_total, drop, ain, aout)
+  switch (bits) {
+    case 8: GS_SCATTER(8); break;
+    case 7: GS_SCATTER(7); break;
+    case 6: GS_SCATTER(6); break;
+    case 5: GS_SCATTER(5); break;
+    case 4: GS_SCATTER(4); break;
+    case 3: GS_SCATTER(3); break;
+    case 2: GS_SCATTER(2); break;
+    default: GS_SCATTER(1); break;
+  }
+#undef GS_SCATTER
+}
+
 // aux0 / aux_a / aux_b (optional): a second value stream in input order (aux0) that travels with
 // the keys; pass p writes aux_a (p even) or aux_b (p odd), so the result is in aux_b after an even
 // number of passes and in aux_a after an odd one.
@@ -531,13 +554,13 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
     GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX), dim3(SORT_THREADS), 0, st, hist, p.nb, row_total);
     const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
     if (aux0) {
-      GS_LAUNCH("radix_scatter", k_radix_scatter<true>, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, vsrc, kout, vout,
-                nd, n_max, shift, bits, p.chunk, p.nb, hist, row_total, drop, ain, aout);
+      launch_scatter<true>(bits, p.nb, st, kin, vsrc, kout, vout, nd, n_max, shift, p.chunk, hist, row_total, drop, ain,
+                           aout);
       ain = aout;
       aout = aout == aux_a ? aux_b : aux_a;
     } else {
-      GS_LAUNCH("radix_scatter", k_radix_scatter<false>, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, vsrc, kout,
-                vout, nd, n_max, shift, bits, p.chunk, p.nb, hist, row_total, drop, nullptr, nullptr);
+      launch_scatter<false>(bits, p.nb, st, kin, vsrc, kout, vout, nd, n_max, shift, p.chunk, hist, row_total, drop,
+                            nullptr, nullptr);
     }
     uint32_t* t;
     t = kin; kin = kout; kout = t;
