@@ -67,6 +67,9 @@ constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x
 #ifndef GS_BWD_NOZERO
 #define GS_BWD_NOZERO 0  // timing experiments only (wrong gradients)
 #endif
+#ifndef GS_PBWD_REG
+#define GS_PBWD_REG 1  // 0: the LDS-staged SH rows variant (113 vs 109.5 us at C3)
+#endif
 #ifndef GS_BWD_MINW
 #define GS_BWD_MINW 1
 #endif
@@ -395,8 +398,9 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
 // ------------------------------------------------------------------------------------------
 
 // SH backward for one Gaussian (order identical to oracle/gs_oracle.c sh_bwd_one).
-template <int DEG>
-// `row` is the Gaussian's SH row (3M floats) staged in LDS; on return it holds dL/dsh.
+// `row` is the Gaussian's SH row (3M floats) staged in LDS, or (REG) its first 3K floats in
+// registers; on return it holds dL/dsh (REG: the caller zero-fills [3K, 3M)).
+template <int DEG, bool REG = false>
 __device__ __forceinline__ void sh_backward(float* row, int M, float vx, float vy, float vz,
                                             uint32_t clamped, const float* dcol, float* dmean) {
   constexpr int K = (DEG + 1) * (DEG + 1);
@@ -462,7 +466,8 @@ __device__ __forceinline__ void sh_backward(float* row, int M, float vx, float v
   for (int k = 0; k < K; k++)
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) row[3 * k + ch] = b[k] * g[ch];
-  for (int k = 3 * K; k < 3 * M; k++) row[k] = 0.0f;
+  if (!REG)
+    for (int k = 3 * K; k < 3 * M; k++) row[k] = 0.0f;
   const float d0 = ddx[0] * g[0] + ddx[1] * g[1] + ddx[2] * g[2];
   const float d1 = ddy[0] * g[0] + ddy[1] * g[1] + ddy[2] * g[2];
   const float d2 = ddz[0] * g[0] + ddz[1] * g[1] + ddz[2] * g[2];
@@ -515,7 +520,7 @@ __device__ __forceinline__ void cov3d_backward(float sx, float sy, float sz, flo
             4.f * z * (dR[0][0] + dR[1][1]);
 }
 
-template <int DEG>
+template <int DEG, bool REG = false>
 __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g, const CameraArgs& c,
                                                    const uint32_t* __restrict__ tiles,
                                                    const uint8_t* __restrict__ clamped,
@@ -538,8 +543,10 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
     out.dmean3D[3 * i + 2] = 0.f;
     if (out.dcov3D)
       for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
-    if (DEG >= 0)
+    if (DEG >= 0 && !REG)
       for (int k = 0; k < 3 * g.M; k++) row[k] = 0.f;
+    if (DEG >= 0 && REG)
+      for (int k = 0; k < 3 * g.M; k++) out.dsh[(size_t)i * 3 * g.M + k] = 0.f;
     if (out.dscale)
       for (int k = 0; k < 3; k++) out.dscale[3 * i + k] = 0.f;
     if (out.drot)
@@ -636,7 +643,7 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
   if (DEG >= 0) {
     float shm[3];
     const float vx = px - c.campos[0], vy = py - c.campos[1], vz = pz - c.campos[2];
-    sh_backward<(DEG < 0 ? 0 : DEG)>(row, g.M, vx, vy, vz, clamped[i], dcol, shm);
+    sh_backward<(DEG < 0 ? 0 : DEG), REG>(row, g.M, vx, vy, vz, clamped[i], dcol, shm);
     dmean[0] = dmean[0] + shm[0];
     dmean[1] = dmean[1] + shm[1];
     dmean[2] = dmean[2] + shm[2];
@@ -679,6 +686,49 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
   }
 }
 
+// Register variant (GS_PBWD_REG, the default): the lane loads its own SH row (first 3K floats, 16-B loads when
+// the rows allow) and stores dL/dsh the same way; no LDS, so occupancy is set by registers alone.
+template <int DEG>
+__global__ __launch_bounds__(256) void k_preprocess_bwd_reg(GaussianArgs g, CameraArgs c,
+                                                            const uint32_t* __restrict__ tiles,
+                                                            const uint8_t* __restrict__ clamped,
+                                                            const float* __restrict__ gsum, GradOut out) {
+  constexpr int KF = 3 * (DEG + 1) * (DEG + 1);
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  if (i >= g.P) return;
+  const int rowf = 3 * g.M;
+  const float* src = g.shs + (size_t)i * rowf;
+  float* dst = out.dsh + (size_t)i * rowf;
+  const bool vec = (KF & 3) == 0 && (rowf & 3) == 0 && ((((uintptr_t)g.shs) | ((uintptr_t)out.dsh)) & 15) == 0;
+  float row[KF];
+  if (vec) {
+#pragma unroll
+    for (int q = 0; q < KF / 4; q++) {
+      const float4 v = reinterpret_cast<const float4*>(src)[q];
+      row[4 * q] = v.x, row[4 * q + 1] = v.y, row[4 * q + 2] = v.z, row[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < KF; k++) row[k] = src[k];
+  }
+  // invisible: every gradient (dL/dsh too) is written as zero by this call; split from the
+  // visible call so each inlined copy is specialised (measured 113 -> 109.5 us at C3)
+  if (tiles[i] == 0) {
+    preprocess_bwd_one<DEG, true>(i, g, c, tiles, clamped, gsum, out, row);
+    return;
+  }
+  preprocess_bwd_one<DEG, true>(i, g, c, tiles, clamped, gsum, out, row);
+  if (vec) {
+#pragma unroll
+    for (int q = 0; q < KF / 4; q++)
+      reinterpret_cast<float4*>(dst)[q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < KF; k++) dst[k] = row[k];
+  }
+  for (int k = KF; k < rowf; k++) dst[k] = 0.0f;
+}
+
 void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, float* gradrec,
                     bool have_records, const GradOut& out, hipStream_t st) {
   if (g.P <= 0) return;
@@ -693,6 +743,23 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
               geo.gsum, out);
     return;
   }
+#if GS_PBWD_REG
+  switch (g.D) {
+    case 0:
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd_reg<0>, grid, block, 0, st, g, c, geo.tiles, geo.clamped, geo.gsum, out);
+      break;
+    case 1:
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd_reg<1>, grid, block, 0, st, g, c, geo.tiles, geo.clamped, geo.gsum, out);
+      break;
+    case 2:
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd_reg<2>, grid, block, 0, st, g, c, geo.tiles, geo.clamped, geo.gsum, out);
+      break;
+    default:
+      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd_reg<3>, grid, block, 0, st, g, c, geo.tiles, geo.clamped, geo.gsum, out);
+      break;
+  }
+  return;
+#endif
   switch (g.D) {
     case 0:
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<0>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,
