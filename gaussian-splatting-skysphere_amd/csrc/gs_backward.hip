@@ -110,7 +110,8 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   const f2 pfy = {(float)pyA, (float)pyB};
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
-  const uint32_t n_eff = min(tile_max[tile], n);
+  const uint4 qm = reinterpret_cast<const uint4*>(tile_max)[tile];  // per-quadrant largest n_contrib
+  const uint32_t n_eff = min(max(max(qm.x, qm.y), max(qm.z, qm.w)), n);
 
   const size_t HW = (size_t)c.W * c.H;
   const size_t pixA = inA ? (size_t)pyA * c.W + px : 0, pixB = inB ? (size_t)pyB * c.W + px : 0;

@@ -459,11 +459,92 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
 // ------------------------------------------------------------------------------------------
 // render forward
 // ------------------------------------------------------------------------------------------
-// Entries are staged as three 16-B LDS records at one byte offset o (o, o + 4 KB, o + 8 KB):
+// Entries are staged as three 16-B LDS records at one byte offset o (o, o + 16 NB, o + 32 NB for
+// a batch of NB entries):
 //   (x, y, r, g) | falloff coefficients + opacity | (b, bits(entry index + 1), -, -)
 // and each quadrant wave's dense list holds the offsets (u16), read FWD_ILP = 4 at a time with one
 // 8-B LDS read: a list entry costs no address arithmetic and no dependent list read per entry.
 constexpr int FWD_ILP = 4;
+
+struct FwdPix {
+  float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+  uint32_t last = 0;
+  bool done;
+};
+
+// Walk one quadrant wave's list of qcnt staged entries (the list is padded with 2 FWD_ILP zero
+// offsets) for the lane's pixel.
+template <bool EXACT, int NB>
+__device__ __forceinline__ void fwd_walk(const char* ent, const uint16_t* qlist, uint32_t qcnt, float pfx, float pfy,
+                                         FwdPix& px) {
+  // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
+  // compositing is then applied entry by entry in list order, exactly as one at a time.  The
+  // next group's offsets are read one trip ahead (one dependent LDS round trip per trip).
+  uint2 wn = *reinterpret_cast<const uint2*>(&qlist[0]);
+  for (uint32_t k = 0; k < qcnt; k += FWD_ILP) {
+    const uint2 w = wn;
+    wn = *reinterpret_cast<const uint2*>(&qlist[k + FWD_ILP]);
+    const uint32_t o[FWD_ILP] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
+    float pw[FWD_ILP], al[FWD_ILP];
+#pragma unroll
+    for (int u = 0; u < FWD_ILP; u++) {
+      const float4 xr = *reinterpret_cast<const float4*>(ent + o[u]);
+      const float4 co = *reinterpret_cast<const float4*>(ent + o[u] + 16 * NB);
+      pw[u] = falloff_log2(co, xr.x - pfx, xr.y - pfy);  // log2(e) * power
+      al[u] = fminf(0.99f, co.w * exp2_m<EXACT>(pw[u]));
+    }
+#pragma unroll
+    for (int u = 0; u < FWD_ILP; u++) {
+      const float4 xr = *reinterpret_cast<const float4*>(ent + o[u]);
+      const float2 bl = *reinterpret_cast<const float2*>(ent + o[u] + 32 * NB);
+      const float rr = xr.z, rg = xr.w, rb = bl.x;
+      // branch-free compositing (selects instead of divergent ifs)
+      // upstream skips power > 0; with a positive-definite conic that only happens by rounding
+      // within ~1e-3 px of a splat centre, so the fast mode leaves the test out (the backward
+      // matches it entry for entry)
+      bool cu = k + u < qcnt && !px.done && (!EXACT || pw[u] <= 0.0f) && al[u] >= 1.0f / 255.0f;
+      if constexpr (EXACT) {  // upstream's order, T (1 - alpha) and (rgb alpha) T, mirrored by the oracle
+        const float tT = px.T * (1.0f - al[u]);
+        const bool su = cu && tT < 0.0001f;  // T would drop below 1e-4: stop before this entry
+        px.done = px.done || su;
+        cu = cu && !su;
+        px.C0 = cu ? px.C0 + rr * al[u] * px.T : px.C0;
+        px.C1 = cu ? px.C1 + rg * al[u] * px.T : px.C1;
+        px.C2 = cu ? px.C2 + rb * al[u] * px.T : px.C2;
+        px.T = cu ? tT : px.T;
+      } else {
+        // T - alpha T as one FMA (one rounding of T (1 - alpha)); one weight, three FMAs (a
+        // skipped entry adds rgb * 0); `keep` as a >= test so both masks come from one compare
+        const float tT = __builtin_fmaf(-al[u], px.T, px.T);
+        const bool keep = tT >= 0.0001f;
+        px.done = px.done || (cu && !keep);
+        cu = cu && keep;
+        const float wgt = cu ? al[u] * px.T : 0.0f;
+        px.C0 = __builtin_fmaf(rr, wgt, px.C0);
+        px.C1 = __builtin_fmaf(rg, wgt, px.C1);
+        px.C2 = __builtin_fmaf(rb, wgt, px.C2);
+        px.T = cu ? tT : px.T;
+      }
+      px.last = cu ? __float_as_uint(bl.y) : px.last;
+    }
+    if (__ballot(!px.done) == 0) break;
+  }
+}
+
+__device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q, bool inside, const FwdPix& px,
+                                          float* __restrict__ out, float* __restrict__ final_T,
+                                          uint32_t* __restrict__ n_contrib) {
+  if (inside) {
+    const size_t pix = (size_t)q.py * c.W + q.px, HW = (size_t)c.W * c.H;
+    final_T[pix] = px.T;
+    n_contrib[pix] = px.last;
+    out[pix] = px.C0 + px.T * c.bg[0];
+    out[HW + pix] = px.C1 + px.T * c.bg[1];
+    out[2 * HW + pix] = px.C2 + px.T * c.bg[2];
+  }
+}
+
+// One 256-lane workgroup per tile; 256-entry batches staged by the whole workgroup.
 template <bool EXACT>
 __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                          const uint32_t* __restrict__ point_list,
@@ -474,23 +555,19 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   __shared__ float4 s_ent[3 * GS_BLOCK];
   __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
   __shared__ __attribute__((aligned(8))) uint16_t s_qlist[4][GS_BLOCK + 2 * FWD_ILP];  // per quadrant wave: byte offsets
-  __shared__ uint32_t s_max;
   const uint32_t tile = blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const QuadPix q = quad_pixel(tx, ty, wid, lane);
   const bool inside = q.px < c.W && q.py < c.H;
-  const float pfx = (float)q.px, pfy = (float)q.py;
   const uint2 range = ranges[tile];
   const uint32_t n = range.y - range.x;
   const char* ent = reinterpret_cast<const char*>(s_ent);
-  if (tid == 0) s_max = 0;
-  float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
-  uint32_t last = 0;
-  bool done = !inside;
+  FwdPix px;
+  px.done = !inside;
   for (uint32_t base = 0; base < n; base += GS_BLOCK) {
-    if (__syncthreads_and(done)) break;
+    if (__syncthreads_and(px.done)) break;
     const uint32_t cnt = min((uint32_t)GS_BLOCK, n - base);
     uint32_t qmask = 0;
     if ((uint32_t)tid < cnt) {
@@ -503,7 +580,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
     }
     publish_masks(qmask, s_mask, tid);
     __syncthreads();
-    if (__ballot(!done) == 0) continue;
+    if (__ballot(!px.done) == 0) continue;
     // dense, in-order list of this quadrant's entries (as LDS byte offsets), built by the wave
     uint32_t qcnt = 0;
 #pragma unroll
@@ -516,76 +593,84 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
     }
     if (lane < 2 * FWD_ILP) s_qlist[wid][qcnt + lane] = 0;  // pad the last group and the prefetch (masked below)
     __builtin_amdgcn_wave_barrier();
-    // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
-    // compositing is then applied entry by entry in list order, exactly as one at a time
-    // the next group's offsets are read one trip ahead (one dependent LDS round trip per trip)
-    uint2 wn = *reinterpret_cast<const uint2*>(&s_qlist[wid][0]);
-    for (uint32_t k = 0; k < qcnt; k += FWD_ILP) {
-      const uint2 w = wn;
-      wn = *reinterpret_cast<const uint2*>(&s_qlist[wid][k + FWD_ILP]);
-      const uint32_t o[FWD_ILP] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
-      float pw[FWD_ILP], al[FWD_ILP];
-#pragma unroll
-      for (int u = 0; u < FWD_ILP; u++) {
-        const float4 xr = *reinterpret_cast<const float4*>(ent + o[u]);
-        const float4 co = *reinterpret_cast<const float4*>(ent + o[u] + 16 * GS_BLOCK);
-        pw[u] = falloff_log2(co, xr.x - pfx, xr.y - pfy);  // log2(e) * power
-        al[u] = fminf(0.99f, co.w * exp2_m<EXACT>(pw[u]));
-      }
-#pragma unroll
-      for (int u = 0; u < FWD_ILP; u++) {
-        const float4 xr = *reinterpret_cast<const float4*>(ent + o[u]);
-        const float2 bl = *reinterpret_cast<const float2*>(ent + o[u] + 32 * GS_BLOCK);
-        const float rr = xr.z, rg = xr.w, rb = bl.x;
-        // branch-free compositing (selects instead of divergent ifs)
-        // upstream skips power > 0; with a positive-definite conic that only happens by rounding
-        // within ~1e-3 px of a splat centre, so the fast mode leaves the test out (the backward
-        // matches it entry for entry)
-        bool cu = k + u < qcnt && !done && (!EXACT || pw[u] <= 0.0f) && al[u] >= 1.0f / 255.0f;
-        if constexpr (EXACT) {  // upstream's order, T (1 - alpha) and (rgb alpha) T, mirrored by the oracle
-          const float tT = T * (1.0f - al[u]);
-          const bool su = cu && tT < 0.0001f;  // T would drop below 1e-4: stop before this entry
-          done = done || su;
-          cu = cu && !su;
-          C0 = cu ? C0 + rr * al[u] * T : C0;
-          C1 = cu ? C1 + rg * al[u] * T : C1;
-          C2 = cu ? C2 + rb * al[u] * T : C2;
-          T = cu ? tT : T;
-        } else {
-          // T - alpha T as one FMA (one rounding of T (1 - alpha)); one weight, three FMAs (a
-          // skipped entry adds rgb * 0); `keep` as a >= test so both masks come from one compare
-          const float tT = __builtin_fmaf(-al[u], T, T);
-          const bool keep = tT >= 0.0001f;
-          done = done || (cu && !keep);
-          cu = cu && keep;
-          const float wgt = cu ? al[u] * T : 0.0f;
-          C0 = __builtin_fmaf(rr, wgt, C0);
-          C1 = __builtin_fmaf(rg, wgt, C1);
-          C2 = __builtin_fmaf(rb, wgt, C2);
-          T = cu ? tT : T;
-        }
-        last = cu ? __float_as_uint(bl.y) : last;
-      }
-      if (__ballot(!done) == 0) break;
-    }
+    fwd_walk<EXACT, GS_BLOCK>(ent, s_qlist[wid], qcnt, (float)q.px, (float)q.py, px);
   }
-  if (inside) {
-    const size_t pix = (size_t)q.py * c.W + q.px, HW = (size_t)c.W * c.H;
-    final_T[pix] = T;
-    n_contrib[pix] = last;
-    out[pix] = C0 + T * c.bg[0];
-    out[HW + pix] = C1 + T * c.bg[1];
-    out[2 * HW + pix] = C2 + T * c.bg[2];
-  }
-  __syncthreads();
-  if (last) atomicMax(&s_max, last);
-  __syncthreads();
-  if (tid == 0) tile_max[tile] = s_max;
+  fwd_store(c, q, inside, px, out, final_T, n_contrib);
+  const uint32_t wmax = wave_max_u32(px.last);
+  if (lane == 0) tile_max[4 * tile + wid] = wmax;
 }
 
+// One wave per (tile, quadrant), no workgroup barriers: each wave stages the tile's entries 64 at
+// a time, culls them to its own quadrant and walks them, and finishes as soon as its 64 pixels
+// are done (the workgroup version waits for its slowest quadrant).  Workgroup b takes tile
+// (b / 32) * 8 + b % 8, quadrant (b / 8) % 4, so the four quadrant waves of a tile share the
+// workgroup-to-XCD round robin (b % 8) and their repeated entry loads hit one L2.
+constexpr int FWDQ_NB = 64;
+template <bool EXACT>
+__global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* __restrict__ ranges,
+                                                     const uint32_t* __restrict__ point_list,
+                                                     const uint32_t* __restrict__ presort_gid,
+                                                     const float4* __restrict__ splat, float* __restrict__ out,
+                                                     float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                                                     uint32_t* __restrict__ tile_max) {
+  __shared__ float4 s_ent[3 * FWDQ_NB];
+  __shared__ __attribute__((aligned(8))) uint16_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
+  const uint32_t b = blockIdx.x;
+  const uint32_t tile = (b >> 5) * 8 + (b & 7);
+  if (tile >= (uint32_t)(c.gx * c.gy)) return;  // (grid padded to whole groups of 8 tiles)
+  const int wid = (int)((b >> 3) & 3);
+  const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
+  const int lane = threadIdx.x;
+  const QuadPix q = quad_pixel(tx, ty, wid, lane);
+  const bool inside = q.px < c.W && q.py < c.H;
+  const uint2 range = ranges[tile];
+  const uint32_t n = range.y - range.x;
+  const char* ent = reinterpret_cast<const char*>(s_ent);
+  const float qx = (float)(tx * GS_TILE + 8 * (wid & 1)), qy = (float)(ty * GS_TILE + 8 * (wid >> 1));
+  FwdPix px;
+  px.done = !inside;
+  for (uint32_t base = 0; base < n; base += FWDQ_NB) {
+    if (__ballot(!px.done) == 0) break;
+    bool meets = false;
+    if (base + lane < n) {
+      const uint32_t gid = presort_gid[point_list[range.x + base + lane]];
+      const float4 a = splat[3 * gid], bb = splat[3 * gid + 1], d = splat[3 * gid + 2];
+      s_ent[lane] = make_float4(a.x, a.y, bb.z, bb.w);
+      s_ent[FWDQ_NB + lane] = fall_coefs(a.z, a.w, bb.x, bb.y);
+      s_ent[2 * FWDQ_NB + lane] = make_float4(d.x, __uint_as_float(base + lane + 1), 0.0f, 0.0f);
+      meets = d.z >= 0.0f && ellipse_meets_rect(a.x, a.y, a.z, a.w, bb.x, d.z, qx, qx + 7.0f, qy, qy + 7.0f);
+    }
+    const uint64_t m = __ballot(meets);
+    if (meets)
+      s_qlist[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+          (uint16_t)(16 * lane);
+    const uint32_t qcnt = (uint32_t)__popcll(m);
+    if (lane < 2 * FWD_ILP) s_qlist[qcnt + lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    fwd_walk<EXACT, FWDQ_NB>(ent, s_qlist, qcnt, (float)q.px, (float)q.py, px);
+    __builtin_amdgcn_wave_barrier();  // the next round overwrites the staged entries
+  }
+  fwd_store(c, q, inside, px, out, final_T, n_contrib);
+  const uint32_t wmax = wave_max_u32(px.last);
+  if (lane == 0) tile_max[4 * tile + wid] = wmax;
+}
+
+#ifndef GS_FWD_WAVE
+#define GS_FWD_WAVE 1
+#endif
 void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
                 hipStream_t st) {
   const int tiles = c.gx * c.gy;
+  if (GS_FWD_WAVE) {
+    const int blocks = ((tiles + 7) / 8) * 32;
+    if (exact_exp())
+      GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
+                bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
+    else
+      GS_LAUNCH("render_fwd", k_render_fwd_q<false>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
+                bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
+    return;
+  }
   if (exact_exp())
     GS_LAUNCH("render_fwd", k_render_fwd<true>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
               bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);

@@ -8,7 +8,8 @@
 //                                    written by preprocess) | offsets u32 |
 //                                    scan partials | sort scratch | counters
 //   binning   (per instance, I)      tile keys/vals x2 u32 | presort_gid u32 | sort scratch
-//   image     (per pixel / tile)     ranges uint2 | final_T f32 | n_contrib u32 | tile_max u32
+//   image     (per pixel / tile)     ranges uint2 | final_T f32 | n_contrib u32 | tile_max u32 x4
+//                                    (largest n_contrib of each 8x8 quadrant)
 //   gradient  (per instance, I)      9 f32 per (Gaussian, tile) instance (backward scratch)
 #pragma once
 #include <stddef.h>
@@ -182,7 +183,7 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t npix = (size_t)W * H;
   if (tiles == 0) tiles = 1;
   if (npix == 0) npix = 1;
-  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 4);
+  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16);
   if (out && base) {
     out->ranges = (uint2*)(base + o_r);
     out->final_T = (float*)(base + o_t);
