@@ -122,10 +122,9 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   const f2 dp1 = {inA ? dL_dpix[HW + pixA] : 0.0f, inB ? dL_dpix[HW + pixB] : 0.0f};
   const f2 dp2 = {inA ? dL_dpix[2 * HW + pixA] : 0.0f, inB ? dL_dpix[2 * HW + pixB] : 0.0f};
   const f2 bg_dot = c.bg[0] * dp0 + c.bg[1] * dp1 + c.bg[2] * dp2;
-  const f2 tbg = -T_final * bg_dot;  // d(T_final bg . dL/dpix)/dalpha = tbg / (1 - alpha)
-  f2 Aacc = 0.0f;  // sum_c accum_rec_c * dL/dpix_c
-  f2 Lc = 0.0f;    // sum_c last_color_c * dL/dpix_c
-  f2 last_alpha = 0.0f;
+  // U = S + T_final bg . dL/dpix, S = sum over the entries behind the current one of
+  // (colour . dL/dpix) alpha T: the suffix the upstream carries as accum_rec / last_alpha
+  f2 U = T_final * bg_dot;
   const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
   const uint32_t wave_last = __builtin_amdgcn_readfirstlane(wave_max_u32(max(lastA, lastB)));
 
@@ -146,11 +145,12 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     // contribute gets dL/dalpha = alpha T = 0, which zeroes all of its terms.
     // The flush maps the wave sums to the upstream record: dmean2D.x = -W/2 (cxx S3 + cxy S4),
     // dmean2D.y = -H/2 (cyy S4 + cxy S3), dconic = -S5/2, -S6/2, -S7/2.
-    // accum_rec is carried as A = sum_c accum_rec_c dL/dpix_c and last_color as
-    // Lc = sum_c last_color_c dL/dpix_c, which is all dL/dalpha needs.
-    // A pixel that does not contribute is run as an alpha = 0 entry: T, accum_rec and last_alpha
-    // then pass through unchanged bit for bit (1 / (1 - 0) = 1, fma(0, x, A) = A) and its colour
-    // terms vanish, so only dL/dalpha needs a mask.
+    // dL/dalpha: upstream's accum_rec recurrence gives T_i accum_rec_i . dL/dpix = S_i / (1 - a_i)
+    // with S_i = sum_{j behind i} Cd_j a_j T_j, so dL/dalpha = T_i Cd_i - U / (1 - a_i) with
+    // U = S_i + T_final bg . dL/dpix, and U grows by Cd_i a_i T_i once entry i is done.
+    // A pixel that does not contribute is run as an alpha = 0 entry: T and U then pass through
+    // unchanged bit for bit (1 / (1 - 0) = 1, fma(x, 0, U) = U) and its colour terms vanish, so
+    // only dL/dalpha needs a mask.
     const f2 ae = {cA ? alpha.x : 0.0f, cB ? alpha.y : 0.0f};
     const f2 omA = 1.f - ae;
     f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
@@ -161,8 +161,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     const f2 Tn = T * inv;
     const f2 dch = ae * Tn;
     const f2 Cd = pk_fma((f2)(rgb.z), dp2, pk_fma((f2)(rgb.y), dp1, rgb.x * dp0));
-    const f2 An = pk_fma(last_alpha, Lc - Aacc, Aacc);  // last_alpha Lc + (1 - last_alpha) Aacc
-    const f2 dLa = pk_fma(Cd - An, Tn, tbg * inv);
+    const f2 dLa = pk_fma(Tn, Cd, -(U * inv));
     const f2 dLm = {cA ? dLa.x : 0.0f, cB ? dLa.y : 0.0f};
     const f2 q = v.oG * dLm;  // dL/dG G = o G dL/dalpha (not gated by the 0.99 clamp)
     const f2 w4 = q * dy;
@@ -177,9 +176,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     s[6] = dx * s[4];
     s[7] = __builtin_fmaf(w4.x, dy.x, w4.y * dy.y);
     T = Tn;
-    Aacc = An;
-    Lc = Cd;
-    last_alpha = ae;
+    U = pk_fma(Cd, dch, U);
     // wave sums: row r of d0 / d1 holds s[r] / s[4 + r]; every row of d8 a quarter of s[8]
     float d0, d1, d8;
     wave_sum9_rows(s, d0, d1, d8);

@@ -462,8 +462,8 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
 // Entries are staged as three 16-B LDS records at one byte offset o (o, o + 16 NB, o + 32 NB for
 // a batch of NB entries):
 //   (x, y, r, g) | falloff coefficients + opacity | (b, bits(entry index + 1), -, -)
-// and each quadrant wave's dense list holds the offsets (u16), read FWD_ILP = 4 at a time with one
-// 8-B LDS read: a list entry costs no address arithmetic and no dependent list read per entry.
+// and each quadrant wave's dense list holds the offsets (u32), read FWD_ILP = 4 at a time with one
+// 16-B LDS read: a list entry costs no address arithmetic, no unpacking and no dependent list read.
 constexpr int FWD_ILP = 4;
 
 struct FwdPix {
@@ -475,16 +475,16 @@ struct FwdPix {
 // Walk one quadrant wave's list of qcnt staged entries (the list is padded with 2 FWD_ILP zero
 // offsets) for the lane's pixel.
 template <bool EXACT, int NB>
-__device__ __forceinline__ void fwd_walk(const char* ent, const uint16_t* qlist, uint32_t qcnt, float pfx, float pfy,
+__device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist, uint32_t qcnt, float pfx, float pfy,
                                          FwdPix& px) {
   // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
   // compositing is then applied entry by entry in list order, exactly as one at a time.  The
   // next group's offsets are read one trip ahead (one dependent LDS round trip per trip).
-  uint2 wn = *reinterpret_cast<const uint2*>(&qlist[0]);
+  uint4 wn = *reinterpret_cast<const uint4*>(&qlist[0]);
   for (uint32_t k = 0; k < qcnt; k += FWD_ILP) {
-    const uint2 w = wn;
-    wn = *reinterpret_cast<const uint2*>(&qlist[k + FWD_ILP]);
-    const uint32_t o[FWD_ILP] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
+    const uint4 w = wn;
+    wn = *reinterpret_cast<const uint4*>(&qlist[k + FWD_ILP]);
+    const uint32_t o[FWD_ILP] = {w.x, w.y, w.z, w.w};
     float pw[FWD_ILP], al[FWD_ILP];
 #pragma unroll
     for (int u = 0; u < FWD_ILP; u++) {
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
                                                          uint32_t* __restrict__ tile_max) {
   __shared__ float4 s_ent[3 * GS_BLOCK];
   __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
-  __shared__ __attribute__((aligned(8))) uint16_t s_qlist[4][GS_BLOCK + 2 * FWD_ILP];  // per quadrant wave: byte offsets
+  __shared__ __attribute__((aligned(16))) uint32_t s_qlist[4][GS_BLOCK + 2 * FWD_ILP];  // per quadrant wave: byte offsets
   const uint32_t tile = blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -588,7 +588,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
       const uint64_t m = uniform_u64(s_mask[g][wid]);
       if ((m >> lane) & 1ull)
         s_qlist[wid][qcnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-            (uint16_t)(16 * (g * 64 + lane));
+            16u * (g * 64 + lane);
       qcnt += (uint32_t)__popcll(m);
     }
     if (lane < 2 * FWD_ILP) s_qlist[wid][qcnt + lane] = 0;  // pad the last group and the prefetch (masked below)
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
                                                      float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                      uint32_t* __restrict__ tile_max) {
   __shared__ float4 s_ent[3 * FWDQ_NB];
-  __shared__ __attribute__((aligned(8))) uint16_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
+  __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
   const uint32_t b = blockIdx.x;
   const uint32_t tile = (b >> 5) * 8 + (b & 7);
   if (tile >= (uint32_t)(c.gx * c.gy)) return;  // (grid padded to whole groups of 8 tiles)
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
     const uint64_t m = __ballot(meets);
     if (meets)
       s_qlist[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-          (uint16_t)(16 * lane);
+          16u * lane;
     const uint32_t qcnt = (uint32_t)__popcll(m);
     if (lane < 2 * FWD_ILP) s_qlist[qcnt + lane] = 0;
     __builtin_amdgcn_wave_barrier();
