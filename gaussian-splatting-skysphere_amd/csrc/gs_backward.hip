@@ -70,6 +70,11 @@ constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x
 #ifndef GS_PBWD_REG
 #define GS_PBWD_REG 1  // 0: the LDS-staged SH rows variant (113 vs 109.5 us at C3)
 #endif
+#ifndef GS_BWD_HALFROW
+#define GS_BWD_HALFROW 1  // 0: row sums (4 DPP steps) with one writer lane per row
+#endif
+// LDS row of one per-wave partial record: s0..7 + the partials of s8 (8 half-row or 4 row ones)
+constexpr int ACC_STRIDE = GS_BWD_HALFROW ? 16 : 12;
 #ifndef GS_BWD_MINW
 #define GS_BWD_MINW 1
 #endif
@@ -131,7 +136,13 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   // this lane's row slot of entry 0's record, as an LDS (32-bit) pointer: the per-entry address
   // is then one 32-bit add instead of a 64-bit multiply-add on a generic pointer
   using lds_float = __attribute__((address_space(3))) float;
+#if GS_BWD_HALFROW
+  // writer lanes 16 r + 8 h: s[r + 4 h] at slot r + 4 h, their s8 partial at slot 8 + r + 4 h
+  lds_float* const acc_lane = (lds_float*)(&s_acc[wid][0][(lane >> 4) + 4 * ((lane >> 3) & 1)]);
+  const bool hi8 = (lane & 8) != 0;
+#else
   lds_float* const acc_lane = (lds_float*)(&s_acc[wid][0][lane >> 4]);
+#endif
   // gradient commit of entry j (walk order) for the lane's contributing pixels
   auto apply = [&](uint32_t j, const Eval& v, const float4 xr) {
     const float4 rgb = make_float4(xr.z, xr.w, s_ent[2 * BWD_BATCH + j].x, 0.0f);
@@ -177,6 +188,18 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     s[7] = __builtin_fmaf(w4.x, dy.x, w4.y * dy.y);
     T = Tn;
     U = pk_fma(Cd, dch, U);
+#if GS_BWD_HALFROW
+    float d, d8;
+    wave_sum9_halfrows(s, hi8, d, d8);
+    asm volatile("" ::"v"(d), "v"(d8));
+    if ((lane & 7) == 0) {
+      uint32_t eo = j * ACC_STRIDE;
+      asm volatile("" : "+s"(eo));
+      lds_float* acc = acc_lane + eo;
+      acc[0] = d;
+      acc[8] = d8;
+    }
+#else
     // wave sums: row r of d0 / d1 holds s[r] / s[4 + r]; every row of d8 a quarter of s[8]
     float d0, d1, d8;
     wave_sum9_rows(s, d0, d1, d8);
@@ -192,6 +215,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
       acc[4] = d1;
       acc[8] = d8;
     }
+#endif
   };
 
   for (uint32_t base = 0; base < n_eff; base += BWD_BATCH) {
@@ -267,8 +291,9 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         float S[GRAD_REC];
 #pragma unroll
         for (int k = 0; k < 8; k++) S[k] = s_acc[0][t][k] + s_acc[1][t][k];
-        S[8] = ((s_acc[0][t][8] + s_acc[0][t][9]) + (s_acc[0][t][10] + s_acc[0][t][11])) +
-               ((s_acc[1][t][8] + s_acc[1][t][9]) + (s_acc[1][t][10] + s_acc[1][t][11]));
+        S[8] = 0.0f;
+#pragma unroll
+        for (int k = 8; k < ACC_STRIDE; k++) S[8] += s_acc[0][t][k] + s_acc[1][t][k];
         const float4 co = s_cr[t];
         Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)s_slot[t] * GRAD_REC);
         r[0] = Rec3{S[0], S[1], S[2]};

@@ -445,6 +445,28 @@ __device__ __forceinline__ void wave_sum9_rows(const float* s, float& d0, float&
   d8 = v[2];
 }
 
+// Nine wave sums down to 8-lane groups, with a half-row transpose after the swaps: on return
+// lanes 16 r + 8 h .. + 7 (r < 4, h < 2) hold in d the 64-lane sum of s[r + 4 h] and in d8 the sum
+// of s[8] over that 8-lane group of the swapped layout (the eight group values add up to the
+// total).  The transpose (two selects and one row_ror:8 add) halves two values at once, so d needs
+// three more DPP steps instead of 2 x 4, and d8 stops at 8-lane sums.  hi: lane bit 3.
+__device__ __forceinline__ void wave_sum9_halfrows(const float* s, bool hi, float& d, float& d8) {
+  const float c0 = swap32_add(s[0], s[2]), c1 = swap32_add(s[1], s[3]);
+  const float c2 = swap32_add(s[4], s[6]), c3 = swap32_add(s[5], s[7]);
+  const float a = swap16_add(c0, c1), b = swap16_add(c2, c3);
+  // lanes 0-7 of a row keep a (plus lane + 8's a), lanes 8-15 keep b (plus lane - 8's b)
+  const float keep = hi ? b : a, send = hi ? a : b;
+  float v[2] = {keep + dpp_f<0x128>(send), s[8]};  // row_ror:8
+#pragma unroll
+  for (int k = 0; k < 2; k++) v[k] = v[k] + dpp_f<0xB1>(v[k]);
+#pragma unroll
+  for (int k = 0; k < 2; k++) v[k] = v[k] + dpp_f<0x4E>(v[k]);
+#pragma unroll
+  for (int k = 0; k < 2; k++) v[k] = v[k] + dpp_f<0x141>(v[k]);
+  d = v[0];
+  d8 = v[1];
+}
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {

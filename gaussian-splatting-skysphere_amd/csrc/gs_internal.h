@@ -25,7 +25,6 @@ namespace gs {
 bool exact_exp();
 
 constexpr int GRAD_REC = 9;    // dcolor(3), dmean2D(2), dconic(xx, xy, yy), dopacity
-constexpr int ACC_STRIDE = 12;  // LDS row of one per-wave partial record: s0..7 + 4 partials of s8
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 

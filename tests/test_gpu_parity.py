@@ -130,20 +130,23 @@ def _check_forward_exact(oracle_fw, cam, sc, device, colors=None, cov3D=None, de
     np.testing.assert_array_equal(color.cpu().numpy(), oracle_fw["color"])
 
 
-def _check_backward(gr, leaves, colors=None, cov3D=None, rtol=RTOL):
+def _check_backward(gr, leaves, colors=None, cov3D=None, rtol=RTOL, chain_frac=None):
+    """chain_frac: bound (fraction of the max) for the gradients reached through the conic ->
+    covariance chain (dmeans3D, dscales, drotations, dcov3D); default rtol."""
     g = lambda k: leaves[k].grad.detach().cpu().numpy()  # noqa: E731
+    cf = rtol if chain_frac is None else chain_frac
     _tol_check(g("means2D"), gr["dmeans2D"], "dmeans2D", rtol, rtol)
     _tol_check(g("opacities"), gr["dopacity"], "dopacity", rtol, rtol)
-    _tol_check(g("means3D"), gr["dmeans3D"], "dmeans3D", rtol, rtol)
+    _tol_check(g("means3D"), gr["dmeans3D"], "dmeans3D", rtol, cf)
     if colors is None:
         _tol_check(g("shs"), gr["dsh"], "dsh", rtol, rtol)
     else:
         _tol_check(g("colors"), gr["dcolors"], "dcolors", rtol, rtol)
     if cov3D is None:
-        _tol_check(g("scales"), gr["dscales"], "dscales", rtol, rtol)
-        _tol_check(g("rotations"), gr["drotations"], "drotations", rtol, rtol)
+        _tol_check(g("scales"), gr["dscales"], "dscales", rtol, cf)
+        _tol_check(g("rotations"), gr["drotations"], "drotations", rtol, cf)
     else:
-        _tol_check(g("cov3D"), gr["dcov3D"], "dcov3D", rtol, rtol)
+        _tol_check(g("cov3D"), gr["dcov3D"], "dcov3D", rtol, cf)
 
 
 CASES = [
@@ -258,7 +261,10 @@ def _large_splat_scene(anisotropy):
 def test_large_and_elongated_splats(oracle, device):
     """Skysphere-like mix: many small splats plus large ones spanning dozens of tiles and several
     duplicate workgroups (row spans over many tile rows, segments crossing workgroups, long
-    per-Gaussian record runs)."""
+    per-Gaussian record runs).  The covariance-chain gradients get 1e-4 of their max: large
+    splats' per-pixel dL/dconic terms cancel across hundreds of tiles, the GPU sums them in fp32
+    wave trees (the oracle in fp64), and the conic -> covariance chain amplifies the ~1e-7
+    relative difference (see test_needle_splats_conditioning for the extreme case)."""
     cam, sc = _large_splat_scene(anisotropy=3.0)
     W, H = cam.image_width, cam.image_height
     bg = np.array([0.1, 0.2, 0.3], np.float32)
@@ -270,7 +276,7 @@ def test_large_and_elongated_splats(oracle, device):
     dpix = gs_scenes.dl_dimage(H, W, seed=23).numpy()
     img, _, leaves = _gpu_run(cam, sc, device, bg, dpix)
     np.testing.assert_array_equal(img.detach().cpu().numpy(), ofw["color"])
-    _check_backward(oracle.backward(osc, dpix), leaves)
+    _check_backward(oracle.backward(osc, dpix), leaves, chain_frac=1e-4)
 
 
 def test_needle_splats_conditioning(oracle, device):
