@@ -24,7 +24,7 @@ namespace gs {
 struct Eval {
   float4 co;
   float dx;
-  f2 dy, G, oG, alpha;
+  f2 dy, oG;
   bool cA, cB;
 };
 template <bool EXACT>
@@ -35,13 +35,15 @@ __device__ __forceinline__ Eval eval_pair(float4 xy, float4 co, float pfx, f2 pf
   v.dx = xy.x - pfx;
   v.dy = xy.y - pfy;
   const f2 power = falloff_log2_pk(co, v.dx, v.dy);  // log2(e) * power (co: fall_coefs)
-  v.G = exp2_pk_m<EXACT>(power);
-  v.oG = co.w * v.G;
-  v.alpha.x = fminf(0.99f, v.oG.x);
-  v.alpha.y = fminf(0.99f, v.oG.y);
-  // fast mode drops upstream's `power > 0` skip exactly as the forward does (k_render_fwd)
-  v.cA = e < lastA && (!EXACT || power.x <= 0.0f) && v.alpha.x >= 1.0f / 255.0f;
-  v.cB = e < lastB && (!EXACT || power.y <= 0.0f) && v.alpha.y >= 1.0f / 255.0f;
+  const f2 G = exp2_pk_m<EXACT>(power);
+  // two scalar multiplies: a packed one would first copy the opacity into a register pair
+  v.oG.x = co.w * G.x;
+  v.oG.y = co.w * G.y;
+  // fast mode drops upstream's `power > 0` skip exactly as the forward does (k_render_fwd).
+  // alpha = min(0.99, o G) >= 1/255 is tested as o G >= 1/255 (the same decision: 0.99 > 1/255);
+  // the clamp itself is applied by the commit, to the contributors only
+  v.cA = e < lastA && (!EXACT || power.x <= 0.0f) && v.oG.x >= 1.0f / 255.0f;
+  v.cB = e < lastB && (!EXACT || power.y <= 0.0f) && v.oG.y >= 1.0f / 255.0f;
   return v;
 }
 
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   // gradient commit of entry j (walk order) for the lane's contributing pixels
   auto apply = [&](uint32_t j, const Eval& v, const float4 xr) {
     const float4 rgb = make_float4(xr.z, xr.w, s_ent[2 * BWD_BATCH + j].x, 0.0f);
-    const f2 alpha = v.alpha, dy = v.dy;
+    const f2 dy = v.dy;
     const float dx = v.dx;
     const bool cA = v.cA, cB = v.cB;
     // Reduced form of the upstream per-pair terms (same quantities, fewer ops per pixel):
@@ -159,10 +161,11 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     // dL/dalpha: upstream's accum_rec recurrence gives T_i accum_rec_i . dL/dpix = S_i / (1 - a_i)
     // with S_i = sum_{j behind i} Cd_j a_j T_j, so dL/dalpha = T_i Cd_i - U / (1 - a_i) with
     // U = S_i + T_final bg . dL/dpix, and U grows by Cd_i a_i T_i once entry i is done.
-    // A pixel that does not contribute is run as an alpha = 0 entry: T and U then pass through
-    // unchanged bit for bit (1 / (1 - 0) = 1, fma(x, 0, U) = U) and its colour terms vanish, so
-    // only dL/dalpha needs a mask.
-    const f2 ae = {cA ? alpha.x : 0.0f, cB ? alpha.y : 0.0f};
+    // A pixel that does not contribute is run as an o G = 0 (alpha = 0) entry: T and U then pass
+    // through unchanged bit for bit (1 / (1 - 0) = 1, fma(x, 0, U) = U), and its colour and
+    // q = o G dL/dalpha terms vanish (dL/dalpha is finite).
+    const f2 oGm = {cA ? v.oG.x : 0.0f, cB ? v.oG.y : 0.0f};
+    const f2 ae = {fminf(0.99f, oGm.x), fminf(0.99f, oGm.y)};
     const f2 omA = 1.f - ae;
     f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
     // exact mode: one Newton step (~0.5 ulp, like the IEEE divide).  Fast mode: the hardware
@@ -173,8 +176,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     const f2 dch = ae * Tn;
     const f2 Cd = pk_fma((f2)(rgb.z), dp2, pk_fma((f2)(rgb.y), dp1, rgb.x * dp0));
     const f2 dLa = pk_fma(Tn, Cd, -(U * inv));
-    const f2 dLm = {cA ? dLa.x : 0.0f, cB ? dLa.y : 0.0f};
-    const f2 q = v.oG * dLm;  // dL/dG G = o G dL/dalpha (not gated by the 0.99 clamp)
+    const f2 q = oGm * dLa;  // dL/dG G = o G dL/dalpha (not gated by the 0.99 clamp)
     const f2 w4 = q * dy;
     float s[GRAD_REC];
     s[0] = __builtin_fmaf(dch.x, dp0.x, dch.y * dp0.y);
