@@ -165,7 +165,8 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     // through unchanged bit for bit (1 / (1 - 0) = 1, fma(x, 0, U) = U), and its colour and
     // q = o G dL/dalpha terms vanish (dL/dalpha is finite).
     const f2 oGm = {cA ? v.oG.x : 0.0f, cB ? v.oG.y : 0.0f};
-    const f2 ae = {fminf(0.99f, oGm.x), fminf(0.99f, oGm.y)};
+    // min(0.99, o G) as a median with 0 (o G >= 0): v_med3 needs no NaN-canonicalising v_max
+    const f2 ae = {__builtin_amdgcn_fmed3f(oGm.x, 0.0f, 0.99f), __builtin_amdgcn_fmed3f(oGm.y, 0.0f, 0.99f)};
     const f2 omA = 1.f - ae;
     f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
     // exact mode: one Newton step (~0.5 ulp, like the IEEE divide).  Fast mode: the hardware

@@ -469,7 +469,7 @@ constexpr int FWD_ILP = 4;
 struct FwdPix {
   float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
   uint32_t last = 0;
-  bool done;
+  uint64_t done;  // lane mask (wave-uniform): pixels that stopped or lie outside the image
 };
 
 // Walk one quadrant wave's list of qcnt staged entries (the list is padded with 2 FWD_ILP zero
@@ -498,36 +498,43 @@ __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist,
       const float4 xr = *reinterpret_cast<const float4*>(ent + o[u]);
       const float2 bl = *reinterpret_cast<const float2*>(ent + o[u] + 32 * NB);
       const float rr = xr.z, rg = xr.w, rb = bl.x;
-      // branch-free compositing (selects instead of divergent ifs)
+      // branch-free compositing (selects instead of divergent ifs); the per-entry decisions are
+      // lane masks combined on the scalar unit (ballot / inverse ballot), so the VALU does the
+      // two threshold compares and the selects only.
       // upstream skips power > 0; with a positive-definite conic that only happens by rounding
       // within ~1e-3 px of a splat centre, so the fast mode leaves the test out (the backward
       // matches it entry for entry)
-      bool cu = k + u < qcnt && !px.done && (!EXACT || pw[u] <= 0.0f) && al[u] >= 1.0f / 255.0f;
+      const uint64_t m_a = __builtin_amdgcn_ballot_w64((!EXACT || pw[u] <= 0.0f) && al[u] >= 1.0f / 255.0f);
+      uint64_t m_cu = k + u < qcnt ? m_a & ~px.done : 0ull;
       if constexpr (EXACT) {  // upstream's order, T (1 - alpha) and (rgb alpha) T, mirrored by the oracle
         const float tT = px.T * (1.0f - al[u]);
-        const bool su = cu && tT < 0.0001f;  // T would drop below 1e-4: stop before this entry
-        px.done = px.done || su;
-        cu = cu && !su;
+        // T would drop below 1e-4: stop before this entry
+        const uint64_t m_stop = m_cu & __builtin_amdgcn_ballot_w64(tT < 0.0001f);
+        px.done |= m_stop;
+        m_cu &= ~m_stop;
+        const bool cu = __builtin_amdgcn_inverse_ballot_w64(m_cu);
         px.C0 = cu ? px.C0 + rr * al[u] * px.T : px.C0;
         px.C1 = cu ? px.C1 + rg * al[u] * px.T : px.C1;
         px.C2 = cu ? px.C2 + rb * al[u] * px.T : px.C2;
         px.T = cu ? tT : px.T;
+        px.last = cu ? __float_as_uint(bl.y) : px.last;
       } else {
         // T - alpha T as one FMA (one rounding of T (1 - alpha)); one weight, three FMAs (a
-        // skipped entry adds rgb * 0); `keep` as a >= test so both masks come from one compare
+        // skipped entry adds rgb * 0)
         const float tT = __builtin_fmaf(-al[u], px.T, px.T);
-        const bool keep = tT >= 0.0001f;
-        px.done = px.done || (cu && !keep);
-        cu = cu && keep;
+        const uint64_t m_keep = __builtin_amdgcn_ballot_w64(tT >= 0.0001f);
+        px.done |= m_cu & ~m_keep;
+        m_cu &= m_keep;
+        const bool cu = __builtin_amdgcn_inverse_ballot_w64(m_cu);
         const float wgt = cu ? al[u] * px.T : 0.0f;
         px.C0 = __builtin_fmaf(rr, wgt, px.C0);
         px.C1 = __builtin_fmaf(rg, wgt, px.C1);
         px.C2 = __builtin_fmaf(rb, wgt, px.C2);
         px.T = cu ? tT : px.T;
+        px.last = cu ? __float_as_uint(bl.y) : px.last;
       }
-      px.last = cu ? __float_as_uint(bl.y) : px.last;
     }
-    if (__ballot(!px.done) == 0) break;
+    if (px.done == ~0ull) break;
   }
 }
 
@@ -565,9 +572,9 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   const uint32_t n = range.y - range.x;
   const char* ent = reinterpret_cast<const char*>(s_ent);
   FwdPix px;
-  px.done = !inside;
+  px.done = __builtin_amdgcn_ballot_w64(!inside);
   for (uint32_t base = 0; base < n; base += GS_BLOCK) {
-    if (__syncthreads_and(px.done)) break;
+    if (__syncthreads_and(px.done == ~0ull)) break;
     const uint32_t cnt = min((uint32_t)GS_BLOCK, n - base);
     uint32_t qmask = 0;
     if ((uint32_t)tid < cnt) {
@@ -580,7 +587,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
     }
     publish_masks(qmask, s_mask, tid);
     __syncthreads();
-    if (__ballot(!px.done) == 0) continue;
+    if (px.done == ~0ull) continue;
     // dense, in-order list of this quadrant's entries (as LDS byte offsets), built by the wave
     uint32_t qcnt = 0;
 #pragma unroll
@@ -628,9 +635,9 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   const char* ent = reinterpret_cast<const char*>(s_ent);
   const float qx = (float)(tx * GS_TILE + 8 * (wid & 1)), qy = (float)(ty * GS_TILE + 8 * (wid >> 1));
   FwdPix px;
-  px.done = !inside;
+  px.done = __builtin_amdgcn_ballot_w64(!inside);
   for (uint32_t base = 0; base < n; base += FWDQ_NB) {
-    if (__ballot(!px.done) == 0) break;
+    if (px.done == ~0ull) break;
     bool meets = false;
     if (base + lane < n) {
       const uint32_t gid = presort_gid[point_list[range.x + base + lane]];
