@@ -405,7 +405,10 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
 }
 
 // tile ranges over the sorted instance list, 4 instances per lane
-__global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __restrict__ tile, uint2* __restrict__ ranges) {
+__global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __restrict__ tile, uint2* __restrict__ ranges,
+                                                uint32_t* __restrict__ sched, uint32_t sched_words) {
+  // clear the render's per-tile completion counters and length buckets (k_render_fwd* epilogue)
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sched_words; i += gridDim.x * 256) sched[i] = 0u;
   const uint32_t k0 = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (k0 >= I) return;
   uint32_t t[6];
@@ -435,6 +438,7 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
   const int tiles = c.gx * c.gy;
   if (I == 0) {
     (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
+    (void)hipMemsetAsync(img.tile_done, 0, sizeof(uint64_t) * (size_t)tiles + sizeof(uint32_t) * ORDER_BUCKETS, st);
     return;
   }
   const int tbits = tile_bits(tiles);
@@ -453,7 +457,8 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
   }
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tbits, bin.sort_scratch, st,
                    false, hist0);
-  GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges);
+  GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges,
+            (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_BUCKETS);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -538,6 +543,23 @@ __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist,
   }
 }
 
+// Epilogue of one quadrant wave (one lane): one 64-bit atomic per wave adds 1 (finished waves, low
+// 3 bits) plus a one-hot bit of the quadrant's walk-length class (bit 8 + class).  The tile's
+// fourth finisher gets the other three from the returned value, with no fence: the highest set
+// bit of the sum is the tile's longest class (or one above it, when classes coincide and carry),
+// which is all the longest-first order needs.  It takes a rank in that bucket; k_tile_order turns
+// (bucket, rank) into the backward's launch order.
+__device__ __forceinline__ void tile_finish(uint32_t tile, uint32_t wave_last, uint64_t* __restrict__ tile_done,
+                                            uint32_t* __restrict__ len_hist, uint32_t* __restrict__ tile_brank) {
+  const uint32_t cls = min(wave_last / ORDER_LEN_STEP, 47u);
+  const uint64_t mine = (1ull << (8 + cls)) + 1ull;
+  const uint64_t old = atomicAdd((unsigned long long*)&tile_done[tile], (unsigned long long)mine);
+  if ((old & 7ull) != 3ull) return;
+  const uint32_t top = 63u - (uint32_t)__builtin_clzll((old + mine) >> 8);  // 0 .. 49
+  const uint32_t b = (uint32_t)ORDER_BUCKETS - 1u - top;                    // descending length
+  tile_brank[tile] = b << 22 | atomicAdd(&len_hist[b], 1u);
+}
+
 __device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q, bool inside, const FwdPix& px,
                                           float* __restrict__ out, float* __restrict__ final_T,
                                           uint32_t* __restrict__ n_contrib) {
@@ -558,7 +580,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
                                                          const uint32_t* __restrict__ presort_gid,
                                                          const float4* __restrict__ splat, float* __restrict__ out,
                                                          float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                                                         uint32_t* __restrict__ tile_max) {
+                                                         uint32_t* __restrict__ tile_max, ImgPtrs img) {
   __shared__ float4 s_ent[3 * GS_BLOCK];
   __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[4][GS_BLOCK + 2 * FWD_ILP];  // per quadrant wave: byte offsets
@@ -604,7 +626,10 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   }
   fwd_store(c, q, inside, px, out, final_T, n_contrib);
   const uint32_t wmax = wave_max_u32(px.last);
-  if (lane == 0) tile_max[4 * tile + wid] = wmax;
+  if (lane == 0) {
+    tile_max[4 * tile + wid] = wmax;
+    tile_finish(tile, wmax, img.tile_done, img.len_hist, img.tile_brank);
+  }
 }
 
 // One wave per (tile, quadrant), no workgroup barriers: each wave stages the tile's entries 64 at
@@ -619,7 +644,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
                                                      const uint32_t* __restrict__ presort_gid,
                                                      const float4* __restrict__ splat, float* __restrict__ out,
                                                      float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                                                     uint32_t* __restrict__ tile_max) {
+                                                     uint32_t* __restrict__ tile_max, ImgPtrs img) {
   __shared__ float4 s_ent[3 * FWDQ_NB];
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
   const uint32_t b = blockIdx.x;
@@ -659,7 +684,10 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   }
   fwd_store(c, q, inside, px, out, final_T, n_contrib);
   const uint32_t wmax = wave_max_u32(px.last);
-  if (lane == 0) tile_max[4 * tile + wid] = wmax;
+  if (lane == 0) {
+    tile_max[4 * tile + wid] = wmax;
+    tile_finish(tile, wmax, img.tile_done, img.len_hist, img.tile_brank);
+  }
 }
 
 #ifndef GS_FWD_WAVE
@@ -672,18 +700,18 @@ void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
     const int blocks = ((tiles + 7) / 8) * 32;
     if (exact_exp())
       GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
+                bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
     else
       GS_LAUNCH("render_fwd", k_render_fwd_q<false>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
+                bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
     return;
   }
   if (exact_exp())
     GS_LAUNCH("render_fwd", k_render_fwd<true>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
+              bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
   else
     GS_LAUNCH("render_fwd", k_render_fwd<false>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max);
+              bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
 }
 
 // ------------------------------------------------------------------------------------------

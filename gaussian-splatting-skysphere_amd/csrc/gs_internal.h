@@ -9,7 +9,8 @@
 //                                    scan partials | sort scratch | counters
 //   binning   (per instance, I)      tile keys/vals x2 u32 | presort_gid u32 | sort scratch
 //   image     (per pixel / tile)     ranges uint2 | final_T f32 | n_contrib u32 | tile_max u32 x4
-//                                    (largest n_contrib of each 8x8 quadrant)
+//                                    (largest n_contrib of each 8x8 quadrant) | tile_order u32 |
+//                                    tile_done u32 + length buckets | bucket rank u32
 //   gradient  (per instance, I)      9 f32 per (Gaussian, tile) instance (backward scratch)
 #pragma once
 #include <stddef.h>
@@ -169,7 +170,15 @@ struct ImgPtrs {
   float* final_T;
   uint32_t* n_contrib;
   uint32_t* tile_max;
+  uint32_t* tile_order;  // backward launch order (k_tile_order)
+  uint64_t* tile_done;   // per tile: finished quadrant waves + their length bits (zeroed by k_ranges),
+  uint32_t* len_hist;    //   then ORDER_BUCKETS walk-length bucket counts
+  uint32_t* tile_brank;  // bucket << 22 | rank within the bucket, per tile
 };
+
+// Backward launch order: tiles bucketed by walk length (largest n_contrib), longest first.
+constexpr int ORDER_BUCKETS = 64;
+constexpr uint32_t ORDER_LEN_STEP = 24;  // walk-length step of one length class (48 classes)
 
 inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t off = 0;
@@ -182,12 +191,17 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t npix = (size_t)W * H;
   if (tiles == 0) tiles = 1;
   if (npix == 0) npix = 1;
-  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16);
+  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16), o_o = take(tiles * 4),
+         o_d = take(tiles * 8 + ORDER_BUCKETS * 4), o_b = take(tiles * 4);
   if (out && base) {
     out->ranges = (uint2*)(base + o_r);
     out->final_T = (float*)(base + o_t);
     out->n_contrib = (uint32_t*)(base + o_n);
     out->tile_max = (uint32_t*)(base + o_m);
+    out->tile_order = (uint32_t*)(base + o_o);
+    out->tile_done = (uint64_t*)(base + o_d);
+    out->len_hist = (uint32_t*)(out->tile_done + tiles);
+    out->tile_brank = (uint32_t*)(base + o_b);
   }
   return off;
 }
