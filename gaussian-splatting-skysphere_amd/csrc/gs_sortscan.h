@@ -314,7 +314,15 @@ inline int radix_width(int end_bit) {
   const int np = radix_passes(end_bit);
   return (end_bit + np - 1) / np;
 }
-inline int radix_first_bits(int end_bit) { return end_bit < radix_width(end_bit) ? end_bit : radix_width(end_bit); }
+#ifndef GS_SORT_NARROW_FIRST
+#define GS_SORT_NARROW_FIRST 1
+#endif
+// width of the first pass: the full width, or (GS_SORT_NARROW_FIRST) the remainder (13 -> 6 + 7)
+inline int radix_first_bits(int end_bit) {
+  const int w = radix_width(end_bit);
+  if (end_bit <= w) return end_bit;
+  return GS_SORT_NARROW_FIRST ? end_bit - (radix_passes(end_bit) - 1) * w : w;
+}
 
 inline SortPlan sort_plan(uint64_t n_max) {
   uint64_t tiles = (n_max + SORT_TILE - 1) / SORT_TILE;
@@ -542,10 +550,10 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
   bool in_b = false;
   const uint32_t* ain = aux0;
   uint32_t* aout = aux_a;
-  // digits of (nearly) equal width: 13 bits -> 7 + 6, not 8 + 5 (longer runs in the first scatter)
+  // digits of (nearly) equal width, the narrower first: 13 bits -> 6 + 7 (scatters 35 + 24 -> 31 + 27 us)
   const int width = radix_width(end_bit);
-  for (int shift = 0; shift < end_bit; shift += width) {
-    int bits = end_bit - shift < width ? end_bit - shift : width;
+  for (int shift = 0; shift < end_bit;) {
+    int bits = shift == 0 ? radix_first_bits(end_bit) : (end_bit - shift < width ? end_bit - shift : width);
     const bool drop = drop_first && shift == 0;
     const uint32_t* nd = drop ? nullptr : n_dev;
     if (!(hist0_ready && shift == 0))
@@ -566,6 +574,7 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
     t = kin; kin = kout; kout = t;
     t = vin; vin = vout; vout = t;
     in_b = !in_b;
+    shift += bits;
   }
   return in_b;
 }
