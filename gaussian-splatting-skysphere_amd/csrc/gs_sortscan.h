@@ -550,7 +550,7 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
   bool in_b = false;
   const uint32_t* ain = aux0;
   uint32_t* aout = aux_a;
-  // digits of (nearly) equal width, the narrower first: 13 bits -> 6 + 7 (scatters 35 + 24 -> 31 + 27 us)
+  // digits of (nearly) equal width, the narrower first: 13 bits -> 6 + 7 (C3: -3.6 us over the six scatters)
   const int width = radix_width(end_bit);
   for (int shift = 0; shift < end_bit;) {
     int bits = shift == 0 ? radix_first_bits(end_bit) : (end_bit - shift < width ? end_bit - shift : width);
