@@ -469,7 +469,11 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
 //   (x, y, r, g) | falloff coefficients + opacity | (b, bits(entry index + 1), -, -)
 // and each quadrant wave's dense list holds the offsets (u32), read FWD_ILP = 4 at a time with one
 // 16-B LDS read: a list entry costs no address arithmetic, no unpacking and no dependent list read.
-constexpr int FWD_ILP = 4;
+#ifndef GS_FWD_ILP
+#define GS_FWD_ILP 4
+#endif
+constexpr int FWD_ILP = GS_FWD_ILP;  // a multiple of 4 (whole 16-B list reads)
+static_assert(FWD_ILP % 4 == 0, "list groups are read 16 B at a time");
 
 struct FwdPix {
   float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
@@ -485,11 +489,17 @@ __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist,
   // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
   // compositing is then applied entry by entry in list order, exactly as one at a time.  The
   // next group's offsets are read one trip ahead (one dependent LDS round trip per trip).
-  uint4 wn = *reinterpret_cast<const uint4*>(&qlist[0]);
+  constexpr int NQ = FWD_ILP / 4;
+  uint4 wn[NQ];
+#pragma unroll
+  for (int r = 0; r < NQ; r++) wn[r] = *reinterpret_cast<const uint4*>(&qlist[4 * r]);
   for (uint32_t k = 0; k < qcnt; k += FWD_ILP) {
-    const uint4 w = wn;
-    wn = *reinterpret_cast<const uint4*>(&qlist[k + FWD_ILP]);
-    const uint32_t o[FWD_ILP] = {w.x, w.y, w.z, w.w};
+    uint32_t o[FWD_ILP];
+#pragma unroll
+    for (int r = 0; r < NQ; r++) {
+      o[4 * r] = wn[r].x, o[4 * r + 1] = wn[r].y, o[4 * r + 2] = wn[r].z, o[4 * r + 3] = wn[r].w;
+      wn[r] = *reinterpret_cast<const uint4*>(&qlist[k + FWD_ILP + 4 * r]);
+    }
     float pw[FWD_ILP], al[FWD_ILP];
 #pragma unroll
     for (int u = 0; u < FWD_ILP; u++) {
