@@ -343,7 +343,7 @@ int gs_backward(int P, int D, int M, const float* background, int W, int H, cons
   img_layout(W, H, &img, (char*)image_buffer);
   GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier};
   float* gradrec = (float*)grad_buffer;
-  if (num_rendered > 0) bwd_render(c, geo, bin, img, dL_dout_color, gradrec, st);
+  if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, st);
   GradOut out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, cov3D_precomp ? dL_dcov3D : nullptr,
               shs ? dL_dsh : nullptr, cov3D_precomp ? nullptr : dL_dscales, cov3D_precomp ? nullptr : dL_drotations};
   bwd_preprocess(g, c, geo, gradrec, num_rendered > 0, out, st);

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   __shared__ uint32_t s_slot[BWD_BATCH];
   __shared__ uint64_t s_mask[BWD_GROUPS][2];  // [64-entry group][half]
   __shared__ float s_acc[2][BWD_BATCH][ACC_STRIDE];
-  const uint32_t tile = tile_order[blockIdx.x];
+  const uint32_t tile = tile_order ? tile_order[blockIdx.x] : blockIdx.x;
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -323,37 +323,45 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
 // n_contrib (the forward's per-quadrant maxima), which varies ~10x across an image, and dense
 // tiles sit together: in index order the last workgroups to start include heavy ones and the
 // grid ends on a long tail.  The forward buckets every tile by that length and ranks it in its
-// bucket (tile_finish); here each thread places one tile at (bucket base + rank), so the heavy
-// tiles start first and the tail is made of light ones (list scheduling, LPT).  The order inside
-// a bucket is arbitrary: a tile's outputs do not depend on when it runs.
+// bucket of its XCD group (tile_finish); here each thread places one tile at (bucket base + rank)
+// within the group's launch positions, so the heavy tiles start first and the tail is made of
+// light ones (list scheduling, LPT).  The order inside a bucket is arbitrary: a tile's outputs do
+// not depend on when it runs.  Used up to ORDER_LPT_MAX_P Gaussians (gs_internal.h).
 constexpr int ORDER_THREADS = 256;
 __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __restrict__ len_hist,
                                                               const uint32_t* __restrict__ tile_brank, uint32_t tiles,
                                                               uint32_t* __restrict__ order) {
-  __shared__ uint32_t s_base[ORDER_BUCKETS];
-  const uint32_t tid = threadIdx.x, t = blockIdx.x * ORDER_THREADS + tid;
+  __shared__ uint32_t s_base[ORDER_GROUPS][ORDER_BUCKETS];
+  const uint32_t tid = threadIdx.x, t = blockIdx.x * ORDER_THREADS + tid, lane = tid & 63, wid = tid >> 6;
   const uint32_t br = t < tiles ? tile_brank[t] : 0u;
-  static_assert(ORDER_BUCKETS == 64, "one wave scans the buckets");
-  if (tid < 64) {
-    const uint32_t v = len_hist[tid];
-    s_base[tid] = wave_incl_scan(v) - v;
+  static_assert(ORDER_BUCKETS == 64 && ORDER_GROUPS == 2 * (ORDER_THREADS / 64), "two groups per wave");
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t g = wid + h * (ORDER_THREADS / 64);
+    const uint32_t v = len_hist[g * ORDER_BUCKETS + lane];
+    s_base[g][lane] = wave_incl_scan(v) - v;
   }
   __syncthreads();
-  if (t < tiles) order[s_base[br >> 22] + (br & 0x3FFFFFu)] = t;
+  // the j-th tile of group g (longest first) takes launch position 8 j + g
+  if (t < tiles) order[ORDER_GROUPS * (s_base[t % ORDER_GROUPS][br >> 22] + (br & 0x3FFFFFu)) + t % ORDER_GROUPS] = t;
 }
 
-void bwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
+void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                 const float* dL_dpix, float* gradrec, hipStream_t st) {
   const int tiles = c.gx * c.gy;
-  GS_LAUNCH("tile_order", k_tile_order, dim3((tiles + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
-            img.len_hist, img.tile_brank, (uint32_t)tiles, img.tile_order);
+  const uint32_t* order = nullptr;  // index order
+  if (P <= ORDER_LPT_MAX_P) {
+    GS_LAUNCH("tile_order", k_tile_order, dim3((tiles + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0,
+              st, img.len_hist, img.tile_brank, (uint32_t)tiles, img.tile_order);
+    order = img.tile_order;
+  }
   if (exact_exp())
     GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,
-              bin.point_list, bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, img.tile_order,
+              bin.point_list, bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
               dL_dpix, gradrec);
   else
     GS_LAUNCH("render_bwd", k_render_bwd<false>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,
-              bin.point_list, bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, img.tile_order,
+              bin.point_list, bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
               dL_dpix, gradrec);
 }
 

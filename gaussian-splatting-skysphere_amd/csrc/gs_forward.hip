@@ -438,7 +438,8 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
   const int tiles = c.gx * c.gy;
   if (I == 0) {
     (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
-    (void)hipMemsetAsync(img.tile_done, 0, sizeof(uint64_t) * (size_t)tiles + sizeof(uint32_t) * ORDER_BUCKETS, st);
+    (void)hipMemsetAsync(img.tile_done, 0,
+                         sizeof(uint64_t) * (size_t)tiles + sizeof(uint32_t) * ORDER_GROUPS * ORDER_BUCKETS, st);
     return;
   }
   const int tbits = tile_bits(tiles);
@@ -458,7 +459,7 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tbits, bin.sort_scratch, st,
                    false, hist0);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges,
-            (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_BUCKETS);
+            (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -561,13 +562,14 @@ __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist,
 // (bucket, rank) into the backward's launch order.
 __device__ __forceinline__ void tile_finish(uint32_t tile, uint32_t wave_last, uint64_t* __restrict__ tile_done,
                                             uint32_t* __restrict__ len_hist, uint32_t* __restrict__ tile_brank) {
-  const uint32_t cls = min(wave_last / ORDER_LEN_STEP, 47u);
+  // length classes on a log scale, four per octave
+  const uint32_t cls = min((uint32_t)(4.0f * __log2f((float)wave_last + 1.0f)), 47u);
   const uint64_t mine = (1ull << (8 + cls)) + 1ull;
   const uint64_t old = atomicAdd((unsigned long long*)&tile_done[tile], (unsigned long long)mine);
   if ((old & 7ull) != 3ull) return;
   const uint32_t top = 63u - (uint32_t)__builtin_clzll((old + mine) >> 8);  // 0 .. 49
   const uint32_t b = (uint32_t)ORDER_BUCKETS - 1u - top;                    // descending length
-  tile_brank[tile] = b << 22 | atomicAdd(&len_hist[b], 1u);
+  tile_brank[tile] = b << 22 | atomicAdd(&len_hist[(tile % ORDER_GROUPS) * ORDER_BUCKETS + b], 1u);
 }
 
 __device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q, bool inside, const FwdPix& px,

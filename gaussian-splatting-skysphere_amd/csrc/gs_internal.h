@@ -172,13 +172,20 @@ struct ImgPtrs {
   uint32_t* tile_max;
   uint32_t* tile_order;  // backward launch order (k_tile_order)
   uint64_t* tile_done;   // per tile: finished quadrant waves + their length bits (zeroed by k_ranges),
-  uint32_t* len_hist;    //   then ORDER_BUCKETS walk-length bucket counts
+  uint32_t* len_hist;    //   then ORDER_GROUPS x ORDER_BUCKETS walk-length bucket counts
   uint32_t* tile_brank;  // bucket << 22 | rank within the bucket, per tile
 };
 
 // Backward launch order: tiles bucketed by walk length (largest n_contrib), longest first.
 constexpr int ORDER_BUCKETS = 64;
-constexpr uint32_t ORDER_LEN_STEP = 24;  // walk-length step of one length class (48 classes)
+// Tiles are ordered within ORDER_GROUPS groups (tile % 8): group g fills launch positions
+// g, g + 8, g + 16, ..., the workgroups the dispatcher sends to XCD g as in index order (and the
+// forward's bucket counters are spread over 8x more addresses).
+constexpr int ORDER_GROUPS = 8;
+// The longest-first order is used up to this many Gaussians.  Measured: C3 (1M) render_bwd
+// 441 -> 411 us; C5 (5M, 240 MB of splat records, 2650 instances per tile) 673 -> 1000 us, where
+// the index order's reuse of neighbouring tiles' splats in the caches is worth more than the tail.
+constexpr int ORDER_LPT_MAX_P = 2 << 20;
 
 inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t off = 0;
@@ -192,7 +199,7 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   if (tiles == 0) tiles = 1;
   if (npix == 0) npix = 1;
   size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16), o_o = take(tiles * 4),
-         o_d = take(tiles * 8 + ORDER_BUCKETS * 4), o_b = take(tiles * 4);
+         o_d = take(tiles * 8 + ORDER_GROUPS * ORDER_BUCKETS * 4), o_b = take(tiles * 4);
   if (out && base) {
     out->ranges = (uint2*)(base + o_r);
     out->final_T = (float*)(base + o_t);
@@ -215,7 +222,7 @@ void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
                 hipStream_t st);
 void mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
                   hipStream_t st);
-void bwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
+void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                 const float* dL_dpix, float* gradrec, hipStream_t st);
 struct GradOut {
   float* dmean2D;   // [P, 3]
