@@ -376,7 +376,10 @@ void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& 
 // large splat's tile partials cancel, so the cross-tile sum is kept in fp64).  The total goes
 // back into the owner's first record.  Fixed order throughout: deterministic.
 // ------------------------------------------------------------------------------------------
-constexpr int SUMREC_WAVES = 4;
+#ifndef GS_SUMREC_WAVES
+#define GS_SUMREC_WAVES 4
+#endif
+constexpr int SUMREC_WAVES = GS_SUMREC_WAVES;
 // one step of the segmented wave scan: v += (shifted v) when the shifted lane has the same owner
 // (owners are carried +1 so a lane without a source (0) never matches)
 template <int CTRL, int ROW_MASK>
