@@ -649,7 +649,11 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
 // are done (the workgroup version waits for its slowest quadrant).  Workgroup b takes tile
 // (b / 32) * 8 + b % 8, quadrant (b / 8) % 4, so the four quadrant waves of a tile share the
 // workgroup-to-XCD round robin (b % 8) and their repeated entry loads hit one L2.
-constexpr int FWDQ_NB = 64;
+#ifndef GS_FWDQ_NB
+#define GS_FWDQ_NB 64
+#endif
+constexpr int FWDQ_NB = GS_FWDQ_NB;  // entries staged per round (<= 64: one per lane)
+static_assert(FWDQ_NB <= 64, "one staged entry per lane");
 template <bool EXACT>
 __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ point_list,
@@ -676,7 +680,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   for (uint32_t base = 0; base < n; base += FWDQ_NB) {
     if (px.done == ~0ull) break;
     bool meets = false;
-    if (base + lane < n) {
+    if (lane < (uint32_t)FWDQ_NB && base + lane < n) {
       const uint32_t gid = presort_gid[point_list[range.x + base + lane]];
       const float4 a = splat[3 * gid], bb = splat[3 * gid + 1], d = splat[3 * gid + 2];
       s_ent[lane] = make_float4(a.x, a.y, bb.z, bb.w);
