@@ -346,7 +346,7 @@ int gs_backward(int P, int D, int M, const float* background, int W, int H, cons
   if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, st);
   GradOut out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, cov3D_precomp ? dL_dcov3D : nullptr,
               shs ? dL_dsh : nullptr, cov3D_precomp ? nullptr : dL_dscales, cov3D_precomp ? nullptr : dL_drotations};
-  bwd_preprocess(g, c, geo, gradrec, num_rendered > 0, out, st);
+  bwd_preprocess(g, c, geo, bin, img, gradrec, num_rendered > 0, out, st);
   return t_failed ? 1 : 0;
 }
 

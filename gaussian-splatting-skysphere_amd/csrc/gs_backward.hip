@@ -66,9 +66,6 @@ constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x
 #ifndef GS_BWD_ILP
 #define GS_BWD_ILP 1
 #endif
-#ifndef GS_BWD_NOZERO
-#define GS_BWD_NOZERO 0  // timing experiments only (wrong gradients)
-#endif
 #ifndef GS_PBWD_REG
 #define GS_PBWD_REG 1  // 0: the LDS-staged SH rows variant (113 vs 109.5 us at C3)
 #endif
@@ -308,14 +305,8 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     }
   }
 
-  // instances past the last contributor of every pixel get zero records (at the end: the
-  // walk's VALU work starts without waiting on these loads)
-  for (uint32_t e = n_eff + tid; e < (GS_BWD_NOZERO ? 0u : n); e += BWD_THREADS) {
-    Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)point_list[range.x + e] * GRAD_REC);
-    r[0] = Rec3{0.0f, 0.0f, 0.0f};
-    r[1] = Rec3{0.0f, 0.0f, 0.0f};
-    r[2] = Rec3{0.0f, 0.0f, 0.0f};
-  }
+  // instances past the last contributor of every pixel have no record: k_sum_records skips them
+  // (tile_cut)
 
 }
 
@@ -328,11 +319,26 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
 // light ones (list scheduling, LPT).  The order inside a bucket is arbitrary: a tile's outputs do
 // not depend on when it runs.  Used up to ORDER_LPT_MAX_P Gaussians (gs_internal.h).
 constexpr int ORDER_THREADS = 256;
+// Also (always) each tile's record cut: records exist only for a tile's first n_eff instances
+// (those its walk reaches, n_eff = its largest n_contrib); tile_cut = 1 + the slot of the last
+// of them.  A tile's list is in slot order, so k_sum_records keeps a record of slot s in tile T
+// iff s < tile_cut[T] and the backward writes no zero records for the rest.
 __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __restrict__ len_hist,
                                                               const uint32_t* __restrict__ tile_brank, uint32_t tiles,
-                                                              uint32_t* __restrict__ order) {
+                                                              uint32_t* __restrict__ order,
+                                                              const uint32_t* __restrict__ tile_max,
+                                                              const uint2* __restrict__ ranges,
+                                                              const uint32_t* __restrict__ point_list,
+                                                              uint32_t* __restrict__ tile_cut) {
   __shared__ uint32_t s_base[ORDER_GROUPS][ORDER_BUCKETS];
   const uint32_t tid = threadIdx.x, t = blockIdx.x * ORDER_THREADS + tid, lane = tid & 63, wid = tid >> 6;
+  if (t < tiles) {
+    const uint4 q = reinterpret_cast<const uint4*>(tile_max)[t];
+    const uint2 r = ranges[t];
+    const uint32_t n_eff = min(max(max(q.x, q.y), max(q.z, q.w)), r.y - r.x);
+    tile_cut[t] = n_eff ? point_list[r.x + n_eff - 1] + 1u : 0u;
+  }
+  if (!order) return;  // (uniform)
   const uint32_t br = t < tiles ? tile_brank[t] : 0u;
   static_assert(ORDER_BUCKETS == 64 && ORDER_GROUPS == 2 * (ORDER_THREADS / 64), "two groups per wave");
 #pragma unroll
@@ -349,12 +355,10 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __
 void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                 const float* dL_dpix, float* gradrec, hipStream_t st) {
   const int tiles = c.gx * c.gy;
-  const uint32_t* order = nullptr;  // index order
-  if (P <= ORDER_LPT_MAX_P) {
-    GS_LAUNCH("tile_order", k_tile_order, dim3((tiles + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0,
-              st, img.len_hist, img.tile_brank, (uint32_t)tiles, img.tile_order);
-    order = img.tile_order;
-  }
+  const uint32_t* order = P <= ORDER_LPT_MAX_P ? img.tile_order : nullptr;  // (else index order)
+  GS_LAUNCH("tile_order", k_tile_order, dim3((tiles + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
+            img.len_hist, img.tile_brank, (uint32_t)tiles, (uint32_t*)order, img.tile_max, img.ranges, bin.point_list,
+            img.tile_cut);
   if (exact_exp())
     GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,
               bin.point_list, bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
@@ -393,6 +397,8 @@ __device__ __forceinline__ void seg_scan_step(float* v, uint32_t own1) {
 __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_t* __restrict__ counters,
                                                                    const uint32_t* __restrict__ offsets,
                                                                    const uint32_t* __restrict__ sorted_gid,
+                                                                   const uint32_t* __restrict__ slot_tile,
+                                                                   const uint32_t* __restrict__ tile_cut,
                                                                    const float* __restrict__ gradrec,
                                                                    float* __restrict__ gsum) {
   __shared__ double s_acc[SUMREC_WAVES][64][GRAD_REC];
@@ -412,18 +418,21 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
   // records of the next chunk are loaded one chunk ahead (their HBM latency overlaps this chunk)
   float vn[GRAD_REC];
   {
-    const size_t kk = (size_t)min(S0 + lane, S1 - 1);
+    const uint32_t kk = S0 + lane;
 #pragma unroll
     for (int c = 0; c < GRAD_REC; c++) vn[c] = 0.0f;
-    if (S0 < S1) load_rec(gradrec + kk * GRAD_REC, vn);
+    if (kk < S1 && kk < tile_cut[slot_tile[kk]]) load_rec(gradrec + (size_t)kk * GRAD_REC, vn);
   }
   for (uint32_t base = S0; base < S1; base += 64) {
     float v[GRAD_REC];
 #pragma unroll
     for (int c = 0; c < GRAD_REC; c++) v[c] = vn[c];
     if (base + 64 < S1) {
-      const size_t kn = (size_t)min(base + 64 + lane, S1 - 1);
-      load_rec(gradrec + kn * GRAD_REC, vn);
+      // records past their tile's cut were never written: zeros (no load)
+      const uint32_t kn = base + 64 + lane;
+#pragma unroll
+      for (int c = 0; c < GRAD_REC; c++) vn[c] = 0.0f;
+      if (kn < S1 && kn < tile_cut[slot_tile[kn]]) load_rec(gradrec + (size_t)kn * GRAD_REC, vn);
     }
     // slots of the chunk that start an owner -> bit mask -> owner of my slot by popcount
     if (lane == 0) s_mark[wid] = 0ull;
@@ -794,12 +803,14 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd_reg(GaussianArgs g, Came
   for (int k = KF; k < rowf; k++) dst[k] = 0.0f;
 }
 
-void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, float* gradrec,
+void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
+                    const ImgPtrs& img, float* gradrec,
                     bool have_records, const GradOut& out, hipStream_t st) {
   if (g.P <= 0) return;
   if (have_records)
     GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
-              dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, gradrec, geo.gsum);
+              dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
+              gradrec, geo.gsum);
   dim3 grid((g.P + 255) / 256), block(256);
   const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
   const size_t lds = sh ? (size_t)256 * (3 * g.M + 1) * sizeof(float) : 0;

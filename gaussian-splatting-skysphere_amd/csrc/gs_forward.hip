@@ -449,15 +449,15 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
     hist0 = sort_plan(I).chunk == DUP_SLOTS;
     GS_LAUNCH("duplicate", k_duplicate_lb, dim3((I + DUP_SLOTS - 1) / DUP_SLOTS), dim3(DUP_THREADS), 0, st, I,
               geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy,
-              bin.keys_a, bin.presort_gid, img.ranges, hist0 ? bin.sort_scratch : nullptr,
+              bin.slot_tile, bin.presort_gid, img.ranges, hist0 ? bin.sort_scratch : nullptr,
               (1u << radix_first_bits(tbits)) - 1u);
   } else {
     (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
     GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
-              geo.sorted_gid, geo.offsets, geo.binrec, c.gx, bin.keys_a, bin.presort_gid);
+              geo.sorted_gid, geo.offsets, geo.binrec, c.gx, bin.slot_tile, bin.presort_gid);
   }
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tbits, bin.sort_scratch, st,
-                   false, hist0);
+                   false, hist0, nullptr, nullptr, nullptr, bin.slot_tile);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges,
             (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS);
 }

@@ -132,6 +132,8 @@ struct BinPtrs {
   uint32_t* sort_scratch;
   uint32_t* point_list;  // sorted presort slots (= vals_a or vals_b after the tile sort)
   uint32_t* sorted_tile;
+  uint32_t* slot_tile;   // tile of every instance slot (duplicate output, kept: the tile sort's
+                         // first pass reads it and writes keys_b)
 };
 
 inline int tile_bits(int tiles) {
@@ -149,7 +151,7 @@ inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base) {
   };
   size_t In = I ? I : 1;
   size_t o_ka = take(In * 4), o_va = take(In * 4), o_kb = take(In * 4), o_vb = take(In * 4);
-  size_t o_pg = take(In * 4);
+  size_t o_pg = take(In * 4), o_st = take(In * 4);
   size_t o_ss = take(sort_scratch_words(In) * 4);
   if (out && base) {
     out->keys_a = (uint32_t*)(base + o_ka);
@@ -157,6 +159,7 @@ inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base) {
     out->keys_b = (uint32_t*)(base + o_kb);
     out->vals_b = (uint32_t*)(base + o_vb);
     out->presort_gid = (uint32_t*)(base + o_pg);
+    out->slot_tile = (uint32_t*)(base + o_st);
     out->sort_scratch = (uint32_t*)(base + o_ss);
     bool in_b = radix_passes(tile_bits(tiles)) % 2 == 1;
     out->point_list = in_b ? out->vals_b : out->vals_a;
@@ -171,6 +174,7 @@ struct ImgPtrs {
   uint32_t* n_contrib;
   uint32_t* tile_max;
   uint32_t* tile_order;  // backward launch order (k_tile_order)
+  uint32_t* tile_cut;    // per tile: 1 + the slot of its last walked instance (0: none), k_tile_order
   uint64_t* tile_done;   // per tile: finished quadrant waves + their length bits (zeroed by k_ranges),
   uint32_t* len_hist;    //   then ORDER_GROUPS x ORDER_BUCKETS walk-length bucket counts
   uint32_t* tile_brank;  // bucket << 22 | rank within the bucket, per tile
@@ -185,7 +189,10 @@ constexpr int ORDER_GROUPS = 8;
 // The longest-first order is used up to this many Gaussians.  Measured: C3 (1M) render_bwd
 // 441 -> 411 us; C5 (5M, 240 MB of splat records, 2650 instances per tile) 673 -> 1000 us, where
 // the index order's reuse of neighbouring tiles' splats in the caches is worth more than the tail.
-constexpr int ORDER_LPT_MAX_P = 2 << 20;
+#ifndef GS_ORDER_LPT_MAX_P
+#define GS_ORDER_LPT_MAX_P (2 << 20)
+#endif
+constexpr int ORDER_LPT_MAX_P = GS_ORDER_LPT_MAX_P;
 
 inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t off = 0;
@@ -198,7 +205,7 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t npix = (size_t)W * H;
   if (tiles == 0) tiles = 1;
   if (npix == 0) npix = 1;
-  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16), o_o = take(tiles * 4),
+  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16), o_o = take(tiles * 4), o_c = take(tiles * 4),
          o_d = take(tiles * 8 + ORDER_GROUPS * ORDER_BUCKETS * 4), o_b = take(tiles * 4);
   if (out && base) {
     out->ranges = (uint2*)(base + o_r);
@@ -206,6 +213,7 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
     out->n_contrib = (uint32_t*)(base + o_n);
     out->tile_max = (uint32_t*)(base + o_m);
     out->tile_order = (uint32_t*)(base + o_o);
+    out->tile_cut = (uint32_t*)(base + o_c);
     out->tile_done = (uint64_t*)(base + o_d);
     out->len_hist = (uint32_t*)(out->tile_done + tiles);
     out->tile_brank = (uint32_t*)(base + o_b);
@@ -234,7 +242,8 @@ struct GradOut {
   float* dscale;    // [P, 3] or null
   float* drot;      // [P, 4] or null
 };
-void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, float* gradrec,
+void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
+                    const ImgPtrs& img, float* gradrec,
                     bool have_records, const GradOut& out, hipStream_t st);
 void knn_mean_dist2(int P, const float* pts, float* out, char* scratch, hipStream_t st);
 void ssim_forward(int planes, int H, int W, const float* win11, const float* img1, const float* img2, float* dmaps,

@@ -541,7 +541,8 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
                                     bool vals_identity, const uint32_t* n_dev, uint32_t n_max, int end_bit,
                                     uint32_t* scratch, hipStream_t st, bool drop_first = false,
                                     bool hist0_ready = false, const uint32_t* aux0 = nullptr,
-                                    uint32_t* aux_a = nullptr, uint32_t* aux_b = nullptr) {
+                                    uint32_t* aux_a = nullptr, uint32_t* aux_b = nullptr,
+                                    const uint32_t* keys_in0 = nullptr) {
   SortPlan p = sort_plan(n_max);
   uint32_t* hist = scratch;
   const size_t hist_n = (size_t)RADIX * p.nb;
@@ -556,18 +557,20 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
     int bits = shift == 0 ? radix_first_bits(end_bit) : (end_bit - shift < width ? end_bit - shift : width);
     const bool drop = drop_first && shift == 0;
     const uint32_t* nd = drop ? nullptr : n_dev;
+    // keys_in0: the first pass reads its keys from there (kept), not from keys_a
+    const uint32_t* kin_p = (shift == 0 && keys_in0) ? keys_in0 : kin;
     if (!(hist0_ready && shift == 0))
-      GS_LAUNCH("radix_hist", k_radix_hist, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin, nd, n_max, shift, bits,
+      GS_LAUNCH("radix_hist", k_radix_hist, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin_p, nd, n_max, shift, bits,
                 p.chunk, p.nb, hist, drop);
     GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX), dim3(SORT_THREADS), 0, st, hist, p.nb, row_total);
     const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
     if (aux0) {
-      launch_scatter<true>(bits, p.nb, st, kin, vsrc, kout, vout, nd, n_max, shift, p.chunk, hist, row_total, drop, ain,
+      launch_scatter<true>(bits, p.nb, st, kin_p, vsrc, kout, vout, nd, n_max, shift, p.chunk, hist, row_total, drop, ain,
                            aout);
       ain = aout;
       aout = aout == aux_a ? aux_b : aux_a;
     } else {
-      launch_scatter<false>(bits, p.nb, st, kin, vsrc, kout, vout, nd, n_max, shift, p.chunk, hist, row_total, drop,
+      launch_scatter<false>(bits, p.nb, st, kin_p, vsrc, kout, vout, nd, n_max, shift, p.chunk, hist, row_total, drop,
                             nullptr, nullptr);
     }
     uint32_t* t;
