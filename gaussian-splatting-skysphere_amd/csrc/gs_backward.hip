@@ -317,7 +317,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
 // bucket of its XCD group (tile_finish); here each thread places one tile at (bucket base + rank)
 // within the group's launch positions, so the heavy tiles start first and the tail is made of
 // light ones (list scheduling, LPT).  The order inside a bucket is arbitrary: a tile's outputs do
-// not depend on when it runs.  Used up to ORDER_LPT_MAX_P Gaussians (gs_internal.h).
+// not depend on when it runs.
 constexpr int ORDER_THREADS = 256;
 // Also (always) each tile's record cut: records exist only for a tile's first n_eff instances
 // (those its walk reaches, n_eff = its largest n_contrib); tile_cut = 1 + the slot of the last
@@ -355,9 +355,9 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __
 void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                 const float* dL_dpix, float* gradrec, hipStream_t st) {
   const int tiles = c.gx * c.gy;
-  const uint32_t* order = P <= ORDER_LPT_MAX_P ? img.tile_order : nullptr;  // (else index order)
+  uint32_t* order = img.tile_order;
   GS_LAUNCH("tile_order", k_tile_order, dim3((tiles + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
-            img.len_hist, img.tile_brank, (uint32_t)tiles, (uint32_t*)order, img.tile_max, img.ranges, bin.point_list,
+            img.len_hist, img.tile_brank, (uint32_t)tiles, order, img.tile_max, img.ranges, bin.point_list,
             img.tile_cut);
   if (exact_exp())
     GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,

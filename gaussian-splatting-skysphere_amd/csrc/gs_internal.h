@@ -186,13 +186,6 @@ constexpr int ORDER_BUCKETS = 64;
 // g, g + 8, g + 16, ..., the workgroups the dispatcher sends to XCD g as in index order (and the
 // forward's bucket counters are spread over 8x more addresses).
 constexpr int ORDER_GROUPS = 8;
-// The longest-first order is used up to this many Gaussians.  Measured: C3 (1M) render_bwd
-// 441 -> 411 us; C5 (5M, 240 MB of splat records, 2650 instances per tile) 673 -> 1000 us, where
-// the index order's reuse of neighbouring tiles' splats in the caches is worth more than the tail.
-#ifndef GS_ORDER_LPT_MAX_P
-#define GS_ORDER_LPT_MAX_P (2 << 20)
-#endif
-constexpr int ORDER_LPT_MAX_P = GS_ORDER_LPT_MAX_P;
 
 inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t off = 0;
