@@ -50,15 +50,18 @@ WORKLOADS = {
 }
 
 
-def kernel_bytes(name, P, V, I, M, W, H, tiles):
-    """Algorithmic (minimum) HBM bytes of ONE launch of each kernel."""
+def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None):
+    """Algorithmic (minimum) HBM bytes of ONE launch of each kernel.
+    E: instances the render walks reach (sum over tiles of min(largest n_contrib, list length));
+    only those are staged, and only those have backward records."""
     npix = W * H
     sh = 12 * M
+    E = I if E is None else E
     return {
         "preprocess": P * (44 + sh + 4 + 4) + V * (48 + 32 + 4 + 1),
-        "render_fwd": I * (4 + 4 + 48) + npix * 20 + tiles * 12,
-        "render_bwd": I * (4 + 4 + 48 + 36) + npix * 20 + tiles * 12,
-        "sum_records": I * 36 + V * (4 + 36),
+        "render_fwd": E * (4 + 4 + 48) + npix * 20 + tiles * 12,
+        "render_bwd": E * (4 + 4 + 48 + 36) + npix * 20 + tiles * 12,
+        "sum_records": E * 36 + I * 4 + V * (4 + 36),
         "preprocess_bwd": P * (8 + 44 + sh + 1 + 32 + 24 + sh) + V * 36,
         "duplicate": V * (4 + 4 + 32 + 4) + I * 8,
         "ranges": I * 4 + tiles * 8,
@@ -128,11 +131,20 @@ def main():
 
     # workload counters (one extra forward, untimed)
     e = torch.Tensor([])
-    num_rendered, _, radii, *_ = _C.rasterize_gaussians(
+    num_rendered, _, radii, geom_b, bin_b, img_b = _C.rasterize_gaussians(
         settings.bg, d.means3D, e, d.opacities, d.scales, d.rotations, 1.0, e, settings.viewmatrix,
         settings.projmatrix, settings.tanfovx, settings.tanfovy, H, W, d.shs, deg, settings.campos, False, False)
     visible = int((radii > 0).sum())
     tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    # instances the render walks reach: per tile min(largest n_contrib, list length)
+    ex = _C.debug_export(P, W, H, num_rendered, geom_b, bin_b, img_b, dev)
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    ncp = torch.zeros((gy * 16, gx * 16), dtype=torch.int64, device=dev)
+    ncp[:H, :W] = ex["n_contrib"].to(torch.int64)
+    tmax = ncp.view(gy, 16, gx, 16).amax(dim=(1, 3)).reshape(-1)
+    rg = ex["ranges"].to(torch.int64)
+    walked = int(torch.minimum(tmax, rg[:, 1] - rg[:, 0]).sum())
+    del ex, geom_b, bin_b, img_b
 
     for _ in range(args.warmup):
         step()
@@ -189,13 +201,13 @@ def main():
     kernels = {}
     for name, (ms, n) in prof.items():
         per_launch_ms = ms / max(n, 1)
-        b = kernel_bytes(name, P, visible, num_rendered, M, W, H, tiles)
+        b = kernel_bytes(name, P, visible, num_rendered, M, W, H, tiles, walked)
         kernels[name] = dict(total_ms_per_step=round(ms / args.steps, 4), launches_per_step=round(n / args.steps, 2),
                              avg_us=round(1e3 * per_launch_ms, 2),
                              algo_GBs=(round(b / (per_launch_ms * 1e-3) / 1e9, 1) if b else None))
     dom = max(kernels, key=lambda k: kernels[k]["total_ms_per_step"])
     dom_avg_ms = kernels[dom]["avg_us"] / 1e3
-    dom_bytes = kernel_bytes(dom, P, visible, num_rendered, M, W, H, tiles)
+    dom_bytes = kernel_bytes(dom, P, visible, num_rendered, M, W, H, tiles, walked)
     achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9 if dom_bytes else None
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -219,7 +231,7 @@ def main():
             roofline["valu"] = dict(insts_per_launch=vi, peak_insts_per_s=VALU_PEAK_IPS,
                                     frac=round(vi / (dom_avg_ms * 1e-3) / VALU_PEAK_IPS, 4))
     # whole-step algorithmic bytes (P*a_G + I*a_I + Npix*a_px)
-    step_bytes = sum(kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles) or 0 for k in
+    step_bytes = sum(kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles, walked) or 0 for k in
                      ("preprocess", "render_fwd", "render_bwd", "sum_records", "preprocess_bwd", "duplicate",
                       "ranges"))
 
@@ -249,6 +261,7 @@ def main():
         "render_mpix_s": round(W * H / t_render / 1e6, 1),
         "render_ms": round(1e3 * t_render, 4),
         "num_rendered": int(num_rendered),
+        "walked_instances": walked,
         "visible": visible,
         "hbm": {"peak_allocated_GB": round(peak_hbm / 1e9, 3),
                 "scene_params_GB": round(sum(p.numel() for p in params) * 4 / 1e9, 3),
