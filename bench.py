@@ -8,10 +8,11 @@ Workload (N=1): BASELINE.json configs[2] "C3" -- 1M Gaussians, SH degree 3, 1920
 tiles (synthetic scene per SURVEY.md §8d: frustum-uniform means, seed 0).  One iteration = one
 view's GaussianRasterizer forward + backward (dL/dimage fixed, seed 1) through the drop-in
 package, i.e. exactly what train.py:86-93 runs on the rasterizer; `value` counts iterations
-(views) per second over the whole job.  A step = --views-per-rank views per rank (default 1 on
-one GPU, 4 with N > 1; gradients accumulated) followed, with --gpus N>1 (torchrun, one rank per
-GPU, RCCL), by one all-reduce of the 59-float/Gaussian gradient bucket (view-parallel data
-parallelism, weak scaling; DESIGN.md §7 on why the all-reduce is amortised over several views).
+(views) per second over the whole job.  A step = --views-per-rank views per rank (default 4 at
+every N, so the 1/2/4/8-GPU lines divide the same step) whose gradients accumulate in one flat
+59-float/Gaussian bucket (the .grad tensors are views into it; the rasterizer's backward writes
+/ adds straight into them), followed with --gpus N>1 (torchrun, one rank per GPU, RCCL) by ONE
+all-reduce of that bucket (view-parallel data parallelism, weak scaling).
 
 Output: one JSON line (rank 0) with the metric, a per-kernel HIP-event breakdown, the roofline of
 the dominant kernel and the CPU oracle baseline timed on this host.
@@ -50,10 +51,12 @@ WORKLOADS = {
 }
 
 
-def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None):
+def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None, acc_frac=0.0):
     """Algorithmic (minimum) HBM bytes of ONE launch of each kernel.
     E: instances the render walks reach (sum over tiles of min(largest n_contrib, list length));
-    only those are staged, and only those have backward records."""
+    only those are staged, and only those have backward records.  acc_frac: fraction of the
+    preprocess_bwd launches that add into the gradient bucket (views after a step's first), which
+    also read the old gradients (means3D 12 + sh 12M + opacity 4 + scales 12 + rotations 16 B)."""
     npix = W * H
     sh = 12 * M
     E = I if E is None else E
@@ -62,7 +65,7 @@ def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None):
         "render_fwd": E * (4 + 4 + 48) + npix * 20 + tiles * 12,
         "render_bwd": E * (4 + 4 + 48 + 36) + npix * 20 + tiles * 12,
         "sum_records": E * 36 + I * 4 + V * (4 + 36),
-        "preprocess_bwd": P * (8 + 44 + sh + 1 + 32 + 24 + sh) + V * 36,
+        "preprocess_bwd": P * (8 + 44 + sh + 1 + 32 + 24 + sh) + V * 36 + int(acc_frac * P * (44 + sh)),
         "duplicate": V * (4 + 4 + 32 + 4) + I * 8,
         "ranges": I * 4 + tiles * 8,
     }.get(name)
@@ -75,11 +78,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = all host cores, max 16)")
-    ap.add_argument("--views-per-rank", type=int, default=0,
-                    help="C1-C3/C5: views each rank renders (fwd+bwd, gradients accumulated) per step, "
-                         "i.e. per gradient all-reduce (DESIGN.md §7); value counts views. "
-                         "0 = 1 on one GPU, 4 with N > 1")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle threads (0 = the CPUs this job may use: affinity, cgroup quota, OMP_NUM_THREADS)")
+    ap.add_argument("--cpu-runs", type=int, default=3, help="timed CPU-oracle runs after one warm-up (median)")
+    ap.add_argument("--views-per-rank", type=int, default=4,
+                    help="C1-C3/C5: views each rank renders (fwd+bwd, gradients accumulated in the bucket) per "
+                         "step, i.e. per gradient all-reduce (DESIGN.md §7); value counts views")
+    ap.add_argument("--sustain-s", type=float, default=2.0,
+                    help="after the timed steps, keep stepping for this long (untimed for `value`) and report "
+                         "the sustained rate too")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,7 +112,7 @@ def main():
         cam = cams[my_views[0]]
     else:
         cam = gs_scenes.identity_camera(W, H)
-        k_views = args.views_per_rank or (4 if world > 1 else 1)
+        k_views = max(1, args.views_per_rank)
         cams, my_views = [cam], [0] * k_views
         sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=0)
     settings = gs_scenes.raster_settings_for(cam, deg, device=dev)
@@ -116,18 +123,21 @@ def main():
     dpix = gs_scenes.dl_dimage(H, W, seed=1).to(dev)
     rasts = [GaussianRasterizer(gs_scenes.raster_settings_for(cams[v], deg, device=dev)) for v in my_views]
     rast = rasts[0]
-    bucket = vp.GradBucket(params) if world > 1 else None
+    # the parameters' .grad are views of ONE flat bucket; the rasterizer is the only gradient
+    # producer here, so the step's first backward overwrites and the others add (lazy zeroing)
+    bucket = vp.GradBucket(params, lazy_zero=True)
 
     def step():
-        for r in rasts:  # gradients of this rank's views accumulate in .grad
+        bucket.zero_grad()
+        means2D.grad = None
+        for r in rasts:  # this rank's views: gradients accumulate in the bucket
             img, _ = r(means3D=params[0], means2D=means2D, opacities=params[2], shs=params[1], scales=params[3],
                        rotations=params[4])
             img.backward(dpix)
         if world > 1:
-            bucket.allreduce(unpack=False)  # one RCCL all-reduce of the 59-f32/Gaussian bucket
-        for p in params:
-            p.grad = None
-        means2D.grad = None
+            bucket.allreduce()  # one RCCL all-reduce of the 59-f32/Gaussian bucket, in place
+        else:
+            bucket.finalize()
 
     # workload counters (one extra forward, untimed)
     e = torch.Tensor([])
@@ -165,6 +175,31 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # sustained rate: keep stepping for ~--sustain-s (a longer region than the K timed steps,
+    # which last only tens of ms; the same step, reported beside `value`, not instead of it)
+    sustained = None
+    if args.sustain_s > 0:
+        n_s = max(1, int(args.sustain_s / max(elapsed / args.steps, 1e-4)))
+        if world > 1:
+            nt = torch.tensor([n_s], dtype=torch.int64, device=dev)
+            dist.all_reduce(nt, op=dist.ReduceOp.MIN)
+            n_s = int(nt.item())
+            dist.barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(n_s):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el_s = time.perf_counter() - ts
+        if world > 1:
+            t = torch.tensor([el_s], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_s = float(t.item())
+        sustained = dict(steps=n_s, seconds=round(el_s, 3),
+                         iters_s=round((n_views or world * len(my_views)) * n_s / el_s, 2))
+
     # per-kernel durations: a second pass of the same K steps with HIP events around every launch
     # (on the launch stream); kept out of the timed pass above because the event records add
     # host work and small gaps between kernels
@@ -198,16 +233,18 @@ def main():
     value = views_per_step * args.steps / elapsed
 
     # per-kernel breakdown + roofline of the dominant kernel
+    k_local = len(my_views)
+    acc_frac = (k_local - 1) / k_local  # preprocess_bwd launches that add into the bucket
     kernels = {}
     for name, (ms, n) in prof.items():
         per_launch_ms = ms / max(n, 1)
-        b = kernel_bytes(name, P, visible, num_rendered, M, W, H, tiles, walked)
+        b = kernel_bytes(name, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac)
         kernels[name] = dict(total_ms_per_step=round(ms / args.steps, 4), launches_per_step=round(n / args.steps, 2),
                              avg_us=round(1e3 * per_launch_ms, 2),
                              algo_GBs=(round(b / (per_launch_ms * 1e-3) / 1e9, 1) if b else None))
     dom = max(kernels, key=lambda k: kernels[k]["total_ms_per_step"])
     dom_avg_ms = kernels[dom]["avg_us"] / 1e3
-    dom_bytes = kernel_bytes(dom, P, visible, num_rendered, M, W, H, tiles, walked)
+    dom_bytes = kernel_bytes(dom, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac)
     achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9 if dom_bytes else None
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -230,14 +267,18 @@ def main():
         if vi:
             roofline["valu"] = dict(insts_per_launch=vi, peak_insts_per_s=VALU_PEAK_IPS,
                                     frac=round(vi / (dom_avg_ms * 1e-3) / VALU_PEAK_IPS, 4))
-    # whole-step algorithmic bytes (P*a_G + I*a_I + Npix*a_px)
-    step_bytes = sum(kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles, walked) or 0 for k in
+    # whole-step algorithmic bytes (P*a_G + I*a_I + Npix*a_px), per view
+    step_bytes = sum(kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac) or 0 for k in
                      ("preprocess", "render_fwd", "render_bwd", "sum_records", "preprocess_bwd", "duplicate",
                       "ranges"))
+    ms_per_view = ms_per_step / k_local
+    step_roofline = dict(algo_bytes_per_view=int(step_bytes), ms_per_view=round(ms_per_view, 4),
+                         achieved=round(step_bytes / (ms_per_view * 1e-3) / 1e9, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                         frac=round(step_bytes / (ms_per_view * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(sc, cam, deg, W, H, dpix.cpu(), args.cpu_threads)
+        cpu = cpu_baseline(sc, cam, deg, W, H, dpix.cpu(), args.cpu_threads, args.cpu_runs)
 
     out = {
         "metric": "train iters/sec (fwd+bwd) + render Mpix/s @1080p, 1M Gaussians SH=3",
@@ -270,8 +311,9 @@ def main():
                 "image_buffer_GB": round(lib.gs_image_buffer_bytes(W, H) / 1e9, 3),
                 "grad_scratch_GB": round(lib.gs_grad_buffer_bytes(int(num_rendered)) / 1e9, 3)},
         "roofline": roofline,
-        "ms_per_view": round(ms_per_step / len(my_views), 4),
-        "step_algo_GBs": round(step_bytes / (ms_per_step / len(my_views) * 1e-3) / 1e9, 1),
+        "ms_per_view": round(ms_per_view, 4),
+        "step_roofline": step_roofline,
+        "sustained": sustained,
         "kernels": kernels,
         "cpu_baseline": cpu,
     }
@@ -281,28 +323,69 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(sc, cam, deg, W, H, dpix, threads):
+def job_cpus():
+    """CPUs this job may use: the affinity mask, capped by a cgroup v2 CPU quota and by
+    OMP_NUM_THREADS when the launcher sets it (the GPU box allots each job a share of the host:
+    os.cpu_count() there shows the whole machine).  Returns (n, how)."""
+    n = len(os.sched_getaffinity(0))
+    how = [f"affinity {n}"]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n_q = max(1, int(int(q) / int(per)))
+            how.append(f"cgroup quota {n_q}")
+            n = min(n, n_q)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        how.append(f"OMP_NUM_THREADS {omp}")
+        n = min(n, int(omp))
+    return n, ", ".join(how)
+
+
+def cpu_model():
+    try:
+        import subprocess
+
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(sc, cam, deg, W, H, dpix, threads, runs):
     """CPU oracle (oracle/gs_oracle.c: this repo's C restatement of the algorithm; the reference has
-    no CPU rasterizer) timed on the host for one full fwd+bwd step of the same workload."""
+    no CPU rasterizer) timed on the host for full fwd+bwd steps of the same workload: one warm-up,
+    then the median of `runs` (BASELINE.md §2 protocol), on every CPU the job may use."""
     import numpy as np
 
     from oracle import gs_oracle
 
     gs_oracle.build()
-    n = threads or min(16, os.cpu_count() or 1)
+    n, how = (threads, "--cpu-threads") if threads else job_cpus()
     gs_oracle.set_threads(n)
     osc = gs_oracle.Scene(bg=np.zeros(3, np.float32), means3D=sc.means3D.numpy(), opacities=sc.opacities.numpy(),
                           W=W, H=H, viewmatrix=cam.world_view_transform.numpy(),
                           projmatrix=cam.full_proj_transform.numpy(), campos=cam.camera_center.numpy(),
                           tanfovx=math.tan(cam.FoVx / 2), tanfovy=math.tan(cam.FoVy / 2), shs=sc.shs.numpy(),
                           sh_degree=deg, scales=sc.scales.numpy(), rotations=sc.rotations.numpy())
-    t = time.perf_counter()
-    gs_oracle.forward(osc)
-    gs_oracle.backward(osc, dpix.numpy())
-    dt = time.perf_counter() - t
+    times = []
+    for r in range(1 + max(1, runs)):
+        t = time.perf_counter()
+        gs_oracle.forward(osc)
+        gs_oracle.backward(osc, dpix.numpy())
+        if r > 0:  # run 0 is the warm-up
+            times.append(time.perf_counter() - t)
+    dt = sorted(times)[len(times) // 2]
     return {"value": round(1.0 / dt, 5), "unit": "iters/s", "cores": n, "kind": "port",
-            "sample": f"one full fwd+bwd step of the same workload ({sc.P} Gaussians, {W}x{H}), "
-                      f"{dt:.1f} s on {n} host threads"}
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "cores_from": how,
+            "runs_s": [round(x, 3) for x in times],
+            "sample": f"full fwd+bwd steps of the same workload ({sc.P} Gaussians, {W}x{H}): one warm-up, median "
+                      f"of {len(times)} runs = {dt:.2f} s on {n} threads"}
 
 
 if __name__ == "__main__":

@@ -179,6 +179,8 @@ bool exact_exp() {
 }  // namespace gs
 
 namespace gs {
+static std::atomic<uint32_t> g_spin_limit{LB_SPIN_LIMIT};
+uint32_t scan_spin_limit() { return g_spin_limit.load(std::memory_order_relaxed); }
 uint32_t next_scan_epoch() {
   static std::atomic<uint32_t> e{0};
   return (e.fetch_add(1, std::memory_order_relaxed) % ((1u << 30) - 1u)) + 1u;
@@ -203,8 +205,10 @@ size_t gs_grad_buffer_bytes(long long num_rendered) {
 // Per-thread, per-device pinned readback word block + event (reused call after call: a call
 // waits on its event before returning, so the slot is free again when the next call starts).
 struct ReadbackSlot {
-  uint32_t* host = nullptr;
-  hipEvent_t ev = nullptr;
+  uint32_t* host = nullptr;   // [0, 8): counters after preprocess; [8, 16): counters after fwd_order
+  hipEvent_t ev = nullptr;    // preprocess done (num_rendered readable)
+  hipEvent_t ev2 = nullptr;   // depth order + offsets scan done (its error flags readable)
+  bool order_pending = false;  // ev2 recorded by gs_forward_preprocess, not yet checked
 };
 static ReadbackSlot* readback_slot() {
   static thread_local ReadbackSlot slots[64];
@@ -216,6 +220,7 @@ static ReadbackSlot* readback_slot() {
     void* p = nullptr;
     if (!check_hip(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc")) return nullptr;
     if (!check_hip(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate")) return nullptr;
+    if (!check_hip(hipEventCreateWithFlags(&s.ev2, hipEventDisableTiming), "hipEventCreate")) return nullptr;
     s.host = (uint32_t*)p;
   }
   return &s;
@@ -248,6 +253,12 @@ int gs_forward_preprocess(int P, int D, int M, const float* background, int W, i
   check_hip(hipMemcpyAsync(rb->host, geo.counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
   check_hip(hipEventRecord(rb->ev, st), "hipEventRecord");
   fwd_order(P, geo, st);
+  // the ordering scan's error flags (look-back timeout) are read after fwd_order, behind a second
+  // event; gs_forward_render checks them once its own launches are queued, so the host wait
+  // never idles the device
+  check_hip(hipMemcpyAsync(rb->host + 8, geo.counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
+  check_hip(hipEventRecord(rb->ev2, st), "hipEventRecord");
+  rb->order_pending = true;
   check_hip(hipEventSynchronize(rb->ev), "hipEventSynchronize");
   if (t_failed) return 1;
   const uint32_t err = rb->host[CNT_ERR], I = rb->host[CNT_NREND];
@@ -276,11 +287,13 @@ int gs_forward_render(int P, const float* background, int W, int H, const float*
   img_layout(W, H, &img, (char*)image_buffer);
   fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
   fwd_render(c, geo, bin, img, out_color, st);
-  if (debug && !t_failed) {  // debug: surface a look-back wait that ran out (never expected)
-    uint32_t err = 0;
-    if (check_hip(hipMemcpyAsync(&err, &geo.counters[CNT_ERR], 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(err)") &&
-        check_hip(hipStreamSynchronize(st), "hipStreamSynchronize") && (err & 4u))
-      return set_error("ordering scan: look-back wait timed out"), 1;
+  // surface a look-back wait of the offsets scan that ran out (never expected: the scan's grid
+  // is resident), in every mode: the preprocess call left the flags behind ev2
+  ReadbackSlot* rb = readback_slot();
+  if (rb && rb->order_pending && !t_failed) {
+    rb->order_pending = false;
+    if (check_hip(hipEventSynchronize(rb->ev2), "hipEventSynchronize") && (rb->host[8 + CNT_ERR] & 4u))
+      return set_error("ordering scan: look-back wait timed out (instance offsets are invalid)"), 1;
   }
   return t_failed ? 1 : 0;
 }
@@ -314,16 +327,15 @@ long long gs_rasterize_forward(int P, int D, int M, const float* background, int
   return I;
 }
 
-int gs_backward(int P, int D, int M, const float* background, int W, int H, const float* means3D, const float* shs,
-                const float* colors_precomp, const float* opacities, const float* scales, float scale_modifier,
-                const float* rotations, const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
-                const float* campos, float tan_fovx, float tan_fovy, const int* radii, const void* geom_buffer,
-                long long num_rendered, const void* binning_buffer, const void* image_buffer,
-                const float* dL_dout_color, void* grad_buffer, float* dL_dmeans2D, float* dL_dcolors,
-                float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
-                float* dL_drotations, int debug, void* stream) {
+static int backward_impl(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                         const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                         float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                         const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                         float tan_fovy, const void* geom_buffer, long long num_rendered, const void* binning_buffer,
+                         const void* image_buffer, const float* dL_dout_color, void* grad_buffer, float* dL_dmeans2D,
+                         float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                         float* dL_dscales, float* dL_drotations, unsigned accumulate, int debug, void* stream) {
   clear_error(debug);
-  (void)radii;
   (void)opacities;  // the opacity is carried by the forward's splat records
   if (!validate(P, D, M, W, H, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, viewmatrix,
                 projmatrix, campos, background, false))
@@ -333,6 +345,7 @@ int gs_backward(int P, int D, int M, const float* background, int W, int H, cons
     return set_error("missing buffer pointer"), 1;
   if (!dL_dmeans2D || !dL_dopacity || !dL_dmeans3D) return set_error("missing gradient output pointer"), 1;
   if (num_rendered < 0 || num_rendered > 0xFFFFFFFFll) return set_error("num_rendered out of range"), 1;
+  if (accumulate & ~0xFFu) return set_error("accumulate: unknown GS_ACC bits 0x%x", accumulate), 1;
   hipStream_t st = (hipStream_t)stream;
   CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, 0);
   GeomPtrs geo;
@@ -344,10 +357,47 @@ int gs_backward(int P, int D, int M, const float* background, int W, int H, cons
   GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier};
   float* gradrec = (float*)grad_buffer;
   if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, st);
-  GradOut out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, cov3D_precomp ? dL_dcov3D : nullptr,
-              shs ? dL_dsh : nullptr, cov3D_precomp ? nullptr : dL_dscales, cov3D_precomp ? nullptr : dL_drotations};
+  // dL_dcov3D is filled whenever the caller passes it: upstream writes it for scale/rotation
+  // inputs too (the covariance gradient the scale / rotation chain starts from)
+  GradOut out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+              shs ? dL_dsh : nullptr, cov3D_precomp ? nullptr : dL_dscales, cov3D_precomp ? nullptr : dL_drotations,
+              accumulate};
   bwd_preprocess(g, c, geo, bin, img, gradrec, num_rendered > 0, out, st);
   return t_failed ? 1 : 0;
+}
+
+int gs_backward(int P, int D, int M, const float* background, int W, int H, const float* means3D, const float* shs,
+                const float* colors_precomp, const float* opacities, const float* scales, float scale_modifier,
+                const float* rotations, const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                const float* campos, float tan_fovx, float tan_fovy, const int* radii, const void* geom_buffer,
+                long long num_rendered, const void* binning_buffer, const void* image_buffer,
+                const float* dL_dout_color, void* grad_buffer, float* dL_dmeans2D, float* dL_dcolors,
+                float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                float* dL_drotations, int debug, void* stream) {
+  (void)radii;
+  return backward_impl(P, D, M, background, W, H, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
+                       rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, geom_buffer,
+                       num_rendered, binning_buffer, image_buffer, dL_dout_color, grad_buffer, dL_dmeans2D,
+                       dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, 0u, debug,
+                       stream);
+}
+
+int gs_backward_accumulate(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                           const float* shs, const float* colors_precomp, const float* opacities,
+                           const float* scales, float scale_modifier, const float* rotations,
+                           const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                           const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                           const void* geom_buffer, long long num_rendered, const void* binning_buffer,
+                           const void* image_buffer, const float* dL_dout_color, void* grad_buffer,
+                           float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                           float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                           unsigned accumulate, int debug, void* stream) {
+  (void)radii;
+  return backward_impl(P, D, M, background, W, H, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
+                       rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, geom_buffer,
+                       num_rendered, binning_buffer, image_buffer, dL_dout_color, grad_buffer, dL_dmeans2D,
+                       dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, accumulate,
+                       debug, stream);
 }
 
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
@@ -368,6 +418,10 @@ int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, voi
   if (!points || !out || !scratch) return set_error("missing pointer"), 1;
   knn_mean_dist2(P, points, out, (char*)scratch, (hipStream_t)stream);
   return t_failed ? 1 : 0;
+}
+
+unsigned gs_debug_set_scan_spin_limit(unsigned limit) {
+  return gs::g_spin_limit.exchange(limit, std::memory_order_relaxed);
 }
 
 /* ---- numerics mode of the render loops ---- */
@@ -565,6 +619,25 @@ int gs_debug_export(int P, int W, int H, long long num_rendered, const void* geo
     check_hip(hipMemcpyAsync(final_T, img.final_T, sizeof(float) * W * H, hipMemcpyDeviceToDevice, st), "copy");
   if (n_contrib)
     check_hip(hipMemcpyAsync(n_contrib, img.n_contrib, sizeof(uint32_t) * W * H, hipMemcpyDeviceToDevice, st), "copy");
+  return t_failed ? 1 : 0;
+}
+
+int gs_debug_export_slots(int W, int H, long long num_rendered, const void* binning_buffer, const void* image_buffer,
+                          uint32_t* slots, uint32_t* tile_cut, void* stream) {
+  clear_error(0);
+  hipStream_t st = (hipStream_t)stream;
+  if (W <= 0 || H <= 0 || num_rendered < 0) return set_error("debug_export_slots: bad arguments"), 1;
+  const int gx = (W + GS_TILE - 1) / GS_TILE, gy = (H + GS_TILE - 1) / GS_TILE;
+  BinPtrs bin;
+  ImgPtrs img;
+  bin_layout((size_t)num_rendered, gx * gy, &bin, (char*)binning_buffer);
+  img_layout(W, H, &img, (char*)image_buffer);
+  if (slots && num_rendered > 0)
+    check_hip(hipMemcpyAsync(slots, bin.point_list, sizeof(uint32_t) * (size_t)num_rendered, hipMemcpyDeviceToDevice,
+                             st), "copy");
+  if (tile_cut)
+    check_hip(hipMemcpyAsync(tile_cut, img.tile_cut, sizeof(uint32_t) * (size_t)gx * gy, hipMemcpyDeviceToDevice, st),
+              "copy");
   return t_failed ? 1 : 0;
 }
 

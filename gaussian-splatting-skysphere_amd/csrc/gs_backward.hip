@@ -594,6 +594,12 @@ __device__ __forceinline__ void cov3d_backward(float sx, float sy, float sz, flo
             4.f * z * (dR[0][0] + dR[1][1]);
 }
 
+// one gradient output element: written, or (GS_ACC bit set for the output) added to the caller's
+// buffer as autograd's `grad += g` does (fp32 old + new)
+__device__ __forceinline__ void gput(float* p, size_t k, float v, uint32_t acc, uint32_t bit) {
+  p[k] = (acc & bit) ? p[k] + v : v;
+}
+
 template <int DEG, bool REG = false>
 __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g, const CameraArgs& c,
                                                    const uint32_t* __restrict__ tiles,
@@ -601,29 +607,35 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
                                                    const float* __restrict__ gsum, const GradOut& out,
                                                    float* row) {
   const uint32_t cnt = tiles[i];
+  const uint32_t acc = out.acc;
   if (cnt == 0) {
-    // invisible: every gradient is zero (upstream: zero-initialised outputs, radii == 0 skipped)
-    out.dmean2D[3 * i] = 0.f;
-    out.dmean2D[3 * i + 1] = 0.f;
-    out.dmean2D[3 * i + 2] = 0.f;
-    if (out.dcolor) {
+    // invisible: every gradient is zero (upstream: zero-initialised outputs, radii == 0 skipped);
+    // an accumulated output keeps what it holds (+ 0)
+    if (!(acc & GS_ACC_MEANS2D)) {
+      out.dmean2D[3 * i] = 0.f;
+      out.dmean2D[3 * i + 1] = 0.f;
+      out.dmean2D[3 * i + 2] = 0.f;
+    }
+    if (out.dcolor && !(acc & GS_ACC_COLORS)) {
       out.dcolor[3 * i] = 0.f;
       out.dcolor[3 * i + 1] = 0.f;
       out.dcolor[3 * i + 2] = 0.f;
     }
-    out.dopacity[i] = 0.f;
-    out.dmean3D[3 * i] = 0.f;
-    out.dmean3D[3 * i + 1] = 0.f;
-    out.dmean3D[3 * i + 2] = 0.f;
-    if (out.dcov3D)
+    if (!(acc & GS_ACC_OPACITY)) out.dopacity[i] = 0.f;
+    if (!(acc & GS_ACC_MEANS3D)) {
+      out.dmean3D[3 * i] = 0.f;
+      out.dmean3D[3 * i + 1] = 0.f;
+      out.dmean3D[3 * i + 2] = 0.f;
+    }
+    if (out.dcov3D && !(acc & GS_ACC_COV3D))
       for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
     if (DEG >= 0 && !REG)
       for (int k = 0; k < 3 * g.M; k++) row[k] = 0.f;
-    if (DEG >= 0 && REG)
+    if (DEG >= 0 && REG && !(acc & GS_ACC_SH))
       for (int k = 0; k < 3 * g.M; k++) out.dsh[(size_t)i * 3 * g.M + k] = 0.f;
-    if (out.dscale)
+    if (out.dscale && !(acc & GS_ACC_SCALES))
       for (int k = 0; k < 3; k++) out.dscale[3 * i + k] = 0.f;
-    if (out.drot)
+    if (out.drot && !(acc & GS_ACC_ROTATIONS))
       for (int k = 0; k < 4; k++) out.drot[4 * i + k] = 0.f;
     return;
   }
@@ -636,14 +648,14 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
   const float dm2x = a[3], dm2y = a[4];
   const float dcon0 = a[5], dcon1 = a[6], dcon2 = a[7];
   if (out.dcolor) {
-    out.dcolor[3 * i] = dcol[0];
-    out.dcolor[3 * i + 1] = dcol[1];
-    out.dcolor[3 * i + 2] = dcol[2];
+    gput(out.dcolor, 3 * i, dcol[0], acc, GS_ACC_COLORS);
+    gput(out.dcolor, 3 * i + 1, dcol[1], acc, GS_ACC_COLORS);
+    gput(out.dcolor, 3 * i + 2, dcol[2], acc, GS_ACC_COLORS);
   }
-  out.dmean2D[3 * i] = dm2x;
-  out.dmean2D[3 * i + 1] = dm2y;
-  out.dmean2D[3 * i + 2] = 0.0f;
-  out.dopacity[i] = a[8];
+  gput(out.dmean2D, 3 * i, dm2x, acc, GS_ACC_MEANS2D);
+  gput(out.dmean2D, 3 * i + 1, dm2y, acc, GS_ACC_MEANS2D);
+  gput(out.dmean2D, 3 * i + 2, 0.0f, acc, GS_ACC_MEANS2D);
+  gput(out.dopacity, i, a[8], acc, GS_ACC_OPACITY);
 
   const float px = g.means3D[3 * i], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
   float cov3[6];
@@ -701,7 +713,7 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
   dmean[2] = v[8] * dL_dtx + v[9] * dL_dty + v[10] * dL_dtz;
   if (out.dcov3D)
 #pragma unroll
-    for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = dcv[k];
+    for (int k = 0; k < 6; k++) gput(out.dcov3D, 6 * i + k, dcv[k], acc, GS_ACC_COV3D);
   // projection: NDC mean2D -> mean3D
   const float* P = c.proj;
   const float hw = xf44w(P, px, py, pz);
@@ -722,20 +734,17 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
     dmean[1] = dmean[1] + shm[1];
     dmean[2] = dmean[2] + shm[2];
   }
-  out.dmean3D[3 * i] = dmean[0];
-  out.dmean3D[3 * i + 1] = dmean[1];
-  out.dmean3D[3 * i + 2] = dmean[2];
+  gput(out.dmean3D, 3 * i, dmean[0], acc, GS_ACC_MEANS3D);
+  gput(out.dmean3D, 3 * i + 1, dmean[1], acc, GS_ACC_MEANS3D);
+  gput(out.dmean3D, 3 * i + 2, dmean[2], acc, GS_ACC_MEANS3D);
   if (!g.cov3D && out.dscale && out.drot) {
     float ds[3], dr[4];
     cov3d_backward(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
                    g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], dcv, ds, dr);
-    out.dscale[3 * i] = ds[0];
-    out.dscale[3 * i + 1] = ds[1];
-    out.dscale[3 * i + 2] = ds[2];
-    out.drot[4 * i] = dr[0];
-    out.drot[4 * i + 1] = dr[1];
-    out.drot[4 * i + 2] = dr[2];
-    out.drot[4 * i + 3] = dr[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) gput(out.dscale, 3 * i + k, ds[k], acc, GS_ACC_SCALES);
+#pragma unroll
+    for (int k = 0; k < 4; k++) gput(out.drot, 4 * i + k, dr[k], acc, GS_ACC_ROTATIONS);
   }
 }
 
@@ -755,6 +764,11 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
   }
   if (i < g.P) preprocess_bwd_one<DEG>(i, g, c, tiles, clamped, gsum, out, row);
   if (DEG >= 0) {
+    if (out.acc & GS_ACC_SH) {  // (uniform) accumulation: the lane adds its own row
+      if (i < g.P)
+        for (int k = 0; k < rowf; k++) out.dsh[(size_t)i * rowf + k] += row[k];
+      return;
+    }
     __syncthreads();
     lds_to_rows(s_sh, out.dsh + (size_t)i0 * rowf, nG, rowf, stride);
   }
@@ -792,6 +806,20 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd_reg(GaussianArgs g, Came
     return;
   }
   preprocess_bwd_one<DEG, true>(i, g, c, tiles, clamped, gsum, out, row);
+  if (out.acc & GS_ACC_SH) {  // (uniform) multi-view accumulation: dL/dsh += this view's
+    if (vec) {
+#pragma unroll
+      for (int q = 0; q < KF / 4; q++) {
+        const float4 o = reinterpret_cast<const float4*>(dst)[q];
+        reinterpret_cast<float4*>(dst)[q] =
+            make_float4(o.x + row[4 * q], o.y + row[4 * q + 1], o.z + row[4 * q + 2], o.w + row[4 * q + 3]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < KF; k++) dst[k] = dst[k] + row[k];
+    }
+    return;  // coefficients past (D + 1)^2 get + 0
+  }
   if (vec) {
 #pragma unroll
     for (int q = 0; q < KF / 4; q++)

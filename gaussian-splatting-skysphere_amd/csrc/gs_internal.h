@@ -16,6 +16,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../../include/gsrast.h"  // GS_ACC_* bits
 #include "gs_common.h"
 #include "gs_sortscan.h"
 
@@ -234,6 +235,9 @@ struct GradOut {
   float* dsh;       // [P, M, 3] or null
   float* dscale;    // [P, 3] or null
   float* drot;      // [P, 4] or null
+  // GS_ACC_* bits: the output is ADDED to what the buffer holds (multi-view gradient
+  // accumulation into a caller-owned bucket, gsrast.h gs_backward_accumulate) instead of written
+  uint32_t acc;
 };
 void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
                     const ImgPtrs& img, float* gradrec,

@@ -179,7 +179,8 @@ __device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
 template <class Src, class Dst>
 __global__ __launch_bounds__(LB_THREADS) void k_scan_lb(Src src, Dst dst, const uint32_t* n_dev, uint32_t n_max,
                                                         uint64_t* __restrict__ status, uint32_t* tile_counter,
-                                                        uint32_t epoch, uint32_t* total_out, uint32_t* err_flag) {
+                                                        uint32_t epoch, uint32_t* total_out, uint32_t* err_flag,
+                                                        uint32_t spin_limit) {
   __shared__ uint32_t sh[4];
   __shared__ uint32_t s_tile, s_excl;
   // Tile ids: with a grid every CU can hold at once (LB_STATIC_MAX workgroups, a quarter of the
@@ -217,7 +218,8 @@ __global__ __launch_bounds__(LB_THREADS) void k_scan_lb(Src src, Dst dst, const 
         ready = ready && (uint32_t)(w[k] >> 34) == epoch;
       }
       uint32_t spins = 0;
-      while (__ballot(!ready) != 0) {  // wait until every word of the window has been published
+      bool forced = spin_limit == 0;  // test hook (gs_debug_set_scan_spin_limit(0)): time out at once
+      while (forced || __ballot(!ready) != 0) {  // wait until every word of the window has been published
         __builtin_amdgcn_s_sleep(1);
         ready = true;
 #pragma unroll
@@ -226,11 +228,12 @@ __global__ __launch_bounds__(LB_THREADS) void k_scan_lb(Src src, Dst dst, const 
           if ((uint32_t)(w[k] >> 34) != epoch) w[k] = lb_load(&status[idx]);
           ready = ready && (uint32_t)(w[k] >> 34) == epoch;
         }
-        if (++spins > LB_SPIN_LIMIT) {
+        if (forced || ++spins > spin_limit) {
           if (lane == 0) atomicOr(err_flag, 4u);
 #pragma unroll
           for (int k = 0; k < 4; k++) w[k] = lb_word(epoch, LB_PREFIX, 0);
           ready = true;
+          forced = false;
         }
       }
       // nearest inclusive prefix: first (lane, k) in window order
@@ -266,6 +269,7 @@ __global__ __launch_bounds__(LB_THREADS) void k_scan_lb(Src src, Dst dst, const 
 }
 
 uint32_t next_scan_epoch();  // host: a fresh non-zero epoch per call (gs_api.hip)
+uint32_t scan_spin_limit();  // host: LB_SPIN_LIMIT unless a test lowered it (gs_api.hip)
 
 // host: one-launch scan.  status needs lb_tiles(n_max) u64; *tile_counter must be 0.
 template <class Src, class Dst>
@@ -273,7 +277,7 @@ inline void scan_exclusive_lb(Src src, Dst dst, const uint32_t* n_dev, uint32_t 
                               uint32_t* tile_counter, uint32_t* total_out, uint32_t* err_flag, hipStream_t st) {
   const uint32_t tiles = lb_tiles(n_max);
   GS_LAUNCH("scan_lb", (k_scan_lb<Src, Dst>), dim3(tiles), dim3(LB_THREADS), 0, st, src, dst, n_dev, n_max, status,
-            tile_counter, next_scan_epoch(), total_out, err_flag);
+            tile_counter, next_scan_epoch(), total_out, err_flag, scan_spin_limit());
 }
 
 // simple functors

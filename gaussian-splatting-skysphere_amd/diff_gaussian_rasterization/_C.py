@@ -15,6 +15,7 @@ device.  There is no CPU path: CPU tensors raise.
 from __future__ import annotations
 
 import ctypes
+import math
 
 import torch
 
@@ -31,8 +32,10 @@ def _dev_check(t: torch.Tensor, name: str):
         )
 
 
-def _f32(t, name, device, allow_empty=True):
-    """Contiguous fp32 device tensor, or None for an absent / empty input."""
+def _f32(t, name, device, allow_empty=True, host_ok=False):
+    """Contiguous fp32 device tensor, or None for an absent / empty input.  host_ok: a camera-side
+    input (bg, viewmatrix, projmatrix, campos) may come from the host and is copied over; every
+    per-Gaussian tensor must already live on means3D's device."""
     if t is None:
         return None
     if t.numel() == 0:
@@ -42,8 +45,7 @@ def _f32(t, name, device, allow_empty=True):
     if t.dtype != torch.float32:
         raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
     if t.device != device:
-        # small camera-side tensors (bg, matrices, campos) may be handed over on the host
-        if t.numel() <= 16:
+        if host_ok and t.numel() <= 16:
             t = t.to(device)
         else:
             _dev_check(t, name)
@@ -71,16 +73,16 @@ class _Inputs:
         d = self.device
         self.P = means3D.size(0)
         self.means3D = _f32(means3D, "means3D", d)
-        self.bg = _f32(background, "background", d)
+        self.bg = _f32(background, "background", d, host_ok=True)
         self.colors = _f32(colors, "colors_precomp", d)
         self.opacity = _f32(opacity, "opacities", d)
         self.scales = _f32(scales, "scales", d)
         self.rotations = _f32(rotations, "rotations", d)
         self.cov3D = _f32(cov3D_precomp, "cov3D_precomp", d)
-        self.view = _f32(viewmatrix, "viewmatrix", d)
-        self.proj = _f32(projmatrix, "projmatrix", d)
+        self.view = _f32(viewmatrix, "viewmatrix", d, host_ok=True)
+        self.proj = _f32(projmatrix, "projmatrix", d, host_ok=True)
         self.sh = _f32(sh, "sh", d)
-        self.campos = _f32(campos, "campos", d)
+        self.campos = _f32(campos, "campos", d, host_ok=True)
         self.M = 0 if self.sh is None else (self.sh.size(1) if self.sh.ndimension() == 3 else self.sh.numel() // max(1, 3 * self.P))
         if self.P > 0:
             if self.colors is not None and self.colors.numel() != 3 * self.P:
@@ -131,48 +133,72 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     return num_rendered, out_color, radii, geom, binning, img
 
 
+# gradient outputs of the backward, in the upstream return order, with their GS_ACC_* bit
+GRAD_NAMES = ("means2D", "colors", "opacity", "means3D", "cov3D", "sh", "scales", "rotations")
+GS_ACC = {n: 1 << k for k, n in enumerate(GRAD_NAMES)}
+
+
 def backward_impl(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
                   projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R, binningBuffer,
-                  imageBuffer, debug, want_all=True):
+                  imageBuffer, debug, want_all=True, sinks=None):
     """Shared backward.  With want_all=False the gradients that no autograd input can receive
     (colours when SHs drive the colour, cov3D when scale/rotation drive it, ...) are None and
-    not computed."""
+    not computed.  sinks: {name: (buffer, accumulate)} -- that gradient is written into (or, with
+    accumulate, added to) the caller's buffer, which is returned in its place
+    (gs_backward_accumulate; multi-view gradient buckets, gs_view_parallel.GradBucket)."""
     x = _Inputs(background, means3D, colors, None, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
                 campos, need_opacity=False)
     P, dev = x.P, x.device
     f32 = dict(dtype=torch.float32, device=dev)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     M = x.M
+    sinks = sinks or {}
     need_col = want_all or x.colors is not None
     need_cov = want_all or x.cov3D is not None
     need_sh = want_all or x.sh is not None
     need_sr = want_all or (x.scales is not None and x.rotations is not None)
-    dmeans2D = torch.empty((P, 3), **f32)
-    dopacity = torch.empty((P, 1), **f32)
-    dmeans3D = torch.empty((P, 3), **f32)
-    dcolors = (torch.empty if x.colors is not None else torch.zeros)((P, 3), **f32) if need_col else None
-    dcov3D = (torch.empty if x.cov3D is not None else torch.zeros)((P, 6), **f32) if need_cov else None
-    dsh = (torch.empty if x.sh is not None else torch.zeros)((P, M, 3), **f32) if need_sh else None
     has_sr = x.scales is not None and x.rotations is not None and x.cov3D is None
-    dscales = (torch.empty if has_sr else torch.zeros)((P, 3), **f32) if need_sr else None
-    drot = (torch.empty if has_sr else torch.zeros)((P, 4), **f32) if need_sr else None
+    shapes = dict(means2D=(P, 3), colors=(P, 3), opacity=(P, 1), means3D=(P, 3), cov3D=(P, 6), sh=(P, M, 3),
+                  scales=(P, 3), rotations=(P, 4))
+    # is the gradient computed by the kernels (else zero-filled or absent)?
+    computed = dict(means2D=True, colors=True, opacity=True, means3D=True,
+                    cov3D=x.cov3D is not None or (want_all and has_sr), sh=x.sh is not None, scales=has_sr,
+                    rotations=has_sr)
+    needed = dict(means2D=True, colors=need_col, opacity=True, means3D=True, cov3D=need_cov, sh=need_sh,
+                  scales=need_sr, rotations=need_sr)
+    acc = 0
+    outs = {}
+    for n in GRAD_NAMES:
+        if n in sinks and computed[n]:
+            buf, accumulate = sinks[n]
+            if (buf.dtype != torch.float32 or buf.device != dev or not buf.is_contiguous()
+                    or buf.numel() != math.prod(shapes[n])):
+                raise RuntimeError(f"gradient sink for {n}: expected a contiguous float32 buffer of "
+                                   f"{math.prod(shapes[n])} elements on {dev}")
+            outs[n] = buf
+            acc |= GS_ACC[n] if accumulate else 0
+        elif needed[n]:
+            outs[n] = (torch.empty if computed[n] else torch.zeros)(shapes[n], **f32)
+        else:
+            outs[n] = None
+    ret = tuple(outs[n] for n in GRAD_NAMES)
     if P == 0:
-        return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
+        return ret
     dpix = _f32(dL_dout_color, "dL_dout_color", dev)
+    o = {n: (outs[n] if computed[n] else None) for n in GRAD_NAMES}
     with torch.cuda.device(dev):
         st = _stream(dev)
         grad_scratch = torch.empty((_lib.gs_grad_buffer_bytes(int(R)),), dtype=torch.uint8, device=dev)
         _native.check(
-            _lib.gs_backward(
+            _lib.gs_backward_accumulate(
                 P, int(degree), M, _ptr(x.bg), W, H, _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors), _ptr(x.opacity),
                 _ptr(x.scales), float(scale_modifier), _ptr(x.rotations), _ptr(x.cov3D), _ptr(x.view), _ptr(x.proj),
                 _ptr(x.campos), float(tan_fovx), float(tan_fovy), _ptr(radii), _ptr(geomBuffer), int(R),
-                _ptr(binningBuffer), _ptr(imageBuffer), _ptr(dpix), _ptr(grad_scratch), _ptr(dmeans2D),
-                _ptr(dcolors if x.colors is not None or need_col else None), _ptr(dopacity), _ptr(dmeans3D),
-                _ptr(dcov3D if x.cov3D is not None else None), _ptr(dsh if x.sh is not None else None),
-                _ptr(dscales if has_sr else None), _ptr(drot if has_sr else None), int(bool(debug)), st),
+                _ptr(binningBuffer), _ptr(imageBuffer), _ptr(dpix), _ptr(grad_scratch), _ptr(o["means2D"]),
+                _ptr(o["colors"]), _ptr(o["opacity"]), _ptr(o["means3D"]), _ptr(o["cov3D"]), _ptr(o["sh"]),
+                _ptr(o["scales"]), _ptr(o["rotations"]), acc, int(bool(debug)), st),
             "rasterize_gaussians_backward")
-    return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
+    return ret
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
@@ -193,8 +219,8 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     if P == 0:
         return present
     m = _f32(means3D, "means3D", dev)
-    v = _f32(viewmatrix, "viewmatrix", dev)
-    p = _f32(projmatrix, "projmatrix", dev)
+    v = _f32(viewmatrix, "viewmatrix", dev, host_ok=True)
+    p = _f32(projmatrix, "projmatrix", dev, host_ok=True)
     with torch.cuda.device(dev):
         _native.check(_lib.gs_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(dev)), "mark_visible")
     return present
@@ -226,3 +252,15 @@ def debug_export(P, W, H, num_rendered, geomBuffer, binningBuffer, imageBuffer, 
                 "debug_export")
     out["point_list"] = out["point_list"][:num_rendered]
     return out
+
+
+def debug_export_slots(W, H, num_rendered, binningBuffer, imageBuffer, device):
+    """(slots[num_rendered], tile_cut[tiles]) as int32 device tensors: the depth-ordered instance slot of
+    each entry of the tile-sorted list and each tile's backward record cut (valid after a backward)."""
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    slots = torch.zeros((max(int(num_rendered), 1),), dtype=torch.int32, device=device)
+    cuts = torch.zeros((gx * gy,), dtype=torch.int32, device=device)
+    with torch.cuda.device(device):
+        _native.check(_lib.gs_debug_export_slots(W, H, int(num_rendered), _ptr(binningBuffer), _ptr(imageBuffer),
+                                                 _ptr(slots), _ptr(cuts), _stream(device)), "debug_export_slots")
+    return slots[:int(num_rendered)], cuts

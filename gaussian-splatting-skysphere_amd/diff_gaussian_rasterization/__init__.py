@@ -21,6 +21,7 @@ them, including `means2D`, whose .grad holds the NDC-space screen gradient read 
 """
 from __future__ import annotations
 
+import weakref
 from typing import NamedTuple
 
 import torch
@@ -28,7 +29,43 @@ import torch.nn as nn
 
 from . import _C
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "cpu_deep_copy_tuple"]
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "cpu_deep_copy_tuple",
+           "register_gradient_sink", "unregister_gradient_sink"]
+
+# ------------------------------------------------------------------------------------------
+# Gradient sinks (an extension beyond the upstream API, used by gs_view_parallel.GradBucket).
+# A leaf tensor registered here gets its rasterizer gradient written -- or, once the step already
+# holds one, ADDED (gs_backward_accumulate) -- straight into the buffer its owner hands out
+# (normally the tensor's own .grad, a view into a flat all-reduce bucket), and the autograd
+# Function returns None for it.  The result equals autograd's `grad += g` with no extra pass over
+# the gradients and no pack/unpack copy.  owner.claim(tensor) -> (buffer, accumulate) or None
+# (None: the normal autograd path).
+# ------------------------------------------------------------------------------------------
+_SINKS: dict = {}  # id(tensor) -> (weakref to the tensor, owner)
+
+
+def register_gradient_sink(tensor: torch.Tensor, owner) -> None:
+    if not tensor.is_leaf:
+        raise ValueError("register_gradient_sink: only leaf tensors can own a gradient sink")
+    _SINKS[id(tensor)] = (weakref.ref(tensor), owner)
+
+
+def unregister_gradient_sink(tensor: torch.Tensor) -> None:
+    e = _SINKS.get(id(tensor))
+    if e is not None and e[0]() is tensor:
+        del _SINKS[id(tensor)]
+
+
+def _sink_owner(t):
+    if t is None or not isinstance(t, torch.Tensor) or not t.requires_grad:
+        return None
+    e = _SINKS.get(id(t))
+    return e[1] if e is not None and e[0]() is t else None
+
+
+# autograd input index -> gradient name (_C.GRAD_NAMES)
+_SINK_INPUTS = ((0, "means3D"), (1, "means2D"), (2, "sh"), (3, "colors"), (4, "opacity"), (5, "scales"),
+                (6, "rotations"), (7, "cov3D"))
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -90,6 +127,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii)
+        inputs = (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
+        ctx.sinks = [(k, name, inputs[k], _sink_owner(inputs[k])) for k, name in _SINK_INPUTS
+                     if _sink_owner(inputs[k]) is not None] if _SINKS else []
         return color, radii
 
     @staticmethod
@@ -104,13 +144,24 @@ class _RasterizeGaussians(torch.autograd.Function):
                 view, proj, s.tanfovx, s.tanfovy, grad_out_color.contiguous(), sh, s.sh_degree,
                 s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.debug)
 
+        sinks, sunk = {}, set()
+        for k, name, t, owner in ctx.sinks:
+            if ctx.needs_input_grad[k]:
+                claim = owner.claim(t)
+                if claim is not None:
+                    sinks[name] = claim
+                    sunk.add(k)
+
         def _bwd(*a):
-            return _C.backward_impl(*a, want_all=False)
+            return _C.backward_impl(*a, want_all=False, sinks=sinks)
 
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
          grad_rotations) = _run_with_snapshot(_bwd, args, s.debug, "snapshot_bw.dump", "backward")
-        return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
-                grad_rotations, grad_cov3Ds_precomp, None)
+        grads = [grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
+                 grad_rotations, grad_cov3Ds_precomp, None]
+        for k in sunk:  # already in the sink's buffer (the tensor's .grad)
+            grads[k] = None
+        return tuple(grads)
 
 
 class GaussianRasterizer(nn.Module):

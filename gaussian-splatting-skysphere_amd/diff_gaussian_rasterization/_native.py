@@ -47,6 +47,12 @@ SIGNATURES = {
          _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
          _c_i, _c_p],
     ),
+    "gs_backward_accumulate": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+         ctypes.c_uint, _c_i, _c_p],
+    ),
     "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),
     "gs_knn_mean_dist2": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p]),
@@ -67,6 +73,8 @@ SIGNATURES = {
         _c_i,
         [_c_i, _c_i, _c_i, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
     ),
+    "gs_debug_export_slots": (_c_i, [_c_i, _c_i, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "gs_debug_set_scan_spin_limit": (ctypes.c_uint, [ctypes.c_uint]),
     "gs_profile_enable": (None, [_c_i]),
     "gs_profile_collect": (_c_i, []),
     "gs_profile_reset": (None, []),

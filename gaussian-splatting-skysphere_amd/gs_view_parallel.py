@@ -27,53 +27,112 @@ def shard_views(num_views: int, rank: int, world: int) -> List[int]:
 
 
 class GradBucket:
-    """One flat fp32 buffer holding the gradients of `params` for a single all-reduce."""
+    """One flat fp32 buffer that IS the gradient storage of `params`: every `p.grad` is a view
+    into it, so the all-reduce runs over the .grad tensors themselves (no pack / unpack copy).
 
-    def __init__(self, params: Sequence[torch.Tensor]):
+    The rasterizer writes its gradients straight into those views through the gradient sink of
+    diff_gaussian_rasterization (gs_backward_accumulate): the first view of a step overwrites,
+    later views add in the same kernel, exactly as autograd's `grad += g` would, with no extra
+    pass.  Other autograd producers accumulate into the views as usual.
+
+    lazy_zero=True (the rasterizer is the only gradient producer, as in the reference loop where
+    the loss reaches the parameters only through render(); bench.py): zero_grad() writes nothing,
+    the step's first rasterizer write overwrites, and views no backward wrote are zeroed before
+    the all-reduce.  An in-place write by any other op into a not-yet-written view raises (it
+    would have added to the previous step's values).  lazy_zero=False: zero_grad() zero-fills
+    the bucket (one memset) and every write accumulates.
+    """
+
+    def __init__(self, params: Sequence[torch.Tensor], lazy_zero: bool = False):
+        from diff_gaussian_rasterization import register_gradient_sink
+
         self.params = list(params)
+        self.lazy_zero = lazy_zero
         self.numel = sum(p.numel() for p in self.params)
         dev = self.params[0].device if self.params else torch.device("cpu")
-        self.flat = torch.empty((self.numel,), dtype=torch.float32, device=dev)
-
-    def _resize_if_needed(self):
-        n = sum(p.numel() for p in self.params)
-        if n != self.numel:  # densification changed P
-            self.numel = n
-            self.flat = torch.empty((n,), dtype=torch.float32, device=self.flat.device)
-
-    def pack(self) -> torch.Tensor:
-        self._resize_if_needed()
-        grads = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in self.params]
-        torch.cat(grads, out=self.flat)
-        return self.flat
-
-    def unpack(self):
+        self.flat = torch.zeros((self.numel,), dtype=torch.float32, device=dev)
+        self.views = {}
         off = 0
         for p in self.params:
-            n = p.numel()
-            g = self.flat[off:off + n].view_as(p)
-            if p.grad is None:
-                p.grad = g.clone()
-            else:
-                p.grad.copy_(g)
-            off += n
+            if p.dtype != torch.float32:
+                raise TypeError("GradBucket: float32 parameters only")
+            v = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+            p.grad = v
+            self.views[id(p)] = v
+            register_gradient_sink(p, self)
+        self._fresh = {}  # id(p) -> _version of the view at zero_grad (lazy mode: not written yet)
+        self.zero_grad()
 
-    def allreduce(self, group=None, average: bool = False, unpack: bool = True):
-        """Sum (or mean) the gradients across the process group in one collective.  With
-        unpack=False the reduced gradients stay in `self.flat` (for an optimizer that steps on the
-        flat buffer) and the per-parameter .grad tensors are left as they were."""
-        flat = self.pack()
+    def close(self):
+        from diff_gaussian_rasterization import unregister_gradient_sink
+
+        for p in self.params:
+            unregister_gradient_sink(p)
+
+    def zero_grad(self):
+        if self.lazy_zero:
+            self._fresh = {id(p): self.views[id(p)]._version for p in self.params}
+        else:
+            self.flat.zero_()
+            self._fresh = {}
+
+    def claim(self, p):
+        """Gradient sink protocol: (buffer, accumulate) for the rasterizer backward."""
+        v = self.views.get(id(p))
+        if v is None or p.grad is not v:
+            return None  # .grad was replaced by the user: plain autograd
+        ver = self._fresh.pop(id(p), None)
+        if ver is None:
+            return v, True
+        if v._version != ver:
+            raise RuntimeError("GradBucket(lazy_zero=True): another op accumulated into a gradient view before the "
+                               "rasterizer's first write of the step; use lazy_zero=False")
+        return v, False
+
+    def finalize(self):
+        """Zero the views no backward wrote this step (lazy mode); then the bucket holds the step's
+        gradient sums."""
+        for p in self.params:
+            ver = self._fresh.pop(id(p), None)
+            if ver is not None:
+                v = self.views[id(p)]
+                if v._version != ver:
+                    raise RuntimeError("GradBucket(lazy_zero=True): a gradient view was accumulated into without "
+                                       "a rasterizer write in the step")
+                v.zero_()
+        return self.flat
+
+    def allreduce(self, group=None, average: bool = False, async_op: bool = False):
+        """Sum (or mean) the gradients across the process group in ONE collective over the flat
+        bucket; the .grad views hold the result afterwards."""
+        flat = self.finalize()
+        work = None
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+            work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
             if average:
+                if async_op:
+                    work.wait()
+                    work = None
                 flat.div_(dist.get_world_size(group))
-        if unpack:
-            self.unpack()
-        return flat
+        return work if async_op else flat
 
 
 def allreduce_grads(params: Iterable[torch.Tensor], group=None, average: bool = False):
-    GradBucket(list(params)).allreduce(group=group, average=average)
+    """One-off all-reduce of the .grad of `params` through a flat bucket (copies in and out; a
+    training loop keeps a GradBucket instead, whose views ARE the gradients)."""
+    params = [p for p in params]
+    grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+        if average:
+            flat.div_(dist.get_world_size(group))
+    off = 0
+    for p in params:
+        n = p.numel()
+        p.grad = flat[off:off + n].view_as(p).clone()
+        off += n
 
 
 def reduce_densify_stats(xyz_gradient_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,

@@ -13,6 +13,10 @@
  *        callback into the host language is needed.  gs_rasterize_forward() is the one-call
  *        variant with the upstream-style allocator callback.)
  *   gs_backward                                <-  _C.rasterize_gaussians_backward(...)
+ *   gs_backward_accumulate                     <-  same, adding into caller gradient buffers
+ *                                                  (multi-view gradient accumulation; the
+ *                                                  reference's `param.grad += g` of autograd,
+ *                                                  train.py:93, fused into the last kernel)
  *   gs_mark_visible                            <-  _C.mark_visible(...)
  *   gs_knn_mean_dist2                          <-  simple_knn._C.distCUDA2(points)
  *                                                  (/root/reference/scene/gaussian_model.py:20,134)
@@ -50,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 1
+#define GSRAST_ABI_VERSION 2
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -111,6 +115,30 @@ int gs_backward(int P, int D, int M, const float* background, int image_width, i
                 void* grad_buffer, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
                 float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
                 int debug, void* stream);
+
+/* ---- backward, accumulating ----
+ * Same arguments and outputs as gs_backward; bit k of `accumulate` (GS_ACC_*) makes output k
+ * ADDED to the buffer's current contents (fp32 `old + new`, as autograd's in-place `grad += g`)
+ * instead of overwriting it.  Used to sum several views' gradients into one flat gradient
+ * bucket with no extra pass over it (view-parallel training). */
+#define GS_ACC_MEANS2D 1u
+#define GS_ACC_COLORS 2u
+#define GS_ACC_OPACITY 4u
+#define GS_ACC_MEANS3D 8u
+#define GS_ACC_COV3D 16u
+#define GS_ACC_SH 32u
+#define GS_ACC_SCALES 64u
+#define GS_ACC_ROTATIONS 128u
+int gs_backward_accumulate(int P, int D, int M, const float* background, int image_width, int image_height,
+                           const float* means3D, const float* shs, const float* colors_precomp,
+                           const float* opacities, const float* scales, float scale_modifier,
+                           const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                           const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                           const int* radii, const void* geom_buffer, long long num_rendered,
+                           const void* binning_buffer, const void* image_buffer, const float* dL_dout_color,
+                           void* grad_buffer, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                           float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                           float* dL_drotations, unsigned accumulate, int debug, void* stream);
 
 /* ---- mark_visible: present[P] (uint8 0/1), near-plane test ---- */
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
@@ -215,6 +243,19 @@ int gs_debug_export(int P, int image_width, int image_height, long long num_rend
                     const void* binning_buffer, const void* image_buffer, uint32_t* point_list,
                     uint32_t* ranges, float* xy, float* conic_opacity, float* rgb, float* depth,
                     uint32_t* tiles_touched, float* final_T, uint32_t* n_contrib, void* stream);
+
+/* ---- test hook: spin limit of the offsets scan's look-back waits (process-wide) ----
+ * 0 makes every waiting workgroup time out at once: the forward must then fail with
+ * "look-back wait timed out" (gs_forward_render).  Returns the previous limit (default 1 << 22). */
+unsigned gs_debug_set_scan_spin_limit(unsigned limit);
+
+/* ---- debug export of the raw tile-sorted instance slots (tests) ----
+ * slots[num_rendered]: the depth-ordered instance slot of every entry of the tile-sorted list
+ * (the backward writes entry k's gradient record at slots[k]); tile_cut[tiles]: 1 + the slot
+ * of the last instance each tile's backward walk reaches (valid after a backward).  Within a
+ * tile the slots must be strictly increasing (the record cut relies on it). */
+int gs_debug_export_slots(int image_width, int image_height, long long num_rendered, const void* binning_buffer,
+                          const void* image_buffer, uint32_t* slots, uint32_t* tile_cut, void* stream);
 
 /* ---- per-kernel timing with HIP events on the launch stream (bench / profiling) ----
  * While enabled every launch is bracketed by a hipEvent pair.  gs_profile_collect() waits for the

@@ -12,6 +12,12 @@ for p in (ROOT, PKG, os.path.join(ROOT, "tests")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); parity tests through the C ABI")
+    config.addinivalue_line("markers", "spawn_first: starts child processes on the GPU; runs before any other test, "
+                                       "while this process has not touched the GPU")
+
+
+def pytest_collection_modifyitems(config, items):
+    items.sort(key=lambda it: 0 if it.get_closest_marker("spawn_first") else 1)  # stable: keeps the rest in order
 
 
 @pytest.fixture(scope="session")

@@ -1,0 +1,316 @@
+"""GPU tests of the multi-view / view-parallel path (BASELINE config C4) and of the
+boundary details the per-view parity tests do not reach:
+
+  - gradient buckets: the rasterizer writing / adding into the .grad views of a flat bucket
+    (gs_backward_accumulate) equals autograd's per-view gradients summed with `+=`, bit for bit;
+  - C4 at full size: 1M Gaussians in a ball seen from the 8 ring cameras, every view through
+    GaussianRasterizer, one view against the oracle;
+  - two ranks (gloo, both on cuda:0) each rendering its share of the 8 C4 views, one all-reduce of
+    the bucket, against the single-process sum of all 8 views (test_two_rank_* runs first: its
+    children start before this process touches the GPU);
+  - the raw upstream backward tuple (dL_dcov3D for scale / rotation inputs), the record-cut
+    invariant of the backward (slots strictly increasing within a tile), and the reporting of a
+    timed-out look-back wait in the offsets scan.
+"""
+import math
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import gs_scenes
+from test_gpu_parity import RTOL, _check_backward, _check_forward_exact, _gpu_run, _oracle_scene, _tol_check
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _lib():
+    from diff_gaussian_rasterization import _native
+
+    return _native.load()
+
+
+@pytest.fixture
+def exact_mode():
+    prev = _lib().gs_set_exact_exp(1)
+    yield
+    _lib().gs_set_exact_exp(prev)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.spawn_first
+def test_two_rank_view_parallel_matches_single_process_sum(tmp_path):
+    """C4 view parallelism end to end on one GPU: torchrun starts 2 ranks (gloo; RCCL needs one GPU
+    per rank), each renders views v = rank (mod 2) of the 8 ring cameras through the HIP
+    rasterizer into its GradBucket, one all-reduce sums the buckets, and rank 0 compares the
+    result with the 8 views rendered and summed in one process (tolerance 1e-5 |ref| + 1e-5 max:
+    the two sums associate differently)."""
+    out = tmp_path / "vp_result.txt"
+    env = dict(os.environ, GS_VP_OUT=str(out), HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "vp_gpu_worker.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, f"workers failed ({r.returncode}):\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    res = out.read_text()
+    print(res)
+    assert res.startswith("OK"), res
+
+
+def _leaves(d):
+    return [d.means3D.clone().requires_grad_(True), d.shs.clone().requires_grad_(True),
+            d.opacities.clone().requires_grad_(True), d.scales.clone().requires_grad_(True),
+            d.rotations.clone().requires_grad_(True)]
+
+
+def _render(rast, p, means2D):
+    img, radii = rast(means3D=p[0], means2D=means2D, opacities=p[2], shs=p[1], scales=p[3], rotations=p[4])
+    return img, radii
+
+
+@pytest.mark.parametrize("lazy", [True, False], ids=["lazy_zero", "zero_filled"])
+def test_bucket_accumulation_equals_autograd_sum(device, lazy):
+    import gs_view_parallel as vp
+    from diff_gaussian_rasterization import GaussianRasterizer
+
+    W, H = 320, 240
+    cams = gs_scenes.circle_cameras(3, 6.0, W, H)
+    d = gs_scenes.random_gaussians(20_000, 3, seed=5, ball_radius=2.0).to(device)
+    rasts = [GaussianRasterizer(gs_scenes.raster_settings_for(c, 3, device=device)) for c in cams]
+    dpix = [gs_scenes.dl_dimage(H, W, seed=40 + v).to(device) for v in range(3)]
+    # reference: plain autograd, one fresh gradient per view, summed with += in view order
+    ref = None
+    for r, dp in zip(rasts, dpix):
+        p = _leaves(d)
+        m2 = torch.zeros_like(p[0], requires_grad=True)
+        img, _ = _render(r, p, m2)
+        img.backward(dp)
+        g = [t.grad for t in p]
+        if ref is None:
+            ref = [x.clone() for x in g]
+        else:
+            for a, b in zip(ref, g):
+                a += b
+    p = _leaves(d)
+    b = vp.GradBucket(p, lazy_zero=lazy)
+    calls = []
+    orig = b.claim
+    b.claim = lambda t: calls.append(1) or orig(t)  # noqa: E731
+    for step in range(2):  # the second step reuses the bucket (stale values must not leak)
+        b.zero_grad()
+        for r, dp in zip(rasts, dpix):
+            m2 = torch.zeros_like(p[0], requires_grad=True)
+            img, _ = _render(r, p, m2)
+            img.backward(dp)
+        b.finalize()
+        torch.cuda.synchronize()
+        for k, (t, x) in enumerate(zip(p, ref)):
+            assert t.grad.data_ptr() == b.views[id(t)].data_ptr()
+            assert torch.equal(t.grad, x), (step, k, float((t.grad - x).abs().max()))
+    assert len(calls) == 2 * 3 * 5  # every view's backward wrote through the sink
+    b.close()
+
+
+def test_raw_backward_returns_every_upstream_gradient(oracle, device, exact_mode):
+    """_C.rasterize_gaussians_backward returns upstream's 8-tuple: dL_dcov3D is filled for
+    scale / rotation inputs too (the covariance gradient the scale / rotation chain starts from),
+    dL_dcolors for SH inputs (the per-Gaussian colour gradient); all against the oracle."""
+    from diff_gaussian_rasterization import _C
+
+    W, H = 160, 120
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(3000, 2, cam=cam, seed=17)
+    bg = np.array([0.1, 0.0, 0.2], np.float32)
+    s = gs_scenes.raster_settings_for(cam, 2, bg=torch.tensor(bg, device=device), device=device)
+    dsc = sc.to(device)
+    e = torch.Tensor([])
+    num, color, radii, geom, binb, imgb = _C.rasterize_gaussians(
+        s.bg, dsc.means3D, e, dsc.opacities, dsc.scales, dsc.rotations, 1.0, e, s.viewmatrix, s.projmatrix,
+        s.tanfovx, s.tanfovy, H, W, dsc.shs, 2, s.campos, False, False)
+    dpix = gs_scenes.dl_dimage(H, W, seed=18)
+    out = _C.rasterize_gaussians_backward(s.bg, dsc.means3D, radii, e, dsc.scales, dsc.rotations, 1.0, e,
+                                          s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, dpix.to(device),
+                                          dsc.shs, 2, s.campos, geom, num, binb, imgb, False)
+    assert len(out) == 8
+    gr = oracle.backward(_oracle_scene(oracle, cam, sc, bg), dpix.numpy())
+    for t, k in zip(out, ("dmeans2D", "dcolors", "dopacity", "dmeans3D", "dcov3D", "dsh", "dscales",
+                          "drotations")):
+        ref = gr[k].reshape(t.shape)
+        assert np.abs(ref).max() > 0, k
+        _tol_check(t.cpu().numpy(), ref, k)
+
+
+def _occluded_scene():
+    """Two layers of small opaque splats tile the left half of the image (every pixel there
+    saturates, T < 1e-4, before depth 2) and one large splat at depth 6 spans the whole width: its
+    instances in the left tiles lie past every pixel's last contributor (no backward record:
+    cut), in the right tiles they are walked (kept).  Plus 2000 random splats."""
+    W, H = 256, 128
+    cam = gs_scenes.identity_camera(W, H)
+    rnd = gs_scenes.random_gaussians(2000, 1, cam=cam, seed=50)
+    fx = W / (2.0 * math.tan(cam.FoVx / 2))
+    fy = H / (2.0 * math.tan(cam.FoVy / 2))
+    layers = []
+    for z in (1.5, 1.7):
+        px, py = np.meshgrid(np.arange(0.0, 128.0, 2.0), np.arange(-2.0, 130.0, 2.0))
+        n = px.size
+        m = torch.tensor(np.stack([(px.ravel() - W / 2) / fx * z, (py.ravel() - H / 2) / fy * z,
+                                   np.full(n, z)], 1), dtype=torch.float32)
+        lay = gs_scenes.random_gaussians(n, 1, cam=cam, seed=int(z * 10))
+        lay.means3D = m
+        lay.scales = torch.full((n, 3), 3.0 * z / fx)
+        lay.rotations = torch.tensor([[1.0, 0.0, 0.0, 0.0]]).repeat(n, 1)
+        lay.opacities = torch.full((n, 1), 0.999)
+        layers.append(lay)
+    back = gs_scenes.random_gaussians(1, 1, cam=cam, seed=52)
+    back.means3D[0] = torch.tensor([0.0, 0.0, 6.0])
+    back.scales[0] = torch.tensor([60.0 * 6.0 / fx, 30.0 * 6.0 / fy, 0.05])
+    back.rotations[0] = torch.tensor([1.0, 0.0, 0.0, 0.0])
+    back.opacities[0] = 0.6
+    return cam, gs_scenes.concat_scenes(rnd, *layers, back)
+
+
+def test_record_cut_invariant_and_partly_cut_gaussian(oracle, device, exact_mode):
+    """k_sum_records keeps a tile's record of slot s iff s < tile_cut (1 + the slot of the last
+    instance the tile's walk reaches): that needs the slots strictly increasing within every
+    tile's list.  Checked directly on the exported slots, plus a Gaussian that is cut in some
+    tiles and kept in others, against the oracle."""
+    from diff_gaussian_rasterization import _C
+
+    cam, sc = _occluded_scene()
+    W, H = cam.image_width, cam.image_height
+    bg = np.zeros(3, np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg)
+    ofw = oracle.forward(osc, intermediates=True)
+    ofw["bg"] = bg
+    _check_forward_exact(ofw, cam, sc, device)
+    dpix = gs_scenes.dl_dimage(H, W, seed=53).numpy()
+    img, _, leaves = _gpu_run(cam, sc, device, bg, dpix)
+    _check_backward(oracle.backward(osc, dpix), leaves)
+    # slots / cuts of a forward + backward through the raw entry points
+    s = gs_scenes.raster_settings_for(cam, 1, device=device)
+    d = sc.to(device)
+    e = torch.Tensor([])
+    num, color, radii, geom, binb, imgb = _C.rasterize_gaussians(
+        s.bg, d.means3D, e, d.opacities, d.scales, d.rotations, 1.0, e, s.viewmatrix, s.projmatrix, s.tanfovx,
+        s.tanfovy, H, W, d.shs, 1, s.campos, False, False)
+    _C.rasterize_gaussians_backward(s.bg, d.means3D, radii, e, d.scales, d.rotations, 1.0, e, s.viewmatrix,
+                                    s.projmatrix, s.tanfovx, s.tanfovy, torch.tensor(dpix, device=device), d.shs, 1,
+                                    s.campos, geom, num, binb, imgb, False)
+    slots, cuts = _C.debug_export_slots(W, H, num, binb, imgb, device)
+    ex = _C.debug_export(sc.P, W, H, num, geom, binb, imgb, device)
+    rng = ex["ranges"].long().cpu().numpy()
+    sl = slots.long().cpu().numpy()
+    cuts = cuts.long().cpu().numpy()
+    lst = ex["point_list"].long().cpu().numpy()
+    back = sc.P - 1
+    cut_tiles = kept_tiles = 0
+    for t, (a, b) in enumerate(rng):
+        if b <= a:
+            continue
+        assert (np.diff(sl[a:b]) > 0).all(), f"tile {t}: slots not strictly increasing"
+        hit = np.nonzero(lst[a:b] == back)[0]
+        if hit.size:
+            if sl[a + hit[0]] < cuts[t]:
+                kept_tiles += 1
+            else:
+                cut_tiles += 1
+    assert cut_tiles > 0 and kept_tiles > 0, (cut_tiles, kept_tiles)
+
+
+def test_lookback_timeout_is_reported(device):
+    """A look-back wait of the offsets scan that runs out leaves invalid instance offsets: the
+    forward must fail loudly in every mode (not only debug).  The test hook makes every waiting
+    workgroup time out at once."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+
+    lib = _lib()
+    cam = gs_scenes.identity_camera(320, 240)
+    d = gs_scenes.random_gaussians(200_000, 0, cam=cam, seed=60).to(device)
+    rast = GaussianRasterizer(gs_scenes.raster_settings_for(cam, 0, device=device))
+    prev = lib.gs_debug_set_scan_spin_limit(0)
+    try:
+        with pytest.raises(RuntimeError, match="look-back wait timed out"):
+            rast(means3D=d.means3D, means2D=torch.zeros_like(d.means3D), opacities=d.opacities, shs=d.shs,
+                 scales=d.scales, rotations=d.rotations)
+            torch.cuda.synchronize()
+    finally:
+        lib.gs_debug_set_scan_spin_limit(prev)
+    img, _ = rast(means3D=d.means3D, means2D=torch.zeros_like(d.means3D), opacities=d.opacities, shs=d.shs,
+                  scales=d.scales, rotations=d.rotations)
+    assert torch.isfinite(img).all()
+
+
+def _c4_properties(ex, num, color, W, H):
+    lst = ex["point_list"].long()
+    rng = ex["ranges"].long()
+    assert num == int(ex["tiles_touched"].sum())
+    nonempty = rng[:, 1] > rng[:, 0]
+    starts, ends = rng[nonempty, 0], rng[nonempty, 1]
+    assert starts[0] == 0 and ends[-1] == num and torch.all(starts[1:] == ends[:-1])
+    depth_bits = ex["depth"].view(torch.int32).long()
+    tile_of = torch.repeat_interleave(torch.arange(rng.shape[0], device=lst.device)[nonempty], ends - starts)
+    same = tile_of[1:] == tile_of[:-1]
+    d0, d1 = depth_bits[lst[:-1]], depth_bits[lst[1:]]
+    assert torch.all(((d1 > d0) | ((d1 == d0) & (lst[1:] > lst[:-1])))[same])
+    assert int(ex["n_contrib"].long().max()) <= int((ends - starts).max())
+    assert torch.isfinite(color).all() and (color >= 0).all()
+
+
+def test_c4_ring_views_full_size(oracle, device):
+    """BASELINE C4: 1M Gaussians SH3 in a ball of radius 2, the 8 ring cameras at radius 6,
+    1920x1080.  Every view goes through GaussianRasterizer forward + backward (size-independent
+    properties: list ordered by (tile, depth, index), ranges partition the list, finite image and
+    gradients, bit-identical rerun of the forward); view 3 is compared with the oracle at full
+    size in the bit-exact mode (forward bit-exact, gradients at 1e-5)."""
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+
+    W, H = 1920, 1080
+    cams = gs_scenes.circle_cameras(8, 6.0, W, H)
+    sc = gs_scenes.random_gaussians(1_000_000, 3, seed=0, ball_radius=2.0)
+    d = sc.to(device)
+    e = torch.Tensor([])
+    dpix = gs_scenes.dl_dimage(H, W, seed=1).to(device)
+    for v, cam in enumerate(cams):
+        s = gs_scenes.raster_settings_for(cam, 3, device=device)
+        args = (s.bg, d.means3D, e, d.opacities, d.scales, d.rotations, 1.0, e, s.viewmatrix, s.projmatrix,
+                s.tanfovx, s.tanfovy, H, W, d.shs, 3, s.campos, False, False)
+        num, color, radii, geom, binb, imgb = _C.rasterize_gaussians(*args)
+        num2, color2, radii2, *_ = _C.rasterize_gaussians(*args)
+        assert num == num2 and torch.equal(color, color2) and torch.equal(radii, radii2)
+        assert int((radii > 0).sum()) > 500_000, f"view {v}: only {int((radii > 0).sum())} visible"
+        _c4_properties(_C.debug_export(sc.P, W, H, num, geom, binb, imgb, device), num, color, W, H)
+        p = _leaves(d)
+        m2 = torch.zeros_like(p[0], requires_grad=True)
+        img, _ = _render(GaussianRasterizer(s), p, m2)
+        assert torch.equal(img, color)
+        img.backward(dpix)
+        for t in p + [m2]:
+            assert torch.isfinite(t.grad).all()
+        assert float(p[1].grad.abs().max()) > 0
+        del geom, binb, imgb, p, m2, img
+    prev = _lib().gs_set_exact_exp(1)
+    try:
+        cam = cams[3]
+        bg = np.zeros(3, np.float32)
+        osc = _oracle_scene(oracle, cam, sc, bg)
+        ofw = oracle.forward(osc, intermediates=True)
+        ofw["bg"] = bg
+        _check_forward_exact(ofw, cam, sc, device)
+        dp = dpix.cpu().numpy()
+        _, _, leaves = _gpu_run(cam, sc, device, bg, dp)
+        _check_backward(oracle.backward(osc, dp), leaves)
+    finally:
+        _lib().gs_set_exact_exp(prev)

@@ -176,7 +176,10 @@ def test_forward_bitexact_and_backward_vs_oracle(oracle, device, name, P, deg, W
 
 def _check_forward_fast(ofw, cam, sc, device, bg):
     """Fast-mode forward: bit-exact up to the render loop, tolerance in it (module docstring).
-    Returns the Gaussian ids to exclude from gradient checks."""
+    Pixels the oracle flags as near an alpha / T decision get the decision-flip bound instead:
+    one flipped entry moves a pixel's colour by at most 0.01 (T stop: alpha T c with T (1 - alpha)
+    ~ 1e-4, alpha <= 0.99) or alpha T c ~ c / 255 (alpha test), plus the background term.
+    Returns (colour, Gaussians listed in a flagged pixel's tile, near mask)."""
     from diff_gaussian_rasterization import _C
 
     s = gs_scenes.raster_settings_for(cam, sc.sh_degree, bg=torch.tensor(bg, device=device), device=device)
@@ -200,7 +203,14 @@ def _check_forward_fast(ofw, cam, sc, device, bg):
     keep = ~near
     np.testing.assert_array_equal(ex["n_contrib"].cpu().numpy().astype(np.uint32)[keep], ofw["n_contrib"][keep])
     _tol_check(ex["final_T"].cpu().numpy()[keep], ofw["final_T"][keep], "final_T")
-    _tol_check(color.cpu().numpy()[:, keep], ofw["color"][:, keep], "color")
+    col = color.cpu().numpy()
+    _tol_check(col[:, keep], ofw["color"][:, keep], "color")
+    if near.any():  # decision-flip bound at the flagged pixels
+        cmax = float(np.abs(ofw["rgb"][vis]).max(initial=0.0)) + float(np.abs(bg).max())
+        dT = np.abs(ex["final_T"].cpu().numpy()[near] - ofw["final_T"][near])
+        dC = np.abs(col[:, near] - ofw["color"][:, near])
+        assert dT.max() <= 0.01 + 1e-6, f"final_T at flagged pixels: max |d| = {dT.max():.3e}"
+        assert dC.max() <= 0.02 * cmax + 1e-6, f"colour at flagged pixels: max |d| = {dC.max():.3e} (cmax {cmax})"
     # Gaussians listed in a tile that holds a flagged pixel
     excl = np.zeros(sc.P, bool)
     gx = (W + 15) // 16
@@ -208,15 +218,59 @@ def _check_forward_fast(ofw, cam, sc, device, bg):
         t = (y // 16) * gx + x // 16
         a, b = ofw["ranges"][t]
         excl[ofw["point_list"][a:b]] = True
-    return color, excl
+    return color, excl, near
+
+
+_GRADS = (("means2D", "dmeans2D"), ("opacities", "dopacity"), ("means3D", "dmeans3D"), ("shs", "dsh"),
+          ("scales", "dscales"), ("rotations", "drotations"))
 
 
 def _check_backward_masked(gr, leaves, excl, rtol=RTOL):
     keep = ~excl
     g = lambda k: leaves[k].grad.detach().cpu().numpy()[keep]  # noqa: E731
-    for k, o in (("means2D", "dmeans2D"), ("opacities", "dopacity"), ("means3D", "dmeans3D"), ("shs", "dsh"),
-                 ("scales", "dscales"), ("rotations", "drotations")):
+    for k, o in _GRADS:
         _tol_check(g(k), gr[o][keep], o, rtol, rtol)
+
+
+def _fast_mode_parity(oracle, device, cam, sc, bg, dpix_seed=1):
+    """Fast mode vs the oracle with no Gaussian left unchecked:
+      (1) dL/dimage zeroed at the flagged pixels, on both sides: every gradient of EVERY Gaussian
+          at the strict tolerance (the backward is per pixel, so this is exactly the gradient over
+          all unflagged pixels);
+      (2) the full dL/dimage: the Gaussians listed in no flagged pixel's tile at the strict
+          tolerance; the others within the strict tolerance plus twice the flagged pixels' own
+          contribution to them, measured on each side as full - masked (a decision flip changes
+          a flagged pixel's terms, never an unflagged one's).
+    Prints the flagged-pixel and bounded-Gaussian fractions."""
+    W, H = cam.image_width, cam.image_height
+    osc = _oracle_scene(oracle, cam, sc, bg)
+    ofw = oracle.forward(osc, intermediates=True, near=True)
+    color, excl, near = _check_forward_fast(ofw, cam, sc, device, bg)
+    dpix = gs_scenes.dl_dimage(H, W, seed=dpix_seed).numpy()
+    dpix_m = dpix * (~near)[None].astype(np.float32)
+    img, _, lm = _gpu_run(cam, sc, device, bg, dpix_m)
+    assert torch.equal(img, color)  # the autograd path renders the same image
+    gm = oracle.backward(osc, dpix_m)
+    gpu_m = {o: lm[k].grad.detach().cpu().numpy() for k, o in _GRADS}
+    for k, o in _GRADS:
+        _tol_check(gpu_m[o], gm[o], o + " (all Gaussians, unflagged pixels)")
+    del lm
+    _, _, lf = _gpu_run(cam, sc, device, bg, dpix)
+    gf = oracle.backward(osc, dpix)
+    _check_backward_masked(gf, lf, excl)
+    worst = 0.0
+    for k, o in _GRADS:
+        gpu_f = lf[k].grad.detach().cpu().numpy()
+        ref = gf[o].astype(np.float64)
+        scale = max(np.abs(ref).max(), 1e-30)
+        flag = np.abs(gf[o].astype(np.float64) - gm[o]) + np.abs(gpu_f.astype(np.float64) - gpu_m[o])
+        d = np.abs(gpu_f - ref)[excl]
+        tol = (RTOL * np.abs(ref) + RTOL * scale + 2.0 * flag)[excl]
+        assert (d <= tol).all(), f"{o}: flagged-tile Gaussians beyond the flip bound, max|d| {d.max():.3e}"
+        if d.size:
+            worst = max(worst, float(d.max() / scale))
+    print(f"\n[fast parity {W}x{H} P={sc.P}] flagged pixels {near.mean():.2e}, Gaussians in flagged tiles "
+          f"{excl.mean():.2e} (bounded), worst bounded |d|/max {worst:.2e}")
 
 
 FAST_CASES = [c for c in CASES if c[0] != "tiny"] + [("C3_crop_sh3_1080", 60_000, 3, 480, 1080, 0.0)]
@@ -226,15 +280,15 @@ FAST_CASES = [c for c in CASES if c[0] != "tiny"] + [("C3_crop_sh3_1080", 60_000
 def test_fast_mode_forward_and_backward_vs_oracle(oracle, device, fast_mode, name, P, deg, W, H, bgv):
     cam = gs_scenes.identity_camera(W, H)
     sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=0)
-    bg = np.full(3, bgv, np.float32)
-    osc = _oracle_scene(oracle, cam, sc, bg)
-    ofw = oracle.forward(osc, intermediates=True, near=True)
-    color, excl = _check_forward_fast(ofw, cam, sc, device, bg)
-    dpix = gs_scenes.dl_dimage(H, W, seed=1).numpy()
-    img, radii, leaves = _gpu_run(cam, sc, device, bg, dpix)
-    assert torch.equal(img, color)  # the autograd path renders the same image
-    assert excl.mean() < 0.05
-    _check_backward_masked(oracle.backward(osc, dpix), leaves, excl)
+    _fast_mode_parity(oracle, device, cam, sc, np.full(3, bgv, np.float32))
+
+
+def test_fast_mode_full_c3_vs_oracle(oracle, device, fast_mode):
+    """The benchmarked configuration itself: C3 = 1M Gaussians SH3 at 1920x1080 in the default
+    (fast) numerics mode, against the oracle at full size (no crop)."""
+    cam = gs_scenes.identity_camera(1920, 1080)
+    sc = gs_scenes.random_gaussians(1_000_000, 3, cam=cam, seed=0)
+    _fast_mode_parity(oracle, device, cam, sc, np.zeros(3, np.float32))
 
 
 def test_fast_mode_is_deterministic(device, fast_mode):

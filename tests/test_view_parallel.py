@@ -26,12 +26,15 @@ def _worker(rank, world, port, P, out_q):
         g = torch.Generator().manual_seed(rank)
         shapes = [(P, 3), (P, 1, 3), (P, 15, 3), (P, 1), (P, 3), (P, 4)]  # xyz f_dc f_rest opacity scaling rotation
         params = [torch.zeros(s, requires_grad=True) for s in shapes]
-        for p in params:
-            p.grad = torch.randn(p.shape, generator=g)
-        local = [p.grad.clone() for p in params]
         b = vp.GradBucket(params)
         assert b.numel == 59 * P
+        for p in params:  # the .grad tensors ARE views of the bucket
+            assert p.grad.data_ptr() >= b.flat.data_ptr()
+            p.grad.copy_(torch.randn(p.shape, generator=g))
+        local = [p.grad.clone() for p in params]
+        ptrs = [p.grad.data_ptr() for p in params]
         b.allreduce()
+        assert ptrs == [p.grad.data_ptr() for p in params]  # reduced in place, no unpack
         acc = torch.zeros(P, 1) + rank
         den = torch.ones(P, 1)
         mr = torch.full((P,), float(rank + 1))
@@ -77,3 +80,38 @@ def test_single_process_allreduce_is_identity():
     p.grad = torch.arange(15.0).reshape(5, 3)
     vp.allreduce_grads([p])
     assert torch.equal(p.grad, torch.arange(15.0).reshape(5, 3))
+
+
+def test_bucket_views_are_the_gradients_and_autograd_accumulates_into_them():
+    a = torch.zeros(4, 3, requires_grad=True)
+    c = torch.zeros(4, 1, requires_grad=True)
+    b = vp.GradBucket([a, c])
+    assert a.grad.data_ptr() == b.flat.data_ptr() and c.grad.data_ptr() == b.flat.data_ptr() + 12 * 4
+    ((a * 2).sum() + (c * 3).sum()).backward()
+    ((a * 1).sum()).backward()
+    assert torch.all(a.grad == 3) and torch.all(c.grad == 3)
+    assert torch.equal(b.flat[:12], torch.full((12,), 3.0))
+    b.zero_grad()
+    assert torch.all(b.flat == 0)
+
+
+def test_lazy_bucket_claim_protocol():
+    """lazy_zero: the first rasterizer claim of a step overwrites, later ones accumulate; views
+    nobody wrote are zeroed before the all-reduce; a foreign write into an unwritten view raises."""
+    a = torch.zeros(6, requires_grad=True)
+    c = torch.zeros(2, requires_grad=True)
+    b = vp.GradBucket([a, c], lazy_zero=True)
+    b.flat.fill_(7.0)  # stale values from an earlier step
+    b.zero_grad()
+    buf, acc = b.claim(a)
+    assert buf is a.grad and acc is False
+    assert b.claim(a)[1] is True
+    b.finalize()
+    assert torch.all(c.grad == 0) and torch.all(a.grad == 7.0)  # a: left to the (simulated) kernel
+    b.zero_grad()
+    c.grad.add_(1.0)  # someone else accumulates into a view the rasterizer has not written yet
+    with pytest.raises(RuntimeError, match="lazy_zero"):
+        b.claim(c)
+    a.grad = torch.zeros(6)  # replaced by the user: the sink steps aside
+    assert b.claim(a) is None
+    b.close()
