@@ -286,6 +286,7 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* _
   if (s >= P || s >= counters[CNT_V]) return;
   const uint32_t gid = sorted_gid[s];
   uint32_t off = offsets[s];
+  // (a timed-out offsets scan only under-estimates offsets: every write stays below I)
   int y0, y1;
   const SpanCtx sp = span_of(binrec, gid, y0, y1);
   for (int ty = y0; ty < y1; ty++) {
@@ -330,6 +331,20 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   const uint32_t V = counters[CNT_V];
   const uint32_t k0 = b * DUP_SLOTS;
   const uint32_t k1 = min(k0 + DUP_SLOTS, I);
+  if (counters[CNT_ERR] & 4u) {
+    // the offsets scan timed out (the host raises after this call): the owner table is not
+    // valid, so fill the block's slots with a safe placeholder -- tile 0, Gaussian
+    // sorted_gid[0] -- that keeps every later kernel in bounds instead of following it
+    const uint32_t g0 = sorted_gid[0];
+    for (uint32_t k = k0 + tid; k < k1; k += DUP_THREADS) {
+      tile_keys[k] = 0u;
+      presort_gid[k] = g0;
+    }
+    if (hist0) {
+      hist0[(size_t)tid * gridDim.x + b] = tid == 0 ? k1 - k0 : 0u;
+    }
+    return;
+  }
   const uint32_t s_lo = dup_first[b];
   const uint32_t s_hi = (k1 < I) ? dup_first[b + 1] : V - 1;
   const uint32_t nG = s_hi - s_lo + 1;
