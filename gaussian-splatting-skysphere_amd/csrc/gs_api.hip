@@ -135,9 +135,9 @@ static bool validate(int P, int D, int M, int W, int H, const float* means3D, co
 // ------------------------------------------------------------------------------------------
 // debug export kernel
 // ------------------------------------------------------------------------------------------
-__global__ void k_export_list(uint32_t I, const uint32_t* point_list, const uint32_t* presort_gid, uint32_t* out) {
+__global__ void k_export_list(uint32_t I, const uint32_t* point_list, const uint32_t* ids, uint32_t* out) {
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k < I) out[k] = presort_gid[point_list[k]];
+  if (k < I) out[k] = GS_SORT_GID ? ids[k] : ids[point_list[k]];
 }
 __global__ void k_export_splat(int P, const float4* splat, float* xy, float* co, float* rgb, float* depth) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -608,7 +608,7 @@ int gs_debug_export(int P, int W, int H, long long num_rendered, const void* geo
   img_layout(W, H, &img, (char*)image_buffer);
   if (point_list && num_rendered > 0)
     GS_LAUNCH("export_list", k_export_list, dim3((unsigned)((num_rendered + 255) / 256)), dim3(256), 0, st,
-              (uint32_t)num_rendered, bin.point_list, bin.presort_gid, point_list);
+              (uint32_t)num_rendered, bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, point_list);
   if (ranges) check_hip(hipMemcpyAsync(ranges, img.ranges, sizeof(uint2) * gx * gy, hipMemcpyDeviceToDevice, st), "copy");
   if (xy || conic_opacity || rgb || depth)
     GS_LAUNCH("export_splat", k_export_splat, dim3((P + 255) / 256), dim3(256), 0, st, P, geo.splat, xy, conic_opacity,

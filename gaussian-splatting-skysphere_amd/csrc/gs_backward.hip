@@ -69,6 +69,9 @@ constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x
 #ifndef GS_PBWD_REG
 #define GS_PBWD_REG 1  // 0: the LDS-staged SH rows variant (113 vs 109.5 us at C3)
 #endif
+#ifndef GS_BWD_PREFETCH
+#define GS_BWD_PREFETCH 1
+#endif
 #ifndef GS_BWD_HALFROW
 #define GS_BWD_HALFROW 1  // 0: row sums (4 DPP steps) with one writer lane per row
 #endif
@@ -89,7 +92,8 @@ static_assert(BWD_BATCH % 64 == 0, "batch must be whole waves");
 template <bool EXACT>
 __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ point_list,
-                                                            const uint32_t* __restrict__ presort_gid,
+                                                            // GS_SORT_GID: ids by list position, else by slot
+                                                            const uint32_t* __restrict__ point_gid,
                                                             const float4* __restrict__ splat,
                                                             const float* __restrict__ final_T,
                                                             const uint32_t* __restrict__ n_contrib,
@@ -219,9 +223,69 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
 #endif
   };
 
+#if GS_BWD_PREFETCH
+  // staging pipeline (wave 0 stages, one entry per lane): while batch k is walked, the splat
+  // records of batch k + 1, the ids of batch k + 2 and (ids by slot) the slots of batch k + 3
+  // are in flight; the walk issues no global loads, so they overlap it.  Batch k's entry of
+  // lane t sits at list position range.x + e0 - 64 k, e0 = n_eff - 1 - t.
+  static_assert(BWD_BATCH == 64, "prefetch: one staged entry per lane of wave 0");
+  const int64_t e0 = (int64_t)n_eff - 1 - tid;
+  const uint32_t* const plist = point_list + range.x;
+  uint32_t slot_c = 0, S1 = 0, G1 = 0, S2 = 0;
+  float4 pa, pb, pd;
+  if (tid < 64) {
+    if (e0 >= 0) {
+      slot_c = plist[e0];
+      const uint32_t g0 = GS_SORT_GID ? point_gid[range.x + e0] : point_gid[slot_c];
+      pa = splat[3 * g0], pb = splat[3 * g0 + 1], pd = splat[3 * g0 + 2];
+    }
+    if (e0 - 64 >= 0) {
+      S1 = plist[e0 - 64];
+      G1 = GS_SORT_GID ? point_gid[range.x + e0 - 64] : point_gid[S1];
+    }
+    if (!GS_SORT_GID && e0 - 128 >= 0) S2 = plist[e0 - 128];
+  }
+#endif
   for (uint32_t base = 0; base < n_eff; base += BWD_BATCH) {
     const uint32_t cnt = min((uint32_t)BWD_BATCH, n_eff - base);
-    __syncthreads();
+    lds_barrier();
+#if GS_BWD_PREFETCH
+    if (tid < 64) {
+      uint32_t hm = 0;
+      const int t = tid;
+      if ((uint32_t)t < cnt) {
+        const uint32_t slot = slot_c;
+        const float4 a = pa, b = pb, d = pd;
+        s_ent[t] = make_float4(a.x, a.y, b.z, b.w);
+        s_ent[BWD_BATCH + t] = fall_coefs(a.z, a.w, b.x, b.y);
+        s_ent[2 * BWD_BATCH + t] = make_float4(d.x, 0.0f, 0.0f, 0.0f);
+        s_cr[t] = make_float4(a.z, a.w, b.x, b.y);  // raw conic + opacity
+        s_slot[t] = slot;
+        hm = half_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
+      }
+      // issue the next batch's splat loads, the ids after it and (ids by slot) the slots after those
+      const int64_t e1 = e0 - (int64_t)(base + 64);
+      if (e1 >= 0) {
+        slot_c = S1;
+        pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
+      }
+      if (e1 - 64 >= 0) {
+        if (GS_SORT_GID) {
+          S1 = plist[e1 - 64];
+          G1 = point_gid[range.x + e1 - 64];
+        } else {
+          S1 = S2;
+          G1 = point_gid[S2];
+        }
+      }
+      if (!GS_SORT_GID && e1 - 128 >= 0) S2 = plist[e1 - 128];
+      const uint64_t b0 = __ballot(hm & 1u), b1 = __ballot(hm & 2u);
+      if (lane == 0) {
+        s_mask[0][0] = b0;
+        s_mask[0][1] = b1;
+      }
+    }
+#else
 #pragma unroll
     for (int h = 0; h < BWD_STAGE_ROUNDS; h++) {
       const int t = tid + BWD_THREADS * h;
@@ -230,7 +294,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
       if ((uint32_t)t < cnt) {
         const uint32_t e = n_eff - 1 - (base + t);
         const uint32_t slot = point_list[range.x + e];
-        const uint32_t gid = presort_gid[slot];
+        const uint32_t gid = GS_SORT_GID ? point_gid[range.x + e] : point_gid[slot];
         const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
         s_ent[t] = make_float4(a.x, a.y, b.z, b.w);
         s_ent[BWD_BATCH + t] = fall_coefs(a.z, a.w, b.x, b.y);
@@ -245,13 +309,14 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         s_mask[t >> 6][1] = b1;
       }
     }
+#endif
     {
       float4* z4 = reinterpret_cast<float4*>(&s_acc[wid][0][0]);
 #pragma unroll
       for (int k = 0; k < (ACC_STRIDE * BWD_BATCH / 4 + 63) / 64; k++)
         if (k * 64 + lane < ACC_STRIDE * BWD_BATCH / 4) z4[k * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll 1
     for (int g = 0; g < BWD_GROUPS; g++) {
       uint64_t m = uniform_u64(s_mask[g][wid]);
@@ -284,7 +349,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
       }
 #endif
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int h = 0; h < BWD_STAGE_ROUNDS; h++) {
       const int t = tid + BWD_THREADS * h;
@@ -347,7 +412,7 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __
     const uint32_t v = len_hist[g * ORDER_BUCKETS + lane];
     s_base[g][lane] = wave_incl_scan(v) - v;
   }
-  __syncthreads();
+  lds_barrier();
   // the j-th tile of group g (longest first) takes launch position 8 j + g
   if (t < tiles) order[ORDER_GROUPS * (s_base[t % ORDER_GROUPS][br >> 22] + (br & 0x3FFFFFu)) + t % ORDER_GROUPS] = t;
 }
@@ -361,11 +426,11 @@ void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& 
             img.tile_cut);
   if (exact_exp())
     GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,
-              bin.point_list, bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
+              bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
               dL_dpix, gradrec);
   else
     GS_LAUNCH("render_bwd", k_render_bwd<false>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,
-              bin.point_list, bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
+              bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
               dL_dpix, gradrec);
 }
 
@@ -760,7 +825,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
   float* row = s_sh + threadIdx.x * stride;
   if (DEG >= 0) {
     rows_to_lds(g.shs + (size_t)i0 * rowf, s_sh, nG, rowf, stride);
-    __syncthreads();
+    lds_barrier();
   }
   if (i < g.P) preprocess_bwd_one<DEG>(i, g, c, tiles, clamped, gsum, out, row);
   if (DEG >= 0) {
@@ -769,7 +834,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
         for (int k = 0; k < rowf; k++) out.dsh[(size_t)i * rowf + k] += row[k];
       return;
     }
-    __syncthreads();
+    lds_barrier();
     lds_to_rows(s_sh, out.dsh + (size_t)i0 * rowf, nG, rowf, stride);
   }
 }

@@ -15,6 +15,19 @@
 
 namespace gs {
 
+// Workgroup barrier that first drains this wave's LDS operations (s_waitcnt lgkmcnt(0)).
+// __syncthreads() is a workgroup-scope release fence + s_barrier, and the gfx950 compiler may
+// leave the release's lgkmcnt(0) wait out (its memory model takes LDS operations of all waves as
+// totally ordered).  Measured on MI355X: the backward's flush, reading the partner wave's LDS
+// accumulators right after the barrier, missed that wave's last ds_write about once per few
+// thousand tiles when two processes shared the GPU (C4 ring views: dcolor / dmean2D of 1-5
+// Gaussians differed run to run), and in single-process runs more rarely.  Every barrier that
+// orders LDS writes of one wave before reads of another goes through here.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------
 // launch tracing (gs_api.cpp): error capture after every launch, optional per-launch sync
 // (settings.debug) and optional HIP-event timing per kernel name (bench / profiling).

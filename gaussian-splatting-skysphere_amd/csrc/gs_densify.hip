@@ -71,7 +71,7 @@ __global__ __launch_bounds__(DENS_T) void k_dens_classify(int P, DensifyParams d
   const uint32_t nA = __popcll(ballot64(f & DF_KEEP_A)), nB = __popcll(ballot64(f & DF_KEEP_B)),
                  nS = __popcll(ballot64(f & DF_SPLIT)), nC = __popcll(ballot64(f & DF_KEEP_C));
   if (lane == 0) s_cnt[w][0] = nA, s_cnt[w][1] = nB, s_cnt[w][2] = nS, s_cnt[w][3] = nC;
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x < 4) {
     uint32_t t = 0;
     for (int q = 0; q < DENS_T / 64; q++) t += s_cnt[q][threadIdx.x];
@@ -90,13 +90,13 @@ __global__ __launch_bounds__(1024) void k_dens_scan(int blocks, uint32_t* __rest
   for (int b = b0; b < b1; b++)
     for (int q = 0; q < 4; q++) sum[q] += counts[(size_t)b * 4 + q];
   for (int q = 0; q < 4; q++) s_part[t][q] = sum[q];
-  __syncthreads();
+  lds_barrier();
   for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan over the 1024 partials
     uint32_t v[4];
     for (int q = 0; q < 4; q++) v[q] = t >= d ? s_part[t - d][q] : 0u;
-    __syncthreads();
+    lds_barrier();
     for (int q = 0; q < 4; q++) s_part[t][q] += v[q];
-    __syncthreads();
+    lds_barrier();
   }
   uint32_t run[4];
   for (int q = 0; q < 4; q++) run[q] = s_part[t][q] - sum[q];
@@ -122,7 +122,7 @@ __device__ __forceinline__ DensRanks dens_ranks(uint8_t f, const uint32_t* __res
                  bC = ballot64(f & DF_KEEP_C);
   if (lane == 0) s_cnt[w][0] = __popcll(bA), s_cnt[w][1] = __popcll(bB), s_cnt[w][2] = __popcll(bS),
                  s_cnt[w][3] = __popcll(bC);
-  __syncthreads();
+  lds_barrier();
   DensRanks r;
   r.a = bases[(size_t)blockIdx.x * 4 + 0] + __popcll(bA & lt);
   r.b = bases[(size_t)blockIdx.x * 4 + 1] + __popcll(bB & lt);

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c
     s_sum[threadIdx.x >> 6] = area;
     s_vis[threadIdx.x >> 6] = vis;
   }
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x == 0) {
     const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
     const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   const uint32_t nG = s_hi - s_lo + 1;
   for (uint32_t i = tid; i < DUP_SLOTS + DUP_SLOTS / 8; i += DUP_THREADS) s_own[i] = 0;
   if (tid == 0) s_nseg = 0;
-  __syncthreads();
+  lds_barrier();
   // row segments of the block's splats that meet [k0, k1): any segment numbering works, the
   // marks carry their slot so the scan below picks the segment that starts last at or before
   // each slot (deterministic output)
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
       pos += w;
     }
   }
-  __syncthreads();
+  lds_barrier();
   // inclusive max-scan of the marks over the block's slots (consecutive DUP_ITEMS per thread)
   uint32_t v[DUP_ITEMS];
   uint32_t run = 0;
@@ -394,11 +394,11 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   if (lane == 63) s_wmax[tid >> 6] = incl;
   uint32_t excl = (uint32_t)__shfl_up((int)incl, 1, 64);
   if (lane == 0) excl = 0;
-  __syncthreads();
+  lds_barrier();
   for (uint32_t w = 0; w < (tid >> 6); w++) excl = max(excl, s_wmax[w]);
 #pragma unroll
   for (int r = 0; r < DUP_ITEMS; r++) s_own[own_idx(tid * DUP_ITEMS + r)] = max(v[r], excl);
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int r = 0; r < DUP_ITEMS; r++) {
     const uint32_t i = (uint32_t)r * DUP_THREADS + tid;
@@ -414,7 +414,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   // the tile sort's first-pass digit counts of this block's slots (its sort tile is the same 2048
   // slots): the sort skips that pass's counting launch
   if (hist0) {
-    __syncthreads();
+    lds_barrier();
     hist0[(size_t)tid * gridDim.x + b] = s_hist[tid];
   }
 }
@@ -471,8 +471,10 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
     GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
               geo.sorted_gid, geo.offsets, geo.binrec, c.gx, bin.slot_tile, bin.presort_gid);
   }
+  // the Gaussian ids travel with the slots (aux stream): the renders then read point_gid
+  // contiguously instead of gathering presort_gid[slot] (one 128-B line per 4-B id)
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tbits, bin.sort_scratch, st,
-                   false, hist0, nullptr, nullptr, nullptr, bin.slot_tile);
+                   false, hist0, GS_SORT_GID ? bin.presort_gid : nullptr, bin.aux_a, bin.presort_gid, bin.slot_tile);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges,
             (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS);
 }
@@ -604,7 +606,7 @@ __device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q,
 template <bool EXACT>
 __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                          const uint32_t* __restrict__ point_list,
-                                                         const uint32_t* __restrict__ presort_gid,
+                                                         const uint32_t* __restrict__ point_gid,
                                                          const float4* __restrict__ splat, float* __restrict__ out,
                                                          float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                          uint32_t* __restrict__ tile_max, ImgPtrs img) {
@@ -623,11 +625,12 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   FwdPix px;
   px.done = __builtin_amdgcn_ballot_w64(!inside);
   for (uint32_t base = 0; base < n; base += GS_BLOCK) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (__syncthreads_and(px.done == ~0ull)) break;
     const uint32_t cnt = min((uint32_t)GS_BLOCK, n - base);
     uint32_t qmask = 0;
     if ((uint32_t)tid < cnt) {
-      const uint32_t gid = presort_gid[point_list[range.x + base + tid]];
+      const uint32_t gid = GS_SORT_GID ? point_gid[range.x + base + tid] : point_gid[point_list[range.x + base + tid]];
       const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
       s_ent[tid] = make_float4(a.x, a.y, b.z, b.w);
       s_ent[GS_BLOCK + tid] = fall_coefs(a.z, a.w, b.x, b.y);
@@ -635,7 +638,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
       qmask = quadrant_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
     }
     publish_masks(qmask, s_mask, tid);
-    __syncthreads();
+    lds_barrier();
     if (px.done == ~0ull) continue;
     // dense, in-order list of this quadrant's entries (as LDS byte offsets), built by the wave
     uint32_t qcnt = 0;
@@ -664,6 +667,12 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
 // are done (the workgroup version waits for its slowest quadrant).  Workgroup b takes tile
 // (b / 32) * 8 + b % 8, quadrant (b / 8) % 4, so the four quadrant waves of a tile share the
 // workgroup-to-XCD round robin (b % 8) and their repeated entry loads hit one L2.
+#ifndef GS_FWD_PREFETCH
+#define GS_FWD_PREFETCH 0  // 1 (needs GS_SORT_GID): measured 168 -> 179 us at C3, the loads past the stop are wasted
+#endif
+#if GS_FWD_PREFETCH && !GS_SORT_GID
+#error "GS_FWD_PREFETCH reads the ids by list position (GS_SORT_GID)"
+#endif
 #ifndef GS_FWDQ_NB
 #define GS_FWDQ_NB 64
 #endif
@@ -672,7 +681,7 @@ static_assert(FWDQ_NB <= 64, "one staged entry per lane");
 template <bool EXACT>
 __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ point_list,
-                                                     const uint32_t* __restrict__ presort_gid,
+                                                     const uint32_t* __restrict__ point_gid,
                                                      const float4* __restrict__ splat, float* __restrict__ out,
                                                      float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                      uint32_t* __restrict__ tile_max, ImgPtrs img) {
@@ -692,17 +701,36 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   const float qx = (float)(tx * GS_TILE + 8 * (wid & 1)), qy = (float)(ty * GS_TILE + 8 * (wid >> 1));
   FwdPix px;
   px.done = __builtin_amdgcn_ballot_w64(!inside);
+#if GS_FWD_PREFETCH
+  // two-deep staging pipeline: while batch k is walked, the splat records of batch k + 1 and the
+  // ids of batch k + 2 are in flight (the walk issues no global loads, so they overlap it)
+  const bool stager = lane < (uint32_t)FWDQ_NB;
+  const uint32_t* ids = point_gid + range.x + lane;
+  uint32_t gid_n = stager && lane < n ? ids[0] : 0u;
+  float4 pa, pb, pd;
+  if (stager && lane < n) pa = splat[3 * gid_n], pb = splat[3 * gid_n + 1], pd = splat[3 * gid_n + 2];
+  gid_n = stager && FWDQ_NB + lane < n ? ids[FWDQ_NB] : 0u;
+#endif
   for (uint32_t base = 0; base < n; base += FWDQ_NB) {
     if (px.done == ~0ull) break;
     bool meets = false;
+#if GS_FWD_PREFETCH
+    if (stager && base + lane < n) {
+      const float4 a = pa, bb = pb, d = pd;
+#else
     if (lane < (uint32_t)FWDQ_NB && base + lane < n) {
-      const uint32_t gid = presort_gid[point_list[range.x + base + lane]];
+      const uint32_t gid = GS_SORT_GID ? point_gid[range.x + base + lane] : point_gid[point_list[range.x + base + lane]];
       const float4 a = splat[3 * gid], bb = splat[3 * gid + 1], d = splat[3 * gid + 2];
+#endif
       s_ent[lane] = make_float4(a.x, a.y, bb.z, bb.w);
       s_ent[FWDQ_NB + lane] = fall_coefs(a.z, a.w, bb.x, bb.y);
       s_ent[2 * FWDQ_NB + lane] = make_float4(d.x, __uint_as_float(base + lane + 1), 0.0f, 0.0f);
       meets = d.z >= 0.0f && ellipse_meets_rect(a.x, a.y, a.z, a.w, bb.x, d.z, qx, qx + 7.0f, qy, qy + 7.0f);
     }
+#if GS_FWD_PREFETCH
+    if (stager && base + FWDQ_NB + lane < n) pa = splat[3 * gid_n], pb = splat[3 * gid_n + 1], pd = splat[3 * gid_n + 2];
+    gid_n = stager && base + 2 * FWDQ_NB + lane < n ? ids[base + 2 * FWDQ_NB] : 0u;
+#endif
     const uint64_t m = __ballot(meets);
     if (meets)
       s_qlist[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
@@ -731,18 +759,18 @@ void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
     const int blocks = ((tiles + 7) / 8) * 32;
     if (exact_exp())
       GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
+                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
     else
       GS_LAUNCH("render_fwd", k_render_fwd_q<false>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
+                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
     return;
   }
   if (exact_exp())
     GS_LAUNCH("render_fwd", k_render_fwd<true>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
+              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
   else
     GS_LAUNCH("render_fwd", k_render_fwd<false>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
+              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -39,14 +39,14 @@ __global__ __launch_bounds__(256) void k_knn_bbox(int P, const float* __restrict
     smin[k][threadIdx.x] = mn[k];
     smax[k][threadIdx.x] = mx[k];
   }
-  __syncthreads();
+  lds_barrier();
   for (int s = 128; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s)
       for (int k = 0; k < 3; k++) {
         smin[k][threadIdx.x] = min(smin[k][threadIdx.x], smin[k][threadIdx.x + s]);
         smax[k][threadIdx.x] = max(smax[k][threadIdx.x], smax[k][threadIdx.x + s]);
       }
-    __syncthreads();
+    lds_barrier();
   }
   if (threadIdx.x == 0)
     for (int k = 0; k < 3; k++) {

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, SsimWin win, con
     sx[r][c] = ld_plane(p1, H, W, y0 - SS_R + r, x0 - SS_R + c);
     sy[r][c] = ld_plane(p2, H, W, y0 - SS_R + r, x0 - SS_R + c);
   }
-  __syncthreads();
+  lds_barrier();
   // horizontal pass: 26 rows x 16 columns, five moments
   for (int i = tid; i < SS_IN * SS_T; i += 256) {
     const int r = i / SS_T, c = i - r * SS_T;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, SsimWin win, con
     sh[3][r][c] = bb;
     sh[4][r][c] = ab;
   }
-  __syncthreads();
+  lds_barrier();
   const int tx = tid & (SS_T - 1), ty = tid / SS_T;
   float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
 #pragma unroll
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, SsimWin win, con
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
   if ((tid & 63) == 0) s_red[tid >> 6] = v;
-  __syncthreads();
+  lds_barrier();
   if (tid == 0)
     partial[((size_t)plane * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] =
         (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
@@ -114,10 +114,10 @@ __global__ __launch_bounds__(256) void k_ssim_plane_sum(int tiles, const float* 
   double a = 0.0;
   for (int i = threadIdx.x; i < tiles; i += 256) a += (double)p[i];
   s[threadIdx.x] = a;
-  __syncthreads();
+  lds_barrier();
   for (int d = 128; d >= 1; d >>= 1) {
     if ((int)threadIdx.x < d) s[threadIdx.x] += s[threadIdx.x + d];
-    __syncthreads();
+    lds_barrier();
   }
   if (threadIdx.x == 0) plane_sum[blockIdx.x] = (float)s[0];
 }
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, int C, SsimWin w
 #pragma unroll
     for (int q = 0; q < 3; q++) sd[q][r][c] = ld_plane(dmaps + q * PHW + plane * HW, H, W, y, x);
   }
-  __syncthreads();
+  lds_barrier();
   for (int i = tid; i < SS_IN * SS_T; i += 256) {
     const int r = i / SS_T, c = i - r * SS_T;
     float a = 0.f, b = 0.f, d = 0.f;
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, int C, SsimWin w
     sh[1][r][c] = b;
     sh[2][r][c] = d;
   }
-  __syncthreads();
+  lds_barrier();
   const int tx = tid & (SS_T - 1), ty = tid / SS_T;
   const int px = x0 + tx, py = y0 + ty;
   if (px >= W || py >= H) return;

@@ -60,11 +60,11 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, ui
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   uint32_t inc = wave_incl_scan(v);
   if (lane == 63) sh[wid] = inc;
-  __syncthreads();
+  lds_barrier();
   uint32_t w0 = sh[0], w1 = sh[1], w2 = sh[2], w3 = sh[3];
   uint32_t before = (wid > 0 ? w0 : 0) + (wid > 1 ? w1 : 0) + (wid > 2 ? w2 : 0);
   *total = w0 + w1 + w2 + w3;
-  __syncthreads();
+  lds_barrier();
   return before + inc - v;
 }
 
@@ -92,7 +92,7 @@ static __global__ __launch_bounds__(1024) void k_scan_partials(uint32_t* partial
     uint32_t v = i < nb ? partial[i] : 0u;
     uint32_t inc = wave_incl_scan(v);
     if (lane == 63) sh[wid] = inc;
-    __syncthreads();
+    lds_barrier();
     uint32_t before = 0, tot = 0;
     for (uint32_t w = 0; w < 16; w++) {
       uint32_t x = sh[w];
@@ -101,7 +101,7 @@ static __global__ __launch_bounds__(1024) void k_scan_partials(uint32_t* partial
     }
     if (i < nb) partial[i] = carry + before + inc - v;
     carry += tot;
-    __syncthreads();
+    lds_barrier();
   }
   if (threadIdx.x == 0 && total_out) *total_out = carry;
 }
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(LB_THREADS) void k_scan_lb(Src src, Dst dst, const 
   uint32_t tile = blockIdx.x;
   if (gridDim.x > LB_STATIC_MAX) {
     if (threadIdx.x == 0) s_tile = atomicAdd(tile_counter, 1u);
-    __syncthreads();
+    lds_barrier();
     tile = s_tile;
   }
   const uint32_t n = resolve_n(n_dev, n_max);
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(LB_THREADS) void k_scan_lb(Src src, Dst dst, const 
       if (tile == gridDim.x - 1 && total_out) *total_out = excl + agg;
     }
   }
-  __syncthreads();
+  lds_barrier();
   ex += s_excl;
 #pragma unroll
   for (int k = 0; k < LB_ITEMS; k++) {
@@ -364,7 +364,7 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32
   __shared__ uint32_t h[RADIX];
   const uint32_t n = resolve_n(n_dev, n_max);
   h[threadIdx.x] = 0;
-  __syncthreads();
+  lds_barrier();
   const uint64_t start = (uint64_t)blockIdx.x * chunk;
   const uint64_t end = start + chunk < n ? start + chunk : n;
   const uint32_t mask = (1u << bits) - 1u;
@@ -382,7 +382,7 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32
     for (int k = 0; k < SORT_ITEMS; k++)
       if (v[k]) atomicAdd(&h[d[k]], 1u);  // counts only: order-free, deterministic
   }
-  __syncthreads();
+  lds_barrier();
   hist[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     s_wcnt[1][tid] = 0;
     s_wcnt[2][tid] = 0;
     s_wcnt[3][tid] = 0;
-    __syncthreads();
+    lds_barrier();
     // wave wid ranks positions t0 + wid*512 + r*64 + lane, r = 0..7 (in order -> stable)
     uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS], aux[AUX ? SORT_ITEMS : 1];
 #pragma unroll
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
       if (v && before == 0) s_wcnt[wid][d] = run + (uint32_t)__popcll(peers);
       __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
+    lds_barrier();
     // digit tid: prefix over waves, tile total, then exclusive scan of totals over digits
     const uint32_t c0 = s_wcnt[0][tid], c1 = s_wcnt[1][tid], c2 = s_wcnt[2][tid], c3 = s_wcnt[3][tid];
     const uint32_t tot = c0 + c1 + c2 + c3;
@@ -481,7 +481,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     s_wcnt[3][tid] = c0 + c1 + c2;
     s_loc[tid] = loc;
     s_tot[tid] = tot;
-    __syncthreads();
+    lds_barrier();
     // reorder the tile by digit in LDS
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
         if constexpr (AUX) s_aux[slot] = aux[r];
       }
     }
-    __syncthreads();
+    lds_barrier();
     // write runs of equal digits contiguously
     const uint32_t ntile = tot_all;  // keys kept in this tile
 #pragma unroll
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
         if constexpr (AUX) aux_out[pos] = s_aux[slot];
       }
     }
-    __syncthreads();
+    lds_barrier();
     s_base[tid] += s_tot[tid];
   }
 }

@@ -69,6 +69,22 @@ def test_two_rank_view_parallel_matches_single_process_sum(tmp_path):
     assert res.startswith("OK"), res
 
 
+@pytest.mark.spawn_first
+def test_concurrent_processes_are_deterministic():
+    """Two processes render the 8 C4 views forward + backward on the same GPU at once, four passes
+    each; every image and gradient must be bitwise identical across passes.  Sharing the GPU
+    shifts the waves' relative timing: this caught a barrier that did not drain the LDS writes of
+    the partner wave (render_bwd flush; gs_common.h lds_barrier), which flipped the dcolor /
+    dmean2D sums of a few Gaussians in ~1 of 5 C4 views."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "det_gpu_worker.py"), "3"]
+    procs = [subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for _ in range(2)]
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0 and o.startswith("OK"), f"rc {p.returncode}: {o[-2000:]}\n{e[-2000:]}"
+
+
 def _leaves(d):
     return [d.means3D.clone().requires_grad_(True), d.shs.clone().requires_grad_(True),
             d.opacities.clone().requires_grad_(True), d.scales.clone().requires_grad_(True),

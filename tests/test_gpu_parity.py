@@ -57,8 +57,12 @@ def _tol_check(gpu, ref, name, rtol=RTOL, frac=RTOL):
     scale = max(np.abs(ref).max(), 1e-30)
     tol = rtol * np.abs(ref) + frac * scale
     bad = np.abs(gpu - ref) > tol
-    assert not bad.any(), (f"{name}: {int(bad.sum())}/{bad.size} beyond tol; max|d|={np.abs(gpu - ref).max():.3e} "
-                           f"max|ref|={scale:.3e}")
+    if bad.any():
+        idx = np.argwhere(bad)[:5]
+        detail = "; ".join(f"{tuple(int(x) for x in i)}: gpu {gpu[tuple(i)]:.6e} ref {ref[tuple(i)]:.6e} "
+                           f"tol {tol[tuple(i)]:.2e}" for i in idx)
+        raise AssertionError(f"{name}: {int(bad.sum())}/{bad.size} beyond tol; max|d|={np.abs(gpu - ref).max():.3e} "
+                             f"max|ref|={scale:.3e}; first: {detail}")
 
 
 def _oracle_scene(oracle, cam, sc, bg, colors=None, cov3D=None, deg=None, mod=1.0):
