@@ -84,6 +84,9 @@ def main():
     ap.add_argument("--views-per-rank", type=int, default=4,
                     help="C1-C3/C5: views each rank renders (fwd+bwd, gradients accumulated in the bucket) per "
                          "step, i.e. per gradient all-reduce (DESIGN.md §7); value counts views")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the views of a step are spread over (view k on stream k mod n): one "
+                         "view's sorts and scans overlap another's tile passes; 1 = strictly serial")
     ap.add_argument("--sustain-s", type=float, default=2.0,
                     help="after the timed steps, keep stepping for this long (untimed for `value`) and report "
                          "the sustained rate too")
@@ -127,13 +130,24 @@ def main():
     # producer here, so the step's first backward overwrites and the others add (lazy zeroing)
     bucket = vp.GradBucket(params, lazy_zero=True)
 
-    def step():
-        bucket.zero_grad()
-        means2D.grad = None
-        for r in rasts:  # this rank's views: gradients accumulate in the bucket
-            img, _ = r(means3D=params[0], means2D=means2D, opacities=params[2], shs=params[1], scales=params[3],
+    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+
+    def view_fn(r):
+        def run():
+            # a fresh screen-space carrier per render, as the reference's render() makes
+            # (gaussian_renderer/__init__.py:24); its gradient is not kept here
+            m2 = torch.zeros_like(params[0], requires_grad=True)
+            img, _ = r(means3D=params[0], means2D=m2, opacities=params[2], shs=params[1], scales=params[3],
                        rotations=params[4])
             img.backward(dpix)
+        return run
+
+    view_fns = [view_fn(r) for r in rasts]
+
+    def step(sts=streams):
+        bucket.zero_grad()
+        # this rank's views, round-robin over the streams: gradients accumulate in the bucket
+        vp.run_views(view_fns, sts)
         if world > 1:
             bucket.allreduce()  # one RCCL all-reduce of the 59-f32/Gaussian bucket, in place
         else:
@@ -200,14 +214,37 @@ def main():
         sustained = dict(steps=n_s, seconds=round(el_s, 3),
                          iters_s=round((n_views or world * len(my_views)) * n_s / el_s, 2))
 
+    # the same step with the views strictly in sequence on one stream (no overlap between views)
+    serial = None
+    if len(streams) > 1:
+        for _ in range(2):
+            step(streams[:1])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tq = time.perf_counter()
+        for _ in range(args.steps):
+            step(streams[:1])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el_q = time.perf_counter() - tq
+        if world > 1:
+            t = torch.tensor([el_q], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_q = float(t.item())
+        serial = dict(iters_s=round((n_views or world * len(my_views)) * args.steps / el_q, 2),
+                      ms_per_step=round(1e3 * el_q / args.steps, 4))
+
     # per-kernel durations: a second pass of the same K steps with HIP events around every launch
     # (on the launch stream); kept out of the timed pass above because the event records add
-    # host work and small gaps between kernels
+    # host work and small gaps between kernels.  Views run on one stream here, so a kernel's time
+    # is its own (with two streams, kernels of two views share the CUs and each looks slower)
     lib = _native.load()
     lib.gs_profile_reset()
     lib.gs_profile_enable(1)
     for _ in range(args.steps):
-        step()
+        step(streams[:1])
     torch.cuda.synchronize()
     lib.gs_profile_enable(0)
     prof = _native.profile_stats()
@@ -314,6 +351,8 @@ def main():
         "ms_per_view": round(ms_per_view, 4),
         "step_roofline": step_roofline,
         "sustained": sustained,
+        "streams": len(streams),
+        "serial_one_stream": serial,
         "kernels": kernels,
         "cpu_baseline": cpu,
     }

@@ -205,10 +205,8 @@ size_t gs_grad_buffer_bytes(long long num_rendered) {
 // Per-thread, per-device pinned readback word block + event (reused call after call: a call
 // waits on its event before returning, so the slot is free again when the next call starts).
 struct ReadbackSlot {
-  uint32_t* host = nullptr;   // [0, 8): counters after preprocess; [8, 16): counters after fwd_order
-  hipEvent_t ev = nullptr;    // preprocess done (num_rendered readable)
-  hipEvent_t ev2 = nullptr;   // depth order + offsets scan done (its error flags readable)
-  bool order_pending = false;  // ev2 recorded by gs_forward_preprocess, not yet checked
+  uint32_t* host = nullptr;  // [0, 8): counters after preprocess
+  hipEvent_t ev = nullptr;   // preprocess done (num_rendered readable)
 };
 static ReadbackSlot* readback_slot() {
   static thread_local ReadbackSlot slots[64];
@@ -220,10 +218,58 @@ static ReadbackSlot* readback_slot() {
     void* p = nullptr;
     if (!check_hip(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc")) return nullptr;
     if (!check_hip(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate")) return nullptr;
-    if (!check_hip(hipEventCreateWithFlags(&s.ev2, hipEventDisableTiming), "hipEventCreate")) return nullptr;
     s.host = (uint32_t*)p;
   }
   return &s;
+}
+
+// Error flags of the last forward's sorts / scans, per device (not per thread: the backward of a
+// forward runs on the autograd engine's device thread).  gs_forward_render queues their readback
+// behind an event; the next forward or backward call on the device checks them (bit 4: a look-back
+// wait ran out) once its own launches are queued or before it starts, so no host wait idles the GPU.
+struct OrderFlags {
+  std::mutex mu;
+  uint32_t* host = nullptr;  // counters after the forward's binning
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+static OrderFlags g_order[64];
+
+// true: failed (error set)
+static bool check_order_flags() {
+  int dev = 0;
+  if (!check_hip(hipGetDevice(&dev), "hipGetDevice") || dev < 0 || dev >= 64) return true;
+  OrderFlags& o = g_order[dev];
+  std::lock_guard<std::mutex> lk(o.mu);
+  if (!o.pending) return false;
+  o.pending = false;
+  if (!check_hip(hipEventSynchronize(o.ev), "hipEventSynchronize")) return true;
+  if (o.host[CNT_ERR] & 4u) {
+    set_error("forward ordering: a look-back wait of the offsets scan or a one-sweep sort timed out "
+              "(the instance list of that forward is invalid)");
+    return true;
+  }
+  return false;
+}
+
+// queue the readback of this forward's ordering flags (after checking the previous forward's)
+static bool queue_order_flags(const uint32_t* counters, hipStream_t st) {
+  if (check_order_flags()) return true;
+  int dev = 0;
+  if (!check_hip(hipGetDevice(&dev), "hipGetDevice") || dev < 0 || dev >= 64) return true;
+  OrderFlags& o = g_order[dev];
+  std::lock_guard<std::mutex> lk(o.mu);
+  if (!o.host) {
+    void* p = nullptr;
+    if (!check_hip(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc")) return true;
+    if (!check_hip(hipEventCreateWithFlags(&o.ev, hipEventDisableTiming), "hipEventCreate")) return true;
+    o.host = (uint32_t*)p;
+  }
+  if (!check_hip(hipMemcpyAsync(o.host, counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)") ||
+      !check_hip(hipEventRecord(o.ev, st), "hipEventRecord"))
+    return true;
+  o.pending = true;
+  return false;
 }
 
 int gs_forward_preprocess(int P, int D, int M, const float* background, int W, int H, const float* means3D,
@@ -249,16 +295,11 @@ int gs_forward_preprocess(int P, int D, int M, const float* background, int W, i
   // sort and the instance offsets, so the host round trip overlaps device work.
   ReadbackSlot* rb = readback_slot();
   if (!rb) return 1;
+  if (check_order_flags()) return 1;  // an earlier forward's look-back waits
   fwd_preprocess(g, c, radii_out, geo, st);
   check_hip(hipMemcpyAsync(rb->host, geo.counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
   check_hip(hipEventRecord(rb->ev, st), "hipEventRecord");
   fwd_order(P, geo, st);
-  // the ordering scan's error flags (look-back timeout) are read after fwd_order, behind a second
-  // event; gs_forward_render checks them once its own launches are queued, so the host wait
-  // never idles the device
-  check_hip(hipMemcpyAsync(rb->host + 8, geo.counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
-  check_hip(hipEventRecord(rb->ev2, st), "hipEventRecord");
-  rb->order_pending = true;
   check_hip(hipEventSynchronize(rb->ev), "hipEventSynchronize");
   if (t_failed) return 1;
   const uint32_t err = rb->host[CNT_ERR], I = rb->host[CNT_NREND];
@@ -287,14 +328,10 @@ int gs_forward_render(int P, const float* background, int W, int H, const float*
   img_layout(W, H, &img, (char*)image_buffer);
   fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
   fwd_render(c, geo, bin, img, out_color, st);
-  // surface a look-back wait of the offsets scan that ran out (never expected: the scan's grid
-  // is resident), in every mode: the preprocess call left the flags behind ev2
-  ReadbackSlot* rb = readback_slot();
-  if (rb && rb->order_pending && !t_failed) {
-    rb->order_pending = false;
-    if (check_hip(hipEventSynchronize(rb->ev2), "hipEventSynchronize") && (rb->host[8 + CNT_ERR] & 4u))
-      return set_error("ordering scan: look-back wait timed out (instance offsets are invalid)"), 1;
-  }
+  // the look-back waits of the offsets scan and of the one-sweep sorts (never expected to run out:
+  // the waited-for workgroups are running) leave error bit 4; its readback rides behind an event
+  // that the next backward or forward call of this thread checks, so no host wait idles the device
+  if (!t_failed && queue_order_flags(geo.counters, st)) return 1;
   return t_failed ? 1 : 0;
 }
 
@@ -334,7 +371,8 @@ static int backward_impl(int P, int D, int M, const float* background, int W, in
                          float tan_fovy, const void* geom_buffer, long long num_rendered, const void* binning_buffer,
                          const void* image_buffer, const float* dL_dout_color, void* grad_buffer, float* dL_dmeans2D,
                          float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
-                         float* dL_dscales, float* dL_drotations, unsigned accumulate, int debug, void* stream) {
+                         float* dL_dscales, float* dL_drotations, unsigned accumulate, void* wait_event, int debug,
+                         void* stream) {
   clear_error(debug);
   (void)opacities;  // the opacity is carried by the forward's splat records
   if (!validate(P, D, M, W, H, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, viewmatrix,
@@ -362,7 +400,11 @@ static int backward_impl(int P, int D, int M, const float* background, int W, in
   GradOut out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
               shs ? dL_dsh : nullptr, cov3D_precomp ? nullptr : dL_dscales, cov3D_precomp ? nullptr : dL_drotations,
               accumulate};
+  // the gradient outputs may be shared with views on other streams: order only this last kernel
+  if (wait_event && !check_hip(hipStreamWaitEvent(st, (hipEvent_t)wait_event, 0), "hipStreamWaitEvent")) return 1;
   bwd_preprocess(g, c, geo, bin, img, gradrec, num_rendered > 0, out, st);
+  // the forward's ordering flags, now that this backward's kernels are queued
+  if (!t_failed && check_order_flags()) return 1;
   return t_failed ? 1 : 0;
 }
 
@@ -378,8 +420,8 @@ int gs_backward(int P, int D, int M, const float* background, int W, int H, cons
   return backward_impl(P, D, M, background, W, H, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
                        rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, geom_buffer,
                        num_rendered, binning_buffer, image_buffer, dL_dout_color, grad_buffer, dL_dmeans2D,
-                       dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, 0u, debug,
-                       stream);
+                       dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, 0u, nullptr,
+                       debug, stream);
 }
 
 int gs_backward_accumulate(int P, int D, int M, const float* background, int W, int H, const float* means3D,
@@ -391,13 +433,13 @@ int gs_backward_accumulate(int P, int D, int M, const float* background, int W, 
                            const void* image_buffer, const float* dL_dout_color, void* grad_buffer,
                            float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
                            float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
-                           unsigned accumulate, int debug, void* stream) {
+                           unsigned accumulate, void* wait_event, int debug, void* stream) {
   (void)radii;
   return backward_impl(P, D, M, background, W, H, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
                        rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, geom_buffer,
                        num_rendered, binning_buffer, image_buffer, dL_dout_color, grad_buffer, dL_dmeans2D,
                        dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, accumulate,
-                       debug, stream);
+                       wait_event, debug, stream);
 }
 
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,

@@ -465,12 +465,18 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
                                                                    const uint32_t* __restrict__ slot_tile,
                                                                    const uint32_t* __restrict__ tile_cut,
                                                                    const float* __restrict__ gradrec,
-                                                                   float* __restrict__ gsum) {
+                                                                   float* __restrict__ gsum, uint32_t P) {
   __shared__ double s_acc[SUMREC_WAVES][64][GRAD_REC];
   __shared__ unsigned long long s_mark[SUMREC_WAVES];
   const uint32_t V = counters[CNT_V], I = counters[CNT_I];
   const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t r0 = (blockIdx.x * SUMREC_WAVES + wid) * 64;
+  if (counters[CNT_ERR] & 4u) {
+    // the forward's ordering timed out (reported by the host): no valid records, zero sums
+    if (r0 + lane < P)
+      for (int c = 0; c < GRAD_REC; c++) gsum[(size_t)(r0 + lane) * GRAD_REC + c] = 0.0f;
+    return;
+  }
   if (r0 >= V) return;  // wave-uniform; the kernel has no workgroup barrier
   const uint32_t nr = min(64u, V - r0);
   const uint32_t my_off = lane < nr ? offsets[r0 + lane] : 0xFFFFFFFFu;
@@ -903,7 +909,7 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
   if (have_records)
     GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
               dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
-              gradrec, geo.gsum);
+              gradrec, geo.gsum, (uint32_t)g.P);
   dim3 grid((g.P + 255) / 256), block(256);
   const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
   const size_t lds = sh ? (size_t)256 * (3 * g.M + 1) * sizeof(float) : 0;

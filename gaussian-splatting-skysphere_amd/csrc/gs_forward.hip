@@ -224,7 +224,12 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
 
 struct SrcTilesByRank {
   const uint32_t *tiles, *sorted_gid;
-  __device__ uint32_t operator()(uint32_t s) const { return tiles[sorted_gid[s]]; }
+  uint32_t P;
+  // (a depth sort whose look-back timed out leaves stale ids: stay in bounds, the forward raises)
+  __device__ uint32_t operator()(uint32_t s) const {
+    const uint32_t g = sorted_gid[s];
+    return g < P ? tiles[g] : 0u;
+  }
 };
 
 // instance offsets in depth order; also records, for every DUP_SLOTS-aligned slot, the depth rank
@@ -236,8 +241,9 @@ struct DstOffsets {
   uint32_t P;
   __device__ void operator()(uint32_t s, uint32_t ex, uint32_t v) const {
     offsets[s] = ex;
-    if (!dup_balanced(counters[CNT_NREND], P)) return;
-    for (uint32_t m = (ex + DUP_SLOTS - 1) / DUP_SLOTS; m * DUP_SLOTS < ex + v; m++) first[m] = s;
+    const uint32_t I = counters[CNT_NREND];
+    if (!dup_balanced(I, P)) return;
+    for (uint32_t m = (ex + DUP_SLOTS - 1) / DUP_SLOTS; m * DUP_SLOTS < ex + v && m * DUP_SLOTS < I; m++) first[m] = s;
   }
 };
 
@@ -251,7 +257,7 @@ void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
     // counts through the four sort passes)
     radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
                      geo.sort_scratch, st, /*drop_first=*/true);
-    scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
+    scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid, n}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
                       &geo.counters[CNT_V], n, geo.lb_status, &geo.counters[CNT_LB_TILE], &geo.counters[CNT_I],
                       &geo.counters[CNT_ERR], st);
   } else {
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* _
                                                    uint32_t* __restrict__ tile_keys,
                                                    uint32_t* __restrict__ presort_gid) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-  if (s >= P || s >= counters[CNT_V]) return;
+  if (s >= P || s >= counters[CNT_V] || (counters[CNT_ERR] & 4u)) return;  // (timed-out sort: write nothing)
   const uint32_t gid = sorted_gid[s];
   uint32_t off = offsets[s];
   // (a timed-out offsets scan only under-estimates offsets: every write stays below I)
@@ -332,10 +338,10 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   const uint32_t k0 = b * DUP_SLOTS;
   const uint32_t k1 = min(k0 + DUP_SLOTS, I);
   if (counters[CNT_ERR] & 4u) {
-    // the offsets scan timed out (the host raises after this call): the owner table is not
-    // valid, so fill the block's slots with a safe placeholder -- tile 0, Gaussian
-    // sorted_gid[0] -- that keeps every later kernel in bounds instead of following it
-    const uint32_t g0 = sorted_gid[0];
+    // a look-back wait of the depth sort or the offsets scan timed out (the host raises at its next
+    // call): the owner table is not valid, so fill the block's slots with a safe placeholder --
+    // tile 0, Gaussian 0 -- that keeps every later kernel in bounds instead of following it
+    const uint32_t g0 = 0u;
     for (uint32_t k = k0 + tid; k < k1; k += DUP_THREADS) {
       tile_keys[k] = 0u;
       presort_gid[k] = g0;
@@ -421,7 +427,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
 
 // tile ranges over the sorted instance list, 4 instances per lane
 __global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __restrict__ tile, uint2* __restrict__ ranges,
-                                                uint32_t* __restrict__ sched, uint32_t sched_words) {
+                                                uint32_t* __restrict__ sched, uint32_t sched_words, uint32_t tiles) {
   // clear the render's per-tile completion counters and length buckets (k_render_fwd* epilogue)
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sched_words; i += gridDim.x * 256) sched[i] = 0u;
   const uint32_t k0 = (blockIdx.x * 256 + threadIdx.x) * 4;
@@ -443,6 +449,7 @@ __global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __re
   for (int r = 0; r < 4; r++) {
     const uint32_t k = k0 + r;
     if (k >= I) break;
+    if (t[r + 1] >= tiles) continue;  // only after a timed-out sort (reported): stay in bounds
     if (t[r + 1] != t[r]) ranges[t[r + 1]].x = k;
     if (t[r + 2] != t[r + 1]) ranges[t[r + 1]].y = k + 1;
   }
@@ -471,12 +478,12 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
     GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
               geo.sorted_gid, geo.offsets, geo.binrec, c.gx, bin.slot_tile, bin.presort_gid);
   }
-  // the Gaussian ids travel with the slots (aux stream): the renders then read point_gid
-  // contiguously instead of gathering presort_gid[slot] (one 128-B line per 4-B id)
+  // GS_SORT_GID: the Gaussian ids travel with the slots (aux stream): the renders then read
+  // point_gid contiguously instead of gathering presort_gid[slot]
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tbits, bin.sort_scratch, st,
                    false, hist0, GS_SORT_GID ? bin.presort_gid : nullptr, bin.aux_a, bin.presort_gid, bin.slot_tile);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges,
-            (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS);
+            (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS, (uint32_t)tiles);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -609,7 +616,8 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
                                                          const uint32_t* __restrict__ point_gid,
                                                          const float4* __restrict__ splat, float* __restrict__ out,
                                                          float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                                                         uint32_t* __restrict__ tile_max, ImgPtrs img) {
+                                                         uint32_t* __restrict__ tile_max, ImgPtrs img,
+                                                         const uint32_t* __restrict__ err) {
   __shared__ float4 s_ent[3 * GS_BLOCK];
   __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[4][GS_BLOCK + 2 * FWD_ILP];  // per quadrant wave: byte offsets
@@ -620,7 +628,8 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   const QuadPix q = quad_pixel(tx, ty, wid, lane);
   const bool inside = q.px < c.W && q.py < c.H;
   const uint2 range = ranges[tile];
-  const uint32_t n = range.y - range.x;
+  // a sort / scan look-back that timed out (reported by the host) leaves no valid list: render none
+  const uint32_t n = (*err & 4u) ? 0u : range.y - range.x;
   const char* ent = reinterpret_cast<const char*>(s_ent);
   FwdPix px;
   px.done = __builtin_amdgcn_ballot_w64(!inside);
@@ -684,7 +693,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
                                                      const uint32_t* __restrict__ point_gid,
                                                      const float4* __restrict__ splat, float* __restrict__ out,
                                                      float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                                                     uint32_t* __restrict__ tile_max, ImgPtrs img) {
+                                                     uint32_t* __restrict__ tile_max, ImgPtrs img,
+                                                     const uint32_t* __restrict__ err) {
   __shared__ float4 s_ent[3 * FWDQ_NB];
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
   const uint32_t b = blockIdx.x;
@@ -696,7 +706,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   const QuadPix q = quad_pixel(tx, ty, wid, lane);
   const bool inside = q.px < c.W && q.py < c.H;
   const uint2 range = ranges[tile];
-  const uint32_t n = range.y - range.x;
+  // a sort / scan look-back that timed out (reported by the host) leaves no valid list: render none
+  const uint32_t n = (*err & 4u) ? 0u : range.y - range.x;
   const char* ent = reinterpret_cast<const char*>(s_ent);
   const float qx = (float)(tx * GS_TILE + 8 * (wid & 1)), qy = (float)(ty * GS_TILE + 8 * (wid >> 1));
   FwdPix px;
@@ -759,18 +770,22 @@ void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
     const int blocks = ((tiles + 7) / 8) * 32;
     if (exact_exp())
       GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
+                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
+                &geo.counters[CNT_ERR]);
     else
       GS_LAUNCH("render_fwd", k_render_fwd_q<false>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
+                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
+                &geo.counters[CNT_ERR]);
     return;
   }
   if (exact_exp())
     GS_LAUNCH("render_fwd", k_render_fwd<true>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
+              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
+                &geo.counters[CNT_ERR]);
   else
     GS_LAUNCH("render_fwd", k_render_fwd<false>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img);
+              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
+                &geo.counters[CNT_ERR]);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -586,4 +586,5 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
   return in_b;
 }
 
+
 }  // namespace gs

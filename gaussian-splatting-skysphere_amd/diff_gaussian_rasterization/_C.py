@@ -140,12 +140,14 @@ GS_ACC = {n: 1 << k for k, n in enumerate(GRAD_NAMES)}
 
 def backward_impl(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
                   projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R, binningBuffer,
-                  imageBuffer, debug, want_all=True, sinks=None):
+                  imageBuffer, debug, want_all=True, sinks=None, wait_event=None):
     """Shared backward.  With want_all=False the gradients that no autograd input can receive
     (colours when SHs drive the colour, cov3D when scale/rotation drive it, ...) are None and
     not computed.  sinks: {name: (buffer, accumulate)} -- that gradient is written into (or, with
     accumulate, added to) the caller's buffer, which is returned in its place
-    (gs_backward_accumulate; multi-view gradient buckets, gs_view_parallel.GradBucket)."""
+    (gs_backward_accumulate; multi-view gradient buckets, gs_view_parallel.GradBucket).
+    wait_event: torch.cuda.Event the stream waits for before the kernel that writes the gradients
+    (a sink shared with views on other streams)."""
     x = _Inputs(background, means3D, colors, None, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
                 campos, need_opacity=False)
     P, dev = x.P, x.device
@@ -196,7 +198,8 @@ def backward_impl(background, means3D, radii, colors, scales, rotations, scale_m
                 _ptr(x.campos), float(tan_fovx), float(tan_fovy), _ptr(radii), _ptr(geomBuffer), int(R),
                 _ptr(binningBuffer), _ptr(imageBuffer), _ptr(dpix), _ptr(grad_scratch), _ptr(o["means2D"]),
                 _ptr(o["colors"]), _ptr(o["opacity"]), _ptr(o["means3D"]), _ptr(o["cov3D"]), _ptr(o["sh"]),
-                _ptr(o["scales"]), _ptr(o["rotations"]), acc, int(bool(debug)), st),
+                _ptr(o["scales"]), _ptr(o["rotations"]), acc,
+                ctypes.c_void_p(wait_event.cuda_event) if wait_event is not None else None, int(bool(debug)), st),
             "rasterize_gaussians_backward")
     return ret
 

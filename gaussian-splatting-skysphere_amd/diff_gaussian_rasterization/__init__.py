@@ -39,7 +39,9 @@ __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gau
 # (normally the tensor's own .grad, a view into a flat all-reduce bucket), and the autograd
 # Function returns None for it.  The result equals autograd's `grad += g` with no extra pass over
 # the gradients and no pack/unpack copy.  owner.claim(tensor) -> (buffer, accumulate) or None
-# (None: the normal autograd path).
+# (None: the normal autograd path).  Optional: owner.write_order(stream) -> torch.cuda.Event or None
+# (the stream waits for it before the gradient-writing kernel) and owner.written(stream), called
+# once the backward is enqueued -- an owner shared by views on several streams orders its writes.
 # ------------------------------------------------------------------------------------------
 _SINKS: dict = {}  # id(tensor) -> (weakref to the tensor, owner)
 
@@ -144,19 +146,33 @@ class _RasterizeGaussians(torch.autograd.Function):
                 view, proj, s.tanfovx, s.tanfovy, grad_out_color.contiguous(), sh, s.sh_degree,
                 s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.debug)
 
-        sinks, sunk = {}, set()
+        sinks, sunk, owners = {}, set(), []
         for k, name, t, owner in ctx.sinks:
             if ctx.needs_input_grad[k]:
                 claim = owner.claim(t)
                 if claim is not None:
                     sinks[name] = claim
                     sunk.add(k)
+                    if all(o is not owner for o in owners):
+                        owners.append(owner)
+        # sink owners may order their buffer's writes across streams (views rendered on several
+        # streams, GradBucket): the last kernel waits for the owner's previous write
+        wait = None
+        if owners:
+            st = torch.cuda.current_stream(grad_out_color.device)
+            evs = [e for e in (o.write_order(st) for o in owners if hasattr(o, "write_order")) if e is not None]
+            for e in evs[1:]:
+                st.wait_event(e)
+            wait = evs[0] if evs else None
 
         def _bwd(*a):
-            return _C.backward_impl(*a, want_all=False, sinks=sinks)
+            return _C.backward_impl(*a, want_all=False, sinks=sinks, wait_event=wait)
 
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
          grad_rotations) = _run_with_snapshot(_bwd, args, s.debug, "snapshot_bw.dump", "backward")
+        for o in owners:
+            if hasattr(o, "written"):
+                o.written(st)
         grads = [grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
                  grad_rotations, grad_cov3Ds_precomp, None]
         for k in sunk:  # already in the sink's buffer (the tensor's .grad)

@@ -51,7 +51,7 @@ SIGNATURES = {
         _c_i,
         [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
          _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
-         ctypes.c_uint, _c_i, _c_p],
+         ctypes.c_uint, _c_p, _c_i, _c_p],
     ),
     "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),

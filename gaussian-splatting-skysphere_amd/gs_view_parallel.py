@@ -62,6 +62,11 @@ class GradBucket:
             self.views[id(p)] = v
             register_gradient_sink(p, self)
         self._fresh = {}  # id(p) -> _version of the view at zero_grad (lazy mode: not written yet)
+        # stream ordering of the writes into the bucket: the last writer's event and stream (views
+        # rendered on several streams add into one bucket one after another; their forward passes,
+        # sorts and tile backward passes overlap)
+        self._events = {}
+        self._last = None
         self.zero_grad()
 
     def close(self):
@@ -76,6 +81,31 @@ class GradBucket:
         else:
             self.flat.zero_()
             self._fresh = {}
+        # the step's first write, on whichever stream, follows everything queued on this one
+        # (the previous step's all-reduce / optimizer reads, or the zero fill)
+        if self.flat.is_cuda:
+            self.written(torch.cuda.current_stream(self.flat.device))
+
+    def write_order(self, stream):
+        """Event a write on `stream` must wait for (the previous write was on another stream)."""
+        if self._last is None or self._last[1] == stream:
+            return None
+        return self._last[0]
+
+    def written(self, stream):
+        """A write into the bucket was enqueued on `stream`: later writers on other streams wait for it."""
+        ev = self._events.get(stream)
+        if ev is None:
+            ev = self._events[stream] = torch.cuda.Event()
+        ev.record(stream)
+        self._last = (ev, stream)
+
+    def _join(self):
+        # reads of the bucket on the current stream follow the last write on any stream
+        if self.flat.is_cuda and self._last is not None:
+            cur = torch.cuda.current_stream(self.flat.device)
+            if self._last[1] != cur:
+                cur.wait_event(self._last[0])
 
     def claim(self, p):
         """Gradient sink protocol: (buffer, accumulate) for the rasterizer backward."""
@@ -92,7 +122,8 @@ class GradBucket:
 
     def finalize(self):
         """Zero the views no backward wrote this step (lazy mode); then the bucket holds the step's
-        gradient sums."""
+        gradient sums (on the current stream: it waits for the last write on any stream)."""
+        self._join()
         for p in self.params:
             ver = self._fresh.pop(id(p), None)
             if ver is not None:
@@ -116,6 +147,22 @@ class GradBucket:
                     work = None
                 flat.div_(dist.get_world_size(group))
         return work if async_op else flat
+
+
+def run_views(view_fns: Sequence, streams: Sequence) -> None:
+    """Run the views of one step round-robin on `streams` (view k on streams[k % n]): each view's
+    forward (host-synchronous only up to its preprocess) and backward are enqueued on its stream,
+    so one view's depth / tile sorts and scans overlap another view's tile passes.  Writes into a
+    shared GradBucket are ordered by the bucket (write_order / written); the current stream then
+    waits for every view stream.  Tensors a view allocates belong to its stream's allocator pool."""
+    main = torch.cuda.current_stream()
+    for s in streams:
+        s.wait_stream(main)
+    for k, fn in enumerate(view_fns):
+        with torch.cuda.stream(streams[k % len(streams)]):
+            fn()
+    for s in streams:
+        main.wait_stream(s)
 
 
 def allreduce_grads(params: Iterable[torch.Tensor], group=None, average: bool = False):

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 2
+#define GSRAST_ABI_VERSION 3
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -120,7 +120,10 @@ int gs_backward(int P, int D, int M, const float* background, int image_width, i
  * Same arguments and outputs as gs_backward; bit k of `accumulate` (GS_ACC_*) makes output k
  * ADDED to the buffer's current contents (fp32 `old + new`, as autograd's in-place `grad += g`)
  * instead of overwriting it.  Used to sum several views' gradients into one flat gradient
- * bucket with no extra pass over it (view-parallel training). */
+ * bucket with no extra pass over it (view-parallel training).
+ * wait_event (hipEvent_t or NULL): the stream waits for it after the per-tile work and before the
+ * kernel that writes / adds the gradient outputs, so views rendered on two streams can share one
+ * bucket: their forward, sort and tile backward overlap, only the bucket updates are ordered. */
 #define GS_ACC_MEANS2D 1u
 #define GS_ACC_COLORS 2u
 #define GS_ACC_OPACITY 4u
@@ -138,7 +141,7 @@ int gs_backward_accumulate(int P, int D, int M, const float* background, int ima
                            const void* binning_buffer, const void* image_buffer, const float* dL_dout_color,
                            void* grad_buffer, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
-                           float* dL_drotations, unsigned accumulate, int debug, void* stream);
+                           float* dL_drotations, unsigned accumulate, void* wait_event, int debug, void* stream);
 
 /* ---- mark_visible: present[P] (uint8 0/1), near-plane test ---- */
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -97,7 +97,11 @@ def _render(rast, p, means2D):
 
 
 @pytest.mark.parametrize("lazy", [True, False], ids=["lazy_zero", "zero_filled"])
-def test_bucket_accumulation_equals_autograd_sum(device, lazy):
+@pytest.mark.parametrize("nstreams", [1, 2, 3], ids=["1stream", "2streams", "3streams"])
+def test_bucket_accumulation_equals_autograd_sum(device, lazy, nstreams):
+    """The bucket equals autograd's per-view gradients summed with += in view order, bit for bit,
+    also when the views run round-robin on several streams (vp.run_views: the forward passes and
+    tile backward passes overlap; the bucket orders its writes by events)."""
     import gs_view_parallel as vp
     from diff_gaussian_rasterization import GaussianRasterizer
 
@@ -124,12 +128,18 @@ def test_bucket_accumulation_equals_autograd_sum(device, lazy):
     calls = []
     orig = b.claim
     b.claim = lambda t: calls.append(1) or orig(t)  # noqa: E731
-    for step in range(2):  # the second step reuses the bucket (stale values must not leak)
-        b.zero_grad()
-        for r, dp in zip(rasts, dpix):
+    streams = [torch.cuda.Stream(device) for _ in range(nstreams)]
+
+    def view(r, dp):
+        def run():
             m2 = torch.zeros_like(p[0], requires_grad=True)
             img, _ = _render(r, p, m2)
             img.backward(dp)
+        return run
+
+    for step in range(2):  # the second step reuses the bucket (stale values must not leak)
+        b.zero_grad()
+        vp.run_views([view(r, dp) for r, dp in zip(rasts, dpix)], streams)
         b.finalize()
         torch.cuda.synchronize()
         for k, (t, x) in enumerate(zip(p, ref)):
@@ -247,25 +257,46 @@ def test_record_cut_invariant_and_partly_cut_gaussian(oracle, device, exact_mode
 
 
 def test_lookback_timeout_is_reported(device):
-    """A look-back wait of the offsets scan that runs out leaves invalid instance offsets: the
-    forward must fail loudly in every mode (not only debug).  The test hook makes every waiting
-    workgroup time out at once."""
+    """A look-back wait that runs out (offsets scan or a one-sweep sort pass) leaves an invalid
+    instance list: every later kernel of that forward stays in bounds (the render draws no list,
+    the record sums are zero) and the NEXT call of the thread -- its backward or another forward --
+    fails loudly, in every mode (not only debug).  The test hook makes every waiting workgroup time
+    out at once."""
     from diff_gaussian_rasterization import GaussianRasterizer
 
     lib = _lib()
     cam = gs_scenes.identity_camera(320, 240)
     d = gs_scenes.random_gaussians(200_000, 0, cam=cam, seed=60).to(device)
     rast = GaussianRasterizer(gs_scenes.raster_settings_for(cam, 0, device=device))
+
+    def fwd(means3D):
+        return rast(means3D=means3D, means2D=torch.zeros_like(d.means3D), opacities=d.opacities, shs=d.shs,
+                    scales=d.scales, rotations=d.rotations)
+
+    # forward only: the next forward reports it
     prev = lib.gs_debug_set_scan_spin_limit(0)
     try:
-        with pytest.raises(RuntimeError, match="look-back wait timed out"):
-            rast(means3D=d.means3D, means2D=torch.zeros_like(d.means3D), opacities=d.opacities, shs=d.shs,
-                 scales=d.scales, rotations=d.rotations)
-            torch.cuda.synchronize()
+        img, _ = fwd(d.means3D)
+        torch.cuda.synchronize()
     finally:
         lib.gs_debug_set_scan_spin_limit(prev)
-    img, _ = rast(means3D=d.means3D, means2D=torch.zeros_like(d.means3D), opacities=d.opacities, shs=d.shs,
-                  scales=d.scales, rotations=d.rotations)
+    assert torch.isfinite(img).all()
+    with pytest.raises(RuntimeError, match="look-back wait"):
+        fwd(d.means3D)
+    img, _ = fwd(d.means3D)
+    assert torch.isfinite(img).all() and float(img.abs().max()) > 0
+    # forward + backward: the backward reports it (after queuing its own, in-bounds, kernels)
+    m = d.means3D.clone().requires_grad_(True)
+    prev = lib.gs_debug_set_scan_spin_limit(0)
+    try:
+        img, _ = fwd(m)
+    finally:
+        lib.gs_debug_set_scan_spin_limit(prev)
+    with pytest.raises(RuntimeError, match="look-back wait"):
+        img.sum().backward()
+    torch.cuda.synchronize()
+    img, _ = fwd(d.means3D)
+    torch.cuda.synchronize()
     assert torch.isfinite(img).all()
 
 
