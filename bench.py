@@ -51,12 +51,14 @@ WORKLOADS = {
 }
 
 
-def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None, acc_frac=0.0):
+def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None, acc_frac=0.0, K=1):
     """Algorithmic (minimum) HBM bytes of ONE launch of each kernel.
     E: instances the render walks reach (sum over tiles of min(largest n_contrib, list length));
     only those are staged, and only those have backward records.  acc_frac: fraction of the
     preprocess_bwd launches that add into the gradient bucket (views after a step's first), which
-    also read the old gradients (means3D 12 + sh 12M + opacity 4 + scales 12 + rotations 16 B)."""
+    also read the old gradients (means3D 12 + sh 12M + opacity 4 + scales 12 + rotations 16 B).
+    K: views per backward_gaussians launch (its inputs and outputs once, the K views' record sums,
+    tile counts and clamp bits each)."""
     npix = W * H
     sh = 12 * M
     E = I if E is None else E
@@ -66,6 +68,8 @@ def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None, acc_frac=0.0):
         "render_bwd": E * (4 + 4 + 48 + 36) + npix * 20 + tiles * 12,
         "sum_records": E * 36 + I * 4 + V * (4 + 36),
         "preprocess_bwd": P * (8 + 44 + sh + 1 + 32 + 24 + sh) + V * 36 + int(acc_frac * P * (44 + sh)),
+        "backward_gaussians": P * (40 + sh + 44 + sh) + K * (P * 5 + V * 36),
+        "mean2d_grad": P * (4 + 12) + V * 8,
         "duplicate": V * (4 + 4 + 32 + 4) + I * 8,
         "ranges": I * 4 + tiles * 8,
     }.get(name)
@@ -87,6 +91,9 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the views of a step are spread over (view k on stream k mod n): one "
                          "view's sorts and scans overlap another's tile passes; 1 = strictly serial")
+    ap.add_argument("--no-defer", action="store_true",
+                    help="run the per-Gaussian backward per view (gs_backward_accumulate) instead of once per "
+                         "step for all views (gs_backward_gaussians)")
     ap.add_argument("--sustain-s", type=float, default=2.0,
                     help="after the timed steps, keep stepping for this long (untimed for `value`) and report "
                          "the sustained rate too")
@@ -128,7 +135,9 @@ def main():
     rast = rasts[0]
     # the parameters' .grad are views of ONE flat bucket; the rasterizer is the only gradient
     # producer here, so the step's first backward overwrites and the others add (lazy zeroing)
-    bucket = vp.GradBucket(params, lazy_zero=True)
+    # defer: the per-Gaussian half of the backward runs once for all of the step's views (at
+    # finalize / allreduce) instead of once per view (--no-defer: per view)
+    bucket = vp.GradBucket(params, lazy_zero=True, defer=not args.no_defer)
 
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
 
@@ -275,13 +284,13 @@ def main():
     kernels = {}
     for name, (ms, n) in prof.items():
         per_launch_ms = ms / max(n, 1)
-        b = kernel_bytes(name, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac)
+        b = kernel_bytes(name, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac, k_local)
         kernels[name] = dict(total_ms_per_step=round(ms / args.steps, 4), launches_per_step=round(n / args.steps, 2),
                              avg_us=round(1e3 * per_launch_ms, 2),
                              algo_GBs=(round(b / (per_launch_ms * 1e-3) / 1e9, 1) if b else None))
     dom = max(kernels, key=lambda k: kernels[k]["total_ms_per_step"])
     dom_avg_ms = kernels[dom]["avg_us"] / 1e3
-    dom_bytes = kernel_bytes(dom, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac)
+    dom_bytes = kernel_bytes(dom, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac, k_local)
     achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9 if dom_bytes else None
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -304,10 +313,10 @@ def main():
         if vi:
             roofline["valu"] = dict(insts_per_launch=vi, peak_insts_per_s=VALU_PEAK_IPS,
                                     frac=round(vi / (dom_avg_ms * 1e-3) / VALU_PEAK_IPS, 4))
-    # whole-step algorithmic bytes (P*a_G + I*a_I + Npix*a_px), per view
-    step_bytes = sum(kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac) or 0 for k in
-                     ("preprocess", "render_fwd", "render_bwd", "sum_records", "preprocess_bwd", "duplicate",
-                      "ranges"))
+    # whole-step algorithmic bytes (P*a_G + I*a_I + Npix*a_px), per view: every kernel's
+    # bytes per launch times its launches per step, over the step's views
+    step_bytes = sum((kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac, k_local) or 0)
+                     * v["launches_per_step"] for k, v in kernels.items()) / k_local
     ms_per_view = ms_per_step / k_local
     step_roofline = dict(algo_bytes_per_view=int(step_bytes), ms_per_view=round(ms_per_view, 4),
                          achieved=round(step_bytes / (ms_per_view * 1e-3) / 1e9, 1), peak=HBM_PEAK_GBS, unit="GB/s",

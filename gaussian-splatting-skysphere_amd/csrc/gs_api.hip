@@ -442,6 +442,86 @@ int gs_backward_accumulate(int P, int D, int M, const float* background, int W, 
                        wait_event, debug, stream);
 }
 
+int gs_backward_render(int P, int D, int M, const float* background, int W, int H, const float* viewmatrix,
+                       const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                       const void* geom_buffer, long long num_rendered, const void* binning_buffer,
+                       const void* image_buffer, const float* dL_dout_color, void* grad_buffer, float* dL_dmeans2D,
+                       unsigned accumulate, int debug, void* stream) {
+  clear_error(debug);
+  if (P < 0) return set_error("P must be >= 0"), 1;
+  if (W <= 0 || H <= 0) return set_error("image size must be positive (got %d x %d)", W, H), 1;
+  if (P == 0) return 0;
+  if (!viewmatrix || !projmatrix || !background) return set_error("missing required input pointer"), 1;
+  if (!geom_buffer || !binning_buffer || !image_buffer || !dL_dout_color || !grad_buffer)
+    return set_error("missing buffer pointer"), 1;
+  if (num_rendered < 0 || num_rendered > 0xFFFFFFFFll) return set_error("num_rendered out of range"), 1;
+  if (accumulate & ~GS_ACC_MEANS2D) return set_error("accumulate: only GS_ACC_MEANS2D applies here"), 1;
+  hipStream_t st = (hipStream_t)stream;
+  CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, 0);
+  GeomPtrs geo;
+  BinPtrs bin;
+  ImgPtrs img;
+  geom_layout((size_t)P, &geo, (char*)geom_buffer);
+  bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer);
+  img_layout(W, H, &img, (char*)image_buffer);
+  GaussianArgs g{P, D, M, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1.0f};
+  float* gradrec = (float*)grad_buffer;
+  if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, st);
+  bwd_records(g, geo, bin, img, gradrec, num_rendered > 0, dL_dmeans2D, accumulate, st);
+  if (!t_failed && check_order_flags()) return 1;
+  return t_failed ? 1 : 0;
+}
+
+int gs_backward_gaussians(int P, int D, int M, const float* means3D, const float* shs, const float* colors_precomp,
+                          const float* scales, float scale_modifier, const float* rotations,
+                          const float* cov3D_precomp, int num_views, const gs_view_grad* views, float* dL_dcolors,
+                          float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                          float* dL_dscales, float* dL_drotations, unsigned accumulate, void* wait_event, int debug,
+                          void* stream) {
+  clear_error(debug);
+  if (P < 0) return set_error("P must be >= 0"), 1;
+  if (num_views < 0 || (num_views > 0 && !views)) return set_error("bad view list"), 1;
+  if (P == 0 || num_views == 0) return 0;
+  if (!means3D) return set_error("missing required input pointer"), 1;
+  if ((shs == nullptr) == (colors_precomp == nullptr))
+    return set_error("Please provide excatly one of either SHs or precomputed colors!"), 1;
+  if (((scales == nullptr || rotations == nullptr) && cov3D_precomp == nullptr) ||
+      ((scales || rotations) && cov3D_precomp))
+    return set_error("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!"), 1;
+  if (shs && (D < 0 || D > 3 || M < (D + 1) * (D + 1))) return set_error("bad SH degree / coefficient count"), 1;
+  if (!dL_dopacity || !dL_dmeans3D) return set_error("missing gradient output pointer"), 1;
+  if (accumulate & ~0xFFu) return set_error("accumulate: unknown GS_ACC bits 0x%x", accumulate), 1;
+  for (int v = 0; v < num_views; v++) {
+    const gs_view_grad& w = views[v];
+    if (!w.viewmatrix || !w.projmatrix || !w.geom_buffer || (shs && !w.campos))
+      return set_error("view %d: missing pointer", v), 1;
+    if (w.image_width <= 0 || w.image_height <= 0) return set_error("view %d: bad image size", v), 1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (wait_event && !check_hip(hipStreamWaitEvent(st, (hipEvent_t)wait_event, 0), "hipStreamWaitEvent")) return 1;
+  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, nullptr, scales, rotations, cov3D_precomp, scale_modifier};
+  // passes of up to FUSED_MAX_VIEWS views; the later passes add to what the earlier wrote
+  for (int v0 = 0; v0 < num_views; v0 += FUSED_MAX_VIEWS) {
+    FusedViews fv;
+    fv.K = num_views - v0 < FUSED_MAX_VIEWS ? num_views - v0 : FUSED_MAX_VIEWS;
+    for (int k = 0; k < fv.K; k++) {
+      const gs_view_grad& w = views[v0 + k];
+      GeomPtrs geo;
+      geom_layout((size_t)P, &geo, (char*)w.geom_buffer);
+      fv.v[k].c = make_camera(nullptr, w.image_width, w.image_height, w.viewmatrix, w.projmatrix, w.campos,
+                              w.tan_fovx, w.tan_fovy, 0);
+      fv.v[k].tiles = geo.tiles;
+      fv.v[k].clamped = geo.clamped;
+      fv.v[k].gsum = geo.gsum;
+    }
+    GradOut out{nullptr, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, shs ? dL_dsh : nullptr,
+                cov3D_precomp ? nullptr : dL_dscales, cov3D_precomp ? nullptr : dL_drotations,
+                v0 == 0 ? accumulate : 0xFFu};
+    bwd_gaussians(g, fv, out, st);
+  }
+  return t_failed ? 1 : 0;
+}
+
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
                     void* stream) {
   clear_error(0);

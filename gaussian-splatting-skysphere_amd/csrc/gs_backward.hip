@@ -545,9 +545,12 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
 // SH backward for one Gaussian (order identical to oracle/gs_oracle.c sh_bwd_one).
 // `row` is the Gaussian's SH row (3M floats) staged in LDS, or (REG) its first 3K floats in
 // registers; on return it holds dL/dsh (REG: the caller zero-fills [3K, 3M)).
-template <int DEG, bool REG = false>
+// ACC (multi-view pass): `row` is left alone and dL/dsh goes to acc[0, 3K): written when `first`,
+// else added (fp32 acc + new, the arithmetic of a bucket's `grad += g`).
+template <int DEG, bool REG = false, bool ACC = false>
 __device__ __forceinline__ void sh_backward(float* row, int M, float vx, float vy, float vz,
-                                            uint32_t clamped, const float* dcol, float* dmean) {
+                                            uint32_t clamped, const float* dcol, float* dmean,
+                                            float* acc = nullptr, bool first = true) {
   constexpr int K = (DEG + 1) * (DEG + 1);
   const float len = sqrtf(vx * vx + vy * vy + vz * vz);
   const float x = vx / len, y = vy / len, z = vz / len;
@@ -610,8 +613,13 @@ __device__ __forceinline__ void sh_backward(float* row, int M, float vx, float v
 #pragma unroll
   for (int k = 0; k < K; k++)
 #pragma unroll
-    for (int ch = 0; ch < 3; ch++) row[3 * k + ch] = b[k] * g[ch];
-  if (!REG)
+    for (int ch = 0; ch < 3; ch++) {
+      if constexpr (ACC)
+        acc[3 * k + ch] = first ? b[k] * g[ch] : acc[3 * k + ch] + b[k] * g[ch];
+      else
+        row[3 * k + ch] = b[k] * g[ch];
+    }
+  if (!REG && !ACC)
     for (int k = 3 * K; k < 3 * M; k++) row[k] = 0.0f;
   const float d0 = ddx[0] * g[0] + ddx[1] * g[1] + ddx[2] * g[2];
   const float d1 = ddy[0] * g[0] + ddy[1] * g[1] + ddy[2] * g[2];
@@ -663,6 +671,71 @@ __device__ __forceinline__ void cov3d_backward(float sx, float sy, float sz, flo
             4.f * y * (dR[0][0] + dR[2][2]);
   drot[3] = 2.f * r * (dR[1][0] - dR[0][1]) + 2.f * x * (dR[0][2] + dR[2][0]) + 2.f * y * (dR[1][2] + dR[2][1]) -
             4.f * z * (dR[0][0] + dR[1][1]);
+}
+
+// Camera-dependent part of the per-Gaussian backward (upstream computeCov2DCUDA + the projection
+// term of preprocessCUDA's backward, order identical to oracle/gs_oracle.c): conic gradient ->
+// cov2D -> cov3D gradient (dcv) and the view-space mean gradient incl. the NDC-mean term (dmean).
+__device__ __forceinline__ void camera_grads(const CameraArgs& c, float px, float py, float pz, const float* cov3,
+                                             float dcon0, float dcon1, float dcon2, float dm2x, float dm2y,
+                                             float* dcv, float* dmean) {
+#pragma unroll
+  for (int k = 0; k < 6; k++) dcv[k] = 0.f;
+  // conic -> cov2D -> cov3D and view-space mean
+  const Cov2D cv = cov2d(c.view, px, py, pz, cov3, c.fx, c.fy, c.tanfovx, c.tanfovy);
+  const float A = cv.a, Bv = cv.b, Cc = cv.c;
+  const float denom = A * Cc - Bv * Bv;
+  float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+  const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+  const float(*Tm)[3] = cv.T;
+  if (denom2inv != 0.0f) {
+    dL_da = denom2inv * (-Cc * Cc * dcon0 + 2.f * Bv * Cc * dcon1 + (denom - A * Cc) * dcon2);
+    dL_dc = denom2inv * (-A * A * dcon2 + 2.f * A * Bv * dcon1 + (denom - A * Cc) * dcon0);
+    dL_db = denom2inv * 2.f * (Bv * Cc * dcon0 - (denom + 2.f * Bv * Bv) * dcon1 + A * Bv * dcon2);
+    dcv[0] = Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc;
+    dcv[3] = Tm[0][1] * Tm[0][1] * dL_da + Tm[0][1] * Tm[1][1] * dL_db + Tm[1][1] * Tm[1][1] * dL_dc;
+    dcv[5] = Tm[0][2] * Tm[0][2] * dL_da + Tm[0][2] * Tm[1][2] * dL_db + Tm[1][2] * Tm[1][2] * dL_dc;
+    dcv[1] = 2.f * Tm[0][0] * Tm[0][1] * dL_da + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_db +
+             2.f * Tm[1][0] * Tm[1][1] * dL_dc;
+    dcv[2] = 2.f * Tm[0][0] * Tm[0][2] * dL_da + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_db +
+             2.f * Tm[1][0] * Tm[1][2] * dL_dc;
+    dcv[4] = 2.f * Tm[0][2] * Tm[0][1] * dL_da + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_db +
+             2.f * Tm[1][1] * Tm[1][2] * dL_dc;
+  }
+  const float V[3][3] = {{cov3[0], cov3[1], cov3[2]}, {cov3[1], cov3[3], cov3[4]}, {cov3[2], cov3[4], cov3[5]}};
+  float dT0[3], dT1[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const float tv0 = Tm[0][0] * V[r][0] + Tm[0][1] * V[r][1] + Tm[0][2] * V[r][2];
+    const float tv1 = Tm[1][0] * V[r][0] + Tm[1][1] * V[r][1] + Tm[1][2] * V[r][2];
+    dT0[r] = 2.f * tv0 * dL_da + tv1 * dL_db;
+    dT1[r] = 2.f * tv1 * dL_dc + tv0 * dL_db;
+  }
+  const float* v = c.view;
+  const float dJ00 = v[0] * dT0[0] + v[4] * dT0[1] + v[8] * dT0[2];
+  const float dJ02 = v[2] * dT0[0] + v[6] * dT0[1] + v[10] * dT0[2];
+  const float dJ11 = v[1] * dT1[0] + v[5] * dT1[1] + v[9] * dT1[2];
+  const float dJ12 = v[2] * dT1[0] + v[6] * dT1[1] + v[10] * dT1[2];
+  const float tz = 1.f / cv.tz, tz2 = tz * tz, tz3 = tz2 * tz;
+  const float dL_dtx = cv.gmx * -c.fx * tz2 * dJ02;
+  const float dL_dty = cv.gmy * -c.fy * tz2 * dJ12;
+  const float dL_dtz =
+      -c.fx * tz2 * dJ00 - c.fy * tz2 * dJ11 + (2.f * c.fx * cv.tx) * tz3 * dJ02 + (2.f * c.fy * cv.ty) * tz3 * dJ12;
+  dmean[0] = v[0] * dL_dtx + v[1] * dL_dty + v[2] * dL_dtz;
+  dmean[1] = v[4] * dL_dtx + v[5] * dL_dty + v[6] * dL_dtz;
+  dmean[2] = v[8] * dL_dtx + v[9] * dL_dty + v[10] * dL_dtz;
+  // projection: NDC mean2D -> mean3D
+  const float* P = c.proj;
+  const float hw = xf44w(P, px, py, pz);
+  const float m_w = 1.0f / (hw + 0.0000001f);
+  const float mul1 = (P[0] * px + P[4] * py + P[8] * pz + P[12]) * m_w * m_w;
+  const float mul2 = (P[1] * px + P[5] * py + P[9] * pz + P[13]) * m_w * m_w;
+  const float pm0 = (P[0] * m_w - P[3] * mul1) * dm2x + (P[1] * m_w - P[3] * mul2) * dm2y;
+  const float pm1 = (P[4] * m_w - P[7] * mul1) * dm2x + (P[5] * m_w - P[7] * mul2) * dm2y;
+  const float pm2 = (P[8] * m_w - P[11] * mul1) * dm2x + (P[9] * m_w - P[11] * mul2) * dm2y;
+  dmean[0] = dmean[0] + pm0;
+  dmean[1] = dmean[1] + pm1;
+  dmean[2] = dmean[2] + pm2;
 }
 
 // one gradient output element: written, or (GS_ACC bit set for the output) added to the caller's
@@ -737,66 +810,11 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
     cov3d(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
           g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], cov3);
   }
-  // conic -> cov2D -> cov3D and view-space mean
-  const Cov2D cv = cov2d(c.view, px, py, pz, cov3, c.fx, c.fy, c.tanfovx, c.tanfovy);
-  const float A = cv.a, Bv = cv.b, Cc = cv.c;
-  const float denom = A * Cc - Bv * Bv;
-  float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
-  const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-  float dcv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const float(*Tm)[3] = cv.T;
-  if (denom2inv != 0.0f) {
-    dL_da = denom2inv * (-Cc * Cc * dcon0 + 2.f * Bv * Cc * dcon1 + (denom - A * Cc) * dcon2);
-    dL_dc = denom2inv * (-A * A * dcon2 + 2.f * A * Bv * dcon1 + (denom - A * Cc) * dcon0);
-    dL_db = denom2inv * 2.f * (Bv * Cc * dcon0 - (denom + 2.f * Bv * Bv) * dcon1 + A * Bv * dcon2);
-    dcv[0] = Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc;
-    dcv[3] = Tm[0][1] * Tm[0][1] * dL_da + Tm[0][1] * Tm[1][1] * dL_db + Tm[1][1] * Tm[1][1] * dL_dc;
-    dcv[5] = Tm[0][2] * Tm[0][2] * dL_da + Tm[0][2] * Tm[1][2] * dL_db + Tm[1][2] * Tm[1][2] * dL_dc;
-    dcv[1] = 2.f * Tm[0][0] * Tm[0][1] * dL_da + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_db +
-             2.f * Tm[1][0] * Tm[1][1] * dL_dc;
-    dcv[2] = 2.f * Tm[0][0] * Tm[0][2] * dL_da + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_db +
-             2.f * Tm[1][0] * Tm[1][2] * dL_dc;
-    dcv[4] = 2.f * Tm[0][2] * Tm[0][1] * dL_da + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_db +
-             2.f * Tm[1][1] * Tm[1][2] * dL_dc;
-  }
-  const float V[3][3] = {{cov3[0], cov3[1], cov3[2]}, {cov3[1], cov3[3], cov3[4]}, {cov3[2], cov3[4], cov3[5]}};
-  float dT0[3], dT1[3];
-#pragma unroll
-  for (int r = 0; r < 3; r++) {
-    const float tv0 = Tm[0][0] * V[r][0] + Tm[0][1] * V[r][1] + Tm[0][2] * V[r][2];
-    const float tv1 = Tm[1][0] * V[r][0] + Tm[1][1] * V[r][1] + Tm[1][2] * V[r][2];
-    dT0[r] = 2.f * tv0 * dL_da + tv1 * dL_db;
-    dT1[r] = 2.f * tv1 * dL_dc + tv0 * dL_db;
-  }
-  const float* v = c.view;
-  const float dJ00 = v[0] * dT0[0] + v[4] * dT0[1] + v[8] * dT0[2];
-  const float dJ02 = v[2] * dT0[0] + v[6] * dT0[1] + v[10] * dT0[2];
-  const float dJ11 = v[1] * dT1[0] + v[5] * dT1[1] + v[9] * dT1[2];
-  const float dJ12 = v[2] * dT1[0] + v[6] * dT1[1] + v[10] * dT1[2];
-  const float tz = 1.f / cv.tz, tz2 = tz * tz, tz3 = tz2 * tz;
-  const float dL_dtx = cv.gmx * -c.fx * tz2 * dJ02;
-  const float dL_dty = cv.gmy * -c.fy * tz2 * dJ12;
-  const float dL_dtz =
-      -c.fx * tz2 * dJ00 - c.fy * tz2 * dJ11 + (2.f * c.fx * cv.tx) * tz3 * dJ02 + (2.f * c.fy * cv.ty) * tz3 * dJ12;
-  float dmean[3];
-  dmean[0] = v[0] * dL_dtx + v[1] * dL_dty + v[2] * dL_dtz;
-  dmean[1] = v[4] * dL_dtx + v[5] * dL_dty + v[6] * dL_dtz;
-  dmean[2] = v[8] * dL_dtx + v[9] * dL_dty + v[10] * dL_dtz;
+  float dcv[6], dmean[3];
+  camera_grads(c, px, py, pz, cov3, dcon0, dcon1, dcon2, dm2x, dm2y, dcv, dmean);
   if (out.dcov3D)
 #pragma unroll
     for (int k = 0; k < 6; k++) gput(out.dcov3D, 6 * i + k, dcv[k], acc, GS_ACC_COV3D);
-  // projection: NDC mean2D -> mean3D
-  const float* P = c.proj;
-  const float hw = xf44w(P, px, py, pz);
-  const float m_w = 1.0f / (hw + 0.0000001f);
-  const float mul1 = (P[0] * px + P[4] * py + P[8] * pz + P[12]) * m_w * m_w;
-  const float mul2 = (P[1] * px + P[5] * py + P[9] * pz + P[13]) * m_w * m_w;
-  const float pm0 = (P[0] * m_w - P[3] * mul1) * dm2x + (P[1] * m_w - P[3] * mul2) * dm2y;
-  const float pm1 = (P[4] * m_w - P[7] * mul1) * dm2x + (P[5] * m_w - P[7] * mul2) * dm2y;
-  const float pm2 = (P[8] * m_w - P[11] * mul1) * dm2x + (P[9] * m_w - P[11] * mul2) * dm2y;
-  dmean[0] = dmean[0] + pm0;
-  dmean[1] = dmean[1] + pm1;
-  dmean[2] = dmean[2] + pm2;
   if (DEG >= 0) {
     float shm[3];
     const float vx = px - c.campos[0], vy = py - c.campos[1], vz = pz - c.campos[2];
@@ -900,6 +918,187 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd_reg(GaussianArgs g, Came
     for (int k = 0; k < KF; k++) dst[k] = row[k];
   }
   for (int k = KF; k < rowf; k++) dst[k] = 0.0f;
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-Gaussian backward of K views at once (view-parallel step, gs_backward_gaussians).
+//
+// A step that renders K views of one set of Gaussians into one gradient bucket would run the
+// per-Gaussian backward K times, each reading the 192-B SH row and read-modify-writing the 236-B
+// gradient row of every Gaussian (C3: ~0.7 GB per view, HBM-bound).  Here one lane per Gaussian
+// reads its inputs once, walks the K views' record sums (36 B per view, summed by each view's
+// k_sum_records) and cameras, forms every view's gradient with the single-view arithmetic, and
+// writes (or adds once into) the bucket: the per-view outputs are combined in view order as
+// `g = g0; g = g + g1; ...`, exactly the fp32 sums the sequential accumulate path produces.
+// ------------------------------------------------------------------------------------------
+// r = (first ? v : r + v): the bucket arithmetic of one view's write / `grad += g`
+__device__ __forceinline__ void vput(float& r, float v, bool first) { r = first ? v : r + v; }
+
+template <int DEG>  // -1: colours precomputed (no SH gradient)
+__global__ __launch_bounds__(256) void k_backward_gaussians(GaussianArgs g, FusedViews fv, GradOut out) {
+  constexpr int D = DEG < 0 ? 0 : DEG;
+  constexpr int KF = DEG < 0 ? 1 : 3 * (D + 1) * (D + 1);
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  if (i >= g.P) return;
+  const uint32_t acc = out.acc;
+  const int rowf = 3 * g.M;
+  // the SH row (its first 3K floats) and the accumulators; an output with its GS_ACC bit starts
+  // from the caller's value and every view adds
+  float row[KF], dsh[KF];
+  const bool vec = DEG >= 0 && (KF & 3) == 0 && (rowf & 3) == 0 &&
+                   ((((uintptr_t)g.shs) | ((uintptr_t)out.dsh)) & 15) == 0;
+  if (DEG >= 0) {
+    const float* src = g.shs + (size_t)i * rowf;
+    if (vec) {
+#pragma unroll
+      for (int q = 0; q < KF / 4; q++) {
+        const float4 v = reinterpret_cast<const float4*>(src)[q];
+        row[4 * q] = v.x, row[4 * q + 1] = v.y, row[4 * q + 2] = v.z, row[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < KF; k++) row[k] = src[k];
+    }
+  }
+  const float px = g.means3D[3 * i], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
+  float cov3[6];
+  if (g.cov3D) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) cov3[k] = g.cov3D[6 * i + k];
+  } else {
+    cov3d(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
+          g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], cov3);
+  }
+  const bool sr = !g.cov3D && out.dscale && out.drot;
+  float a_col[3], a_op, a_mean[3], a_cov[6], a_s[3], a_r[4];
+  bool f_col = !(acc & GS_ACC_COLORS), f_op = !(acc & GS_ACC_OPACITY), f_mean = !(acc & GS_ACC_MEANS3D),
+       f_cov = !(acc & GS_ACC_COV3D), f_sh = !(acc & GS_ACC_SH), f_s = !(acc & GS_ACC_SCALES),
+       f_r = !(acc & GS_ACC_ROTATIONS);
+  if (out.dcolor && !f_col)
+    for (int k = 0; k < 3; k++) a_col[k] = out.dcolor[3 * i + k];
+  if (!f_op) a_op = out.dopacity[i];
+  if (!f_mean)
+    for (int k = 0; k < 3; k++) a_mean[k] = out.dmean3D[3 * i + k];
+  if (out.dcov3D && !f_cov)
+    for (int k = 0; k < 6; k++) a_cov[k] = out.dcov3D[6 * i + k];
+  if (DEG >= 0 && !f_sh) {
+    const float* d = out.dsh + (size_t)i * rowf;
+#pragma unroll
+    for (int k = 0; k < KF; k++) dsh[k] = d[k];
+  }
+  if (sr && !f_s)
+    for (int k = 0; k < 3; k++) a_s[k] = out.dscale[3 * i + k];
+  if (sr && !f_r)
+    for (int k = 0; k < 4; k++) a_r[k] = out.drot[4 * i + k];
+
+  for (int v = 0; v < fv.K; v++) {
+    const ViewGrad& w = fv.v[v];
+    float dcol[3] = {0.f, 0.f, 0.f}, dop = 0.f, dmean[3] = {0.f, 0.f, 0.f}, dcv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float ds[3] = {0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f};
+    const bool vis = w.tiles[i] != 0;
+    if (vis) {
+      const float* rec = w.gsum + (size_t)i * GRAD_REC;
+      float a[GRAD_REC];
+#pragma unroll
+      for (int k = 0; k < GRAD_REC; k++) a[k] = rec[k];
+      dcol[0] = a[0], dcol[1] = a[1], dcol[2] = a[2];
+      dop = a[8];
+      camera_grads(w.c, px, py, pz, cov3, a[5], a[6], a[7], a[3], a[4], dcv, dmean);
+      if (DEG >= 0) {
+        float shm[3];
+        const float vx = px - w.c.campos[0], vy = py - w.c.campos[1], vz = pz - w.c.campos[2];
+        sh_backward<D, true, true>(row, g.M, vx, vy, vz, w.clamped[i], dcol, shm, dsh, f_sh);
+        dmean[0] = dmean[0] + shm[0];
+        dmean[1] = dmean[1] + shm[1];
+        dmean[2] = dmean[2] + shm[2];
+      }
+      if (sr)
+        cov3d_backward(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier,
+                       g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3],
+                       dcv, ds, dr);
+    } else if (DEG >= 0) {
+#pragma unroll
+      for (int k = 0; k < KF; k++) vput(dsh[k], 0.0f, f_sh);
+    }
+    if (DEG >= 0) f_sh = false;
+    for (int k = 0; k < 3; k++) vput(a_col[k], dcol[k], f_col);
+    f_col = false;
+    vput(a_op, dop, f_op);
+    f_op = false;
+    for (int k = 0; k < 3; k++) vput(a_mean[k], dmean[k], f_mean);
+    f_mean = false;
+    for (int k = 0; k < 6; k++) vput(a_cov[k], dcv[k], f_cov);
+    f_cov = false;
+    for (int k = 0; k < 3; k++) vput(a_s[k], ds[k], f_s);
+    f_s = false;
+    for (int k = 0; k < 4; k++) vput(a_r[k], dr[k], f_r);
+    f_r = false;
+  }
+  if (out.dcolor)
+    for (int k = 0; k < 3; k++) out.dcolor[3 * i + k] = a_col[k];
+  out.dopacity[i] = a_op;
+  for (int k = 0; k < 3; k++) out.dmean3D[3 * i + k] = a_mean[k];
+  if (out.dcov3D)
+    for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = a_cov[k];
+  if (sr) {
+    for (int k = 0; k < 3; k++) out.dscale[3 * i + k] = a_s[k];
+    for (int k = 0; k < 4; k++) out.drot[4 * i + k] = a_r[k];
+  }
+  if (DEG >= 0 && out.dsh) {
+    float* dst = out.dsh + (size_t)i * rowf;
+    if (vec) {
+#pragma unroll
+      for (int q = 0; q < KF / 4; q++)
+        reinterpret_cast<float4*>(dst)[q] = make_float4(dsh[4 * q], dsh[4 * q + 1], dsh[4 * q + 2], dsh[4 * q + 3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < KF; k++) dst[k] = dsh[k];
+    }
+    if (!(acc & GS_ACC_SH))  // coefficients past (D + 1)^2: zero (accumulated: + 0)
+      for (int k = KF; k < rowf; k++) dst[k] = 0.0f;
+  }
+}
+
+void bwd_gaussians(const GaussianArgs& g, const FusedViews& fv, const GradOut& out, hipStream_t st) {
+  if (g.P <= 0 || fv.K <= 0) return;
+  dim3 grid((g.P + 255) / 256), block(256);
+  const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
+  if (!sh) {
+    GS_LAUNCH("backward_gaussians", k_backward_gaussians<-1>, grid, block, 0, st, g, fv, out);
+    return;
+  }
+  switch (g.D) {
+    case 0: GS_LAUNCH("backward_gaussians", k_backward_gaussians<0>, grid, block, 0, st, g, fv, out); break;
+    case 1: GS_LAUNCH("backward_gaussians", k_backward_gaussians<1>, grid, block, 0, st, g, fv, out); break;
+    case 2: GS_LAUNCH("backward_gaussians", k_backward_gaussians<2>, grid, block, 0, st, g, fv, out); break;
+    default: GS_LAUNCH("backward_gaussians", k_backward_gaussians<3>, grid, block, 0, st, g, fv, out); break;
+  }
+}
+
+// dL/dmeans2D of one view straight from its record sums (the per-view output of the split
+// backward; the per-Gaussian half runs later, over all of the step's views at once)
+__global__ __launch_bounds__(256) void k_mean2d_grad(int P, const uint32_t* __restrict__ tiles,
+                                                     const float* __restrict__ gsum, float* __restrict__ dmean2D,
+                                                     uint32_t acc) {
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  if (i >= P) return;
+  const bool vis = tiles[i] != 0;
+  const float x = vis ? gsum[(size_t)i * GRAD_REC + 3] : 0.0f, y = vis ? gsum[(size_t)i * GRAD_REC + 4] : 0.0f;
+  gput(dmean2D, 3 * i, x, acc, GS_ACC_MEANS2D);
+  gput(dmean2D, 3 * i + 1, y, acc, GS_ACC_MEANS2D);
+  gput(dmean2D, 3 * i + 2, 0.0f, acc, GS_ACC_MEANS2D);
+}
+
+void bwd_records(const GaussianArgs& g, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* gradrec,
+                 bool have_records, float* dmean2D, uint32_t acc, hipStream_t st) {
+  if (g.P <= 0) return;
+  if (have_records)
+    GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
+              dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
+              gradrec, geo.gsum, (uint32_t)g.P);
+  if (dmean2D)
+    GS_LAUNCH("mean2d_grad", k_mean2d_grad, dim3((g.P + 255) / 256), dim3(256), 0, st, g.P, geo.tiles, geo.gsum,
+              dmean2D, acc);
 }
 
 void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,

@@ -252,6 +252,22 @@ struct GradOut {
   // accumulation into a caller-owned bucket, gsrast.h gs_backward_accumulate) instead of written
   uint32_t acc;
 };
+// multi-view per-Gaussian backward (gs_backward_gaussians): K views of one set of Gaussians
+constexpr int FUSED_MAX_VIEWS = 8;
+struct ViewGrad {
+  CameraArgs c;
+  const uint32_t* tiles;   // that view's geom buffer: tile counts (0 = invisible), SH clamp bits and
+  const uint8_t* clamped;  //   per-Gaussian record sums (k_sum_records)
+  const float* gsum;
+};
+struct FusedViews {
+  int K;
+  ViewGrad v[FUSED_MAX_VIEWS];
+};
+void bwd_gaussians(const GaussianArgs& g, const FusedViews& fv, const GradOut& out, hipStream_t st);
+// the per-tile half of a split backward: record sums into the geom buffer (+ dL/dmeans2D)
+void bwd_records(const GaussianArgs& g, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* gradrec,
+                 bool have_records, float* dmean2D, uint32_t acc, hipStream_t st);
 void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
                     const ImgPtrs& img, float* gradrec,
                     bool have_records, const GradOut& out, hipStream_t st);

@@ -204,6 +204,66 @@ def backward_impl(background, means3D, radii, colors, scales, rotations, scale_m
     return ret
 
 
+def backward_render(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, dL_dout_color, P, degree, M,
+                    geomBuffer, R, binningBuffer, imageBuffer, want_means2D, debug):
+    """Per-tile half of the backward (gs_backward_render): the view's per-Gaussian record sums,
+    kept in geomBuffer for backward_gaussians, and its dL_dmeans2D [P, 3] (or None)."""
+    dev = geomBuffer.device
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    dm2 = torch.empty((P, 3), dtype=torch.float32, device=dev) if want_means2D else None
+    if P == 0:
+        return dm2
+    bg = _f32(background, "background", dev, host_ok=True)
+    view = _f32(viewmatrix, "viewmatrix", dev, host_ok=True)
+    proj = _f32(projmatrix, "projmatrix", dev, host_ok=True)
+    cam = _f32(campos, "campos", dev, host_ok=True)
+    dpix = _f32(dL_dout_color, "dL_dout_color", dev)
+    with torch.cuda.device(dev):
+        st = _stream(dev)
+        grad_scratch = torch.empty((_lib.gs_grad_buffer_bytes(int(R)),), dtype=torch.uint8, device=dev)
+        _native.check(
+            _lib.gs_backward_render(P, int(degree), int(M), _ptr(bg), W, H, _ptr(view), _ptr(proj), _ptr(cam),
+                                    float(tan_fovx), float(tan_fovy), _ptr(geomBuffer), int(R), _ptr(binningBuffer),
+                                    _ptr(imageBuffer), _ptr(dpix), _ptr(grad_scratch), _ptr(dm2), 0,
+                                    int(bool(debug)), st),
+            "rasterize_gaussians_backward (render half)")
+    return dm2
+
+
+def backward_gaussians(means3D, sh, colors, scales, rotations, cov3D_precomp, scale_modifier, degree, views, outs,
+                       accumulate, wait_event=None, debug=False):
+    """Per-Gaussian half of the backward for several views at once (gs_backward_gaussians).
+    views: [(viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, W, H, geomBuffer)] in order (each
+    after its backward_render); outs: {name: buffer} for colors / opacity / means3D / cov3D / sh /
+    scales / rotations (absent: not produced); accumulate: GS_ACC bits of the first view."""
+    x = _Inputs(None, means3D, colors, None, scales, rotations, cov3D_precomp, views[0][0],
+                views[0][1], sh, views[0][2], need_opacity=False)
+    P, dev = x.P, x.device
+    if P == 0 or not views:
+        return
+    arr = (_native.ViewGrad * len(views))()
+    keep = []
+    for k, (vm, pm, cp, tx, ty, W, H, geom) in enumerate(views):
+        vm, pm = _f32(vm, "viewmatrix", dev, host_ok=True), _f32(pm, "projmatrix", dev, host_ok=True)
+        cp = _f32(cp, "campos", dev, host_ok=True)
+        keep += [vm, pm, cp]
+        arr[k] = _native.ViewGrad(vm.data_ptr(), pm.data_ptr(), cp.data_ptr() if cp is not None else None,
+                                  float(tx), float(ty), int(W), int(H), geom.data_ptr())
+    o = {n: outs.get(n) for n in ("colors", "opacity", "means3D", "cov3D", "sh", "scales", "rotations")}
+    for n, t in o.items():
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev):
+            raise RuntimeError(f"backward_gaussians: {n} output must be a contiguous float32 tensor on {dev}")
+    with torch.cuda.device(dev):
+        _native.check(
+            _lib.gs_backward_gaussians(
+                P, int(degree), x.M, _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors), _ptr(x.scales), float(scale_modifier),
+                _ptr(x.rotations), _ptr(x.cov3D), len(views), arr, _ptr(o["colors"]), _ptr(o["opacity"]),
+                _ptr(o["means3D"]), _ptr(o["cov3D"]), _ptr(o["sh"]), _ptr(o["scales"]), _ptr(o["rotations"]),
+                int(accumulate), ctypes.c_void_p(wait_event.cuda_event) if wait_event is not None else None,
+                int(bool(debug)), _stream(dev)),
+            "rasterize_gaussians_backward (per-Gaussian half)")
+
+
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh,
                                  degree, campos, geomBuffer, R, binningBuffer, imageBuffer, debug):

@@ -146,6 +146,22 @@ class _RasterizeGaussians(torch.autograd.Function):
                 view, proj, s.tanfovx, s.tanfovy, grad_out_color.contiguous(), sh, s.sh_degree,
                 s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.debug)
 
+        # a sink owner that defers the per-Gaussian half (GradBucket(defer=True)) takes this view
+        # when every parameter gradient the call needs goes to it: only the per-tile half and
+        # dL_dmeans2D run now, the per-Gaussian half later for all of its views in one pass
+        deferrer = _deferring_owner(ctx)
+        if deferrer is not None:
+            dm2 = _C.backward_render(s.bg, view, proj, s.campos, s.tanfovx, s.tanfovy, grad_out_color.contiguous(),
+                                     means3D.size(0), s.sh_degree, sh.size(1) if sh.ndimension() == 3 else 0,
+                                     geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, ctx.needs_input_grad[1],
+                                     s.debug)
+            deferrer.defer_view(ctx, dict(means3D=means3D, sh=sh, colors=colors_precomp, scales=scales,
+                                          rotations=rotations, cov3D=cov3Ds_precomp, scale_modifier=s.scale_modifier,
+                                          degree=s.sh_degree, debug=s.debug),
+                                (view, proj, s.campos, s.tanfovx, s.tanfovy, s.image_width, s.image_height,
+                                 geomBuffer))
+            return (None, dm2) + (None,) * 7
+
         sinks, sunk, owners = {}, set(), []
         for k, name, t, owner in ctx.sinks:
             if ctx.needs_input_grad[k]:
@@ -178,6 +194,21 @@ class _RasterizeGaussians(torch.autograd.Function):
         for k in sunk:  # already in the sink's buffer (the tensor's .grad)
             grads[k] = None
         return tuple(grads)
+
+
+def _deferring_owner(ctx):
+    """The one sink owner with `defer_view` that receives every input gradient this backward must
+    produce (means2D aside), or None."""
+    if not ctx.sinks:
+        return None
+    owner = ctx.sinks[0][3]
+    if not getattr(owner, "defers", False):
+        return None
+    sunk = {k for k, _name, _t, o in ctx.sinks if o is owner}
+    for k in range(8):
+        if k != 1 and ctx.needs_input_grad[k] and k not in sunk:
+            return None
+    return owner
 
 
 class GaussianRasterizer(nn.Module):

@@ -19,6 +19,15 @@ _c_f = ctypes.c_float
 _c_ll = ctypes.c_longlong
 _c_sz = ctypes.c_size_t
 
+
+
+class ViewGrad(ctypes.Structure):
+    """gs_view_grad (include/gsrast.h): one view of a multi-view per-Gaussian backward."""
+    _fields_ = [("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p), ("campos", ctypes.c_void_p),
+                ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float), ("image_width", ctypes.c_int),
+                ("image_height", ctypes.c_int), ("geom_buffer", ctypes.c_void_p)]
+
+
 # name -> (restype, argtypes); mirrors include/gsrast.h
 SIGNATURES = {
     "gs_abi_version": (_c_i, []),
@@ -52,6 +61,16 @@ SIGNATURES = {
         [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
          _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
          ctypes.c_uint, _c_p, _c_i, _c_p],
+    ),
+    "gs_backward_render": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_f, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_p,
+         _c_p, ctypes.c_uint, _c_i, _c_p],
+    ),
+    "gs_backward_gaussians": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_i, ctypes.POINTER(ViewGrad), _c_p, _c_p,
+         _c_p, _c_p, _c_p, _c_p, _c_p, ctypes.c_uint, _c_p, _c_i, _c_p],
     ),
     "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),

@@ -43,11 +43,17 @@ class GradBucket:
     the bucket (one memset) and every write accumulates.
     """
 
-    def __init__(self, params: Sequence[torch.Tensor], lazy_zero: bool = False):
+    def __init__(self, params: Sequence[torch.Tensor], lazy_zero: bool = False, defer: bool = False):
         from diff_gaussian_rasterization import register_gradient_sink
 
         self.params = list(params)
         self.lazy_zero = lazy_zero
+        # defer=True: a rasterizer backward whose parameter gradients all come here runs only its
+        # per-tile half; the per-Gaussian half of all such views runs in ONE pass at finalize() /
+        # allreduce() (gs_backward_gaussians): every Gaussian's inputs are read and its gradient
+        # row written once per step instead of once per view.  Same fp32 sums as without.
+        self.defers = defer
+        self._deferred = []
         self.numel = sum(p.numel() for p in self.params)
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.zeros((self.numel,), dtype=torch.float32, device=dev)
@@ -120,9 +126,59 @@ class GradBucket:
                                "rasterizer's first write of the step; use lazy_zero=False")
         return v, False
 
+    # ---- deferred per-Gaussian backward (defer=True) ----
+    def defer_view(self, ctx, inputs, view):
+        """Rasterizer protocol: take one view's per-Gaussian backward (its per-tile half and record
+        sums are enqueued on the current stream).  inputs: the Gaussian tensors of the call;
+        view: (viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, W, H, geomBuffer)."""
+        if self._deferred and not _same_inputs(self._deferred[0][0], inputs):
+            self.flush()  # another set of Gaussians: finish the pending views first
+        st = torch.cuda.current_stream(view[7].device)
+        ev = torch.cuda.Event()
+        ev.record(st)
+        sunk = [(name, t) for k, name, t, o in ctx.sinks if o is self and ctx.needs_input_grad[k] and k != 1]
+        self._deferred.append((inputs, view, ev, sunk))
+
+    def flush(self):
+        """Run the pending views' per-Gaussian backward in one pass on the current stream."""
+        if not self._deferred:
+            return
+        from diff_gaussian_rasterization import _C
+
+        inputs = self._deferred[0][0]
+        cur = torch.cuda.current_stream(self.flat.device)
+        for _, _, ev, _ in self._deferred:
+            cur.wait_event(ev)
+        self._join()
+        outs, acc = {}, 0
+        for name, t in self._deferred[0][3]:
+            claim = self.claim(t)
+            if claim is None:
+                raise RuntimeError(f"GradBucket(defer=True): the .grad of the {name} input was replaced before "
+                                   "the deferred backward ran")
+            outs[name], accumulate = claim
+            acc |= _C.GS_ACC[name] if accumulate else 0
+        views = [d[1] for d in self._deferred]
+        _C.backward_gaussians(inputs["means3D"], inputs["sh"], inputs["colors"], inputs["scales"],
+                              inputs["rotations"], inputs["cov3D"], inputs["scale_modifier"], inputs["degree"],
+                              views, outs, acc, debug=inputs["debug"])
+        # the views' buffers were allocated on their own streams: keep them out of reuse there until
+        # this stream's pass is done
+        for v in views:
+            for t in (v[0], v[1], v[2], v[7]):
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(cur)
+        for t in inputs.values():
+            if isinstance(t, torch.Tensor) and t.is_cuda and t.numel():
+                t.record_stream(cur)
+        self.written(cur)
+        self._deferred = []
+
     def finalize(self):
-        """Zero the views no backward wrote this step (lazy mode); then the bucket holds the step's
-        gradient sums (on the current stream: it waits for the last write on any stream)."""
+        """Run any deferred per-Gaussian backward, zero the views no backward wrote this step (lazy
+        mode); then the bucket holds the step's gradient sums (on the current stream: it waits for
+        the last write on any stream)."""
+        self.flush()
         self._join()
         for p in self.params:
             ver = self._fresh.pop(id(p), None)
@@ -147,6 +203,16 @@ class GradBucket:
                     work = None
                 flat.div_(dist.get_world_size(group))
         return work if async_op else flat
+
+
+def _same_inputs(a, b) -> bool:
+    for k in ("means3D", "sh", "colors", "scales", "rotations", "cov3D"):
+        x, y = a[k], b[k]
+        if (x is None) != (y is None):
+            return False
+        if x is not None and (x.data_ptr() != y.data_ptr() or x.shape != y.shape):
+            return False
+    return a["scale_modifier"] == b["scale_modifier"] and a["degree"] == b["degree"]
 
 
 def run_views(view_fns: Sequence, streams: Sequence) -> None:

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 3
+#define GSRAST_ABI_VERSION 4
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -142,6 +142,40 @@ int gs_backward_accumulate(int P, int D, int M, const float* background, int ima
                            void* grad_buffer, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
                            float* dL_drotations, unsigned accumulate, void* wait_event, int debug, void* stream);
+
+/* ---- backward, split for multi-view steps (an extension beyond upstream) ----
+ * A view-parallel step renders K views of ONE set of Gaussians into one gradient bucket
+ * (DESIGN.md §7).  gs_backward splits into its per-tile half and its per-Gaussian half, and the
+ * per-Gaussian half runs once for all K views: every Gaussian's inputs are read and its gradient
+ * row written (or added) once instead of K times.  The bucket receives exactly the fp32 sums that
+ * K gs_backward_accumulate calls in view order produce.
+ *
+ * gs_backward_render: the tile pass and the per-Gaussian record sums of one view, kept in that
+ *   view's geom_buffer (which must stay alive until gs_backward_gaussians has run), plus that
+ *   view's dL_dmeans2D [P,3] (written, or added with GS_ACC_MEANS2D; NULL: not produced).
+ *   Arguments as gs_backward.
+ * gs_backward_gaussians: views[0 .. num_views) in order (any count: more than 8 run as several
+ *   passes); outputs and `accumulate` bits as gs_backward_accumulate (dL_dmeans2D excluded);
+ *   wait_event as gs_backward_accumulate. */
+typedef struct gs_view_grad {
+  const float* viewmatrix; /* 16, device (as the forward's) */
+  const float* projmatrix; /* 16, device */
+  const float* campos;     /* 3, device (NULL only without SHs) */
+  float tan_fovx, tan_fovy;
+  int image_width, image_height;
+  const void* geom_buffer; /* that view's forward state, after its gs_backward_render */
+} gs_view_grad;
+int gs_backward_render(int P, int D, int M, const float* background, int image_width, int image_height,
+                       const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                       float tan_fovy, const void* geom_buffer, long long num_rendered, const void* binning_buffer,
+                       const void* image_buffer, const float* dL_dout_color, void* grad_buffer, float* dL_dmeans2D,
+                       unsigned accumulate, int debug, void* stream);
+int gs_backward_gaussians(int P, int D, int M, const float* means3D, const float* shs, const float* colors_precomp,
+                          const float* scales, float scale_modifier, const float* rotations,
+                          const float* cov3D_precomp, int num_views, const gs_view_grad* views, float* dL_dcolors,
+                          float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                          float* dL_dscales, float* dL_drotations, unsigned accumulate, void* wait_event, int debug,
+                          void* stream);
 
 /* ---- mark_visible: present[P] (uint8 0/1), near-plane test ---- */
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -98,10 +98,12 @@ def _render(rast, p, means2D):
 
 @pytest.mark.parametrize("lazy", [True, False], ids=["lazy_zero", "zero_filled"])
 @pytest.mark.parametrize("nstreams", [1, 2, 3], ids=["1stream", "2streams", "3streams"])
-def test_bucket_accumulation_equals_autograd_sum(device, lazy, nstreams):
+@pytest.mark.parametrize("defer", [False, True], ids=["per_view", "deferred"])
+def test_bucket_accumulation_equals_autograd_sum(device, lazy, nstreams, defer):
     """The bucket equals autograd's per-view gradients summed with += in view order, bit for bit,
     also when the views run round-robin on several streams (vp.run_views: the forward passes and
-    tile backward passes overlap; the bucket orders its writes by events)."""
+    tile backward passes overlap; the bucket orders its writes by events), and when the
+    per-Gaussian half of the backward runs once for all views (defer: gs_backward_gaussians)."""
     import gs_view_parallel as vp
     from diff_gaussian_rasterization import GaussianRasterizer
 
@@ -111,12 +113,13 @@ def test_bucket_accumulation_equals_autograd_sum(device, lazy, nstreams):
     rasts = [GaussianRasterizer(gs_scenes.raster_settings_for(c, 3, device=device)) for c in cams]
     dpix = [gs_scenes.dl_dimage(H, W, seed=40 + v).to(device) for v in range(3)]
     # reference: plain autograd, one fresh gradient per view, summed with += in view order
-    ref = None
+    ref, m2_ref = None, []
     for r, dp in zip(rasts, dpix):
         p = _leaves(d)
         m2 = torch.zeros_like(p[0], requires_grad=True)
         img, _ = _render(r, p, m2)
         img.backward(dp)
+        m2_ref.append(m2.grad.clone())
         g = [t.grad for t in p]
         if ref is None:
             ref = [x.clone() for x in g]
@@ -124,17 +127,20 @@ def test_bucket_accumulation_equals_autograd_sum(device, lazy, nstreams):
             for a, b in zip(ref, g):
                 a += b
     p = _leaves(d)
-    b = vp.GradBucket(p, lazy_zero=lazy)
+    b = vp.GradBucket(p, lazy_zero=lazy, defer=defer)
     calls = []
     orig = b.claim
     b.claim = lambda t: calls.append(1) or orig(t)  # noqa: E731
     streams = [torch.cuda.Stream(device) for _ in range(nstreams)]
+
+    m2s = []
 
     def view(r, dp):
         def run():
             m2 = torch.zeros_like(p[0], requires_grad=True)
             img, _ = _render(r, p, m2)
             img.backward(dp)
+            m2s.append(m2)
         return run
 
     for step in range(2):  # the second step reuses the bucket (stale values must not leak)
@@ -145,7 +151,11 @@ def test_bucket_accumulation_equals_autograd_sum(device, lazy, nstreams):
         for k, (t, x) in enumerate(zip(p, ref)):
             assert t.grad.data_ptr() == b.views[id(t)].data_ptr()
             assert torch.equal(t.grad, x), (step, k, float((t.grad - x).abs().max()))
-    assert len(calls) == 2 * 3 * 5  # every view's backward wrote through the sink
+        for v, (m2, x) in enumerate(zip(m2s, m2_ref)):  # each view's screen-space gradient
+            assert torch.equal(m2.grad, x), (step, v)
+        m2s.clear()
+    # every view's backward wrote through the sink (deferred: one claim per tensor and step)
+    assert len(calls) == (2 * 5 if defer else 2 * 3 * 5)
     b.close()
 
 

@@ -26,7 +26,7 @@ def render_views(d, cams, views, dev):
     params = [d.means3D.clone().requires_grad_(True), d.shs.clone().requires_grad_(True),
               d.opacities.clone().requires_grad_(True), d.scales.clone().requires_grad_(True),
               d.rotations.clone().requires_grad_(True)]
-    bucket = vp.GradBucket(params, lazy_zero=True)
+    bucket = vp.GradBucket(params, lazy_zero=True, defer=True)
     bucket.zero_grad()
     for v in views:
         rast = GaussianRasterizer(gs_scenes.raster_settings_for(cams[v], 3, device=dev))

@@ -1,7 +1,9 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/gputest.log 2>&1; rc=$?
-tail -2 gpurun_out/gputest.log; grep -E "^E  .*Error|FAILED" gpurun_out/gputest.log | head -5
+timeout -k 10 600 python -u -m pytest tests/test_gpu_multiview.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/mv.log 2>&1; rc=$?
+tail -2 gpurun_out/mv.log; grep -E "^E  .*Error|FAILED|^E  " gpurun_out/mv.log | head -8
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py > gpurun_out/bench.json 2>gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
-python -c "import json;d=json.load(open('gpurun_out/bench.json'));print(d['value'], d['ms_per_step'], d['sustained'], d['serial_one_stream'], d['cpu_baseline']['value'])"
+for a in "--no-defer" ""; do
+timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline $a > gpurun_out/b.json 2>gpurun_out/b.err || { tail gpurun_out/b.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/b.json'));print('$a', d['value'], d['ms_per_step'], d['sustained']['iters_s'], d['serial_one_stream'], {k:(v['avg_us'],v['launches_per_step']) for k,v in d['kernels'].items() if 'bwd' in k or 'gauss' in k or 'mean2d' in k or 'sum' in k}, d['step_roofline']['frac'])"
+done
