@@ -6,6 +6,8 @@ scenes only (loops over Gaussians, vectorised over pixels).  Deliberate mirrors 
 behaviour that autograd would not produce on its own:
   - alpha = min(0.99, o*G) with the clamp NOT gating the gradient (straight-through);
   - the quaternion is used un-normalised;
+  - past the 1.3x FoV clamp of the EWA Jacobian the clamped t.x / t.y is held constant (upstream
+    zeroes dL/dt.x there and differentiates J through t.z with the clamped t.x fixed);
   - per-pixel candidate sets are the tile rectangles of the 3-sigma radius (tile binning).
 """
 from __future__ import annotations
@@ -70,8 +72,13 @@ def render(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, b
     fx, fy = W / (2 * tanfovx), H / (2 * tanfovy)
     tz = p_view[:, 2]
     limx, limy = 1.3 * tanfovx, 1.3 * tanfovy
-    tx = torch.clamp(p_view[:, 0] / tz, -limx, limx) * tz
-    ty = torch.clamp(p_view[:, 1] / tz, -limy, limy) * tz
+    txtz, tytz = p_view[:, 0] / tz, p_view[:, 1] / tz
+    tx = torch.clamp(txtz, -limx, limx) * tz
+    ty = torch.clamp(tytz, -limy, limy) * tz
+    # upstream's gradient through the clamp: a clamped t.x / t.y is a constant of the Jacobian
+    # (x_grad_mul = 0 and no tz term through it), not limx * tz
+    tx = torch.where(txtz.abs() > limx, tx.detach(), tx)
+    ty = torch.where(tytz.abs() > limy, ty.detach(), ty)
     zero = torch.zeros_like(tz)
     J = torch.stack([torch.stack([fx / tz, zero, -fx * tx / tz ** 2], -1),
                      torch.stack([zero, fy / tz, -fy * ty / tz ** 2], -1)], -2)

@@ -17,6 +17,10 @@ Reference functions exercised (all on CPU):
                                        on CPU: the module is loaded with empty stand-ins for the two
                                        imports it does not use on this path (plyfile, simple_knn._C) and
                                        the same device="cuda"-dropping torch proxy
+  - gaussian_renderer/__init__.py:18-100  render() with the reference's own Camera (scene/cameras.py:
+                                       17-57; its .cuda() calls made no-ops) and GaussianModel getters
+                                       (:95-118); a recording stand-in for diff_gaussian_rasterization
+                                       captures the settings and inputs it builds (render_golden.npz)
 """
 import math
 import os
@@ -242,6 +246,121 @@ def densify_vectors(gm_mod):
     np.savez_compressed(os.path.join(OUT, "densify_golden.npz"), **out)
 
 
+# render() adapter cases: (W, H, fovy_deg, camera position, target or None for R=I/T=0, sh degree
+# active/max, scale_modifier, compute_cov3D_python, convert_SHs_python)
+RENDER_CASES = {
+    "c1": (256, 256, 60.0, None, None, 0, 0, 1.0, False, False),
+    "c2": (800, 800, 60.0, None, None, 3, 3, 1.0, False, False),
+    "c3": (1920, 1080, 60.0, None, None, 3, 3, 1.0, False, False),
+    "c4v3": (1920, 1080, 60.0, (6.0 * math.cos(2 * math.pi * 3 / 8), 0.0, 6.0 * math.sin(2 * math.pi * 3 / 8)),
+             (0.0, 0.0, 0.0), 3, 3, 1.0, False, False),
+    "ring_py": (96, 64, 50.0, (1.5, -0.4, -3.0), (0.1, 0.2, 0.3), 1, 3, 0.7, True, True),
+}
+
+
+def _look_at_rt(position, target, up=(0.0, -1.0, 0.0)):
+    """(R, T) in the reference loaders' storage convention (R = W2C^T, T = W2C translation) for an
+    OpenCV-axes camera at `position` looking at `target` (the synthetic C4 ring)."""
+    c = np.asarray(position, np.float64)
+    f = np.asarray(target, np.float64) - c
+    f /= np.linalg.norm(f)
+    r = np.cross(f, np.asarray(up, np.float64))
+    r /= np.linalg.norm(r)
+    d = np.cross(f, r)
+    w2c = np.stack([r, d, f], axis=0)
+    return w2c.T, -w2c @ c
+
+
+def render_vectors():
+    """gaussian_renderer/__init__.py:18-100 driven with the reference's own Camera
+    (scene/cameras.py:17-57, its two .cuda() calls made no-ops on CPU) and GaussianModel
+    (getters :95-118), with a recording stand-in for diff_gaussian_rasterization: captures the exact
+    GaussianRasterizationSettings and rasterizer inputs render() hands over."""
+    rec = {}
+
+    class Settings(tuple):
+        _fields = ("image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix",
+                   "projmatrix", "sh_degree", "campos", "prefiltered", "debug")
+
+        def __new__(cls, **kw):
+            rec["settings"] = kw
+            return tuple.__new__(cls, [kw[f] for f in cls._fields])
+
+    class Rasterizer:
+        def __init__(self, raster_settings):
+            self.s = raster_settings
+
+        def __call__(self, **kw):
+            rec["inputs"] = kw
+            P = kw["means3D"].shape[0]
+            return torch.zeros((3, self.s[0], self.s[1])), torch.zeros(P, dtype=torch.int32)
+
+    stub = types.ModuleType("diff_gaussian_rasterization")
+    stub.GaussianRasterizationSettings, stub.GaussianRasterizer = Settings, Rasterizer
+    saved = sys.modules.get("diff_gaussian_rasterization")
+    sys.modules["diff_gaussian_rasterization"] = stub
+    gm = _ref_gaussian_model()
+    sys.modules.pop("gaussian_renderer", None)
+    import gaussian_renderer as gr  # noqa
+    import scene.cameras as cams  # noqa
+    if saved is not None:
+        sys.modules["diff_gaussian_rasterization"] = saved
+
+    class _RendererTorch(_TorchCPUProxy):  # render() allocates its carrier with device="cuda"
+        @staticmethod
+        def zeros_like(*a, **kw):
+            kw.pop("device", None)
+            return torch.zeros_like(*a, **kw)
+
+    gr.torch = _RendererTorch("torch")
+    out = {}
+    cuda = torch.Tensor.cuda
+    for name, (W, H, fovy_deg, pos, tgt, deg_act, deg_max, mod, cov_py, sh_py) in RENDER_CASES.items():
+        if pos is None:
+            R, T = np.eye(3), np.zeros(3)
+        else:
+            R, T = _look_at_rt(pos, tgt)
+        fovy = math.radians(fovy_deg)
+        fovx = 2.0 * math.atan(math.tan(fovy / 2.0) * W / H)
+        torch.Tensor.cuda = lambda self, *a, **k: self
+        try:
+            cam = cams.Camera(colmap_id=0, R=R, T=T, FoVx=fovx, FoVy=fovy, image=torch.zeros((3, H, W)),
+                              gt_alpha_mask=None, image_name=name, uid=0, data_device="cpu")
+        finally:
+            torch.Tensor.cuda = cuda
+        g = torch.Generator().manual_seed(len(name) * 31 + W)
+        P = 64
+        m = gm.GaussianModel(deg_max)
+        m.active_sh_degree = deg_act
+        K = (deg_max + 1) ** 2
+        m._xyz = torch.nn.Parameter(torch.randn((P, 3), generator=g) + torch.tensor([0.0, 0.0, 4.0]))
+        m._features_dc = torch.nn.Parameter(torch.randn((P, 1, 3), generator=g))
+        m._features_rest = torch.nn.Parameter(0.1 * torch.randn((P, K - 1, 3), generator=g))
+        m._opacity = torch.nn.Parameter(torch.randn((P, 1), generator=g))
+        m._scaling = torch.nn.Parameter(math.log(0.05) + torch.randn((P, 3), generator=g))
+        m._rotation = torch.nn.Parameter(torch.randn((P, 4), generator=g))
+        pipe = types.SimpleNamespace(debug=False, compute_cov3D_python=cov_py, convert_SHs_python=sh_py)
+        bg = torch.tensor([0.0, 0.5, 1.0]) if sh_py else torch.zeros(3)
+        rec.clear()
+        gr.render(cam, m, pipe, bg, scaling_modifier=mod)
+        s, x = rec["settings"], rec["inputs"]
+        out[f"{name}_case"] = np.array([W, H, fovy_deg, deg_act, deg_max, mod, cov_py, sh_py], np.float64)
+        out[f"{name}_R"], out[f"{name}_T"] = R, T
+        out[f"{name}_fov"] = np.array([fovx, fovy], np.float64)
+        out[f"{name}_hw"] = np.array([s["image_height"], s["image_width"]], np.int64)
+        out[f"{name}_tanfov"] = np.array([s["tanfovx"], s["tanfovy"]], np.float64)
+        for k in ("bg", "viewmatrix", "projmatrix", "campos"):
+            out[f"{name}_{k}"] = s[k].detach().numpy()
+        out[f"{name}_scalars"] = np.array([s["scale_modifier"], s["sh_degree"], s["prefiltered"], s["debug"]],
+                                          np.float64)
+        for p in ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"):
+            out[f"{name}_param{p}"] = getattr(m, p).detach().numpy()
+        for k, v in x.items():
+            if v is not None:
+                out[f"{name}_in_{k}"] = v.detach().numpy()
+    np.savez_compressed(os.path.join(OUT, "render_golden.npz"), **out)
+
+
 if __name__ == "__main__":
     sh_utils, gu, gfx = _import_ref()
     sh_vectors(sh_utils)
@@ -249,4 +368,5 @@ if __name__ == "__main__":
     camera_vectors(gfx)
     loss_vectors()
     densify_vectors(_ref_gaussian_model())
+    render_vectors()
     print("wrote", sorted(f for f in os.listdir(OUT) if f.endswith(".npz")))

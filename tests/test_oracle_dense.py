@@ -34,8 +34,8 @@ def _oracle_scene(oracle, cam, sc, bg, colors=None, cov3D=None, mod=1.0, deg=Non
                         scale_modifier=mod)
 
 
-def _close(a, b, rtol=2e-4, frac=2e-4, name=""):
-    """|a-b| <= rtol*|b| + frac*max|b| elementwise (fp32 oracle vs fp64 dense)."""
+def _close(a, b, rtol=1e-5, frac=1e-5, name=""):
+    """|a-b| <= rtol*|b| + frac*max|b| elementwise (fp32 oracle vs fp64 dense); default 1e-5 / 1e-5."""
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     tol = rtol * np.abs(b) + frac * max(np.abs(b).max(), 1e-30)
     bad = np.abs(a - b) > tol
@@ -125,3 +125,68 @@ def test_oracle_sorted_list_is_tile_depth_index_ordered(oracle):
         ids = lst[a:b]
         keys = list(zip(depth[ids].view(np.uint32), ids))
         assert keys == sorted(keys)
+
+
+def _wide_scene(P, W, H, deg, seed):
+    """P Gaussians filling a W x H view: centres up to 1.6x the half-FoV (so a share of them sits past
+    the 1.3x tx/tz clamp of the EWA Jacobian while their splats still reach the image), depths 1.5-6,
+    scales 0.04-0.4 (log-uniform; x3 past the clamp), opacities uniform up to 0.999 (the 0.99 alpha clamp fires)."""
+    cam = gs_scenes.identity_camera(W, H, fovy_deg=60.0)
+    g = torch.Generator().manual_seed(seed)
+    tx, ty = math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2)
+    z = 1.5 + 4.5 * torch.rand((P,), generator=g)
+    x = (2 * torch.rand((P,), generator=g) - 1) * 1.6 * tx * z
+    y = (2 * torch.rand((P,), generator=g) - 1) * 1.6 * ty * z
+    sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=seed + 1, scale_range=(0.04, 0.4))
+    sc.means3D = torch.stack([x, y, z], 1).contiguous()  # identity camera: world = camera space
+    outside = (x.abs() > 1.3 * tx * z) | (y.abs() > 1.3 * ty * z)
+    sc.scales[outside] *= 3.0  # big enough to reach into the image from past the clamp
+    sc.opacities = (0.05 + 0.949 * torch.rand((P, 1), generator=g)).contiguous()
+    return cam, sc
+
+
+@pytest.mark.parametrize("deg,W,H,bgv,mod", [(3, 128, 128, 0.0, 1.0), (1, 128, 96, 0.4, 0.8)])
+def test_oracle_vs_dense_500_gaussians_clamp_region(oracle, deg, W, H, bgv, mod):
+    """The oracle's compositing core + analytic backward against the fp64 autograd restatement on 500
+    Gaussians: the tx/tz clamp region, the 0.99 alpha clamp and saturated pixels (T < 1e-4 stop) are
+    all exercised (asserted).  Tolerance 1e-5*|ref| + 1e-5*max|ref| (the north-star bound) on the
+    image and every gradient, the covariance chain (dmeans3D, dscales, drotations) included."""
+    P = 500
+    cam, sc = _wide_scene(P, W, H, deg, seed=100 + deg)
+    bg = np.full(3, bgv, np.float32)
+    osc = _oracle_scene(oracle, cam, sc, bg, mod=mod)
+    fw = oracle.forward(osc, intermediates=True)
+    dpix = gs_scenes.dl_dimage(H, W, seed=7, scale=1.0).numpy()
+    gr = oracle.backward(osc, dpix)
+
+    d = torch.float64
+    m3 = sc.means3D.to(d).requires_grad_(True)
+    m2 = torch.zeros((P, 3), dtype=d, requires_grad=True)
+    op = sc.opacities.to(d).requires_grad_(True)
+    shs = sc.shs.to(d).requires_grad_(True)
+    scl = sc.scales.to(d).requires_grad_(True)
+    rot = sc.rotations.to(d).requires_grad_(True)
+    img, radii = dense_ref.render(m3, m2, op[:, 0], cam.world_view_transform.to(d), cam.full_proj_transform.to(d),
+                                  cam.camera_center.to(d), math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), W, H,
+                                  torch.tensor(bg, dtype=d), shs=shs, deg=deg, scales=scl, rots=rot, mod=mod)
+    np.testing.assert_array_equal(fw["radii"], radii.numpy())
+    vis = fw["radii"] > 0
+    # coverage of the regimes this test is for
+    z = sc.means3D[:, 2].numpy()
+    clamped = (np.abs(sc.means3D[:, 0].numpy() / z) > 1.3 * math.tan(cam.FoVx / 2)) | \
+              (np.abs(sc.means3D[:, 1].numpy() / z) > 1.3 * math.tan(cam.FoVy / 2))
+    assert (clamped & vis).sum() >= 10, f"only {(clamped & vis).sum()} visible Gaussians in the clamp region"
+    assert (sc.opacities.numpy()[vis, 0] > 0.99).sum() >= 3
+    assert (fw["final_T"] < 1e-4).sum() == 0 and (fw["final_T"] < 1e-2).mean() > 0.01  # near-saturated pixels
+    _close(fw["color"], img.detach().numpy(), rtol=1e-5, frac=1e-5, name="image")
+    (img * torch.tensor(dpix, dtype=d)).sum().backward()
+    t = dict(rtol=1e-5, frac=1e-5)
+    _close(gr["dmeans2D"][:, :2], m2.grad[:, :2].numpy(), name="dmeans2D", **t)
+    _close(gr["dopacity"], op.grad.numpy(), name="dopacity", **t)
+    _close(gr["dsh"], shs.grad.numpy(), name="dsh", **t)
+    chain = dict(rtol=1e-5, frac=1e-5)
+    _close(gr["dscales"], scl.grad.numpy(), name="dscales", **chain)
+    _close(gr["drotations"], rot.grad.numpy(), name="drotations", **chain)
+    _close(gr["dmeans3D"], m3.grad.numpy(), name="dmeans3D", **chain)
+    # the clamp region's Gaussians carry gradient through the clamped Jacobian too
+    assert np.abs(gr["dmeans3D"][clamped & vis]).max() > 0
