@@ -109,6 +109,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   __shared__ uint64_t s_mask[BWD_GROUPS][2];  // [64-entry group][half]
   __shared__ float s_acc[2][BWD_BATCH][ACC_STRIDE];
   const uint32_t tile = tile_order ? tile_order[blockIdx.x] : blockIdx.x;
+  if (tile == ~0u) return;  // a hole of the XCD-group launch order (uniform, before any barrier)
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -389,14 +390,15 @@ constexpr int ORDER_THREADS = 256;
 // of them.  A tile's list is in slot order, so k_sum_records keeps a record of slot s in tile T
 // iff s < tile_cut[T] and the backward writes no zero records for the rest.
 __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __restrict__ len_hist,
-                                                              const uint32_t* __restrict__ tile_brank, uint32_t tiles,
-                                                              uint32_t* __restrict__ order,
+                                                              const uint32_t* __restrict__ tile_brank, uint32_t gx,
+                                                              uint32_t gy, uint32_t* __restrict__ order,
                                                               const uint32_t* __restrict__ tile_max,
                                                               const uint2* __restrict__ ranges,
                                                               const uint32_t* __restrict__ point_list,
                                                               uint32_t* __restrict__ tile_cut) {
   __shared__ uint32_t s_base[ORDER_GROUPS][ORDER_BUCKETS];
   const uint32_t tid = threadIdx.x, t = blockIdx.x * ORDER_THREADS + tid, lane = tid & 63, wid = tid >> 6;
+  const uint32_t tiles = gx * gy;
   if (t < tiles) {
     const uint4 q = reinterpret_cast<const uint4*>(tile_max)[t];
     const uint2 r = ranges[t];
@@ -414,22 +416,28 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __
   }
   lds_barrier();
   // the j-th tile of group g (longest first) takes launch position 8 j + g
-  if (t < tiles) order[ORDER_GROUPS * (s_base[t % ORDER_GROUPS][br >> 22] + (br & 0x3FFFFFu)) + t % ORDER_GROUPS] = t;
+  if (t < tiles) {
+    const uint32_t g = xcd_group(t, gx, gy);
+    order[ORDER_GROUPS * (s_base[g][br >> 22] + (br & 0x3FFFFFu)) + g] = t;
+  }
+  // launch positions past the end of their group: holes (the backward skips them)
+  if (t < xcd_slots(tiles) && t / ORDER_GROUPS >= xcd_group_size(t % ORDER_GROUPS, tiles)) order[t] = ~0u;
 }
 
 void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                 const float* dL_dpix, float* gradrec, hipStream_t st) {
   const int tiles = c.gx * c.gy;
   uint32_t* order = img.tile_order;
-  GS_LAUNCH("tile_order", k_tile_order, dim3((tiles + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
-            img.len_hist, img.tile_brank, (uint32_t)tiles, order, img.tile_max, img.ranges, bin.point_list,
-            img.tile_cut);
+  const uint32_t slots = xcd_slots((uint32_t)tiles);
+  GS_LAUNCH("tile_order", k_tile_order, dim3((slots + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
+            img.len_hist, img.tile_brank, (uint32_t)c.gx, (uint32_t)c.gy, order, img.tile_max, img.ranges,
+            bin.point_list, img.tile_cut);
   if (exact_exp())
-    GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,
+    GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(slots), dim3(BWD_THREADS), 0, st, c, img.ranges,
               bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
               dL_dpix, gradrec);
   else
-    GS_LAUNCH("render_bwd", k_render_bwd<false>, dim3(tiles), dim3(BWD_THREADS), 0, st, c, img.ranges,
+    GS_LAUNCH("render_bwd", k_render_bwd<false>, dim3(slots), dim3(BWD_THREADS), 0, st, c, img.ranges,
               bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
               dL_dpix, gradrec);
 }

@@ -584,8 +584,9 @@ __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist,
 // bit of the sum is the tile's longest class (or one above it, when classes coincide and carry),
 // which is all the longest-first order needs.  It takes a rank in that bucket; k_tile_order turns
 // (bucket, rank) into the backward's launch order.
-__device__ __forceinline__ void tile_finish(uint32_t tile, uint32_t wave_last, uint64_t* __restrict__ tile_done,
-                                            uint32_t* __restrict__ len_hist, uint32_t* __restrict__ tile_brank) {
+__device__ __forceinline__ void tile_finish(uint32_t tile, uint32_t grp, uint32_t wave_last,
+                                            uint64_t* __restrict__ tile_done, uint32_t* __restrict__ len_hist,
+                                            uint32_t* __restrict__ tile_brank) {
   // length classes on a log scale, four per octave
   const uint32_t cls = min((uint32_t)(4.0f * __log2f((float)wave_last + 1.0f)), 47u);
   const uint64_t mine = (1ull << (8 + cls)) + 1ull;
@@ -593,7 +594,7 @@ __device__ __forceinline__ void tile_finish(uint32_t tile, uint32_t wave_last, u
   if ((old & 7ull) != 3ull) return;
   const uint32_t top = 63u - (uint32_t)__builtin_clzll((old + mine) >> 8);  // 0 .. 49
   const uint32_t b = (uint32_t)ORDER_BUCKETS - 1u - top;                    // descending length
-  tile_brank[tile] = b << 22 | atomicAdd(&len_hist[(tile % ORDER_GROUPS) * ORDER_BUCKETS + b], 1u);
+  tile_brank[tile] = b << 22 | atomicAdd(&len_hist[grp * ORDER_BUCKETS + b], 1u);
 }
 
 __device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q, bool inside, const FwdPix& px,
@@ -667,15 +668,16 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   const uint32_t wmax = wave_max_u32(px.last);
   if (lane == 0) {
     tile_max[4 * tile + wid] = wmax;
-    tile_finish(tile, wmax, img.tile_done, img.len_hist, img.tile_brank);
+    tile_finish(tile, xcd_group(tile, c.gx, c.gy), wmax, img.tile_done, img.len_hist, img.tile_brank);
   }
 }
 
 // One wave per (tile, quadrant), no workgroup barriers: each wave stages the tile's entries 64 at
 // a time, culls them to its own quadrant and walks them, and finishes as soon as its 64 pixels
-// are done (the workgroup version waits for its slowest quadrant).  Workgroup b takes tile
-// (b / 32) * 8 + b % 8, quadrant (b / 8) % 4, so the four quadrant waves of a tile share the
-// workgroup-to-XCD round robin (b % 8) and their repeated entry loads hit one L2.
+// are done (the workgroup version waits for its slowest quadrant).  Workgroup b takes the
+// (b / 32)-th tile of XCD group b % 8 (xcd_tile), quadrant (b / 8) % 4, so the four quadrant
+// waves of a tile, and (GS_XCD_STRIPS) its neighbour tiles, share the workgroup-to-XCD round
+// robin (b % 8) and their repeated entry loads hit one L2.
 #ifndef GS_FWD_PREFETCH
 #define GS_FWD_PREFETCH 0  // 1 (needs GS_SORT_GID): measured 168 -> 179 us at C3, the loads past the stop are wasted
 #endif
@@ -698,8 +700,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   __shared__ float4 s_ent[3 * FWDQ_NB];
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
   const uint32_t b = blockIdx.x;
-  const uint32_t tile = (b >> 5) * 8 + (b & 7);
-  if (tile >= (uint32_t)(c.gx * c.gy)) return;  // (grid padded to whole groups of 8 tiles)
+  const uint32_t tile = xcd_tile(b & 7, b >> 5, c.gx, c.gy);
+  if (tile == ~0u) return;  // (grid padded to whole groups of 8 tiles)
   const int wid = (int)((b >> 3) & 3);
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int lane = threadIdx.x;
@@ -756,7 +758,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   const uint32_t wmax = wave_max_u32(px.last);
   if (lane == 0) {
     tile_max[4 * tile + wid] = wmax;
-    tile_finish(tile, wmax, img.tile_done, img.len_hist, img.tile_brank);
+    tile_finish(tile, xcd_group(tile, c.gx, c.gy), wmax, img.tile_done, img.len_hist, img.tile_brank);
   }
 }
 
@@ -767,7 +769,7 @@ void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
                 hipStream_t st) {
   const int tiles = c.gx * c.gy;
   if (GS_FWD_WAVE) {
-    const int blocks = ((tiles + 7) / 8) * 32;
+    const int blocks = (int)xcd_span((uint32_t)tiles) * 32;
     if (exact_exp())
       GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
                 GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,

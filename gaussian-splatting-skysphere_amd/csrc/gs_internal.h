@@ -196,10 +196,50 @@ struct ImgPtrs {
 
 // Backward launch order: tiles bucketed by walk length (largest n_contrib), longest first.
 constexpr int ORDER_BUCKETS = 64;
-// Tiles are ordered within ORDER_GROUPS groups (tile % 8): group g fills launch positions
-// g, g + 8, g + 16, ..., the workgroups the dispatcher sends to XCD g as in index order (and the
-// forward's bucket counters are spread over 8x more addresses).
+// Tiles are ordered within ORDER_GROUPS groups: group g fills launch positions g, g + 8, g + 16,
+// ..., the workgroups the dispatcher sends to XCD g (workgroup b runs on XCD b % 8), and the
+// forward places group g's tiles on XCD g the same way.  GS_XCD_STRIPS = 1: group g is the g-th
+// eighth of the tiles in column-major order, a vertical strip of the image, so a splat's
+// neighbouring tiles (both directions) run on one XCD and its record is fetched into one L2;
+// 0: group = tile % 8 (XCD g owns every 8th tile column).
 constexpr int ORDER_GROUPS = 8;
+#ifndef GS_XCD_STRIPS
+#define GS_XCD_STRIPS 0  // 1 measured at C3: render_fwd 174 -> 184 us, render_bwd 404 -> 417 us
+#endif
+// tiles per group (the last groups may hold fewer; their launch positions past it are holes)
+__host__ __device__ inline uint32_t xcd_span(uint32_t tiles) { return (tiles + ORDER_GROUPS - 1) / ORDER_GROUPS; }
+// launch positions of a per-tile grid ordered by XCD group (8 x the largest group)
+__host__ __device__ inline uint32_t xcd_slots(uint32_t tiles) {
+  return GS_XCD_STRIPS ? ORDER_GROUPS * xcd_span(tiles) : tiles;
+}
+__host__ __device__ inline uint32_t xcd_group(uint32_t tile, uint32_t gx, uint32_t gy) {
+#if GS_XCD_STRIPS
+  return ((tile % gx) * gy + tile / gx) / xcd_span(gx * gy);
+#else
+  (void)gx, (void)gy;
+  return tile % ORDER_GROUPS;
+#endif
+}
+__host__ __device__ inline uint32_t xcd_group_size(uint32_t g, uint32_t tiles) {
+#if GS_XCD_STRIPS
+  const uint32_t s = xcd_span(tiles), lo = g * s;
+  return lo >= tiles ? 0u : (tiles - lo < s ? tiles - lo : s);
+#else
+  return (tiles + ORDER_GROUPS - 1 - g) / ORDER_GROUPS;
+#endif
+}
+// the k-th tile of group g (index order within the group; ~0u past its end)
+__host__ __device__ inline uint32_t xcd_tile(uint32_t g, uint32_t k, uint32_t gx, uint32_t gy) {
+  const uint32_t tiles = gx * gy;
+#if GS_XCD_STRIPS
+  const uint32_t p = g * xcd_span(tiles) + k;  // column-major position
+  if (k >= xcd_span(tiles) || p >= tiles) return ~0u;
+  return (p % gy) * gx + p / gy;
+#else
+  const uint32_t t = ORDER_GROUPS * k + g;
+  return t < tiles ? t : ~0u;
+#endif
+}
 
 inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t off = 0;
@@ -212,7 +252,7 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t npix = (size_t)W * H;
   if (tiles == 0) tiles = 1;
   if (npix == 0) npix = 1;
-  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16), o_o = take(tiles * 4), o_c = take(tiles * 4),
+  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16), o_o = take((size_t)xcd_slots((uint32_t)tiles) * 4), o_c = take(tiles * 4),
          o_d = take(tiles * 8 + ORDER_GROUPS * ORDER_BUCKETS * 4), o_b = take(tiles * 4);
   if (out && base) {
     out->ranges = (uint2*)(base + o_r);

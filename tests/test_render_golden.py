@@ -109,7 +109,10 @@ def test_render_inputs_match_reference_getters(device, name):
 @pytest.mark.parametrize("name", CASES)
 def test_reference_render_call_through_rasterizer_vs_oracle(oracle, device, name):
     """The exact settings and inputs render() produced, through the drop-in GaussianRasterizer
-    (exact numerics mode): image bit-exact vs the oracle, gradients at the backward tolerance."""
+    (exact numerics mode): image bit-exact vs the oracle, gradients at the backward tolerance
+    1e-5*|ref| + 1e-5*max|ref|; the conic -> covariance chain (means3D, scales, rotations, cov3D) at
+    1e-5*|ref| + 1e-4*max|ref|, as test_large_and_elongated_splats: the fixture's log-normal
+    scales include splats far larger than the image (conditioning)."""
     from diff_gaussian_rasterization import GaussianRasterizer, _native
 
     lib = _native.load()
@@ -143,7 +146,8 @@ def test_reference_render_call_through_rasterizer_vs_oracle(oracle, device, name
                 continue
             g = leaves[k].grad.detach().cpu().numpy().astype(np.float64)
             r = np.asarray(gr[o], np.float64).reshape(g.shape)
-            tol = 1e-5 * np.abs(r) + 1e-5 * max(np.abs(r).max(), 1e-30)
+            frac = 1e-4 if k in ("means3D", "scales", "rotations", "cov3D_precomp") else 1e-5
+            tol = 1e-5 * np.abs(r) + frac * max(np.abs(r).max(), 1e-30)
             assert (np.abs(g - r) <= tol).all(), f"{k}: max|d| {np.abs(g - r).max():.3e} max|ref| {np.abs(r).max():.3e}"
     finally:
         lib.gs_set_exact_exp(prev)
