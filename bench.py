@@ -94,6 +94,9 @@ def main():
     ap.add_argument("--no-defer", action="store_true",
                     help="run the per-Gaussian backward per view (gs_backward_accumulate) instead of once per "
                          "step for all views (gs_backward_gaussians)")
+    ap.add_argument("--no-train-step", action="store_true",
+                    help="skip the secondary train.py-step measurement (SURVEY §8d metric (2); N=1 only)")
+    ap.add_argument("--train-steps", type=int, default=20, help="timed iterations of the train-step measurement")
     ap.add_argument("--sustain-s", type=float, default=2.0,
                     help="after the timed steps, keep stepping for this long (untimed for `value`) and report "
                          "the sustained rate too")
@@ -322,6 +325,10 @@ def main():
                          achieved=round(step_bytes / (ms_per_view * 1e-3) / 1e9, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                          frac=round(step_bytes / (ms_per_view * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
 
+    train = None
+    if world == 1 and not args.no_train_step and not n_views:
+        train = train_step_bench(sc, cam, deg, dev, args.train_steps, args.workload == "c5")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sc, cam, deg, W, H, dpix.cpu(), args.cpu_threads, args.cpu_runs)
@@ -363,12 +370,65 @@ def main():
         "streams": len(streams),
         "serial_one_stream": serial,
         "kernels": kernels,
+        "train_step": train,
         "cpu_baseline": cpu,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def train_step_bench(sc, cam, deg, dev, steps, densify):
+    """SURVEY §8d metric (2): one full train.py iteration per step (gs_train_step.train_step:
+    render -> L1 + SSIM -> backward -> densification statistics -> Adam -> zero_grad) on the same
+    scene and view against a seeded synthetic target image, with the fused glue and with the
+    reference's torch glue (activations, statistics, Adam); the rasterizer and the loss are the
+    HIP ones in both.  With `densify` (C5): then one densify_and_prune on synthetic statistics
+    (5 % over the threshold, extent 2: clones and splits), and the peak HBM over the train steps
+    and the densify step."""
+    import gs_train_step as ts
+
+    W, H = cam.image_width, cam.image_height
+    settings = gs_scenes.raster_settings_for(cam, deg, device=dev)
+    gt = torch.rand((3, H, W), generator=torch.Generator().manual_seed(2)).to(dev)
+    out = {"what": "train.py:86-128 per iteration (one view): render, L1+SSIM (lambda 0.2), backward, "
+                   "densification stats, Adam step, zero_grad; no loss.item() readback"}
+    for fused in (True, False):
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(dev)
+        base = torch.cuda.memory_allocated(dev)
+        model = ts.TrainModel(sc, dev, fused=fused)
+        for _ in range(3):
+            ts.train_step(model, settings, gt, fused=fused)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(steps):
+            ts.train_step(model, settings, gt, fused=fused)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / steps
+        key = "fused" if fused else "torch_glue"
+        out[key] = {"iters_s": round(1.0 / dt, 2), "ms_per_iter": round(1e3 * dt, 4),
+                    "peak_GB": round((torch.cuda.max_memory_allocated(dev) - base) / 1e9, 3)}
+        if densify and fused:
+            P0 = model.P
+            ts.synthetic_densify_stats(model, frac=0.05, seed=3)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            ts.densify(model, extent=2.0)
+            torch.cuda.synchronize()
+            out["densify"] = {"ms": round(1e3 * (time.perf_counter() - t), 3), "P_before": P0, "P_after": model.P,
+                              "peak_GB_over_train_steps_and_densify":
+                                  round((torch.cuda.max_memory_allocated(dev) - base) / 1e9, 3),
+                              "extent": 2.0, "grad_threshold": ts.DENSIFY_GRAD_THRESHOLD}
+            # one more iteration at the new size (the densified model trains on)
+            ts.train_step(model, settings, gt, fused=True)
+            torch.cuda.synchronize()
+            out["densify"]["peak_GB_incl_next_iteration"] = round(
+                (torch.cuda.max_memory_allocated(dev) - base) / 1e9, 3)
+        del model
+    return out
 
 
 def job_cpus():

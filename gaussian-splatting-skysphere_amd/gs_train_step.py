@@ -1,0 +1,143 @@
+"""One train.py iteration on MI355X, end to end (SURVEY.md §8d metric (2)).
+
+`train_step` runs the per-iteration sequence of /root/reference/train.py:86-128 for one view:
+  render()                      gaussian_renderer/__init__.py:18-100 (activations, screen-space
+                                carrier, GaussianRasterizer forward)
+  loss = (1 - l) L1 + l (1 - SSIM)                     train.py:91-92 (lambda_dssim 0.2)
+  loss.backward()                                      train.py:93
+  max_radii2D / add_densification_stats               train.py:115-116
+  densify_and_prune (`densify`; the caller runs it every 100 iterations)  train.py:118-120
+  optimizer.step(); zero_grad(set_to_none=True)        train.py:127-128
+with this package's HIP paths for every part: gs_train.render_inputs (one activation launch each
+way), the rasterizer, gs_loss.l1_loss / ssim, gs_train.add_densification_stats, FusedAdam,
+gs_train.densify_and_prune.  `fused=False` keeps the rasterizer and the loss but runs the
+reference's own torch glue for activations, densification statistics and Adam (the comparison
+point for the fused glue).
+
+`TrainModel` holds the GaussianModel fields one iteration touches (scene/gaussian_model.py:44-61,
+149-163): the six raw parameters, their Adam groups with training_setup's learning rates, the
+densification statistics, percent_dense and active_sh_degree.  The learning-rate schedule
+(update_learning_rate, only xyz) and reset_opacity stay in the caller, as in the reference.
+"""
+from __future__ import annotations
+
+import torch
+
+import gs_loss
+import gs_train
+from diff_gaussian_rasterization import GaussianRasterizer
+
+# OptimizationParams defaults (/root/reference/arguments/__init__.py:74-83)
+POSITION_LR_INIT = 0.00016
+FEATURE_LR = 0.0025
+OPACITY_LR = 0.05
+SCALING_LR = 0.005
+ROTATION_LR = 0.001
+PERCENT_DENSE = 0.01
+LAMBDA_DSSIM = 0.2
+DENSIFY_GRAD_THRESHOLD = 0.0002
+
+
+class TrainModel:
+    """The GaussianModel state one training iteration reads and writes, built from an activated
+    scene (gs_scenes.GaussianScene): raw parameters are the inverse activations (log scale,
+    inverse-sigmoid opacity; f_dc / f_rest split of the SH rows, gaussian_model.py:133-147)."""
+
+    def __init__(self, scene, device, spatial_lr_scale: float = 1.0, fused: bool = True):
+        d = scene.to(device)
+        P = d.means3D.shape[0]
+        op = d.opacities.clamp(1e-6, 1 - 1e-6)
+        raw = {
+            "_xyz": d.means3D.clone(),
+            "_features_dc": d.shs[:, :1].clone().contiguous(),
+            "_features_rest": d.shs[:, 1:].clone().contiguous(),
+            "_opacity": torch.log(op / (1 - op)),  # inverse_sigmoid (general_utils.py:17)
+            "_scaling": torch.log(d.scales),
+            "_rotation": d.rotations.clone(),
+        }
+        for k, v in raw.items():
+            setattr(self, k, torch.nn.Parameter(v.contiguous().requires_grad_(True)))
+        self.active_sh_degree = self.max_sh_degree = scene.sh_degree
+        self.percent_dense = PERCENT_DENSE
+        self.spatial_lr_scale = spatial_lr_scale
+        groups = [
+            {"params": [self._xyz], "lr": POSITION_LR_INIT * spatial_lr_scale, "name": "xyz"},
+            {"params": [self._features_dc], "lr": FEATURE_LR, "name": "f_dc"},
+            {"params": [self._features_rest], "lr": FEATURE_LR / 20.0, "name": "f_rest"},
+            {"params": [self._opacity], "lr": OPACITY_LR, "name": "opacity"},
+            {"params": [self._scaling], "lr": SCALING_LR, "name": "scaling"},
+            {"params": [self._rotation], "lr": ROTATION_LR, "name": "rotation"},
+        ]
+        opt = gs_train.FusedAdam if fused else torch.optim.Adam
+        self.optimizer = opt(groups, lr=0.0, eps=1e-15)
+        self.max_radii2D = torch.zeros((P,), device=device)
+        self.xyz_gradient_accum = torch.zeros((P, 1), device=device)
+        self.denom = torch.zeros((P, 1), device=device)
+
+    @property
+    def P(self) -> int:
+        return self._xyz.shape[0]
+
+    # the reference getters in torch (gaussian_model.py:95-115), for fused=False
+    def torch_render_inputs(self):
+        return (self._xyz, torch.cat((self._features_dc, self._features_rest), dim=1), torch.sigmoid(self._opacity),
+                torch.exp(self._scaling), torch.nn.functional.normalize(self._rotation))
+
+
+def render(model: TrainModel, settings, fused: bool = True):
+    """gaussian_renderer.render() for the default pipe (SH and covariance in the rasterizer)."""
+    means3D, shs, opacity, scales, rotations = gs_train.render_inputs(model) if fused else model.torch_render_inputs()
+    screenspace_points = torch.zeros_like(means3D, requires_grad=True) + 0  # __init__.py:26
+    screenspace_points.retain_grad()
+    image, radii = GaussianRasterizer(raster_settings=settings)(
+        means3D=means3D, means2D=screenspace_points, shs=shs, colors_precomp=None, opacities=opacity, scales=scales,
+        rotations=rotations, cov3D_precomp=None)
+    return image, screenspace_points, radii
+
+
+def _torch_densification_stats(model: TrainModel, viewspace, radii):
+    vis = radii > 0  # train.py:115-116, gaussian_model.py:405-407
+    model.max_radii2D[vis] = torch.max(model.max_radii2D[vis], radii[vis].to(model.max_radii2D.dtype))
+    model.xyz_gradient_accum[vis] += torch.norm(viewspace.grad[vis, :2], dim=-1, keepdim=True)
+    model.denom[vis] += 1
+
+
+def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool = True, densify_stats: bool = True,
+               lambda_dssim: float = LAMBDA_DSSIM) -> torch.Tensor:
+    """One iteration (module docstring).  Returns the loss tensor (not read back: the reference's
+    `loss.item()` for its progress bar, train.py:99, is left to the caller)."""
+    image, viewspace, radii = render(model, settings, fused)
+    Ll1 = gs_loss.l1_loss(image, gt_image)
+    loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - gs_loss.ssim(image, gt_image))
+    loss.backward()
+    with torch.no_grad():
+        if densify_stats:
+            if fused:
+                gs_train.add_densification_stats(model, viewspace, radii)
+            else:
+                _torch_densification_stats(model, viewspace, radii)
+        model.optimizer.step()
+        model.optimizer.zero_grad(set_to_none=True)
+    return loss
+
+
+def synthetic_densify_stats(model: TrainModel, frac: float = 0.05, seed: int = 0,
+                            threshold: float = DENSIFY_GRAD_THRESHOLD) -> None:
+    """Densification statistics for a densify step on synthetic gradients:
+    denom ~ U{1..4}, mean view-space gradient ~ U(0, threshold / (1 - frac)), so a fraction `frac`
+    of the Gaussians crosses densify_grad_threshold (clone or split by their scale)."""
+    g = torch.Generator(device=model._xyz.device).manual_seed(seed)
+    P = model.P
+    dev = model._xyz.device
+    model.denom = torch.randint(1, 5, (P, 1), generator=g, device=dev).float()
+    mean_grad = torch.rand((P, 1), generator=g, device=dev) * (threshold / (1.0 - frac))
+    model.xyz_gradient_accum = mean_grad * model.denom
+
+
+def densify(model: TrainModel, extent: float, max_screen_size=20,
+            threshold: float = DENSIFY_GRAD_THRESHOLD) -> None:
+    """train.py:118-120: densify_and_prune(densify_grad_threshold, 0.005, cameras_extent, 20).
+    `extent` is scene.cameras_extent (getNerfppNorm's radius, scene/dataset_readers.py:45-66); a
+    single synthetic camera has none, so callers pass one."""
+    gs_train.densify_and_prune(model, threshold, 0.005, extent, max_screen_size)
+
