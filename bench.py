@@ -325,6 +325,17 @@ def main():
                          achieved=round(step_bytes / (ms_per_view * 1e-3) / 1e9, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                          frac=round(step_bytes / (ms_per_view * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
 
+    # initialisation kNN (simple_knn distCUDA2 over the scene's P means, as create_from_pcd calls it,
+    # scene/gaussian_model.py:134): one timed call after a warm-up
+    from simple_knn._C import distCUDA2
+
+    distCUDA2(params[0].detach())
+    torch.cuda.synchronize()
+    tk = time.perf_counter()
+    distCUDA2(params[0].detach())
+    torch.cuda.synchronize()
+    knn = {"points": P, "ms": round(1e3 * (time.perf_counter() - tk), 3)}
+
     train = None
     if world == 1 and not args.no_train_step and not n_views:
         train = train_step_bench(sc, cam, deg, dev, args.train_steps, args.workload == "c5")
@@ -371,6 +382,7 @@ def main():
         "serial_one_stream": serial,
         "kernels": kernels,
         "train_step": train,
+        "init_knn": knn,
         "cpu_baseline": cpu,
     }
     if rank == 0:

@@ -546,6 +546,40 @@ def test_knn_matches_oracle(oracle, device, P):
     np.testing.assert_allclose(got, ref, rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize("P,ball", [(1_000_000, False), (1_000_000, True), (5_000_000, False)],
+                         ids=["C3_1M_frustum", "C4_1M_ball", "C5_5M_frustum"])
+def test_knn_init_scale_vs_kdtree(device, P, ball):
+    """distCUDA2 at the size GaussianModel.create_from_pcd calls it (scene/gaussian_model.py:134: the
+    whole initial point cloud): exact 3-NN mean squared distance of 20k sampled points against a
+    scipy k-d tree over all P points (fp64 distances of the same fp32 coordinates; rtol 1e-6), and
+    the call's time."""
+    from scipy.spatial import cKDTree
+
+    from simple_knn._C import distCUDA2
+
+    cam = gs_scenes.identity_camera(1920, 1080)
+    sc = gs_scenes.random_gaussians(P, 0, cam=None if ball else cam, seed=11, ball_radius=2.0 if ball else None)
+    pts = sc.means3D
+    dp = pts.to(device)
+    distCUDA2(dp)  # warm-up (first-call allocations)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    got = distCUDA2(dp)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    got = got.cpu().numpy()
+    x = pts.numpy().astype(np.float64)
+    tree = cKDTree(x)
+    q = np.random.default_rng(P).choice(P, 20_000, replace=False)
+    d, _ = tree.query(x[q], k=4)  # the point itself first (distance 0)
+    ref = (d[:, 1:] ** 2).mean(axis=1)
+    np.testing.assert_allclose(got[q], ref, rtol=1e-6, atol=0)
+    assert np.isfinite(got).all() and (got > 0).all()
+    print(f"\n[distCUDA2 P={P} {'ball' if ball else 'frustum'}] {ms:.2f} ms")
+
+
 @pytest.mark.parametrize("P", [1_000_000, 5_000_000], ids=["C3_1M", "C5_5M"])
 def test_large_c3_properties(device, P):
     """C3 / C5 sizes (1M / 5M Gaussians SH3, 1920x1080) -- size-independent properties instead of
