@@ -247,6 +247,12 @@ struct DstOffsets {
   }
 };
 
+#ifndef GS_TILE_SORT_BLOCKS
+#define GS_TILE_SORT_BLOCKS 4096  // workgroups per tile-sort pass (sort_plan)
+#endif
+#ifndef GS_DEPTH_SORT_BLOCKS
+#define GS_DEPTH_SORT_BLOCKS 4096  // workgroups per depth-sort pass (sort_plan)
+#endif
 void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
   const uint32_t n = (uint32_t)P;
   // depth sort of the Gaussians with instances: the first pass reads all P keys in index order
@@ -256,7 +262,8 @@ void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
     // tile ids); it gathers each rank's tile count (the gather is cheaper here than carrying the
     // counts through the four sort passes)
     radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
-                     geo.sort_scratch, st, /*drop_first=*/true);
+                     geo.sort_scratch, st, /*drop_first=*/true, false, nullptr, nullptr, nullptr, nullptr,
+                     GS_DEPTH_SORT_BLOCKS);
     scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid, n}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
                       &geo.counters[CNT_V], n, geo.lb_status, &geo.counters[CNT_LB_TILE], &geo.counters[CNT_I],
                       &geo.counters[CNT_ERR], st);
@@ -468,7 +475,7 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
   bool hist0 = false;
   if (dup_balanced(I, (uint32_t)P)) {
     // one duplicate block per sort tile: the duplicate also counts the first sort pass's digits
-    hist0 = sort_plan(I).chunk == DUP_SLOTS;
+    hist0 = sort_plan(I, GS_TILE_SORT_BLOCKS).chunk == DUP_SLOTS;
     GS_LAUNCH("duplicate", k_duplicate_lb, dim3((I + DUP_SLOTS - 1) / DUP_SLOTS), dim3(DUP_THREADS), 0, st, I,
               geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy,
               bin.slot_tile, bin.presort_gid, img.ranges, hist0 ? bin.sort_scratch : nullptr,
@@ -481,7 +488,8 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
   // GS_SORT_GID: the Gaussian ids travel with the slots (aux stream): the renders then read
   // point_gid contiguously instead of gathering presort_gid[slot]
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tbits, bin.sort_scratch, st,
-                   false, hist0, GS_SORT_GID ? bin.presort_gid : nullptr, bin.aux_a, bin.presort_gid, bin.slot_tile);
+                   false, hist0, GS_SORT_GID ? bin.presort_gid : nullptr, bin.aux_a, bin.presort_gid, bin.slot_tile,
+                   GS_TILE_SORT_BLOCKS);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges,
             (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS, (uint32_t)tiles);
 }

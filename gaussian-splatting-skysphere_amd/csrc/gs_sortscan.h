@@ -328,10 +328,13 @@ inline int radix_first_bits(int end_bit) {
   return GS_SORT_NARROW_FIRST ? end_bit - (radix_passes(end_bit) - 1) * w : w;
 }
 
-inline SortPlan sort_plan(uint64_t n_max) {
+// max_blocks: workgroups per pass (each takes whole 2048-key tiles); fewer, longer workgroups
+// make the [digit][block] histogram and its row scan smaller
+inline SortPlan sort_plan(uint64_t n_max, uint32_t max_blocks = SORT_MAX_BLOCKS) {
   uint64_t tiles = (n_max + SORT_TILE - 1) / SORT_TILE;
   if (tiles == 0) tiles = 1;
-  uint64_t per = (tiles + SORT_MAX_BLOCKS - 1) / SORT_MAX_BLOCKS;
+  if (max_blocks == 0 || max_blocks > SORT_MAX_BLOCKS) max_blocks = SORT_MAX_BLOCKS;
+  uint64_t per = (tiles + max_blocks - 1) / max_blocks;
   SortPlan p;
   p.nb = (uint32_t)((tiles + per - 1) / per);
   p.chunk = (uint32_t)(per * SORT_TILE);
@@ -546,8 +549,8 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
                                     uint32_t* scratch, hipStream_t st, bool drop_first = false,
                                     bool hist0_ready = false, const uint32_t* aux0 = nullptr,
                                     uint32_t* aux_a = nullptr, uint32_t* aux_b = nullptr,
-                                    const uint32_t* keys_in0 = nullptr) {
-  SortPlan p = sort_plan(n_max);
+                                    const uint32_t* keys_in0 = nullptr, uint32_t max_blocks = SORT_MAX_BLOCKS) {
+  SortPlan p = sort_plan(n_max, max_blocks);
   uint32_t* hist = scratch;
   const size_t hist_n = (size_t)RADIX * p.nb;
   uint32_t* row_total = scratch + hist_n;
