@@ -62,7 +62,17 @@ def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None, acc_frac=0.0, K=1):
     npix = W * H
     sh = 12 * M
     E = I if E is None else E
+    # sorts, averaged over one view's launches: depth passes (4) -- the first reads the P keys in
+    # index order and writes the V kept (key, id) pairs, the others move V pairs; above 1M
+    # Gaussians the tile counts travel with them (aux); tile passes (2) over I pairs, the first
+    # with identity ids (keys read only).  Histograms read one key per element.
+    aux = P > 1_048_576
+    depth_scatter = P * 4 + V * 8 + 3 * V * 16 + (P * 4 + V * 4 + 3 * V * 8 if aux else 0)
+    tile_scatter = I * (4 + 8) + I * 16
+    tile_hists = 2 if I > 4096 * 2048 else 1  # the duplicate counts the first tile pass up to 8M
     return {
+        "radix_scatter": (depth_scatter + tile_scatter) // 6,
+        "radix_hist": (P * 4 + 3 * V * 4 + tile_hists * I * 4) // (4 + tile_hists),
         "preprocess": P * (44 + sh + 4 + 4) + V * (48 + 32 + 4 + 1),
         "render_fwd": E * (4 + 4 + 48) + npix * 20 + tiles * 12,
         "render_bwd": E * (4 + 4 + 48 + 36) + npix * 20 + tiles * 12,
