@@ -88,8 +88,9 @@ def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None, acc_frac=0.0, K=1):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed steps (4 views each by default: ~0.4 s at C3, long enough for an external utilisation sampler)")
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
