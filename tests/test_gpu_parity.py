@@ -636,3 +636,49 @@ def test_large_scene_sort_path_vs_oracle(oracle, device):
     dpix = gs_scenes.dl_dimage(H, W, seed=22).numpy()
     _, _, leaves = _gpu_run(cam, sc, device, bg, dpix)
     _check_backward(oracle.backward(osc, dpix), leaves)
+
+
+def _random_case(seed, oracle):
+    """One randomized configuration: camera pose, ragged image size, P, SH degree (active <= max),
+    background, scale modifier, precomputed colours / covariances, scale range."""
+    rng = np.random.default_rng(1000 + seed)
+    W, H = int(rng.integers(17, 300)), int(rng.integers(13, 220))
+    fovy = float(rng.uniform(35.0, 80.0))
+    pos = rng.normal(size=3) * rng.uniform(0.0, 2.0)
+    tgt = pos + np.array([0.0, 0.0, 4.0]) + rng.normal(size=3) * 0.8
+    cam = gs_scenes.look_at_camera(tuple(pos), tuple(tgt), W, H, fovy)
+    P = int(rng.integers(1, 6000))
+    deg_max = int(rng.integers(0, 4))
+    deg = int(rng.integers(0, deg_max + 1))
+    lo = float(rng.uniform(0.002, 0.02))
+    sc = gs_scenes.random_gaussians(P, deg_max, cam=cam, seed=2000 + seed, scale_range=(lo, lo * rng.uniform(2, 12)),
+                                    z_range=(float(rng.uniform(0.5, 3.0)), float(rng.uniform(4.0, 20.0))))
+    bg = rng.random(3).astype(np.float32) * (rng.random() < 0.5)
+    mod = float(rng.uniform(0.5, 1.5)) if rng.random() < 0.5 else 1.0
+    colors = rng.random((P, 3), dtype=np.float32) if rng.random() < 0.25 else None
+    cov = None
+    if rng.random() < 0.25:
+        cov = np.ascontiguousarray(oracle.cov3d(sc.scales.numpy(), mod, sc.rotations.numpy()))
+    return cam, sc, bg, mod, deg, colors, cov
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_randomized_configurations_vs_oracle(oracle, device, seed):
+    """Randomized cameras (off-axis poses, FoV 35-80 deg, ragged image sizes), scene sizes, active /
+    max SH degree, background, scale modifier and precomputed colour / covariance inputs, in the
+    exact numerics mode: image and radii bit-exact against the oracle (plus every forward
+    intermediate when scale_modifier is 1), gradients at the backward tolerance (covariance chain
+    at 1e-4 of its max: random scales include large splats)."""
+    cam, sc, bg, mod, deg, colors, cov = _random_case(seed, oracle)
+    W, H = cam.image_width, cam.image_height
+    cov_mod = 1.0 if cov is not None else mod  # a precomputed covariance already carries the modifier
+    osc = _oracle_scene(oracle, cam, sc, bg, colors=colors, cov3D=cov, deg=deg, mod=cov_mod)
+    ofw = oracle.forward(osc, intermediates=True)
+    ofw["bg"] = bg
+    if cov_mod == 1.0:
+        _check_forward_exact(ofw, cam, sc, device, colors=colors, cov3D=cov, deg=deg)
+    dpix = gs_scenes.dl_dimage(H, W, seed=seed, scale=1.0).numpy()
+    img, radii, leaves = _gpu_run(cam, sc, device, bg, dpix, colors=colors, cov3D=cov, deg=deg, mod=cov_mod)
+    np.testing.assert_array_equal(radii.cpu().numpy(), ofw["radii"])
+    np.testing.assert_array_equal(img.detach().cpu().numpy(), ofw["color"])
+    _check_backward(oracle.backward(osc, dpix), leaves, colors=colors, cov3D=cov, chain_frac=1e-4)
