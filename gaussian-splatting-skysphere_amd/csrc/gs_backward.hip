@@ -496,22 +496,34 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
   uint32_t jbase = 0xFFFFFFFFu;  // (number of owners starting before `base`) - 1
   // records of the next chunk are loaded one chunk ahead (their HBM latency overlaps this chunk)
   float vn[GRAD_REC];
+  unsigned long long hn;  // lanes of the next chunk that hold a record
   {
     const uint32_t kk = S0 + lane;
 #pragma unroll
     for (int c = 0; c < GRAD_REC; c++) vn[c] = 0.0f;
-    if (kk < S1 && kk < tile_cut[slot_tile[kk]]) load_rec(gradrec + (size_t)kk * GRAD_REC, vn);
+    const bool h = kk < S1 && kk < tile_cut[slot_tile[kk]];
+    if (h) load_rec(gradrec + (size_t)kk * GRAD_REC, vn);
+    hn = __ballot(h);
   }
   for (uint32_t base = S0; base < S1; base += 64) {
     float v[GRAD_REC];
 #pragma unroll
     for (int c = 0; c < GRAD_REC; c++) v[c] = vn[c];
+    const unsigned long long hc = hn;
     if (base + 64 < S1) {
       // records past their tile's cut were never written: zeros (no load)
       const uint32_t kn = base + 64 + lane;
 #pragma unroll
       for (int c = 0; c < GRAD_REC; c++) vn[c] = 0.0f;
-      if (kn < S1 && kn < tile_cut[slot_tile[kn]]) load_rec(gradrec + (size_t)kn * GRAD_REC, vn);
+      const bool h = kn < S1 && kn < tile_cut[slot_tile[kn]];
+      if (h) load_rec(gradrec + (size_t)kn * GRAD_REC, vn);
+      hn = __ballot(h);
+    }
+    if (hc == 0) {
+      // no record in the chunk (every slot behind its tile's walk, as for most of a dense
+      // scene's instances): only count the owners that start in it
+      jbase += (uint32_t)__popcll(__ballot(my_off >= base && my_off < base + 64));
+      continue;
     }
     // slots of the chunk that start an owner -> bit mask -> owner of my slot by popcount
     if (lane == 0) s_mark[wid] = 0ull;
