@@ -34,7 +34,7 @@ import torch.distributed as dist  # noqa: E402
 
 import gs_scenes  # noqa: E402
 import gs_view_parallel as vp  # noqa: E402
-from diff_gaussian_rasterization import GaussianRasterizer, _C, _native  # noqa: E402
+from diff_gaussian_rasterization import GaussianRasterizer, _C, _native, prepare_views  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E
 # wave64 VALU issue peak: 256 CUs x 4 SIMD32 x 2.4 GHz / 2 cycles per wave64 instruction
@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the views of a step are spread over (view k on stream k mod n): one "
                          "view's sorts and scans overlap another's tile passes; 1 = strictly serial")
+    ap.add_argument("--no-fused-front", action="store_true",
+                    help="run each view's preprocess in its own launch instead of one launch for the step's views "
+                         "(prepare_views / gs_forward_preprocess_views)")
     ap.add_argument("--no-defer", action="store_true",
                     help="run the per-Gaussian backward per view (gs_backward_accumulate) instead of once per "
                          "step for all views (gs_backward_gaussians)")
@@ -155,22 +158,30 @@ def main():
 
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
 
-    def view_fn(r):
+    def view_fn(r, pre=None):
         def run():
             # a fresh screen-space carrier per render, as the reference's render() makes
             # (gaussian_renderer/__init__.py:24); its gradient is not kept here
             m2 = torch.zeros_like(params[0], requires_grad=True)
             img, _ = r(means3D=params[0], means2D=m2, opacities=params[2], shs=params[1], scales=params[3],
-                       rotations=params[4])
+                       rotations=params[4], prepared=pre)
             img.backward(dpix)
         return run
 
     view_fns = [view_fn(r) for r in rasts]
+    fused_front = not args.no_fused_front and len(rasts) > 1
 
     def step(sts=streams):
         bucket.zero_grad()
+        fns = view_fns
+        if fused_front:
+            # the step's views' preprocess in one launch (each Gaussian's inputs read once), each
+            # view's depth order on its stream; then every view's binning, render and backward
+            pre = prepare_views(rasts, params[0], params[2], shs=params[1], scales=params[3], rotations=params[4],
+                                streams=[sts[k % len(sts)] for k in range(len(rasts))])
+            fns = [view_fn(r, p) for r, p in zip(rasts, pre)]
         # this rank's views, round-robin over the streams: gradients accumulate in the bucket
-        vp.run_views(view_fns, sts)
+        vp.run_views(fns, sts)
         if world > 1:
             bucket.allreduce()  # one RCCL all-reduce of the 59-f32/Gaussian bucket, in place
         else:
@@ -390,6 +401,7 @@ def main():
         "step_roofline": step_roofline,
         "sustained": sustained,
         "streams": len(streams),
+        "fused_front": fused_front,
         "serial_one_stream": serial,
         "kernels": kernels,
         "train_step": train,

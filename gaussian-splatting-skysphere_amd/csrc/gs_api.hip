@@ -308,6 +308,68 @@ int gs_forward_preprocess(int P, int D, int M, const float* background, int W, i
   return 0;
 }
 
+int gs_forward_preprocess_views(int K, int P, int D, int M, const float* const* background, const int* image_width,
+                                const int* image_height, const float* means3D, const float* shs,
+                                const float* colors_precomp, const float* opacities, const float* scales,
+                                float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                const float* const* viewmatrix, const float* const* projmatrix,
+                                const float* const* campos, const float* tan_fovx, const float* tan_fovy,
+                                int prefiltered, int* const* radii_out, void* const* geom_buffer,
+                                long long* num_rendered_host, int debug, void* stream, void* const* view_streams) {
+  clear_error(debug);
+  if (K <= 0 || K > FUSED_MAX_VIEWS) return set_error("views: 1 to 8 per call"), 1;
+  if (!background || !image_width || !image_height || !viewmatrix || !projmatrix || !campos || !tan_fovx ||
+      !tan_fovy || !radii_out || !geom_buffer || !num_rendered_host)
+    return set_error("missing per-view argument array"), 1;
+  for (int v = 0; v < K; v++) {
+    num_rendered_host[v] = 0;
+    if (!validate(P, D, M, image_width[v], image_height[v], means3D, shs, colors_precomp, opacities, scales, rotations,
+                  cov3D_precomp, viewmatrix[v], projmatrix[v], campos[v], background[v]))
+      return 1;
+    if (P > 0 && (!radii_out[v] || !geom_buffer[v])) return set_error("missing output pointer"), 1;
+  }
+  if (P == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier};
+  PreViews pv;
+  pv.K = K;
+  for (int v = 0; v < K; v++) {
+    pv.c[v] = make_camera(background[v], image_width[v], image_height[v], viewmatrix[v], projmatrix[v], campos[v],
+                          tan_fovx[v], tan_fovy[v], prefiltered);
+    pv.radii[v] = radii_out[v];
+    geom_layout((size_t)P, &pv.geo[v], (char*)geom_buffer[v]);
+  }
+  static thread_local uint32_t* host = nullptr;  // pinned: K x 8 counters
+  static thread_local hipEvent_t ev = nullptr, ev_pre = nullptr;
+  if (!host) {
+    void* p = nullptr;
+    if (!check_hip(hipHostMalloc(&p, 32 * FUSED_MAX_VIEWS, hipHostMallocDefault), "hipHostMalloc")) return 1;
+    if (!check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate")) return 1;
+    if (!check_hip(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming), "hipEventCreate")) return 1;
+    host = (uint32_t*)p;
+  }
+  if (check_order_flags()) return 1;  // an earlier forward's look-back waits
+  fwd_preprocess_views(g, pv, st);
+  for (int v = 0; v < K; v++)
+    check_hip(hipMemcpyAsync(host + 8 * v, pv.geo[v].counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
+  check_hip(hipEventRecord(ev, st), "hipEventRecord");
+  // each view's ordering on its own stream (view_streams[v], or `stream`), after the preprocess
+  check_hip(hipEventRecord(ev_pre, st), "hipEventRecord");
+  for (int v = 0; v < K; v++) {
+    hipStream_t vs = view_streams && view_streams[v] ? (hipStream_t)view_streams[v] : st;
+    if (vs != st) check_hip(hipStreamWaitEvent(vs, ev_pre, 0), "hipStreamWaitEvent");
+    fwd_order(P, pv.geo[v], vs);
+  }
+  check_hip(hipEventSynchronize(ev), "hipEventSynchronize");
+  if (t_failed) return 1;
+  for (int v = 0; v < K; v++) {
+    if (host[8 * v + CNT_ERR] & 1u)
+      return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
+    num_rendered_host[v] = (long long)host[8 * v + CNT_NREND];
+  }
+  return 0;
+}
+
 int gs_forward_render(int P, const float* background, int W, int H, const float* viewmatrix, const float* projmatrix,
                       const float* campos, float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
                       long long num_rendered, void* binning_buffer, void* image_buffer, float* out_color, int debug,

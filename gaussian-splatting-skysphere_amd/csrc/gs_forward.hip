@@ -218,6 +218,58 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
   }
 }
 
+// K views in one launch: every lane runs the single-view preprocess of its Gaussian for each
+// camera in turn (preprocess_one, so each view's outputs are bit-identical to its own launch);
+// the Gaussian's inputs come from HBM once, the later views read them from the caches.  The
+// per-view workgroup totals go to each view's counters as in k_preprocess.
+template <int DEG>
+__global__ __launch_bounds__(256) void k_preprocess_views(GaussianArgs g, PreViews pv) {
+  __shared__ uint32_t s_sum[4], s_vis[4];
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  for (int v = 0; v < pv.K; v++) {
+    const GeomPtrs& geo = pv.geo[v];
+    uint32_t area = 0, dbits = 0;
+    if (i < g.P) {
+      area = preprocess_one<DEG>(i, g, pv.c[v], pv.radii[v], geo.splat, geo.binrec, dbits, geo.tiles, geo.clamped,
+                                 geo.counters);
+      geo.keys_a[i] = area ? dbits : DEPTH_DROP;
+    }
+    uint32_t vis = area ? 1u : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      area += (uint32_t)__shfl_xor((int)area, d, 64);
+      vis += (uint32_t)__shfl_xor((int)vis, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      s_sum[threadIdx.x >> 6] = area;
+      s_vis[threadIdx.x >> 6] = vis;
+    }
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+      const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
+      if (tot)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&geo.counters[CNT_NREND]), ((unsigned long long)nv << 32) | tot);
+    }
+    lds_barrier();  // s_sum / s_vis are reused by the next view
+  }
+}
+
+void fwd_preprocess_views(const GaussianArgs& g, const PreViews& pv, hipStream_t st) {
+  for (int v = 0; v < pv.K; v++) (void)hipMemsetAsync(pv.geo[v].counters, 0, 64, st);
+  dim3 grid((g.P + 255) / 256), block(256);
+  if (g.colors) {
+    GS_LAUNCH("preprocess_views", k_preprocess_views<-1>, grid, block, 0, st, g, pv);
+    return;
+  }
+  switch (g.D) {
+    case 0: GS_LAUNCH("preprocess_views", k_preprocess_views<0>, grid, block, 0, st, g, pv); break;
+    case 1: GS_LAUNCH("preprocess_views", k_preprocess_views<1>, grid, block, 0, st, g, pv); break;
+    case 2: GS_LAUNCH("preprocess_views", k_preprocess_views<2>, grid, block, 0, st, g, pv); break;
+    default: GS_LAUNCH("preprocess_views", k_preprocess_views<3>, grid, block, 0, st, g, pv); break;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // ordering: compaction -> depth sort -> instance offsets
 // ------------------------------------------------------------------------------------------

@@ -305,6 +305,15 @@ struct FusedViews {
   ViewGrad v[FUSED_MAX_VIEWS];
 };
 void bwd_gaussians(const GaussianArgs& g, const FusedViews& fv, const GradOut& out, hipStream_t st);
+// preprocess of K views of one set of Gaussians in one launch (gs_forward_preprocess_views): each
+// view's outputs exactly as fwd_preprocess writes them into that view's geometry buffer
+struct PreViews {
+  int K;
+  CameraArgs c[FUSED_MAX_VIEWS];
+  int* radii[FUSED_MAX_VIEWS];
+  GeomPtrs geo[FUSED_MAX_VIEWS];
+};
+void fwd_preprocess_views(const GaussianArgs& g, const PreViews& pv, hipStream_t st);
 // the per-tile half of a split backward: record sums into the geom buffer (+ dL/dmeans2D)
 void bwd_records(const GaussianArgs& g, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* gradrec,
                  bool have_records, float* dmean2D, uint32_t acc, hipStream_t st);

@@ -94,9 +94,51 @@ class _Inputs:
         return (_ptr(self.means3D), _ptr(self.sh), _ptr(self.colors), _ptr(self.opacity), _ptr(self.scales))
 
 
+def preprocess_views(backgrounds, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                     viewmatrices, projmatrices, tan_fovx, tan_fovy, image_heights, image_widths, sh, degree, campos,
+                     prefiltered, debug, streams=None):
+    """First half of K views' forwards in one preprocess launch (gs_forward_preprocess_views):
+    returns [(num_rendered, radii, geomBuffer)] per view, each what rasterize_gaussians computes for
+    that camera before its binning; view k's depth ordering is enqueued on streams[k] (default:
+    the current stream).  Pass each view's triple to rasterize_gaussians(..., prepared=)."""
+    K = len(viewmatrices)
+    if not 1 <= K <= 8:
+        raise RuntimeError("preprocess_views: 1 to 8 views per call")
+    xs = [_Inputs(backgrounds[k], means3D, colors, opacity, scales, rotations, cov3D_precomp, viewmatrices[k],
+                  projmatrices[k], sh, campos[k]) for k in range(K)]
+    x, dev = xs[0], xs[0].device
+    u8 = dict(dtype=torch.uint8, device=dev)
+    radii = [torch.empty((x.P,), dtype=torch.int32, device=dev) for _ in range(K)]
+    geoms = [torch.empty((_lib.gs_geom_buffer_bytes(x.P) if x.P else 0,), **u8) for _ in range(K)]
+    if x.P == 0:
+        return [(0, r, g) for r, g in zip(radii, geoms)]
+    arr = lambda ts: (ctypes.c_void_p * K)(*[t.data_ptr() if t is not None else None for t in ts])  # noqa: E731
+    nr = (ctypes.c_longlong * K)()
+    vst = None
+    if streams is not None:
+        vst = (ctypes.c_void_p * K)(*[s.cuda_stream for s in streams])
+    with torch.cuda.device(dev):
+        _native.check(
+            _lib.gs_forward_preprocess_views(
+                K, x.P, int(degree), x.M, arr([y.bg for y in xs]), (ctypes.c_int * K)(*[int(w) for w in image_widths]),
+                (ctypes.c_int * K)(*[int(h) for h in image_heights]), _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors),
+                _ptr(x.opacity), _ptr(x.scales), float(scale_modifier), _ptr(x.rotations), _ptr(x.cov3D),
+                arr([y.view for y in xs]), arr([y.proj for y in xs]), arr([y.campos for y in xs]),
+                (ctypes.c_float * K)(*[float(t) for t in tan_fovx]), (ctypes.c_float * K)(*[float(t) for t in tan_fovy]),
+                int(bool(prefiltered)), arr(radii), arr(geoms), nr, int(bool(debug)), _stream(dev), vst),
+            "preprocess_views")
+    if streams is not None:  # the buffers are used on the views' streams
+        for k, s in enumerate(streams):
+            radii[k].record_stream(s)
+            geoms[k].record_stream(s)
+    return [(int(nr[k]), radii[k], geoms[k]) for k in range(K)]
+
+
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, debug):
+                        prefiltered, debug, prepared=None):
+    """prepared: (num_rendered, radii, geomBuffer) of this call from preprocess_views (the first
+    half already ran); otherwise both halves run here."""
     x = _Inputs(background, means3D, colors, opacity, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
                 campos)
     H, W = int(image_height), int(image_width)
@@ -109,19 +151,24 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                 torch.empty((0,), **u8), torch.empty((0,), **u8), torch.empty((0,), **u8))
     # every pixel of the image and every radius is written by the kernels
     out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
-    radii = torch.empty((x.P,), dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
         st = _stream(dev)
-        geom = torch.empty((_lib.gs_geom_buffer_bytes(x.P),), **u8)
-        nr = ctypes.c_longlong(0)
-        _native.check(
-            _lib.gs_forward_preprocess(
-                x.P, int(degree), x.M, _ptr(x.bg), W, H, _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors),
-                _ptr(x.opacity), _ptr(x.scales), float(scale_modifier), _ptr(x.rotations), _ptr(x.cov3D),
-                _ptr(x.view), _ptr(x.proj), _ptr(x.campos), float(tan_fovx), float(tan_fovy), int(bool(prefiltered)),
-                _ptr(radii), _ptr(geom), ctypes.byref(nr), int(bool(debug)), st),
-            "rasterize_gaussians (preprocess)")
-        num_rendered = int(nr.value)
+        if prepared is not None:
+            num_rendered, radii, geom = prepared
+            if radii.numel() != x.P or geom.numel() != _lib.gs_geom_buffer_bytes(x.P):
+                raise RuntimeError("rasterize_gaussians: the prepared view does not match these inputs")
+        else:
+            radii = torch.empty((x.P,), dtype=torch.int32, device=dev)
+            geom = torch.empty((_lib.gs_geom_buffer_bytes(x.P),), **u8)
+            nr = ctypes.c_longlong(0)
+            _native.check(
+                _lib.gs_forward_preprocess(
+                    x.P, int(degree), x.M, _ptr(x.bg), W, H, _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors),
+                    _ptr(x.opacity), _ptr(x.scales), float(scale_modifier), _ptr(x.rotations), _ptr(x.cov3D),
+                    _ptr(x.view), _ptr(x.proj), _ptr(x.campos), float(tan_fovx), float(tan_fovy),
+                    int(bool(prefiltered)), _ptr(radii), _ptr(geom), ctypes.byref(nr), int(bool(debug)), st),
+                "rasterize_gaussians (preprocess)")
+            num_rendered = int(nr.value)
         binning = torch.empty((_lib.gs_binning_buffer_bytes(num_rendered, W, H),), **u8)
         img = torch.empty((_lib.gs_image_buffer_bytes(W, H),), **u8)
         _native.check(

@@ -30,7 +30,7 @@ import torch.nn as nn
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "cpu_deep_copy_tuple",
-           "register_gradient_sink", "unregister_gradient_sink"]
+           "register_gradient_sink", "unregister_gradient_sink", "prepare_views"]
 
 # ------------------------------------------------------------------------------------------
 # Gradient sinks (an extension beyond the upstream API, used by gs_view_parallel.GradBucket).
@@ -91,9 +91,56 @@ class GaussianRasterizationSettings(NamedTuple):
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                        raster_settings):
+                        raster_settings, prepared=None):
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
-                                     cov3Ds_precomp, raster_settings)
+                                     cov3Ds_precomp, raster_settings, prepared)
+
+
+class PreparedView:
+    """The first half of one view's forward, computed by prepare_views for several views at once
+    (an extension beyond the upstream API).  Hand it to that view's GaussianRasterizer call as
+    `prepared=`; it is checked against the call's settings and inputs and used once."""
+
+    def __init__(self, triple, settings, inputs):
+        self.triple, self.settings, self.inputs = triple, settings, inputs
+
+    def take(self, settings, inputs):
+        if self.triple is None:
+            raise RuntimeError("prepare_views: a prepared view is used once")
+        if settings is not self.settings or any(
+                (a is None) != (b is None) or (a is not None and (a.data_ptr(), a.shape) != (b.data_ptr(), b.shape))
+                for a, b in zip(inputs, self.inputs)):
+            raise RuntimeError("prepare_views: the rasterizer call does not match the prepared view")
+        t, self.triple = self.triple, None
+        return t
+
+
+def prepare_views(rasterizers, means3D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                  cov3D_precomp=None, streams=None):
+    """Run the first half of the forward (preprocess, depth order, instance offsets) of several
+    views of the same Gaussians at once: one preprocess launch reads every Gaussian's inputs once
+    for all cameras (gs_forward_preprocess_views) and one host wait returns every view's instance
+    count.  Returns one PreparedView per rasterizer, to pass as `prepared=` to that rasterizer's
+    call with the same tensors; view k's ordering runs on streams[k] (its call must run there).
+    The rasterizers must share sh_degree, scale_modifier, prefiltered and debug."""
+    ss = [r.raster_settings for r in rasterizers]
+    s0 = ss[0]
+    for s in ss[1:]:
+        if (s.sh_degree, s.scale_modifier, s.prefiltered, s.debug) != (s0.sh_degree, s0.scale_modifier,
+                                                                          s0.prefiltered, s0.debug):
+            raise ValueError("prepare_views: the views must share sh_degree, scale_modifier, prefiltered, debug")
+    empty = torch.Tensor([])
+    e = lambda t: empty if t is None else t  # noqa: E731
+    with torch.no_grad():
+        tri = _C.preprocess_views([s.bg for s in ss], means3D.detach(), e(colors_precomp).detach(), opacities.detach(),
+                                  e(scales).detach(), e(rotations).detach(), s0.scale_modifier,
+                                  e(cov3D_precomp).detach(), [s.viewmatrix.contiguous() for s in ss],
+                                  [s.projmatrix.contiguous() for s in ss], [s.tanfovx for s in ss],
+                                  [s.tanfovy for s in ss], [s.image_height for s in ss], [s.image_width for s in ss],
+                                  e(shs).detach(), s0.sh_degree, [s.campos for s in ss], s0.prefiltered, s0.debug,
+                                  streams)
+    inputs = (means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp)
+    return [PreparedView(t, s, inputs) for t, s in zip(tri, ss)]
 
 
 def _run_with_snapshot(fn, args, debug, dump_name, phase):
@@ -112,7 +159,7 @@ def _run_with_snapshot(fn, args, debug, dump_name, phase):
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings):
+                raster_settings, prepared=None):
         s = raster_settings
         # the camera matrices arrive transposed (cameras.py:54-56 world_view_transform is a
         # .transpose(0, 1) view); make them contiguous once and reuse them in backward
@@ -120,8 +167,15 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
                 view, proj, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
                 s.campos, s.prefiltered, s.debug)
-        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _run_with_snapshot(
-            _C.rasterize_gaussians, args, s.debug, "snapshot_fw.dump", "forward")
+        if prepared is not None:
+            nz = lambda t: None if t is None or t.numel() == 0 else t  # noqa: E731
+            tri = prepared.take(s, (means3D, nz(sh), nz(colors_precomp), opacities, nz(scales), nz(rotations),
+                                    nz(cov3Ds_precomp)))
+            num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(*args,
+                                                                                                     prepared=tri)
+        else:
+            num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _run_with_snapshot(
+                _C.rasterize_gaussians, args, s.debug, "snapshot_fw.dump", "forward")
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
         ctx.matrices = (view, proj)
@@ -138,7 +192,7 @@ class _RasterizeGaussians(torch.autograd.Function):
     def backward(ctx, grad_out_color, _grad_radii):
         s = ctx.raster_settings
         if grad_out_color is None:  # the colour output did not reach the loss
-            return (None,) * 9
+            return (None,) * 10
         colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer, imgBuffer = (
             ctx.saved_tensors)
         view, proj = ctx.matrices
@@ -160,7 +214,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                                           degree=s.sh_degree, debug=s.debug),
                                 (view, proj, s.campos, s.tanfovx, s.tanfovy, s.image_width, s.image_height,
                                  geomBuffer))
-            return (None, dm2) + (None,) * 7
+            return (None, dm2) + (None,) * 8
 
         sinks, sunk, owners = {}, set(), []
         for k, name, t, owner in ctx.sinks:
@@ -190,7 +244,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             if hasattr(o, "written"):
                 o.written(st)
         grads = [grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
-                 grad_rotations, grad_cov3Ds_precomp, None]
+                 grad_rotations, grad_cov3Ds_precomp, None, None]
         for k in sunk:  # already in the sink's buffer (the tensor's .grad)
             grads[k] = None
         return tuple(grads)
@@ -222,7 +276,8 @@ class GaussianRasterizer(nn.Module):
             return _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
 
     def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
-                cov3D_precomp=None):
+                cov3D_precomp=None, prepared=None):
+        """prepared: this call's PreparedView from prepare_views (extension; default: none)."""
         s = self.raster_settings
         if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
             raise Exception("Please provide excatly one of either SHs or precomputed colors!")
@@ -236,4 +291,4 @@ class GaussianRasterizer(nn.Module):
         rotations = empty if rotations is None else rotations
         cov3D_precomp = empty if cov3D_precomp is None else cov3D_precomp
         return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
-                                   s)
+                                   s, prepared)

@@ -41,6 +41,11 @@ SIGNATURES = {
         [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
          _c_f, _c_f, _c_i, _c_p, _c_p, ctypes.POINTER(_c_ll), _c_i, _c_p],
     ),
+    "gs_forward_preprocess_views": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_p, _c_p, _c_i, _c_p, _c_p, ctypes.POINTER(_c_ll), _c_i, _c_p, _c_p],
+    ),
     "gs_forward_render": (
         _c_i,
         [_c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_i, _c_p],

@@ -18,6 +18,7 @@
  *                                                  reference's `param.grad += g` of autograd,
  *                                                  train.py:93, fused into the last kernel)
  *   gs_mark_visible                            <-  _C.mark_visible(...)
+ *   gs_forward_preprocess_views                <-  (extension) the first half of K views' forwards
  *   gs_knn_mean_dist2                          <-  simple_knn._C.distCUDA2(points)
  *                                                  (/root/reference/scene/gaussian_model.py:20,134)
  *   gs_ssim_forward / gs_ssim_backward         <-  utils.loss_utils.ssim(img1, img2)
@@ -54,7 +55,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 4
+#define GSRAST_ABI_VERSION 5
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -77,6 +78,21 @@ int gs_forward_preprocess(int P, int D, int M, const float* background, int imag
                           const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
                           int prefiltered, int* radii_out, void* geom_buffer, long long* num_rendered_host,
                           int debug, void* stream);
+
+/* ---- forward, part 1 for K views of one set of Gaussians (1 <= K <= 8, view-parallel steps) ----
+ * One preprocess launch projects every Gaussian into the K cameras (its inputs are read from HBM
+ * once); view v's radii_out[v] and geom_buffer[v] hold exactly what gs_forward_preprocess writes
+ * for that camera.  Then view v's depth order is enqueued on view_streams[v] (NULL: on `stream`)
+ * after the preprocess, and one host wait reads the K num_rendered.  Per-view arguments are host
+ * arrays of K entries.  Then gs_forward_render per view, on its stream. */
+int gs_forward_preprocess_views(int K, int P, int D, int M, const float* const* background, const int* image_width,
+                                const int* image_height, const float* means3D, const float* shs,
+                                const float* colors_precomp, const float* opacities, const float* scales,
+                                float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                const float* const* viewmatrix, const float* const* projmatrix,
+                                const float* const* campos, const float* tan_fovx, const float* tan_fovy,
+                                int prefiltered, int* const* radii_out, void* const* geom_buffer,
+                                long long* num_rendered_host, int debug, void* stream, void* const* view_streams);
 
 /* ---- forward, part 2: duplicate, tile sort, ranges, compositing ----
  * out_color[3, H, W] fp32 (CHW).  binning_buffer >= gs_binning_buffer_bytes(num_rendered, W, H),

@@ -21,7 +21,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), f"libgsrast.so does not export {s}"
     assert set(syms) == set(_native.SIGNATURES), set(syms) ^ set(_native.SIGNATURES)
-    assert lib.gs_abi_version() == 4
+    assert lib.gs_abi_version() == 5
 
 
 def test_sizing_functions_run_without_gpu():

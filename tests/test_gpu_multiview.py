@@ -371,3 +371,56 @@ def test_c4_ring_views_full_size(oracle, device):
         _check_backward(oracle.backward(osc, dp), leaves)
     finally:
         _lib().gs_set_exact_exp(prev)
+
+
+def test_prepared_views_equal_single_view_calls(device):
+    """prepare_views (one preprocess launch for several cameras, gs_forward_preprocess_views) then
+    each view's call with prepared=: images, radii and every gradient bit-identical to plain
+    per-view calls, with the views' orderings on two streams."""
+    from diff_gaussian_rasterization import GaussianRasterizer, prepare_views
+
+    W, H = 320, 200
+    cams = gs_scenes.circle_cameras(5, 6.0, W, H)
+    sc = gs_scenes.random_gaussians(20000, 3, seed=21, ball_radius=2.0).to(device)
+    rasts = [GaussianRasterizer(gs_scenes.raster_settings_for(c, 3, device=device)) for c in cams]
+    dpix = gs_scenes.dl_dimage(H, W, seed=4, scale=1.0).to(device)
+
+    def run(prepared):
+        leaves = [t.clone().requires_grad_(True) for t in (sc.means3D, sc.shs, sc.opacities, sc.scales, sc.rotations)]
+        sts = [torch.cuda.Stream(device) for _ in range(2)]
+        pre = (prepare_views(rasts, leaves[0], leaves[2], shs=leaves[1], scales=leaves[3], rotations=leaves[4],
+                             streams=[sts[k % 2] for k in range(len(rasts))]) if prepared else [None] * len(rasts))
+        outs = []
+        main = torch.cuda.current_stream()
+        for st in sts:
+            st.wait_stream(main)
+        for k, (r, p) in enumerate(zip(rasts, pre)):
+            with torch.cuda.stream(sts[k % 2]):
+                m2 = torch.zeros_like(leaves[0], requires_grad=True)
+                img, radii = r(means3D=leaves[0], means2D=m2, opacities=leaves[2], shs=leaves[1], scales=leaves[3],
+                               rotations=leaves[4], prepared=p)
+                (img * dpix).sum().backward()
+                outs.append((img.detach().clone(), radii.clone(), m2.grad.clone()))
+        for st in sts:
+            main.wait_stream(st)
+        torch.cuda.synchronize()
+        return outs, [t.grad.clone() for t in leaves]
+
+    a_out, a_grad = run(False)
+    b_out, b_grad = run(True)
+    for (ia, ra, ma), (ib, rb, mb) in zip(a_out, b_out):
+        assert torch.equal(ia, ib) and torch.equal(ra, rb) and torch.equal(ma, mb)
+        assert (ra > 0).any()
+    for ga, gb in zip(a_grad, b_grad):
+        assert torch.equal(ga, gb)
+    # a prepared view is checked against the call and used once
+    pre = prepare_views(rasts[:2], sc.means3D, sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    m2 = torch.zeros_like(sc.means3D)
+    with pytest.raises(RuntimeError, match="does not match"):
+        rasts[1](means3D=sc.means3D, means2D=m2, opacities=sc.opacities, shs=sc.shs, scales=sc.scales,
+                 rotations=sc.rotations, prepared=pre[0])
+    rasts[0](means3D=sc.means3D, means2D=m2, opacities=sc.opacities, shs=sc.shs, scales=sc.scales,
+             rotations=sc.rotations, prepared=pre[0])
+    with pytest.raises(RuntimeError, match="used once"):
+        rasts[0](means3D=sc.means3D, means2D=m2, opacities=sc.opacities, shs=sc.shs, scales=sc.scales,
+                 rotations=sc.rotations, prepared=pre[0])
