@@ -74,6 +74,7 @@ def kernel_bytes(name, P, V, I, M, W, H, tiles, E=None, acc_frac=0.0, K=1):
         "radix_scatter": (depth_scatter + tile_scatter) // 6,
         "radix_hist": (P * 4 + 3 * V * 4 + tile_hists * I * 4) // (4 + tile_hists),
         "preprocess": P * (44 + sh + 4 + 4) + V * (48 + 32 + 4 + 1),
+        "preprocess_views": P * (44 + sh + 4 + 4) + K * V * (48 + 32 + 4 + 1),
         "render_fwd": E * (4 + 4 + 48) + npix * 20 + tiles * 12,
         "render_bwd": E * (4 + 4 + 48 + 36) + npix * 20 + tiles * 12,
         "sum_records": E * 36 + I * 4 + V * (4 + 36),
