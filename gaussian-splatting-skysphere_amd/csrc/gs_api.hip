@@ -636,6 +636,29 @@ int gs_ssim_backward(int planes, int channels, int H, int W, const float* window
   return t_failed ? 1 : 0;
 }
 
+/* ---- fused photometric loss (train.py:91-92) ---- */
+int gs_photometric_loss_forward(int planes, int H, int W, const float* window11_host, const float* img,
+                                const float* gt, float lambda_dssim, float* dmaps, float* partial, float* out3,
+                                void* stream) {
+  clear_error(0);
+  if (planes <= 0 || H <= 0 || W <= 0) return set_error("photometric loss: empty image"), 1;
+  if (!window11_host || !img || !gt || !dmaps || !partial || !out3)
+    return set_error("photometric loss: missing pointer"), 1;
+  photometric_forward(planes, H, W, window11_host, img, gt, lambda_dssim, dmaps, partial, out3, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
+int gs_photometric_loss_backward(int planes, int H, int W, const float* window11_host, const float* img,
+                                 const float* gt, const float* dmaps, float lambda_dssim, const float* grad,
+                                 float* dimg, void* stream) {
+  clear_error(0);
+  if (planes <= 0 || H <= 0 || W <= 0) return set_error("photometric loss: empty image"), 1;
+  if (!window11_host || !img || !gt || !dmaps || !grad || !dimg)
+    return set_error("photometric loss: missing pointer"), 1;
+  photometric_backward(planes, H, W, window11_host, img, gt, dmaps, lambda_dssim, grad, dimg, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
 /* ---- fused optimizer step and densification statistics (train.py:114-124) ---- */
 int gs_adam_step(int count, float* const* params_host, const float* const* grads_host, float* const* exp_avg_host,
                  float* const* exp_avg_sq_host, const long long* numel_host, const double* lr_host,

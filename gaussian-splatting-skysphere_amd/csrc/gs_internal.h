@@ -326,6 +326,10 @@ void ssim_forward(int planes, int H, int W, const float* win11, const float* img
 void ssim_backward(int planes, int C, int H, int W, const float* win11, const float* img1, const float* img2,
                    const float* dmaps, const float* scale, float* dimg1, hipStream_t st);
 size_t ssim_partial_count(int planes, int H, int W);
+void photometric_forward(int planes, int H, int W, const float* win11, const float* img, const float* gt,
+                         float lambda, float* dmaps, float* partial, float* out3, hipStream_t st);
+void photometric_backward(int planes, int H, int W, const float* win11, const float* img, const float* gt,
+                          const float* dmaps, float lambda, const float* grad, float* dimg, hipStream_t st);
 constexpr int ADAM_MAX_TENSORS = 16;  // parameter tensors per Adam launch
 void adam_step(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                float* const* exp_avg_sq, const long long* numel, const double* lr, const long long* step,

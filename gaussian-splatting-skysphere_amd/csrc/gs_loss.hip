@@ -34,10 +34,10 @@ __device__ __forceinline__ float ld_plane(const float* p, int H, int W, int y, i
 
 __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, SsimWin win, const float* __restrict__ img1,
                                                   const float* __restrict__ img2, float* __restrict__ dmaps,
-                                                  float* __restrict__ partial) {
+                                                  float* __restrict__ partial, float* __restrict__ partial_l1) {
   __shared__ float sx[SS_IN][SS_LD], sy[SS_IN][SS_LD];
   __shared__ float sh[5][SS_IN][SS_T + 1];
-  __shared__ float s_red[4];
+  __shared__ float s_red[2][4];
   const int plane = blockIdx.z;
   const int x0 = blockIdx.x * SS_T, y0 = blockIdx.y * SS_T;
   const size_t HW = (size_t)H * W;
@@ -97,13 +97,58 @@ __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, SsimWin win, con
     dmaps[2 * PHW + o] = 2.f * A1 * iB;                                 // dS/dE[xy]
   }
   float v = inside ? S : 0.f;
+  // |x - y| of the pixel (the L1 term of the fused photometric loss), from the staged tile
+  float l = inside ? fabsf(sx[ty + SS_R][tx + SS_R] - sy[ty + SS_R][tx + SS_R]) : 0.f;
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  if ((tid & 63) == 0) s_red[tid >> 6] = v;
+  for (int d = 32; d >= 1; d >>= 1) {
+    v += __shfl_xor(v, d, 64);
+    l += __shfl_xor(l, d, 64);
+  }
+  if ((tid & 63) == 0) {
+    s_red[0][tid >> 6] = v;
+    s_red[1][tid >> 6] = l;
+  }
   lds_barrier();
-  if (tid == 0)
-    partial[((size_t)plane * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] =
-        (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+  const size_t t = ((size_t)plane * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  if (tid == 0) partial[t] = (s_red[0][0] + s_red[0][1]) + (s_red[0][2] + s_red[0][3]);
+  if (tid == 1 && partial_l1) partial_l1[t] = (s_red[1][0] + s_red[1][1]) + (s_red[1][2] + s_red[1][3]);
+}
+
+// The fused photometric loss of train.py:91-92 from the per-tile partials, in a fixed order (fp64):
+// out = [(1 - lambda) L1 + lambda (1 - SSIM), L1, SSIM], means over all n pixels of all planes
+// (loss_utils.py:17-18 and size_average=True of :40, which average over the same elements)
+__global__ __launch_bounds__(1024) void k_loss_finish(int count, double inv_n, float lambda,
+                                                      const float* __restrict__ partial,
+                                                      const float* __restrict__ partial_l1, float* __restrict__ out) {
+  __shared__ double s[2][16];
+  double a = 0.0, b = 0.0;
+  for (int i = threadIdx.x; i < count; i += 1024) {
+    a += (double)partial[i];
+    b += (double)partial_l1[i];
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    a += __shfl_xor(a, d, 64);
+    b += __shfl_xor(b, d, 64);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    s[0][w] = a;
+    s[1][w] = b;
+  }
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    double sa = 0.0, sb = 0.0;
+    for (int k = 0; k < 16; k++) {
+      sa += s[0][k];
+      sb += s[1][k];
+    }
+    // the value as the reference's float32 expression forms it from the two float32 means
+    const float ssim = (float)(sa * inv_n), l1 = (float)(sb * inv_n);
+    out[0] = (1.0f - lambda) * l1 + lambda * (1.0f - ssim);
+    out[1] = l1;
+    out[2] = ssim;
+  }
 }
 
 // per-plane SSIM-map sums in a fixed order (one workgroup per plane)
@@ -122,9 +167,14 @@ __global__ __launch_bounds__(256) void k_ssim_plane_sum(int tiles, const float* 
   if (threadIdx.x == 0) plane_sum[blockIdx.x] = (float)s[0];
 }
 
+// FUSED: the photometric loss's gradient, dimg1 = g (kS dSSIM-sum/dimg1 + kL sign(img1 - img2)) with
+// g = scale[0] (the loss's incoming gradient, on the device), kS = -lambda / n, kL = (1 - lambda) / n;
+// otherwise dimg1 = scale[plane / C] dSSIM-sum/dimg1.
+template <bool FUSED>
 __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, int C, SsimWin win, const float* __restrict__ img1,
                                                   const float* __restrict__ img2, const float* __restrict__ dmaps,
-                                                  const float* __restrict__ scale, float* __restrict__ dimg1) {
+                                                  const float* __restrict__ scale, float kS, float kL,
+                                                  float* __restrict__ dimg1) {
   __shared__ float sd[3][SS_IN][SS_LD];
   __shared__ float sh[3][SS_IN][SS_T + 1];
   const int plane = blockIdx.z;
@@ -166,7 +216,14 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, int C, SsimWin w
   }
   const size_t o = plane * HW + (size_t)py * W + px;
   const float x = img1[o], y = img2[o];
-  dimg1[o] = scale[plane / C] * (g0 + 2.f * x * g1 + y * g2);
+  const float dS = g0 + 2.f * x * g1 + y * g2;
+  if constexpr (FUSED) {
+    // d|u|/du = sign(u), 0 at u = 0 (torch's abs backward)
+    const float u = x - y, sg = u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f);
+    dimg1[o] = scale[0] * __builtin_fmaf(kS, dS, kL * sg);
+  } else {
+    dimg1[o] = scale[plane / C] * dS;
+  }
 }
 
 void ssim_forward(int planes, int H, int W, const float* win11, const float* img1, const float* img2, float* dmaps,
@@ -174,8 +231,29 @@ void ssim_forward(int planes, int H, int W, const float* win11, const float* img
   SsimWin w;
   for (int k = 0; k < 2 * SS_R + 1; k++) w.w[k] = win11[k];
   const dim3 grid((W + SS_T - 1) / SS_T, (H + SS_T - 1) / SS_T, planes);
-  GS_LAUNCH("ssim_fwd", k_ssim_fwd, grid, dim3(256), 0, st, H, W, w, img1, img2, dmaps, partial);
+  GS_LAUNCH("ssim_fwd", k_ssim_fwd, grid, dim3(256), 0, st, H, W, w, img1, img2, dmaps, partial, nullptr);
   GS_LAUNCH("ssim_sum", k_ssim_plane_sum, dim3(planes), dim3(256), 0, st, (int)(grid.x * grid.y), partial, plane_sum);
+}
+
+void photometric_forward(int planes, int H, int W, const float* win11, const float* img, const float* gt,
+                         float lambda, float* dmaps, float* partial, float* out3, hipStream_t st) {
+  SsimWin w;
+  for (int k = 0; k < 2 * SS_R + 1; k++) w.w[k] = win11[k];
+  const dim3 grid((W + SS_T - 1) / SS_T, (H + SS_T - 1) / SS_T, planes);
+  const int count = (int)ssim_partial_count(planes, H, W);
+  GS_LAUNCH("ssim_fwd", k_ssim_fwd, grid, dim3(256), 0, st, H, W, w, img, gt, dmaps, partial, partial + count);
+  GS_LAUNCH("loss_finish", k_loss_finish, dim3(1), dim3(1024), 0, st, count,
+            1.0 / ((double)planes * (double)H * (double)W), lambda, partial, partial + count, out3);
+}
+
+void photometric_backward(int planes, int H, int W, const float* win11, const float* img, const float* gt,
+                          const float* dmaps, float lambda, const float* grad, float* dimg, hipStream_t st) {
+  SsimWin w;
+  for (int k = 0; k < 2 * SS_R + 1; k++) w.w[k] = win11[k];
+  const dim3 grid((W + SS_T - 1) / SS_T, (H + SS_T - 1) / SS_T, planes);
+  const double n = (double)planes * (double)H * (double)W;
+  GS_LAUNCH("ssim_bwd", k_ssim_bwd<true>, grid, dim3(256), 0, st, H, W, 1, w, img, gt, dmaps, grad,
+            (float)(-(double)lambda / n), (float)((1.0 - (double)lambda) / n), dimg);
 }
 
 void ssim_backward(int planes, int C, int H, int W, const float* win11, const float* img1, const float* img2,
@@ -183,7 +261,8 @@ void ssim_backward(int planes, int C, int H, int W, const float* win11, const fl
   SsimWin w;
   for (int k = 0; k < 2 * SS_R + 1; k++) w.w[k] = win11[k];
   const dim3 grid((W + SS_T - 1) / SS_T, (H + SS_T - 1) / SS_T, planes);
-  GS_LAUNCH("ssim_bwd", k_ssim_bwd, grid, dim3(256), 0, st, H, W, C, w, img1, img2, dmaps, scale, dimg1);
+  GS_LAUNCH("ssim_bwd", k_ssim_bwd<false>, grid, dim3(256), 0, st, H, W, C, w, img1, img2, dmaps, scale, 0.0f, 0.0f,
+            dimg1);
 }
 
 size_t ssim_partial_count(int planes, int H, int W) {

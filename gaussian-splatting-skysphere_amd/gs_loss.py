@@ -7,6 +7,12 @@ forward (separable 11-tap window through LDS, SSIM map sum, per-pixel partials) 
 backward (csrc/gs_loss.hip, C ABI gs_ssim_forward / gs_ssim_backward).  Same signature, same
 value (fp32), same gradient w.r.t. the rendered image; the target image gets no gradient (as in
 train.py, where it is data).  Use:  `from gs_loss import l1_loss, ssim`.
+
+`photometric_loss(image, gt, lambda_dssim)` is the whole expression of train.py:91-92 fused
+(SURVEY.md §8f row 4): the SSIM kernel also sums |image - gt| per tile, one fixed-order reduction
+forms `(1 - lambda) L1 + lambda (1 - SSIM)` on the device, and one backward kernel writes both
+terms' gradient -- no elementwise / reduction kernels of torch around it.  It returns the loss and
+the L1 term (detached, for the reference's logging of Ll1, train.py:100).
 """
 from __future__ import annotations
 
@@ -98,3 +104,58 @@ def ssim(img1, img2, window_size=11, size_average=True):
     if img2.requires_grad:
         raise NotImplementedError("gs_loss.ssim differentiates w.r.t. img1 only (img2 is the target)")
     return _SSIM.apply(img1, img2, size_average)
+
+
+class _PhotometricLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, image, gt, lambda_dssim):
+        if not image.is_cuda:
+            raise RuntimeError("gs_loss.photometric_loss (MI355X/HIP) needs device tensors; there is no CPU path")
+        if image.shape != gt.shape:
+            raise ValueError(f"photometric_loss: shapes differ {tuple(image.shape)} vs {tuple(gt.shape)}")
+        B, C, H, W = _planes(image)
+        a = image.detach().to(torch.float32).contiguous()
+        b = gt.detach().to(device=a.device, dtype=torch.float32).contiguous()
+        planes = B * C
+        dev = a.device
+        dmaps = torch.empty((3, planes, H, W), dtype=torch.float32, device=dev)
+        partial = torch.empty((2 * _lib.gs_ssim_partial_count(planes, H, W),), dtype=torch.float32, device=dev)
+        out = torch.empty((3,), dtype=torch.float32, device=dev)
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        with torch.cuda.device(dev):
+            _native.check(_lib.gs_photometric_loss_forward(
+                planes, H, W, _WIN_P, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+                float(lambda_dssim), ctypes.c_void_p(dmaps.data_ptr()), ctypes.c_void_p(partial.data_ptr()),
+                ctypes.c_void_p(out.data_ptr()), st), "photometric loss forward")
+        ctx.save_for_backward(a, b, dmaps)
+        ctx.lam = float(lambda_dssim)
+        ctx.dtype = image.dtype
+        loss, l1 = out[0].to(image.dtype), out[1].to(image.dtype)
+        ctx.mark_non_differentiable(l1)
+        return loss, l1
+
+    @staticmethod
+    def backward(ctx, grad, _grad_l1):
+        a, b, dmaps = ctx.saved_tensors
+        if grad is None:
+            return None, None, None
+        planes, H, W = dmaps.shape[1], dmaps.shape[2], dmaps.shape[3]
+        g = grad.to(torch.float32).reshape(1).contiguous()
+        dimg = torch.empty_like(a)
+        st = ctypes.c_void_p(torch.cuda.current_stream(a.device).cuda_stream)
+        with torch.cuda.device(a.device):
+            _native.check(_lib.gs_photometric_loss_backward(
+                planes, H, W, _WIN_P, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+                ctypes.c_void_p(dmaps.data_ptr()), ctx.lam, ctypes.c_void_p(g.data_ptr()),
+                ctypes.c_void_p(dimg.data_ptr()), st), "photometric loss backward")
+        return dimg.to(ctx.dtype), None, None
+
+
+def photometric_loss(image, gt, lambda_dssim=0.2):
+    """train.py:91-92 in one fused forward and one fused backward: returns (loss, Ll1) with
+    loss = (1 - lambda_dssim) * l1_loss(image, gt) + lambda_dssim * (1 - ssim(image, gt)).
+    Ll1 carries no gradient (the reference only logs it)."""
+    if gt.requires_grad:
+        raise NotImplementedError("gs_loss.photometric_loss differentiates w.r.t. the image only (gt is data)")
+    loss, l1 = _PhotometricLoss.apply(image, gt, lambda_dssim)
+    return loss, l1.detach()

@@ -9,10 +9,11 @@
   densify_and_prune (`densify`; the caller runs it every 100 iterations)  train.py:118-120
   optimizer.step(); zero_grad(set_to_none=True)        train.py:127-128
 with this package's HIP paths for every part: gs_train.render_inputs (one activation launch each
-way), the rasterizer, gs_loss.l1_loss / ssim, gs_train.add_densification_stats, FusedAdam,
-gs_train.densify_and_prune.  `fused=False` keeps the rasterizer and the loss but runs the
-reference's own torch glue for activations, densification statistics and Adam (the comparison
-point for the fused glue).
+way), the rasterizer, gs_loss.photometric_loss (L1 + SSIM in one forward and one backward
+kernel), gs_train.add_densification_stats, FusedAdam, gs_train.densify_and_prune.  `fused=False`
+keeps the rasterizer and the SSIM kernels but runs the reference's own torch glue for
+activations, the L1 term and the loss expression, densification statistics and Adam (the
+comparison point for the fused glue).
 
 `TrainModel` holds the GaussianModel fields one iteration touches (scene/gaussian_model.py:44-61,
 149-163): the six raw parameters, their Adam groups with training_setup's learning rates, the
@@ -107,8 +108,11 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
     """One iteration (module docstring).  Returns the loss tensor (not read back: the reference's
     `loss.item()` for its progress bar, train.py:99, is left to the caller)."""
     image, viewspace, radii = render(model, settings, fused)
-    Ll1 = gs_loss.l1_loss(image, gt_image)
-    loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - gs_loss.ssim(image, gt_image))
+    if fused:  # the whole loss expression in one fused forward / backward (gs_loss.photometric_loss)
+        loss, Ll1 = gs_loss.photometric_loss(image, gt_image, lambda_dssim)
+    else:
+        Ll1 = gs_loss.l1_loss(image, gt_image)
+        loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - gs_loss.ssim(image, gt_image))
     loss.backward()
     with torch.no_grad():
         if densify_stats:

@@ -24,6 +24,7 @@
  *   gs_ssim_forward / gs_ssim_backward         <-  utils.loss_utils.ssim(img1, img2)
  *                                                  (/root/reference/utils/loss_utils.py:33-60,
  *                                                   called at train.py:92)
+ *   gs_photometric_loss_forward / _backward    <-  train.py:91-92 (l1_loss + ssim, lambda_dssim)
  *   gs_adam_step                               <-  torch.optim.Adam.step() of GaussianModel
  *                                                  (/root/reference/scene/gaussian_model.py:163)
  *   gs_densify_stats                           <-  train.py:115-116 / gaussian_model.py:405-407
@@ -55,7 +56,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 5
+#define GSRAST_ABI_VERSION 6
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -221,6 +222,20 @@ int gs_ssim_forward(int planes, int H, int W, const float* window11_host, const 
                     float* dmaps, float* partial, float* plane_sum, void* stream);
 int gs_ssim_backward(int planes, int channels, int H, int W, const float* window11_host, const float* img1,
                      const float* img2, const float* dmaps, const float* scale, float* dimg1, void* stream);
+
+/* ---- fused photometric loss  <-  train.py:91-92
+ *      loss = (1 - lambda) l1_loss(img, gt) + lambda (1 - ssim(img, gt))  (utils/loss_utils.py) ----
+ * img, gt: [planes, H, W] fp32.  Forward: one SSIM pass that also sums |img - gt| per tile, then
+ * one fixed-order fp64 reduction writing out3 = [loss, l1, ssim] (device floats, means over all
+ * planes x H x W elements); dmaps[3, planes, H, W] as gs_ssim_forward; partial holds
+ * 2 x gs_ssim_partial_count(planes, H, W) floats.  Backward: dimg = grad[0] x dloss/dimg (grad: the
+ * loss's incoming gradient, one device float), the SSIM and L1 terms in one kernel. */
+int gs_photometric_loss_forward(int planes, int H, int W, const float* window11_host, const float* img,
+                                const float* gt, float lambda_dssim, float* dmaps, float* partial, float* out3,
+                                void* stream);
+int gs_photometric_loss_backward(int planes, int H, int W, const float* window11_host, const float* img,
+                                 const float* gt, const float* dmaps, float lambda_dssim, const float* grad,
+                                 float* dimg, void* stream);
 
 /* ---- fused Adam step  <-  torch.optim.Adam.step() of GaussianModel's optimizer
  *      (/root/reference/scene/gaussian_model.py:154-163, stepped at train.py:123-124) ----

@@ -21,7 +21,14 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), f"libgsrast.so does not export {s}"
     assert set(syms) == set(_native.SIGNATURES), set(syms) ^ set(_native.SIGNATURES)
-    assert lib.gs_abi_version() == 5
+    want = int(re.search(r"#define GSRAST_ABI_VERSION (\d+)", open(os.path.join(ROOT, "include", "gsrast.h")).read()).group(1))
+    assert want == 6 and lib.gs_abi_version() == want
+
+
+def test_graft_build_checks_the_header_abi():
+    """__graft_entry__.build() compares the loaded library's ABI with include/gsrast.h (not a literal)."""
+    src = open(os.path.join(ROOT, "__graft_entry__.py")).read()
+    assert "GSRAST_ABI_VERSION" in src and "gs_abi_version() ==" not in src
 
 
 def test_sizing_functions_run_without_gpu():

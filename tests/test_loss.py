@@ -88,3 +88,61 @@ def test_gpu_ssim_matches_oracle(shape, device):
     _close(a.grad.cpu().numpy() / 2.5, ref_a.grad.numpy(), name="grad")
     l1 = gs_loss.l1_loss(a, b0.to(device))
     assert abs(l1.item() - ssim_oracle.l1_loss(a0, b0).item()) < 1e-6
+
+
+def test_photometric_loss_cpu_refusal():
+    import gs_loss
+
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        gs_loss.photometric_loss(torch.rand(3, 8, 8), torch.rand(3, 8, 8))
+
+
+def _oracle_photometric(a0, b0, lam):
+    ref_a = a0.clone().requires_grad_(True)
+    l1 = ssim_oracle.l1_loss(ref_a, b0)
+    loss = (1.0 - lam) * l1 + lam * (1.0 - ssim_oracle.ssim(ref_a, b0))
+    loss.backward()
+    return loss.item(), l1.item(), ref_a.grad.numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,lam", [((3, 270, 480), 0.2), ((2, 3, 64, 80), 0.2), ((3, 1080, 1920), 0.2),
+                                       ((3, 37, 53), 0.7), ((1, 16, 16), 0.0), ((3, 20, 21), 1.0)])
+def test_gpu_photometric_loss_matches_oracle(shape, lam, device):
+    """train.py:91-92 fused (gs_loss.photometric_loss) against the fp64 oracle of the same expression:
+    value within 2e-6, gradient within 1e-5 relative + 1e-5 x max; pixels with image == gt (L1
+    subgradient 0, as torch's abs backward) included."""
+    import gs_loss
+
+    g = torch.Generator().manual_seed(11)
+    a0 = torch.rand(shape, generator=g)
+    b0 = (a0 + 0.1 * torch.randn(shape, generator=g)).clamp(0, 1)
+    eq = torch.rand(shape, generator=g) < 0.05
+    b0 = torch.where(eq, a0, b0)
+    ref_loss, ref_l1, ref_grad = _oracle_photometric(a0, b0, lam)
+    a = a0.to(device).requires_grad_(True)
+    loss, l1 = gs_loss.photometric_loss(a, b0.to(device), lam)
+    assert not l1.requires_grad and loss.requires_grad and loss.dim() == 0
+    (3.0 * loss).backward()
+    assert abs(loss.item() - ref_loss) < 2e-6 and abs(l1.item() - ref_l1) < 1e-6
+    _close(a.grad.cpu().numpy() / 3.0, ref_grad, name="grad")
+
+
+@pytest.mark.gpu
+def test_gpu_photometric_loss_matches_separate_terms(device):
+    """The fused expression against gs_loss.l1_loss + gs_loss.ssim composed by torch as train.py does."""
+    import gs_loss
+
+    g = torch.Generator().manual_seed(12)
+    a0 = torch.rand((3, 130, 170), generator=g).to(device)
+    b0 = torch.rand((3, 130, 170), generator=g).to(device)
+    a1 = a0.clone().requires_grad_(True)
+    Ll1 = gs_loss.l1_loss(a1, b0)
+    loss1 = 0.8 * Ll1 + 0.2 * (1.0 - gs_loss.ssim(a1, b0))
+    loss1.backward()
+    a2 = a0.clone().requires_grad_(True)
+    loss2, Ll2 = gs_loss.photometric_loss(a2, b0, 0.2)
+    loss2.backward()
+    assert abs(loss1.item() - loss2.item()) <= 1e-6 * abs(loss1.item())
+    assert abs(Ll1.item() - Ll2.item()) <= 1e-6 * abs(Ll1.item())
+    _close(a2.grad.cpu().numpy(), a1.grad.cpu().numpy(), rtol=1e-5, frac=1e-6, name="grad")

@@ -1,0 +1,33 @@
+"""Minimal runner for profiling one train.py iteration (gs_train_step.train_step) at C3 under
+rocprofv3: W warm-up + K timed iterations, fused glue (default) or the reference's torch glue."""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "gaussian-splatting-skysphere_amd"), ROOT]
+import torch  # noqa: E402
+
+import gs_scenes  # noqa: E402
+import gs_train_step as ts  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--warmup", type=int, default=3)
+ap.add_argument("--torch-glue", action="store_true")
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+cam = gs_scenes.identity_camera(1920, 1080)
+sc = gs_scenes.random_gaussians(1_000_000, 3, cam=cam, seed=0)
+settings = gs_scenes.raster_settings_for(cam, 3, device=dev)
+gt = torch.rand((3, 1080, 1920), generator=torch.Generator().manual_seed(2)).to(dev)
+model = ts.TrainModel(sc, dev, fused=not a.torch_glue)
+for _ in range(a.warmup):
+    ts.train_step(model, settings, gt, fused=not a.torch_glue)
+torch.cuda.synchronize()
+t = time.perf_counter()
+for _ in range(a.steps):
+    ts.train_step(model, settings, gt, fused=not a.torch_glue)
+torch.cuda.synchronize()
+print(f"train step {1e3 * (time.perf_counter() - t) / a.steps:.3f} ms")
