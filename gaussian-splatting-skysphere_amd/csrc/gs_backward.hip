@@ -20,6 +20,20 @@
 
 namespace gs {
 
+#ifdef GS_BWD_STATS
+// instrumentation build only (-DGS_BWD_STATS): [0..64] applied entries by contributing-lane count,
+// [65] evaluated entries, [67] contributing pixels summed over them
+__device__ unsigned long long g_bwd_stats[80];
+extern "C" int gs_debug_bwd_stats(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_bwd_stats), sizeof(g_bwd_stats)) != hipSuccess) return 1;
+  if (reset) {
+    static const unsigned long long z[80] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_stats), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
+
 // culling-side evaluation of one entry for a lane's two pixels (independent of the pixel state)
 struct Eval {
   float4 co;
@@ -346,6 +360,17 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         m &= m - 1;
         const float4 xr = s_ent[j];
         const Eval v = eval_pair<EXACT>(xr, s_ent[BWD_BATCH + j], pfx, pfy, n_eff - 1 - (base + j), lastA, lastB);
+#ifdef GS_BWD_STATS
+        {
+          const uint64_t bm = __ballot(v.cA || v.cB);
+          const unsigned long long npix = __popcll(__ballot(v.cA)) + __popcll(__ballot(v.cB));
+          if (lane == 0) {
+            atomicAdd(&g_bwd_stats[__popcll(bm)], 1ull);
+            atomicAdd(&g_bwd_stats[65], 1ull);
+            atomicAdd(&g_bwd_stats[67], npix);
+          }
+        }
+#endif
         if (__ballot(v.cA || v.cB) != 0) apply(j, v, xr);
       }
 #endif
