@@ -109,6 +109,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
                                                             // GS_SORT_GID: ids by list position, else by slot
                                                             const uint32_t* __restrict__ point_gid,
                                                             const float4* __restrict__ splat,
+                                                            const float4* __restrict__ inst_splat,
                                                             const float* __restrict__ final_T,
                                                             const uint32_t* __restrict__ n_contrib,
                                                             const uint32_t* __restrict__ tile_max,
@@ -248,6 +249,15 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   const uint32_t* const plist = point_list + range.x;
   uint32_t slot_c = 0, S1 = 0, G1 = 0, S2 = 0;
   float4 pa, pb, pd;
+#if GS_INST_REC
+  // the forward's per-instance records, read by list position (contiguous; no id gathers)
+  const float4* const rec = inst_splat + 3 * (size_t)range.x;
+  if (tid < 64 && e0 >= 0) {
+    slot_c = plist[e0];
+    pa = rec[3 * e0], pb = rec[3 * e0 + 1], pd = rec[3 * e0 + 2];
+  }
+  (void)S1, (void)G1, (void)S2, (void)point_gid, (void)splat;
+#else
   if (tid < 64) {
     if (e0 >= 0) {
       slot_c = plist[e0];
@@ -260,6 +270,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
     }
     if (!GS_SORT_GID && e0 - 128 >= 0) S2 = plist[e0 - 128];
   }
+#endif
 #endif
   for (uint32_t base = 0; base < n_eff; base += BWD_BATCH) {
     const uint32_t cnt = min((uint32_t)BWD_BATCH, n_eff - base);
@@ -278,8 +289,15 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         s_slot[t] = slot;
         hm = half_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
       }
-      // issue the next batch's splat loads, the ids after it and (ids by slot) the slots after those
       const int64_t e1 = e0 - (int64_t)(base + 64);
+#if GS_INST_REC
+      // issue the next batch's slot and record loads
+      if (e1 >= 0) {
+        slot_c = plist[e1];
+        pa = rec[3 * e1], pb = rec[3 * e1 + 1], pd = rec[3 * e1 + 2];
+      }
+#else
+      // issue the next batch's splat loads, the ids after it and (ids by slot) the slots after those
       if (e1 >= 0) {
         slot_c = S1;
         pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
@@ -294,6 +312,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         }
       }
       if (!GS_SORT_GID && e1 - 128 >= 0) S2 = plist[e1 - 128];
+#endif
       const uint64_t b0 = __ballot(hm & 1u), b1 = __ballot(hm & 2u);
       if (lane == 0) {
         s_mask[0][0] = b0;
@@ -459,11 +478,11 @@ void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& 
             bin.point_list, img.tile_cut);
   if (exact_exp())
     GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(slots), dim3(BWD_THREADS), 0, st, c, img.ranges,
-              bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
+              bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, img.final_T, img.n_contrib, img.tile_max, order,
               dL_dpix, gradrec);
   else
     GS_LAUNCH("render_bwd", k_render_bwd<false>, dim3(slots), dim3(BWD_THREADS), 0, st, c, img.ranges,
-              bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order,
+              bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, img.final_T, img.n_contrib, img.tile_max, order,
               dL_dpix, gradrec);
 }
 

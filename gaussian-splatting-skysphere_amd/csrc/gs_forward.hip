@@ -675,7 +675,8 @@ template <bool EXACT>
 __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                          const uint32_t* __restrict__ point_list,
                                                          const uint32_t* __restrict__ point_gid,
-                                                         const float4* __restrict__ splat, float* __restrict__ out,
+                                                         const float4* __restrict__ splat,
+                                                         float4* __restrict__ inst_splat, float* __restrict__ out,
                                                          float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                          uint32_t* __restrict__ tile_max, ImgPtrs img,
                                                          const uint32_t* __restrict__ err) {
@@ -702,6 +703,10 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
     if ((uint32_t)tid < cnt) {
       const uint32_t gid = GS_SORT_GID ? point_gid[range.x + base + tid] : point_gid[point_list[range.x + base + tid]];
       const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
+      if (GS_INST_REC) {
+        float4* r = inst_splat + 3 * (size_t)(range.x + base + tid);
+        r[0] = a, r[1] = b, r[2] = d;
+      }
       s_ent[tid] = make_float4(a.x, a.y, b.z, b.w);
       s_ent[GS_BLOCK + tid] = fall_coefs(a.z, a.w, b.x, b.y);
       s_ent[2 * GS_BLOCK + tid] = make_float4(d.x, __uint_as_float(base + tid + 1), 0.0f, 0.0f);
@@ -753,7 +758,8 @@ template <bool EXACT>
 __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ point_list,
                                                      const uint32_t* __restrict__ point_gid,
-                                                     const float4* __restrict__ splat, float* __restrict__ out,
+                                                     const float4* __restrict__ splat,
+                                                     float4* __restrict__ inst_splat, float* __restrict__ out,
                                                      float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                      uint32_t* __restrict__ tile_max, ImgPtrs img,
                                                      const uint32_t* __restrict__ err) {
@@ -795,6 +801,13 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
       const uint32_t gid = GS_SORT_GID ? point_gid[range.x + base + lane] : point_gid[point_list[range.x + base + lane]];
       const float4 a = splat[3 * gid], bb = splat[3 * gid + 1], d = splat[3 * gid + 2];
 #endif
+      if (GS_INST_REC) {
+        // every quadrant wave that stages the batch stores it (identical bytes; the tile's four
+        // waves run on one XCD, so the copies meet in its L2): the union of the waves' batches
+        // covers every entry the backward walks
+        float4* r = inst_splat + 3 * (size_t)(range.x + base + lane);
+        r[0] = a, r[1] = bb, r[2] = d;
+      }
       s_ent[lane] = make_float4(a.x, a.y, bb.z, bb.w);
       s_ent[FWDQ_NB + lane] = fall_coefs(a.z, a.w, bb.x, bb.y);
       s_ent[2 * FWDQ_NB + lane] = make_float4(d.x, __uint_as_float(base + lane + 1), 0.0f, 0.0f);
@@ -832,21 +845,21 @@ void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
     const int blocks = (int)xcd_span((uint32_t)tiles) * 32;
     if (exact_exp())
       GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
+                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
                 &geo.counters[CNT_ERR]);
     else
       GS_LAUNCH("render_fwd", k_render_fwd_q<false>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
+                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
                 &geo.counters[CNT_ERR]);
     return;
   }
   if (exact_exp())
     GS_LAUNCH("render_fwd", k_render_fwd<true>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
+              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
                 &geo.counters[CNT_ERR]);
   else
     GS_LAUNCH("render_fwd", k_render_fwd<false>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
+              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
                 &geo.counters[CNT_ERR]);
 }
 

@@ -145,7 +145,19 @@ struct BinPtrs {
   uint32_t* sorted_tile;
   uint32_t* slot_tile;   // tile of every instance slot (duplicate output, kept: the tile sort's
                          // first pass reads it and writes keys_b)
+  float4* inst_splat;    // GS_INST_REC: the 48-B splat record of every instance the forward staged, by
+                         // list position (the backward streams it instead of gathering slot -> id -> splat)
 };
+
+// GS_INST_REC = 1: the forward's quadrant waves store each staged entry's splat record at its list
+// position; the backward reads those contiguously (no id / splat gathers in the backward).
+// Measured at C3 (one call, both builds): render_bwd PMC traffic 664 -> 324 MB (1.44x its
+// algorithmic bytes) but 401 -> 396 us only -- the kernel is VALU-issue bound, not fetch bound --
+// while the forward's stores (every quadrant wave that stages a batch stores it) cost 175 -> 232
+// us: 1027 -> 983 it/s.  Off by default.
+#ifndef GS_INST_REC
+#define GS_INST_REC 0
+#endif
 
 inline int tile_bits(int tiles) {
   int b = 1;
@@ -164,7 +176,9 @@ inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base) {
   size_t o_ka = take(In * 4), o_va = take(In * 4), o_kb = take(In * 4), o_vb = take(In * 4);
   size_t o_pg = take(In * 4), o_st = take(In * 4), o_ax = take(GS_SORT_GID ? In * 4 : 0);
   size_t o_ss = take(sort_scratch_words(In) * 4);
+  size_t o_is = take(GS_INST_REC ? In * 48 : 0);
   if (out && base) {
+    out->inst_splat = GS_INST_REC ? (float4*)(base + o_is) : nullptr;
     out->keys_a = (uint32_t*)(base + o_ka);
     out->vals_a = (uint32_t*)(base + o_va);
     out->keys_b = (uint32_t*)(base + o_kb);
