@@ -88,8 +88,9 @@ class TrainModel:
 def render(model: TrainModel, settings, fused: bool = True):
     """gaussian_renderer.render() for the default pipe (SH and covariance in the rasterizer)."""
     means3D, shs, opacity, scales, rotations = gs_train.render_inputs(model) if fused else model.torch_render_inputs()
-    screenspace_points = torch.zeros_like(means3D, requires_grad=True) + 0  # __init__.py:26
-    screenspace_points.retain_grad()
+    # __init__.py:26 (zeros_like(...) + 0, then retain_grad): the same zero gradient carrier as a leaf,
+    # one fill launch instead of two
+    screenspace_points = torch.zeros_like(means3D, requires_grad=True)
     image, radii = GaussianRasterizer(raster_settings=settings)(
         means3D=means3D, means2D=screenspace_points, shs=shs, colors_precomp=None, opacities=opacity, scales=scales,
         rotations=rotations, cov3D_precomp=None)
