@@ -679,6 +679,37 @@ int gs_adam_step(int count, float* const* params_host, const float* const* grads
   return t_failed ? 1 : 0;
 }
 
+int gs_adam_step_activated(int count, float* const* params_host, const float* const* grad_src_host,
+                           const int* grad_mode_host, int sh_coeffs, float* const* exp_avg_host,
+                           float* const* exp_avg_sq_host, const long long* numel_host, const double* lr_host,
+                           const long long* step_host, const double* weight_decay_host, double beta1, double beta2,
+                           double eps, int maximize, void* stream) {
+  clear_error(0);
+  if (count < 0) return set_error("adam: count must be >= 0"), 1;
+  if (count == 0) return 0;
+  if (!params_host || !grad_src_host || !grad_mode_host || !exp_avg_host || !exp_avg_sq_host || !numel_host ||
+      !lr_host || !step_host)
+    return set_error("adam: missing pointer"), 1;
+  for (int k = 0; k < count; k++) {
+    const long long n = numel_host[k];
+    const int md = grad_mode_host[k];
+    if (md < AG_PLAIN || md > AG_NORMALIZE) return set_error("adam: unknown gradient mode %d", md), 1;
+    if (n > 0 && (!params_host[k] || !grad_src_host[k] || !exp_avg_host[k] || !exp_avg_sq_host[k]))
+      return set_error("adam: missing tensor pointer"), 1;
+    if (step_host[k] < 1) return set_error("adam: step must be >= 1"), 1;
+    if ((md == AG_SH_DC || md == AG_SH_REST) && sh_coeffs < 1) return set_error("adam: sh_coeffs must be >= 1"), 1;
+    if (md == AG_SH_DC && n % 3) return set_error("adam: features_dc must have 3 floats per Gaussian"), 1;
+    if (md == AG_SH_REST && (sh_coeffs < 2 ? n != 0 : n % (3LL * (sh_coeffs - 1))))
+      return set_error("adam: features_rest must have 3 (sh_coeffs - 1) floats per Gaussian"), 1;
+    if ((md == AG_SH_DC || md == AG_SH_REST) && n >= (1LL << 32)) return set_error("adam: SH tensor too large"), 1;
+    if (md == AG_NORMALIZE && (n % 4 || ((uintptr_t)grad_src_host[k] & 15)))
+      return set_error("adam: rotation rows of 4 floats with a 16-byte aligned gradient source required"), 1;
+  }
+  adam_step(count, params_host, grad_src_host, exp_avg_host, exp_avg_sq_host, numel_host, lr_host, step_host,
+            weight_decay_host, beta1, beta2, eps, maximize != 0, (hipStream_t)stream, grad_mode_host, sh_coeffs);
+  return t_failed ? 1 : 0;
+}
+
 int gs_activate_forward(int P, int sh_rest, const float* features_dc, const float* features_rest,
                         const float* opacity_raw, const float* scaling_raw, const float* rotation_raw, float* shs,
                         float* opacity, float* scales, float* rotations, void* stream) {

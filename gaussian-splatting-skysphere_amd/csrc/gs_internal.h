@@ -345,9 +345,12 @@ void photometric_forward(int planes, int H, int W, const float* win11, const flo
 void photometric_backward(int planes, int H, int W, const float* win11, const float* img, const float* gt,
                           const float* dmaps, float lambda, const float* grad, float* dimg, hipStream_t st);
 constexpr int ADAM_MAX_TENSORS = 16;  // parameter tensors per Adam launch
+// how k_adam forms a tensor's gradient from its source g (gs_adam_step_activated)
+enum AdamGrad { AG_PLAIN = 0, AG_SH_DC = 1, AG_SH_REST = 2, AG_SIGMOID = 3, AG_EXP = 4, AG_NORMALIZE = 5 };
 void adam_step(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                float* const* exp_avg_sq, const long long* numel, const double* lr, const long long* step,
-               const double* weight_decay, double beta1, double beta2, double eps, bool maximize, hipStream_t st);
+               const double* weight_decay, double beta1, double beta2, double eps, bool maximize, hipStream_t st,
+               const int* modes = nullptr, int sh_coeffs = 1);
 void activate_forward(int P, int rest_w, const float* f_dc, const float* f_rest, const float* o_raw,
                       const float* s_raw, const float* q_raw, float* shs, float* opac, float* scales, float* rots,
                       hipStream_t st);

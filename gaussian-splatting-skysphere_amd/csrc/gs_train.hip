@@ -42,9 +42,47 @@ struct AdamLaunch {
   float neg_step_size[ADAM_MAX_TENSORS];  // -lr / (1 - b1^t)
   float bc2_sqrt[ADAM_MAX_TENSORS];       // sqrt(1 - b2^t)
   float wd[ADAM_MAX_TENSORS];
+  int mode[ADAM_MAX_TENSORS];  // AdamGrad: how the tensor's gradient is formed from g
   int count, maximize;
+  int sh_row, sh_rest;    // AG_SH_*: floats per row of the SH gradient source (3M) and of f_rest (3(M - 1))
   float w1, w2, b2, eps;  // 1 - b1, 1 - b2, b2, eps
 };
+
+// The element's gradient, from a gradient source g (base pointer) and the raw parameter values
+// (before this update).  AG_SH_* / AG_SIGMOID / AG_EXP / AG_NORMALIZE apply the adjoint of the
+// activation that render() puts between the parameter and the rasterizer (k_activate_bwd's
+// expressions, operation for operation: the same floats as activate's backward followed by Adam)
+// so the raw-parameter gradients never go through memory.
+__device__ __forceinline__ float act_grad1(const AdamLaunch& a, int k, const float* g, uint64_t e, float praw) {
+  switch (a.mode[k]) {
+    case AG_SH_DC: {
+      const uint64_t gi = e / 3;
+      return g[gi * a.sh_row + (e - 3 * gi)];
+    }
+    case AG_SH_REST: {
+      const uint64_t gi = e / (uint64_t)a.sh_rest;
+      return g[gi * a.sh_row + 3 + (e - gi * a.sh_rest)];
+    }
+    case AG_SIGMOID: {
+      const float y = 1.0f / (1.0f + expf(-praw));
+      return g[e] * (1.0f - y) * y;
+    }
+    case AG_EXP:
+      return g[e] * expf(praw);
+    default:
+      return g[e];
+  }
+}
+
+// AG_NORMALIZE: the quaternion e .. e + 3 (one Gaussian's row)
+__device__ __forceinline__ void normalize_adjoint(const float* gq, const float* q, float* out) {
+  const float len = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const float n = fmaxf(len, 1e-12f);
+  const float dot = gq[0] * q[0] + gq[1] * q[1] + gq[2] * q[2] + gq[3] * q[3];
+  const float c = len > 1e-12f ? dot / (n * n) / len : 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; j++) out[j] = gq[j] / n - c * q[j];
+}
 
 // Operation order of torch's foreach Adam on the device (torch/optim/adam.py _multi_tensor_adam,
 // ATen lerp / addcmul / addcdiv functors, compiled with FMA contraction): scalars rounded to float
@@ -66,41 +104,73 @@ __global__ __launch_bounds__(256) void k_adam(AdamLaunch a, uint64_t total_chunk
   while (k + 1 < a.count && c >= a.end[k]) k++;
   const uint64_t i = (c - (k ? a.end[k - 1] : 0)) * 4;
   const uint64_t n = a.n[k];
+  const int mode = a.mode[k];
   float *p = a.p[k] + i, *m = a.m[k] + i, *v = a.v[k] + i;
-  const float* g = a.g[k] + i;
+  const float* g = a.g[k] + i;  // AG_PLAIN
   const float ss = a.neg_step_size[k], ib = a.bc2_sqrt[k], wd = a.wd[k];
-  const bool vec = i + 4 <= n && (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
+  const bool vec = i + 4 <= n && (((uintptr_t)p | (uintptr_t)m | (uintptr_t)v) & 15) == 0 &&
+                   (mode == AG_SH_DC || mode == AG_SH_REST || (((uintptr_t)g) & 15) == 0);
   if (vec) {
 #if GS_ADAM_NT
     // streaming: every byte is touched once per step and the step's 1.65 GB (C3) exceeds the caches
     typedef float v4f __attribute__((ext_vector_type(4)));
     v4f P = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
-    v4f G = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(g));
     v4f M = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(m));
     v4f V = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(v));
+#else
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    v4f P = *reinterpret_cast<const v4f*>(p), M = *reinterpret_cast<const v4f*>(m), V = *reinterpret_cast<const v4f*>(v);
+#endif
+    float G[4];
+    if (mode == AG_PLAIN) {
+#if GS_ADAM_NT
+      const v4f Gv = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(g));
+#else
+      const v4f Gv = *reinterpret_cast<const v4f*>(g);
+#endif
+      G[0] = Gv.x, G[1] = Gv.y, G[2] = Gv.z, G[3] = Gv.w;
+    } else if (mode == AG_NORMALIZE) {
+      const float4 gq = *reinterpret_cast<const float4*>(g);
+      const float gv[4] = {gq.x, gq.y, gq.z, gq.w}, q[4] = {P.x, P.y, P.z, P.w};
+      normalize_adjoint(gv, q, G);
+    } else if (mode == AG_SH_DC || mode == AG_SH_REST) {
+      // four consecutive elements of f_dc / f_rest: one (row, column) division for the chunk
+      // (32-bit: the tensors hold < 2^32 floats), then column steps with row carries
+      const uint32_t w = mode == AG_SH_DC ? 3u : (uint32_t)a.sh_rest, off = mode == AG_SH_DC ? 0u : 3u;
+      uint32_t r = (uint32_t)i / w, col = (uint32_t)i - r * w;
+      const float* src = a.g[k];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        G[e] = src[(uint64_t)r * a.sh_row + off + col];
+        if (++col == w) col = 0, r++;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; e++) G[e] = act_grad1(a, k, a.g[k], i + e, P[e]);
+    }
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       float pe = P[e], me = M[e], ve = V[e];
       adam_one(pe, G[e], me, ve, a, ss, ib, wd);
       P[e] = pe, M[e] = me, V[e] = ve;
     }
+#if GS_ADAM_NT
     __builtin_nontemporal_store(P, reinterpret_cast<v4f*>(p));
     __builtin_nontemporal_store(M, reinterpret_cast<v4f*>(m));
     __builtin_nontemporal_store(V, reinterpret_cast<v4f*>(v));
 #else
-    float4 P = *reinterpret_cast<float4*>(p), G = *reinterpret_cast<const float4*>(g);
-    float4 M = *reinterpret_cast<float4*>(m), V = *reinterpret_cast<float4*>(v);
-    adam_one(P.x, G.x, M.x, V.x, a, ss, ib, wd);
-    adam_one(P.y, G.y, M.y, V.y, a, ss, ib, wd);
-    adam_one(P.z, G.z, M.z, V.z, a, ss, ib, wd);
-    adam_one(P.w, G.w, M.w, V.w, a, ss, ib, wd);
-    *reinterpret_cast<float4*>(p) = P;
-    *reinterpret_cast<float4*>(m) = M;
-    *reinterpret_cast<float4*>(v) = V;
+    *reinterpret_cast<v4f*>(p) = P, *reinterpret_cast<v4f*>(m) = M, *reinterpret_cast<v4f*>(v) = V;
 #endif
   } else {
     const int cnt = (int)(n - i < 4 ? n - i : 4);
-    for (int j = 0; j < cnt; j++) adam_one(p[j], g[j], m[j], v[j], a, ss, ib, wd);
+    float G[4];
+    if (mode == AG_NORMALIZE) {  // rows of 4 (validated): the chunk is one whole quaternion
+      const float gv[4] = {g[0], g[1], g[2], g[3]}, q[4] = {p[0], p[1], p[2], p[3]};
+      normalize_adjoint(gv, q, G);
+    } else {
+      for (int j = 0; j < cnt; j++) G[j] = mode == AG_PLAIN ? g[j] : act_grad1(a, k, a.g[k], i + j, p[j]);
+    }
+    for (int j = 0; j < cnt; j++) adam_one(p[j], G[j], m[j], v[j], a, ss, ib, wd);
   }
 }
 
@@ -119,7 +189,8 @@ __global__ __launch_bounds__(256) void k_densify_stats(int P, const int* __restr
 
 void adam_step(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                float* const* exp_avg_sq, const long long* numel, const double* lr, const long long* step,
-               const double* weight_decay, double beta1, double beta2, double eps, bool maximize, hipStream_t st) {
+               const double* weight_decay, double beta1, double beta2, double eps, bool maximize, hipStream_t st,
+               const int* modes, int sh_coeffs) {
   for (int base = 0; base < count; base += ADAM_MAX_TENSORS) {
     AdamLaunch a{};
     uint64_t chunks = 0;
@@ -139,8 +210,11 @@ void adam_step(int count, float* const* params, const float* const* grads, float
       a.neg_step_size[j] = (float)(-(lr[k] / bc1));
       a.bc2_sqrt[j] = (float)std::sqrt(bc2);
       a.wd[j] = weight_decay ? (float)weight_decay[k] : 0.0f;
+      a.mode[j] = modes ? modes[k] : AG_PLAIN;
     }
     if (!a.count) continue;
+    a.sh_row = 3 * sh_coeffs;
+    a.sh_rest = 3 * (sh_coeffs - 1);
     a.w1 = (float)(1.0 - beta1);
     a.w2 = (float)(1.0 - beta2);
     a.b2 = (float)beta2;

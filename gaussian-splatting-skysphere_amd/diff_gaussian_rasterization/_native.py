@@ -87,6 +87,8 @@ SIGNATURES = {
     "gs_photometric_loss_forward": (_c_i, [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p]),
     "gs_photometric_loss_backward": (_c_i, [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p]),
     "gs_adam_step": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_d, _c_d, _c_d, _c_i, _c_p]),
+    "gs_adam_step_activated": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_d, _c_d, _c_d,
+                                      _c_i, _c_p]),
     "gs_activate_forward": (_c_i, [_c_i, _c_i] + [_c_p] * 9 + [_c_p]),
     "gs_activate_backward": (_c_i, [_c_i, _c_i] + [_c_p] * 12 + [_c_p]),
     "gs_densify_block_count": (_c_sz, [_c_i]),

@@ -126,6 +126,63 @@ class FusedAdam(torch.optim.Optimizer):
                 self._launch(items[s:s + _MAX_TENSORS], b1, b2, eps, maximize, dev, st)
         return loss
 
+    _MODES = {"plain": 0, "features_dc": 1, "features_rest": 2, "sigmoid": 3, "exp": 4, "normalize": 5}
+
+    @torch.no_grad()
+    def step_activated(self, sources: dict, sh_coeffs: int):
+        """step() whose gradients come from the render() inputs' gradients, through the activation
+        adjoint inside the update kernel (gs_adam_step_activated): `sources` maps a parameter to
+        (mode, gradient source), mode in "features_dc" / "features_rest" (source: dL/dshs
+        [P, sh_coeffs, 3]), "sigmoid" (dL/dopacity), "exp" (dL/dscales), "normalize"
+        (dL/drotations); parameters not in `sources` use their own .grad ("plain").  The floats
+        are those of activate()'s backward followed by step(); the parameters' .grad stay untouched
+        (None for the activated ones)."""
+        batches: dict = {}
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            key_h = (float(b1), float(b2), float(group["eps"]), bool(group.get("maximize", False)))
+            lr = float(group["lr"])
+            wd = float(group.get("weight_decay", 0.0))
+            for p in group["params"]:
+                mode, src = sources.get(p, ("plain", p.grad))
+                if src is None:
+                    continue
+                _check_f32_dense(p, "FusedAdam param")
+                _check_f32_dense(src, "FusedAdam gradient source")
+                if mode == "plain" and src.shape != p.shape:
+                    raise ValueError(f"FusedAdam: grad shape {tuple(src.shape)} != param {tuple(p.shape)}")
+                state = self.state[p]
+                if len(state) == 0:
+                    state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                m, v = state["exp_avg"], state["exp_avg_sq"]
+                step_t = state["step"]
+                if torch.is_tensor(step_t):
+                    step_t += 1
+                    t = int(step_t.item())
+                else:
+                    t = int(step_t) + 1
+                    state["step"] = torch.tensor(float(t), dtype=torch.float32)
+                batches.setdefault((p.device, key_h), []).append((p, src, m, v, lr, t, wd, self._MODES[mode]))
+        for (dev, (b1, b2, eps, maximize)), items in batches.items():
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            for s0 in range(0, len(items), _MAX_TENSORS):
+                it = items[s0:s0 + _MAX_TENSORS]
+                n = len(it)
+                ptrs = ctypes.c_void_p * n
+                P, G, M, V = (ptrs(*[ctypes.c_void_p(x[j].data_ptr()) for x in it]) for j in range(4))
+                numel = (ctypes.c_longlong * n)(*[x[0].numel() for x in it])
+                lr = (ctypes.c_double * n)(*[x[4] for x in it])
+                steps = (ctypes.c_longlong * n)(*[x[5] for x in it])
+                wd = (ctypes.c_double * n)(*[x[6] for x in it])
+                modes = (ctypes.c_int * n)(*[x[7] for x in it])
+                cast = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+                with torch.cuda.device(dev):
+                    _native.check(_lib.gs_adam_step_activated(
+                        n, cast(P), cast(G), cast(modes), int(sh_coeffs), cast(M), cast(V), cast(numel), cast(lr),
+                        cast(steps), cast(wd), b1, b2, eps, int(maximize), st), "adam step (activated)")
+
     @staticmethod
     def _launch(items, b1, b2, eps, maximize, dev, st):
         n = len(items)
@@ -239,6 +296,24 @@ class _Activate(torch.autograd.Function):
                                                         _ptr(g_rest), _ptr(g_o), _ptr(g_s), _ptr(g_q), st),
                               "activate backward")
         return g_dc, g_rest, g_o, g_s, g_q
+
+
+def activate_values(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw):
+    """activate()'s forward only (one launch, no autograd graph): fresh (shs, opacity, scales,
+    rotations) tensors, for a step whose adjoint runs inside FusedAdam.step_activated."""
+    with torch.no_grad():
+        return _Activate.forward(_NoCtx(), features_dc, features_rest, opacity_raw, scaling_raw,
+                                 rotation_raw)
+
+
+class _NoCtx:
+    """stand-in autograd context for calling _Activate.forward outside autograd"""
+
+    def save_for_backward(self, *a):
+        pass
+
+    def set_materialize_grads(self, v):
+        pass
 
 
 def activate(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw):

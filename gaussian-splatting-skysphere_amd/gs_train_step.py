@@ -9,8 +9,9 @@
   densify_and_prune (`densify`; the caller runs it every 100 iterations)  train.py:118-120
   optimizer.step(); zero_grad(set_to_none=True)        train.py:127-128
 with this package's HIP paths for every part: gs_train.render_inputs (one activation launch each
-way), the rasterizer, gs_loss.photometric_loss (L1 + SSIM in one forward and one backward
-kernel), gs_train.add_densification_stats, FusedAdam, gs_train.densify_and_prune.  `fused=False`
+way; by default the backward's activation adjoint runs inside the Adam update,
+FusedAdam.step_activated), the rasterizer, gs_loss.photometric_loss (L1 + SSIM in one forward and
+one backward kernel), gs_train.add_densification_stats, FusedAdam, gs_train.densify_and_prune.  `fused=False`
 keeps the rasterizer and the SSIM kernels but runs the reference's own torch glue for
 activations, the L1 term and the loss expression, densification statistics and Adam (the
 comparison point for the fused glue).
@@ -85,9 +86,21 @@ class TrainModel:
                 torch.exp(self._scaling), torch.nn.functional.normalize(self._rotation))
 
 
-def render(model: TrainModel, settings, fused: bool = True):
-    """gaussian_renderer.render() for the default pipe (SH and covariance in the rasterizer)."""
-    means3D, shs, opacity, scales, rotations = gs_train.render_inputs(model) if fused else model.torch_render_inputs()
+def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | None = None):
+    """gaussian_renderer.render() for the default pipe (SH and covariance in the rasterizer).
+    act_leaves (a list): the activated inputs are made autograd leaves (their adjoint then runs in
+    FusedAdam.step_activated) and appended to it as (shs, opacity, scales, rotations)."""
+    if act_leaves is not None:
+        acts = gs_train.activate_values(model._features_dc, model._features_rest, model._opacity, model._scaling,
+                                        model._rotation)
+        for t in acts:
+            t.requires_grad_(True)
+        act_leaves.extend(acts)
+        means3D, (shs, opacity, scales, rotations) = model._xyz, acts
+    elif fused:
+        means3D, shs, opacity, scales, rotations = gs_train.render_inputs(model)
+    else:
+        means3D, shs, opacity, scales, rotations = model.torch_render_inputs()
     # __init__.py:26 (zeros_like(...) + 0, then retain_grad): the same zero gradient carrier as a leaf,
     # one fill launch instead of two
     screenspace_points = torch.zeros_like(means3D, requires_grad=True)
@@ -105,10 +118,14 @@ def _torch_densification_stats(model: TrainModel, viewspace, radii):
 
 
 def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool = True, densify_stats: bool = True,
-               lambda_dssim: float = LAMBDA_DSSIM) -> torch.Tensor:
+               lambda_dssim: float = LAMBDA_DSSIM, fused_adjoint: bool = True) -> torch.Tensor:
     """One iteration (module docstring).  Returns the loss tensor (not read back: the reference's
-    `loss.item()` for its progress bar, train.py:99, is left to the caller)."""
-    image, viewspace, radii = render(model, settings, fused)
+    `loss.item()` for its progress bar, train.py:99, is left to the caller).
+    fused_adjoint (with fused): the activation's backward runs inside the Adam update
+    (FusedAdam.step_activated), so the raw parameters' gradients are never stored; same floats as
+    activate's backward followed by FusedAdam.step, .grad of the activated parameters stays None."""
+    acts = [] if (fused and fused_adjoint) else None
+    image, viewspace, radii = render(model, settings, fused, acts)
     if fused:  # the whole loss expression in one fused forward / backward (gs_loss.photometric_loss)
         loss, Ll1 = gs_loss.photometric_loss(image, gt_image, lambda_dssim)
     else:
@@ -121,7 +138,14 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
                 gs_train.add_densification_stats(model, viewspace, radii)
             else:
                 _torch_densification_stats(model, viewspace, radii)
-        model.optimizer.step()
+        if acts:
+            shs, opac, scales, rots = acts
+            model.optimizer.step_activated(
+                {model._features_dc: ("features_dc", shs.grad), model._features_rest: ("features_rest", shs.grad),
+                 model._opacity: ("sigmoid", opac.grad), model._scaling: ("exp", scales.grad),
+                 model._rotation: ("normalize", rots.grad)}, sh_coeffs=shs.shape[1])
+        else:
+            model.optimizer.step()
         model.optimizer.zero_grad(set_to_none=True)
     return loss
 

@@ -25,7 +25,7 @@
  *                                                  (/root/reference/utils/loss_utils.py:33-60,
  *                                                   called at train.py:92)
  *   gs_photometric_loss_forward / _backward    <-  train.py:91-92 (l1_loss + ssim, lambda_dssim)
- *   gs_adam_step                               <-  torch.optim.Adam.step() of GaussianModel
+ *   gs_adam_step(_activated)                   <-  torch.optim.Adam.step() of GaussianModel
  *                                                  (/root/reference/scene/gaussian_model.py:163)
  *   gs_densify_stats                           <-  train.py:115-116 / gaussian_model.py:405-407
  *   gs_densify_classify / _split_stds / _emit  <-  GaussianModel.densify_and_prune
@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 6
+#define GSRAST_ABI_VERSION 7
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -250,6 +250,21 @@ int gs_adam_step(int count, float* const* params_host, const float* const* grads
                  float* const* exp_avg_sq_host, const long long* numel_host, const double* lr_host,
                  const long long* step_host, const double* weight_decay_host, double beta1, double beta2, double eps,
                  int maximize, void* stream);
+
+/* gs_adam_step whose gradients are formed from the render() inputs' gradients (the adjoint of
+ * gs_activate_forward, applied inside the update: the raw-parameter gradients are never stored).
+ * grad_mode_host[k] per tensor, with grad_src_host[k] its source:
+ *   0 plain: the tensor's own gradient;
+ *   1 features_dc, 2 features_rest: rows of dL/dshs [P, sh_coeffs, 3] (coefficient 0 / 1..M-1);
+ *   3 sigmoid (opacity): dL/dopacity * (1 - y) * y, y = sigmoid(p) of the raw value before the update;
+ *   4 exp (scaling): dL/dscales * exp(p);
+ *   5 normalize (rotation, rows of 4): the F.normalize adjoint of dL/drotations at q = p.
+ * Same floats as gs_activate_backward followed by gs_adam_step. */
+int gs_adam_step_activated(int count, float* const* params_host, const float* const* grad_src_host,
+                           const int* grad_mode_host, int sh_coeffs, float* const* exp_avg_host,
+                           float* const* exp_avg_sq_host, const long long* numel_host, const double* lr_host,
+                           const long long* step_host, const double* weight_decay_host, double beta1, double beta2,
+                           double eps, int maximize, void* stream);
 
 /* ---- render() inputs from GaussianModel's raw parameters  <-  get_features / get_opacity /
  *      get_scaling / get_rotation (/root/reference/scene/gaussian_model.py:95-115, read at

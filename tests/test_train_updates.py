@@ -272,3 +272,68 @@ def test_activate_partial_gradients(device):
     torch.testing.assert_close(raw[1].grad, 2 * raw[1].detach(), rtol=0, atol=0)
     s = torch.sigmoid(raw[2].detach())
     torch.testing.assert_close(raw[2].grad, s * (1 - s), rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,K", [(1, 15), (5, 0), (1001, 3), (4097, 8), (30011, 15)])
+def test_adam_step_activated_equals_activate_backward_then_step(device, P, K):
+    """FusedAdam.step_activated (the activation adjoint inside the update, csrc/gs_train.hip
+    AG_* modes) against activate()'s autograd backward followed by FusedAdam.step, over 3 steps
+    with per-step learning rates: parameters and both moments bit-identical (the same float
+    operations), the activated parameters' .grad left unset; xyz (plain mode) included."""
+    from gs_train import FusedAdam, activate, activate_values
+
+    raw = _raw_params(P, K, device, seed=3 * P + K)
+    xyz0 = torch.randn((P, 3), generator=torch.Generator().manual_seed(5)).to(device)
+    runs = []
+    for fused_adjoint in (False, True):
+        ps = [torch.nn.Parameter(t.clone()) for t in [xyz0] + raw]
+        opt = FusedAdam([{"params": [p], "lr": lr} for p, lr in zip(ps, LRS)], lr=0.0, eps=1e-15)
+        g = torch.Generator().manual_seed(11)
+        for it in range(3):
+            for grp, lr in zip(opt.param_groups, LRS):
+                grp["lr"] = lr * (1.0 + 0.1 * it)
+            outs_g = [torch.randn(s, generator=g).to(device) for s in ((P, 1 + K, 3), (P, 1), (P, 3), (P, 4))]
+            gxyz = torch.randn((P, 3), generator=g).to(device)
+            if fused_adjoint:
+                acts = activate_values(*ps[1:])
+                assert torch.equal(acts[0], torch.cat((ps[1], ps[2]), 1).detach())
+                ps[0].grad = gxyz.clone()
+                opt.step_activated({ps[1]: ("features_dc", outs_g[0]), ps[2]: ("features_rest", outs_g[0]),
+                                    ps[3]: ("sigmoid", outs_g[1]), ps[4]: ("exp", outs_g[2]),
+                                    ps[5]: ("normalize", outs_g[3])}, sh_coeffs=1 + K)
+                assert all(p.grad is None for p in ps[1:])
+            else:
+                acts = activate(*ps[1:])
+                torch.autograd.backward(acts, outs_g)
+                ps[0].grad = gxyz.clone()
+                opt.step()
+            opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        runs.append((ps, opt))
+    (pa, oa), (pb, ob) = runs
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+        sa, sb = oa.state[a], ob.state[b]
+        assert torch.equal(sa["exp_avg"], sb["exp_avg"]) and torch.equal(sa["exp_avg_sq"], sb["exp_avg_sq"])
+        assert float(sa["step"]) == float(sb["step"]) == 3.0
+
+
+def test_adam_step_activated_validation():
+    """Argument checks of the C entry point run before any device work."""
+    import ctypes
+
+    from diff_gaussian_rasterization import _native
+
+    lib = _native.load()
+    one = (ctypes.c_void_p * 1)(ctypes.c_void_p(16))
+    n = (ctypes.c_longlong * 1)(10)
+    lr = (ctypes.c_double * 1)(1e-3)
+    st = (ctypes.c_longlong * 1)(1)
+    cast = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+    for mode, coeffs, msg in ((9, 16, "unknown gradient mode"), (5, 16, "rows of 4"), (1, 16, "3 floats"),
+                              (2, 16, "features_rest")):
+        modes = (ctypes.c_int * 1)(mode)
+        rc = lib.gs_adam_step_activated(1, cast(one), cast(one), cast(modes), coeffs, cast(one), cast(one), cast(n),
+                                        cast(lr), cast(st), None, 0.9, 0.999, 1e-15, 0, None)
+        assert rc != 0 and msg in _native.last_error(), _native.last_error()
