@@ -418,8 +418,19 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_rowscan(uint32_t*
 
 // AUX: a second value stream travels with the keys (aux_in[i] -> aux_out[pos]).  BITS: the digit
 // width, a template parameter so the ballot ranking unrolls.
+#ifndef GS_SCATTER_WPE
+// > 0: ask for that many waves per SIMD (register budget 512 / WPE).  With the 32-bit positions the
+// scatter takes 86 VGPRs (5 waves / SIMD; 64-bit: 108, 4 waves): C3 1026 -> 1037 it/s, scatter
+// 19.4 -> 18.1 us, C5 486 -> 496 it/s.  6 (80 VGPRs, one spill): no further change.
+#define GS_SCATTER_WPE 0
+#endif
+#if GS_SCATTER_WPE > 0
+#define GS_SCATTER_ATTR __attribute__((amdgpu_waves_per_eu(GS_SCATTER_WPE)))
+#else
+#define GS_SCATTER_ATTR
+#endif
 template <bool AUX, int BITS>
-__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
+__global__ __launch_bounds__(SORT_THREADS) GS_SCATTER_ATTR void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, uint32_t chunk,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ row_total, bool drop,
@@ -439,10 +450,11 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t digit_base = block_excl_scan(row_total[tid], s_scan, &all);
     s_base[tid] = digit_base + hist[(size_t)tid * nb + blockIdx.x];
   }
-  const uint64_t start = (uint64_t)blockIdx.x * chunk;
-  const uint64_t end = start + chunk < n ? start + chunk : n;
+  // 32-bit positions (n < 2^32): fewer registers than 64-bit index math for the 8 items
+  const uint32_t start = blockIdx.x * chunk;
+  const uint32_t end = start + chunk < n ? start + chunk : n;
   constexpr uint32_t mask = (1u << BITS) - 1u;
-  for (uint64_t t0 = start; t0 < end; t0 += SORT_TILE) {
+  for (uint32_t t0 = start; t0 < end; t0 += SORT_TILE) {
     s_wcnt[0][tid] = 0;
     s_wcnt[1][tid] = 0;
     s_wcnt[2][tid] = 0;
@@ -452,7 +464,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS], aux[AUX ? SORT_ITEMS : 1];
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
-      const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
+      const uint32_t i = t0 + wid * (SORT_ITEMS * 64) + (uint32_t)r * 64 + lane;
       const bool v = i < end;
       key[r] = v ? keys_in[i] : 0xFFFFFFFFu;
       val[r] = v ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
@@ -460,7 +472,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     }
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
-      const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
+      const uint32_t i = t0 + wid * (SORT_ITEMS * 64) + (uint32_t)r * 64 + lane;
       const bool v = i < end && !(drop && key[r] == DEPTH_DROP);
       const uint32_t d = (key[r] >> shift) & mask;
       const uint64_t peers = digit_peers(d, v, BITS);
@@ -488,7 +500,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     // reorder the tile by digit in LDS
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
-      const uint64_t i = t0 + (uint64_t)wid * (SORT_ITEMS * 64) + (uint64_t)r * 64 + lane;
+      const uint32_t i = t0 + wid * (SORT_ITEMS * 64) + (uint32_t)r * 64 + lane;
       if (i < end && !(drop && key[r] == DEPTH_DROP)) {
         const uint32_t d = (key[r] >> shift) & mask;
         const uint32_t slot = s_loc[d] + s_wcnt[wid][d] + rank[r];
