@@ -104,7 +104,7 @@ static_assert(BWD_BATCH % 64 == 0, "batch must be whole waves");
 // per-entry gradient terms of the two pixels are pre-summed in the lane, summed over the wave
 // (wave_sum9_rows) and stored into the wave's LDS record by one lane per row.
 template <bool EXACT>
-__global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
+__global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) GS_WPE_ATTR(GS_BWD_WPE) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
                                                             const uint32_t* __restrict__ point_list,
                                                             // GS_SORT_GID: ids by list position, else by slot
                                                             const uint32_t* __restrict__ point_gid,
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
   // are in flight; the walk issues no global loads, so they overlap it.  Batch k's entry of
   // lane t sits at list position range.x + e0 - 64 k, e0 = n_eff - 1 - t.
   static_assert(BWD_BATCH == 64, "prefetch: one staged entry per lane of wave 0");
-  const int64_t e0 = (int64_t)n_eff - 1 - tid;
+  const int32_t e0 = (int32_t)n_eff - 1 - tid;  // (a tile list holds < 2^31 entries)
   const uint32_t* const plist = point_list + range.x;
   uint32_t slot_c = 0, S1 = 0, G1 = 0, S2 = 0;
   float4 pa, pb, pd;
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) void k_render_bwd(CameraA
         s_slot[t] = slot;
         hm = half_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
       }
-      const int64_t e1 = e0 - (int64_t)(base + 64);
+      const int32_t e1 = e0 - (int32_t)(base + 64);
 #if GS_INST_REC
       // issue the next batch's slot and record loads
       if (e1 >= 0) {
@@ -930,7 +930,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
 // Register variant (GS_PBWD_REG, the default): the lane loads its own SH row (first 3K floats, 16-B loads when
 // the rows allow) and stores dL/dsh the same way; no LDS, so occupancy is set by registers alone.
 template <int DEG>
-__global__ __launch_bounds__(256) void k_preprocess_bwd_reg(GaussianArgs g, CameraArgs c,
+__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PBWD_WPE) void k_preprocess_bwd_reg(GaussianArgs g, CameraArgs c,
                                                             const uint32_t* __restrict__ tiles,
                                                             const uint8_t* __restrict__ clamped,
                                                             const float* __restrict__ gsum, GradOut out) {

@@ -160,7 +160,7 @@ __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g,
 // counters[CNT_NREND] / [CNT_V] by one 64-bit atomic add.  depth_key[i] is the depth's bits for those and DEPTH_DROP for every other
 // Gaussian: the first depth-sort pass drops them, which is the visibility compaction.
 template <int DEG>
-__global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
+__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
                                                     float4* __restrict__ splat, float4* __restrict__ binrec,
                                                     uint32_t* __restrict__ depth_key,
                                                     uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
@@ -223,7 +223,7 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
 // the Gaussian's inputs come from HBM once, the later views read them from the caches.  The
 // per-view workgroup totals go to each view's counters as in k_preprocess.
 template <int DEG>
-__global__ __launch_bounds__(256) void k_preprocess_views(GaussianArgs g, PreViews pv) {
+__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PV_WPE) void k_preprocess_views(GaussianArgs g, PreViews pv) {
   __shared__ uint32_t s_sum[4], s_vis[4];
   const int i = blockIdx.x * 256 + (int)threadIdx.x;
   for (int v = 0; v < pv.K; v++) {

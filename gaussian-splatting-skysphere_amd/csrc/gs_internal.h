@@ -149,6 +149,21 @@ struct BinPtrs {
                          // list position (the backward streams it instead of gathering slot -> id -> splat)
 };
 
+// Occupancy requests (amdgpu_waves_per_eu) for register-limited kernels; 0 = the compiler's choice.
+#define GS_WPE_ATTR(n) __attribute__((amdgpu_waves_per_eu((n) > 0 ? (n) : 1)))
+#ifndef GS_BWD_WPE
+#define GS_BWD_WPE 0
+#endif
+#ifndef GS_PV_WPE
+#define GS_PV_WPE 0
+#endif
+#ifndef GS_PBWD_WPE
+#define GS_PBWD_WPE 0
+#endif
+#ifndef GS_PRE_WPE
+#define GS_PRE_WPE 0
+#endif
+
 // GS_INST_REC = 1: the forward's quadrant waves store each staged entry's splat record at its list
 // position; the backward reads those contiguously (no id / splat gathers in the backward).
 // Measured at C3 (one call, both builds): render_bwd PMC traffic 664 -> 324 MB (1.44x its
