@@ -8,7 +8,7 @@ OUT=$R/gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
-timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $OUT/bench_c3.log 2>&1 || { echo "bench c3 failed"; tail -20 $OUT/bench_c3.log; exit 1; }
+timeout -k 10 600 python bench.py > $OUT/bench_c3.log 2>&1 || { echo "bench c3 failed"; tail -20 $OUT/bench_c3.log; exit 1; }
 echo "bench c3 ok"
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof.log; exit 1; }
