@@ -112,6 +112,9 @@ def main():
     ap.add_argument("--no-train-step", action="store_true",
                     help="skip the secondary train.py-step measurement (SURVEY §8d metric (2); N=1 only)")
     ap.add_argument("--train-steps", type=int, default=20, help="timed iterations of the train-step measurement")
+    ap.add_argument("--step-events", action="store_true",
+                    help="diagnostic: record a HIP event after every timed step (no host syncs) and report the "
+                         "per-step times of the timed region in deciles")
     ap.add_argument("--sustain-s", type=float, default=2.0,
                     help="after the timed steps, keep stepping for this long (untimed for `value`) and report "
                          "the sustained rate too")
@@ -212,8 +215,15 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if args.step_events:
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        evs[0].record()
+        for k in range(args.steps):
+            step()
+            evs[k + 1].record()
+    else:
+        for _ in range(args.steps):
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -367,6 +377,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sc, cam, deg, W, H, dpix.cpu(), args.cpu_threads, args.cpu_runs)
 
+    step_deciles = None
+    if args.step_events:
+        st_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
+        nd = max(1, args.steps // 10)
+        step_deciles = [round(sum(st_ms[j:j + nd]) / len(st_ms[j:j + nd]), 4) for j in range(0, args.steps, nd)]
     out = {
         "metric": "train iters/sec (fwd+bwd) + render Mpix/s @1080p, 1M Gaussians SH=3",
         "value": round(value, 2),
@@ -407,6 +422,7 @@ def main():
         "kernels": kernels,
         "train_step": train,
         "init_knn": knn,
+        **({"step_ms_deciles": step_deciles} if step_deciles else {}),
         "cpu_baseline": cpu,
     }
     if rank == 0:

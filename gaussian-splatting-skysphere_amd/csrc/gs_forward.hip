@@ -383,8 +383,10 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     const float4* __restrict__ binrec, int gx, int gy, uint32_t* __restrict__ tile_keys,
     uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges, uint32_t* __restrict__ hist0, uint32_t mask0) {
   __shared__ uint32_t s_own[DUP_SLOTS + DUP_SLOTS / 8];  // (slot + 1) << 16 | segment at segment starts
-  __shared__ uint32_t s_seg_start[DUP_SLOTS];  // first slot of the row segment (may precede the block)
-  __shared__ uint32_t s_seg_tile[DUP_SLOTS];   // tile id of the segment's first slot
+  // per row segment: (tile id of its first slot) - (that slot), mod 2^32 (the slot may precede the
+  // block), so slot k of the segment has key base + k; one table instead of two keeps the LDS at
+  // 26 KB: 6 workgroups per CU
+  __shared__ uint32_t s_seg_base[DUP_SLOTS];
   __shared__ uint32_t s_seg_gid[DUP_SLOTS];
   __shared__ uint32_t s_wmax[DUP_THREADS / 64];
   __shared__ uint32_t s_nseg;
@@ -431,8 +433,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
       const uint32_t w = (uint32_t)(tb - ta);
       if (w && pos + w > k0) {
         const uint32_t seg = atomicAdd(&s_nseg, 1u);
-        s_seg_start[seg] = pos;
-        s_seg_tile[seg] = (uint32_t)(ty * gx + ta);
+        s_seg_base[seg] = (uint32_t)(ty * gx + ta) - pos;
         s_seg_gid[seg] = gid;
         const uint32_t at = (pos > k0 ? pos : k0) - k0;
         s_own[own_idx(at)] = ((at + 1) << 16) | seg;
@@ -470,7 +471,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     const uint32_t k = k0 + i;
     if (k < k1) {
       const uint32_t o = s_own[own_idx(i)] & 0xFFFFu;
-      const uint32_t key = s_seg_tile[o] + (k - s_seg_start[o]);
+      const uint32_t key = s_seg_base[o] + k;
       tile_keys[k] = key;
       presort_gid[k] = s_seg_gid[o];
       if (hist0) atomicAdd(&s_hist[key & mask0], 1u);  // counts only: order-free
