@@ -308,6 +308,29 @@ def main():
         torch.cuda.synchronize()
         t_render = (time.perf_counter() - tr) / nr
 
+        # the same forward in the step's batching: the rank's views per step with the fused front
+        # on the step's streams (render throughput as the fwd+bwd metric batches its views)
+        render_batched = None
+        if len(rasts) > 1 and not args.no_fused_front:
+            def render_step():
+                pre = prepare_views(rasts, params[0], params[2], shs=params[1], scales=params[3],
+                                    rotations=params[4], streams=[streams[k % len(streams)] for k in range(len(rasts))])
+                fns = [(lambda r=r, p=p: r(means3D=params[0], means2D=means2D, opacities=params[2], shs=params[1],
+                                           scales=params[3], rotations=params[4], prepared=p))
+                       for r, p in zip(rasts, pre)]
+                vp.run_views(fns, streams)
+
+            for _ in range(2):
+                render_step()
+            torch.cuda.synchronize()
+            tb = time.perf_counter()
+            for _ in range(nr):
+                render_step()
+            torch.cuda.synchronize()
+            t_rb = (time.perf_counter() - tb) / nr / len(rasts)
+            render_batched = {"views_per_step": len(rasts), "streams": len(streams),
+                              "mpix_s": round(W * H / t_rb / 1e6, 1), "ms_per_view": round(1e3 * t_rb, 4)}
+
     ms_per_step = 1e3 * elapsed / args.steps
     # whole-job views (= reference train iterations) per second: weak scaling (C1-C3, C5) counts
     # every rank's views; a C4 step is the 8-view batch
@@ -403,6 +426,7 @@ def main():
                    (" + RCCL all-reduce of 59 f32/Gaussian" if world > 1 else "")},
         "render_mpix_s": round(W * H / t_render / 1e6, 1),
         "render_ms": round(1e3 * t_render, 4),
+        "render_batched": render_batched,
         "num_rendered": int(num_rendered),
         "walked_instances": walked,
         "visible": visible,
