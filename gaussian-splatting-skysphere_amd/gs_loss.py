@@ -132,6 +132,7 @@ class _PhotometricLoss(torch.autograd.Function):
         ctx.dtype = image.dtype
         loss, l1 = out[0].to(image.dtype), out[1].to(image.dtype)
         ctx.mark_non_differentiable(l1)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the L1 output
         return loss, l1
 
     @staticmethod
