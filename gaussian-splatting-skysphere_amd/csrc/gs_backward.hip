@@ -439,15 +439,24 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __
                                                               const uint32_t* __restrict__ tile_max,
                                                               const uint2* __restrict__ ranges,
                                                               const uint32_t* __restrict__ point_list,
-                                                              uint32_t* __restrict__ tile_cut) {
+                                                              uint32_t* __restrict__ tile_cut,
+                                                              uint32_t* __restrict__ cut_max) {
   __shared__ uint32_t s_base[ORDER_GROUPS][ORDER_BUCKETS];
   const uint32_t tid = threadIdx.x, t = blockIdx.x * ORDER_THREADS + tid, lane = tid & 63, wid = tid >> 6;
   const uint32_t tiles = gx * gy;
+  uint32_t cut = 0;
   if (t < tiles) {
     const uint4 q = reinterpret_cast<const uint4*>(tile_max)[t];
     const uint2 r = ranges[t];
     const uint32_t n_eff = min(max(max(q.x, q.y), max(q.z, q.w)), r.y - r.x);
-    tile_cut[t] = n_eff ? point_list[r.x + n_eff - 1] + 1u : 0u;
+    cut = n_eff ? point_list[r.x + n_eff - 1] + 1u : 0u;
+    tile_cut[t] = cut;
+  }
+  {
+    // the largest cut (all lanes take part in the wave max): k_sum_records stops there -- slots
+    // are in depth order, so past it no tile walked an instance
+    const uint32_t wm = wave_max_u32(cut);
+    if (lane == 0 && wm) atomicMax(cut_max, wm);
   }
   if (!order) return;  // (uniform)
   const uint32_t br = t < tiles ? tile_brank[t] : 0u;
@@ -475,7 +484,7 @@ void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& 
   const uint32_t slots = xcd_slots((uint32_t)tiles);
   GS_LAUNCH("tile_order", k_tile_order, dim3((slots + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
             img.len_hist, img.tile_brank, (uint32_t)c.gx, (uint32_t)c.gy, order, img.tile_max, img.ranges,
-            bin.point_list, img.tile_cut);
+            bin.point_list, img.tile_cut, img.cut_max);
   if (exact_exp())
     GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(slots), dim3(BWD_THREADS), 0, st, c, img.ranges,
               bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, img.final_T, img.n_contrib, img.tile_max, order,
@@ -516,6 +525,7 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
                                                                    const uint32_t* __restrict__ sorted_gid,
                                                                    const uint32_t* __restrict__ slot_tile,
                                                                    const uint32_t* __restrict__ tile_cut,
+                                                                   const uint32_t* __restrict__ cut_max,
                                                                    const float* __restrict__ gradrec,
                                                                    float* __restrict__ gsum, uint32_t P) {
   __shared__ double s_acc[SUMREC_WAVES][64][GRAD_REC];
@@ -533,7 +543,8 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
   const uint32_t nr = min(64u, V - r0);
   const uint32_t my_off = lane < nr ? offsets[r0 + lane] : 0xFFFFFFFFu;
   const uint32_t S0 = (uint32_t)__shfl((int)my_off, 0, 64);
-  const uint32_t S1 = (r0 + 64 < V) ? offsets[r0 + 64] : I;
+  // the wave's records end at its last owner's end or at the largest tile cut, whichever is first
+  const uint32_t S1 = min((r0 + 64 < V) ? offsets[r0 + 64] : I, *cut_max);
 #pragma unroll
   for (int c = 0; c < GRAD_REC; c++) s_acc[wid][lane][c] = 0.0;
   const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
@@ -1159,7 +1170,7 @@ void bwd_records(const GaussianArgs& g, const GeomPtrs& geo, const BinPtrs& bin,
   if (have_records)
     GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
               dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
-              gradrec, geo.gsum, (uint32_t)g.P);
+              img.cut_max, gradrec, geo.gsum, (uint32_t)g.P);
   if (dmean2D)
     GS_LAUNCH("mean2d_grad", k_mean2d_grad, dim3((g.P + 255) / 256), dim3(256), 0, st, g.P, geo.tiles, geo.gsum,
               dmean2D, acc);
@@ -1172,7 +1183,7 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
   if (have_records)
     GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
               dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
-              gradrec, geo.gsum, (uint32_t)g.P);
+              img.cut_max, gradrec, geo.gsum, (uint32_t)g.P);
   dim3 grid((g.P + 255) / 256), block(256);
   const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
   const size_t lds = sh ? (size_t)256 * (3 * g.M + 1) * sizeof(float) : 0;

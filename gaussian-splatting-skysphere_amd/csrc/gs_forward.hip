@@ -521,7 +521,7 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
   if (I == 0) {
     (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
     (void)hipMemsetAsync(img.tile_done, 0,
-                         sizeof(uint64_t) * (size_t)tiles + sizeof(uint32_t) * ORDER_GROUPS * ORDER_BUCKETS, st);
+                         sizeof(uint64_t) * (size_t)tiles + sizeof(uint32_t) * (ORDER_GROUPS * ORDER_BUCKETS + 1), st);
     return;
   }
   const int tbits = tile_bits(tiles);
@@ -544,7 +544,7 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
                    false, hist0, GS_SORT_GID ? bin.presort_gid : nullptr, bin.aux_a, bin.presort_gid, bin.slot_tile,
                    GS_TILE_SORT_BLOCKS);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges,
-            (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS, (uint32_t)tiles);
+            (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS + 1u, (uint32_t)tiles);
 }
 
 // ------------------------------------------------------------------------------------------

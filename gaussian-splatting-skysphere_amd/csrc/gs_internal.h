@@ -221,6 +221,8 @@ struct ImgPtrs {
   uint64_t* tile_done;   // per tile: finished quadrant waves + their length bits (zeroed by k_ranges),
   uint32_t* len_hist;    //   then ORDER_GROUPS x ORDER_BUCKETS walk-length bucket counts
   uint32_t* tile_brank;  // bucket << 22 | rank within the bucket, per tile
+  uint32_t* cut_max;     // the largest tile_cut (after len_hist; zeroed with it): no instance slot at
+                         // or past it has a gradient record
 };
 
 // Backward launch order: tiles bucketed by walk length (largest n_contrib), longest first.
@@ -282,7 +284,7 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   if (tiles == 0) tiles = 1;
   if (npix == 0) npix = 1;
   size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16), o_o = take((size_t)xcd_slots((uint32_t)tiles) * 4), o_c = take(tiles * 4),
-         o_d = take(tiles * 8 + ORDER_GROUPS * ORDER_BUCKETS * 4), o_b = take(tiles * 4);
+         o_d = take(tiles * 8 + ORDER_GROUPS * ORDER_BUCKETS * 4 + 4), o_b = take(tiles * 4);
   if (out && base) {
     out->ranges = (uint2*)(base + o_r);
     out->final_T = (float*)(base + o_t);
@@ -292,6 +294,7 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
     out->tile_cut = (uint32_t*)(base + o_c);
     out->tile_done = (uint64_t*)(base + o_d);
     out->len_hist = (uint32_t*)(out->tile_done + tiles);
+    out->cut_max = out->len_hist + ORDER_GROUPS * ORDER_BUCKETS;
     out->tile_brank = (uint32_t*)(base + o_b);
   }
   return off;
