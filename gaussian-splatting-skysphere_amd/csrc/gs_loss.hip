@@ -3,11 +3,12 @@
 // Restates /root/reference/utils/loss_utils.py:ssim/_ssim (11x11 Gaussian window, sigma 1.5,
 // zero padding 5, C1 = 0.01^2, C2 = 0.03^2, mean of the SSIM map), which the reference evaluates
 // as five depthwise conv2d calls plus their autograd backward every iteration
-// (train.py:91-92).  Here one kernel produces, per plane (image x channel) and 16x16 tile, the
-// five windowed moments by a separable 11-tap filter through LDS, the SSIM map sum and the three
-// per-pixel partials dS/dmu1, dS/dE[x^2], dS/dE[xy]; a second kernel filters those partials with
-// the same window (the adjoint of a symmetric, zero-padded correlation) and forms dL/dimg1.
-// (16x16 tiles without register reuse: fwd 103 / bwd 79 us at 1080p x 3 planes.)
+// (train.py:91-92).  Here one kernel produces, per plane (image x channel) and 32x32 tile, the
+// five windowed moments by a separable 11-tap filter through LDS, the SSIM map sum (and, for the
+// fused photometric loss, the |x - y| sum) and the three per-pixel partials dS/dmu1, dS/dE[x^2],
+// dS/dE[xy]; a second kernel filters those partials with the same window (the adjoint of a
+// symmetric, zero-padded correlation) and forms dL/dimg1 (fused loss: plus the L1 term).
+// 1080p x 3 planes: fwd 64 us, bwd 54 us (round 1's 16x16 tiles without register reuse: 103 / 79).
 //
 //   S = (2 m1 m2 + C1)(2 s12 + C2) / ((m1^2 + m2^2 + C1)(s11 + s22 + C2)),
 //   s11 = E[x^2] - m1^2, s22 = E[y^2] - m2^2, s12 = E[xy] - m1 m2
@@ -15,7 +16,8 @@
 //   dS/dE[xy] = 2 A1 / (B1 B2)
 //   dL/dx(q) = scale * [ (w * dS/dm1)(q) + 2 x(q) (w * dS/dE[x^2])(q) + y(q) (w * dS/dE[xy])(q) ]
 //
-// The map sum is reduced per workgroup and then per plane in a fixed order (deterministic).
+// The sums are reduced per workgroup and then per plane (or over all planes, k_loss_finish) in a
+// fixed order (deterministic).
 #include "gs_internal.h"
 
 namespace gs {
