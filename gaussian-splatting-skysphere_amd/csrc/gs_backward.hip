@@ -1009,12 +1009,24 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PBWD_WPE) void k_preprocess_bwd
 // r = (first ? v : r + v): the bucket arithmetic of one view's write / `grad += g`
 __device__ __forceinline__ void vput(float& r, float v, bool first) { r = first ? v : r + v; }
 
+// GS_BWDG_LDS: the workgroup's 256 SH rows come in (and their gradient rows go out) as one
+// contiguous block through LDS -- coalesced 16-B accesses -- instead of one lane-strided 192-B
+// row per lane (every load instruction touching 64 cache lines).  The kernel runs at 2 waves per
+// SIMD for its registers anyway, so the 53 KB of LDS per workgroup costs no occupancy.
+#ifndef GS_BWDG_LDS
+#define GS_BWDG_LDS 1
+#endif
+constexpr int BG_ROW = 52;  // staged row stride (floats): 16-B aligned, conflict-free 16-B reads
+
 template <int DEG>  // -1: colours precomputed (no SH gradient)
 __global__ __launch_bounds__(256) void k_backward_gaussians(GaussianArgs g, FusedViews fv, GradOut out) {
   constexpr int D = DEG < 0 ? 0 : DEG;
   constexpr int KF = DEG < 0 ? 1 : 3 * (D + 1) * (D + 1);
-  const int i = blockIdx.x * 256 + (int)threadIdx.x;
-  if (i >= g.P) return;
+  constexpr bool LDS = GS_BWDG_LDS && DEG >= 0 && KF % 4 == 0;
+  __shared__ __attribute__((aligned(16))) float s_rows[LDS ? 256 * BG_ROW : 1];
+  const int i0 = blockIdx.x * 256;
+  const int i = i0 + (int)threadIdx.x;
+  const bool live = i < g.P;
   const uint32_t acc = out.acc;
   const int rowf = 3 * g.M;
   // the SH row (its first 3K floats) and the accumulators; an output with its GS_ACC bit starts
@@ -1022,115 +1034,168 @@ __global__ __launch_bounds__(256) void k_backward_gaussians(GaussianArgs g, Fuse
   float row[KF], dsh[KF];
   const bool vec = DEG >= 0 && (KF & 3) == 0 && (rowf & 3) == 0 &&
                    ((((uintptr_t)g.shs) | ((uintptr_t)out.dsh)) & 15) == 0;
-  if (DEG >= 0) {
-    const float* src = g.shs + (size_t)i * rowf;
-    if (vec) {
+  // staged: whole rows of exactly 3K floats (the active degree is the stored one), 16-B aligned
+  const bool stage = LDS && vec && rowf == KF && out.dsh;  // (uniform)
+  const int nG = g.P - i0 < 256 ? g.P - i0 : 256;
+  if (stage) {
+    // all of the block's row loads in flight, then the LDS stores
+    constexpr int PER = LDS ? KF / 4 : 1;  // float4 per row = per thread
+    const float4* src4 = reinterpret_cast<const float4*>(g.shs + (size_t)i0 * KF);
+    const int n4 = nG * PER;
+    float4 v[PER];
 #pragma unroll
-      for (int q = 0; q < KF / 4; q++) {
-        const float4 v = reinterpret_cast<const float4*>(src)[q];
-        row[4 * q] = v.x, row[4 * q + 1] = v.y, row[4 * q + 2] = v.z, row[4 * q + 3] = v.w;
+    for (int q = 0; q < PER; q++) {
+      const int f = (int)threadIdx.x + 256 * q;
+      v[q] = f < n4 ? src4[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      const int f = (int)threadIdx.x + 256 * q;
+      if (f < n4) {
+        const int r = f / PER, c = f - r * PER;
+        *reinterpret_cast<float4*>(&s_rows[r * BG_ROW + 4 * c]) = v[q];
       }
-    } else {
+    }
+    lds_barrier();
 #pragma unroll
-      for (int k = 0; k < KF; k++) row[k] = src[k];
+    for (int q = 0; q < PER; q++) {
+      const float4 t = *reinterpret_cast<const float4*>(&s_rows[threadIdx.x * BG_ROW + 4 * q]);
+      row[4 * q] = t.x, row[4 * q + 1] = t.y, row[4 * q + 2] = t.z, row[4 * q + 3] = t.w;
     }
   }
-  const float px = g.means3D[3 * i], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
-  float cov3[6];
-  if (g.cov3D) {
+  if (live) {
+    if (DEG >= 0 && !stage) {
+      const float* src = g.shs + (size_t)i * rowf;
+      if (vec) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) cov3[k] = g.cov3D[6 * i + k];
-  } else {
-    cov3d(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
-          g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], cov3);
-  }
-  const bool sr = !g.cov3D && out.dscale && out.drot;
-  float a_col[3], a_op, a_mean[3], a_cov[6], a_s[3], a_r[4];
-  bool f_col = !(acc & GS_ACC_COLORS), f_op = !(acc & GS_ACC_OPACITY), f_mean = !(acc & GS_ACC_MEANS3D),
-       f_cov = !(acc & GS_ACC_COV3D), f_sh = !(acc & GS_ACC_SH), f_s = !(acc & GS_ACC_SCALES),
-       f_r = !(acc & GS_ACC_ROTATIONS);
-  if (out.dcolor && !f_col)
-    for (int k = 0; k < 3; k++) a_col[k] = out.dcolor[3 * i + k];
-  if (!f_op) a_op = out.dopacity[i];
-  if (!f_mean)
-    for (int k = 0; k < 3; k++) a_mean[k] = out.dmean3D[3 * i + k];
-  if (out.dcov3D && !f_cov)
-    for (int k = 0; k < 6; k++) a_cov[k] = out.dcov3D[6 * i + k];
-  if (DEG >= 0 && !f_sh) {
-    const float* d = out.dsh + (size_t)i * rowf;
+        for (int q = 0; q < KF / 4; q++) {
+          const float4 v = reinterpret_cast<const float4*>(src)[q];
+          row[4 * q] = v.x, row[4 * q + 1] = v.y, row[4 * q + 2] = v.z, row[4 * q + 3] = v.w;
+        }
+      } else {
 #pragma unroll
-    for (int k = 0; k < KF; k++) dsh[k] = d[k];
-  }
-  if (sr && !f_s)
-    for (int k = 0; k < 3; k++) a_s[k] = out.dscale[3 * i + k];
-  if (sr && !f_r)
-    for (int k = 0; k < 4; k++) a_r[k] = out.drot[4 * i + k];
+        for (int k = 0; k < KF; k++) row[k] = src[k];
+      }
+    }
+    const float px = g.means3D[3 * i], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
+    float cov3[6];
+    if (g.cov3D) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) cov3[k] = g.cov3D[6 * i + k];
+    } else {
+      cov3d(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
+            g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], cov3);
+    }
+    const bool sr = !g.cov3D && out.dscale && out.drot;
+    float a_col[3], a_op, a_mean[3], a_cov[6], a_s[3], a_r[4];
+    bool f_col = !(acc & GS_ACC_COLORS), f_op = !(acc & GS_ACC_OPACITY), f_mean = !(acc & GS_ACC_MEANS3D),
+         f_cov = !(acc & GS_ACC_COV3D), f_sh = !(acc & GS_ACC_SH), f_s = !(acc & GS_ACC_SCALES),
+         f_r = !(acc & GS_ACC_ROTATIONS);
+    if (out.dcolor && !f_col)
+      for (int k = 0; k < 3; k++) a_col[k] = out.dcolor[3 * i + k];
+    if (!f_op) a_op = out.dopacity[i];
+    if (!f_mean)
+      for (int k = 0; k < 3; k++) a_mean[k] = out.dmean3D[3 * i + k];
+    if (out.dcov3D && !f_cov)
+      for (int k = 0; k < 6; k++) a_cov[k] = out.dcov3D[6 * i + k];
+    if (DEG >= 0 && !f_sh) {
+      const float* d = out.dsh + (size_t)i * rowf;
+#pragma unroll
+      for (int k = 0; k < KF; k++) dsh[k] = d[k];
+    }
+    if (sr && !f_s)
+      for (int k = 0; k < 3; k++) a_s[k] = out.dscale[3 * i + k];
+    if (sr && !f_r)
+      for (int k = 0; k < 4; k++) a_r[k] = out.drot[4 * i + k];
 
-  for (int v = 0; v < fv.K; v++) {
-    const ViewGrad& w = fv.v[v];
-    float dcol[3] = {0.f, 0.f, 0.f}, dop = 0.f, dmean[3] = {0.f, 0.f, 0.f}, dcv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float ds[3] = {0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f};
-    const bool vis = w.tiles[i] != 0;
-    if (vis) {
-      const float* rec = w.gsum + (size_t)i * GRAD_REC;
-      float a[GRAD_REC];
+    for (int v = 0; v < fv.K; v++) {
+      const ViewGrad& w = fv.v[v];
+      float dcol[3] = {0.f, 0.f, 0.f}, dop = 0.f, dmean[3] = {0.f, 0.f, 0.f}, dcv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      float ds[3] = {0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f};
+      const bool vis = w.tiles[i] != 0;
+      if (vis) {
+        const float* rec = w.gsum + (size_t)i * GRAD_REC;
+        float a[GRAD_REC];
 #pragma unroll
-      for (int k = 0; k < GRAD_REC; k++) a[k] = rec[k];
-      dcol[0] = a[0], dcol[1] = a[1], dcol[2] = a[2];
-      dop = a[8];
-      camera_grads(w.c, px, py, pz, cov3, a[5], a[6], a[7], a[3], a[4], dcv, dmean);
-      if (DEG >= 0) {
-        float shm[3];
-        const float vx = px - w.c.campos[0], vy = py - w.c.campos[1], vz = pz - w.c.campos[2];
-        sh_backward<D, true, true>(row, g.M, vx, vy, vz, w.clamped[i], dcol, shm, dsh, f_sh);
-        dmean[0] = dmean[0] + shm[0];
-        dmean[1] = dmean[1] + shm[1];
-        dmean[2] = dmean[2] + shm[2];
+        for (int k = 0; k < GRAD_REC; k++) a[k] = rec[k];
+        dcol[0] = a[0], dcol[1] = a[1], dcol[2] = a[2];
+        dop = a[8];
+        camera_grads(w.c, px, py, pz, cov3, a[5], a[6], a[7], a[3], a[4], dcv, dmean);
+        if (DEG >= 0) {
+          float shm[3];
+          const float vx = px - w.c.campos[0], vy = py - w.c.campos[1], vz = pz - w.c.campos[2];
+          sh_backward<D, true, true>(row, g.M, vx, vy, vz, w.clamped[i], dcol, shm, dsh, f_sh);
+          dmean[0] = dmean[0] + shm[0];
+          dmean[1] = dmean[1] + shm[1];
+          dmean[2] = dmean[2] + shm[2];
+        }
+        if (sr)
+          cov3d_backward(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier,
+                         g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3],
+                         dcv, ds, dr);
+      } else if (DEG >= 0) {
+#pragma unroll
+        for (int k = 0; k < KF; k++) vput(dsh[k], 0.0f, f_sh);
       }
-      if (sr)
-        cov3d_backward(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier,
-                       g.rotations[4 * i], g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3],
-                       dcv, ds, dr);
-    } else if (DEG >= 0) {
-#pragma unroll
-      for (int k = 0; k < KF; k++) vput(dsh[k], 0.0f, f_sh);
+      if (DEG >= 0) f_sh = false;
+      for (int k = 0; k < 3; k++) vput(a_col[k], dcol[k], f_col);
+      f_col = false;
+      vput(a_op, dop, f_op);
+      f_op = false;
+      for (int k = 0; k < 3; k++) vput(a_mean[k], dmean[k], f_mean);
+      f_mean = false;
+      for (int k = 0; k < 6; k++) vput(a_cov[k], dcv[k], f_cov);
+      f_cov = false;
+      for (int k = 0; k < 3; k++) vput(a_s[k], ds[k], f_s);
+      f_s = false;
+      for (int k = 0; k < 4; k++) vput(a_r[k], dr[k], f_r);
+      f_r = false;
     }
-    if (DEG >= 0) f_sh = false;
-    for (int k = 0; k < 3; k++) vput(a_col[k], dcol[k], f_col);
-    f_col = false;
-    vput(a_op, dop, f_op);
-    f_op = false;
-    for (int k = 0; k < 3; k++) vput(a_mean[k], dmean[k], f_mean);
-    f_mean = false;
-    for (int k = 0; k < 6; k++) vput(a_cov[k], dcv[k], f_cov);
-    f_cov = false;
-    for (int k = 0; k < 3; k++) vput(a_s[k], ds[k], f_s);
-    f_s = false;
-    for (int k = 0; k < 4; k++) vput(a_r[k], dr[k], f_r);
-    f_r = false;
-  }
-  if (out.dcolor)
-    for (int k = 0; k < 3; k++) out.dcolor[3 * i + k] = a_col[k];
-  out.dopacity[i] = a_op;
-  for (int k = 0; k < 3; k++) out.dmean3D[3 * i + k] = a_mean[k];
-  if (out.dcov3D)
-    for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = a_cov[k];
-  if (sr) {
-    for (int k = 0; k < 3; k++) out.dscale[3 * i + k] = a_s[k];
-    for (int k = 0; k < 4; k++) out.drot[4 * i + k] = a_r[k];
-  }
-  if (DEG >= 0 && out.dsh) {
-    float* dst = out.dsh + (size_t)i * rowf;
-    if (vec) {
-#pragma unroll
-      for (int q = 0; q < KF / 4; q++)
-        reinterpret_cast<float4*>(dst)[q] = make_float4(dsh[4 * q], dsh[4 * q + 1], dsh[4 * q + 2], dsh[4 * q + 3]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < KF; k++) dst[k] = dsh[k];
+    if (out.dcolor)
+      for (int k = 0; k < 3; k++) out.dcolor[3 * i + k] = a_col[k];
+    out.dopacity[i] = a_op;
+    for (int k = 0; k < 3; k++) out.dmean3D[3 * i + k] = a_mean[k];
+    if (out.dcov3D)
+      for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = a_cov[k];
+    if (sr) {
+      for (int k = 0; k < 3; k++) out.dscale[3 * i + k] = a_s[k];
+      for (int k = 0; k < 4; k++) out.drot[4 * i + k] = a_r[k];
     }
-    if (!(acc & GS_ACC_SH))  // coefficients past (D + 1)^2: zero (accumulated: + 0)
-      for (int k = KF; k < rowf; k++) dst[k] = 0.0f;
+    if (DEG >= 0 && out.dsh && !stage) {
+      float* dst = out.dsh + (size_t)i * rowf;
+      if (vec) {
+#pragma unroll
+        for (int q = 0; q < KF / 4; q++)
+          reinterpret_cast<float4*>(dst)[q] = make_float4(dsh[4 * q], dsh[4 * q + 1], dsh[4 * q + 2], dsh[4 * q + 3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < KF; k++) dst[k] = dsh[k];
+      }
+      if (!(acc & GS_ACC_SH))  // coefficients past (D + 1)^2: zero (accumulated: + 0)
+        for (int k = KF; k < rowf; k++) dst[k] = 0.0f;
+    }
+  }
+  if (stage) {
+    // the gradient rows out the same way (rows of exactly 3K floats: nothing past (D + 1)^2)
+    constexpr int PER = LDS ? KF / 4 : 1;
+    lds_barrier();  // every lane has read its staged SH row
+    if (live) {
+#pragma unroll
+      for (int q = 0; q < PER; q++)
+        *reinterpret_cast<float4*>(&s_rows[threadIdx.x * BG_ROW + 4 * q]) =
+            make_float4(dsh[4 * q], dsh[4 * q + 1], dsh[4 * q + 2], dsh[4 * q + 3]);
+    }
+    lds_barrier();
+    float4* dst4 = reinterpret_cast<float4*>(out.dsh + (size_t)i0 * KF);
+    const int n4 = nG * PER;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      const int f = (int)threadIdx.x + 256 * q;
+      if (f < n4) {
+        const int r = f / PER, c = f - r * PER;
+        dst4[f] = *reinterpret_cast<const float4*>(&s_rows[r * BG_ROW + 4 * c]);
+      }
+    }
   }
 }
 
