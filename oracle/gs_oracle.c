@@ -150,6 +150,16 @@ static inline float cull_lim(float op) {
 static int g_exact_tiles = 1;
 void oracle_set_exact_tiles(int on) { g_exact_tiles = on; }
 
+/* Backward accumulation precision.  Default: fp64 sums (the reference answer).  With
+ * oracle_set_acc_f32(1) every per-instance and per-Gaussian sum is rounded to fp32 after each add,
+ * in this file's order (pixels row-major within a tile, then instances in list order): another
+ * valid fp32 summation order, whose distance from the fp64 answer measures how much an fp32
+ * implementation (upstream's atomics, the device's wave trees) can move an ill-conditioned
+ * gradient.  Tests only; it never changes the forward. */
+static int g_acc_f32 = 0;
+void oracle_set_acc_f32(int on) { g_acc_f32 = on; }
+static inline double acc_add(double a, double x) { return g_acc_f32 ? (double)((float)a + (float)x) : a + x; }
+
 typedef struct { float mx, my, A, B, det, R, dyr, AL; int x0, x1, mode; } SpanCtx;
 static SpanCtx span_ctx(float mx, float my, float A, float B, float C, float L, int x0, int x1) {
     SpanCtx s;
@@ -764,7 +774,7 @@ long long oracle_backward(int P, int D, int M, const float* bg, int W, int H, co
                             accum_rec[c] = last_alpha * last_color[c] + (1.f - last_alpha) * accum_rec[c];
                             last_color[c] = col;
                             dL_dalpha += (col - accum_rec[c]) * dpix[c];
-                            a[c] += (double)(dchannel_dcolor * dpix[c]);
+                            a[c] = acc_add(a[c], (double)(dchannel_dcolor * dpix[c]));
                         }
                         dL_dalpha *= T;
                         last_alpha = alpha;
@@ -773,19 +783,22 @@ long long oracle_backward(int P, int D, int M, const float* bg, int W, int H, co
                         float gdx = G * dx, gdy = G * dy;
                         float dG_ddelx = -gdx * o->conic[0] - gdy * o->conic[1];
                         float dG_ddely = -gdy * o->conic[2] - gdx * o->conic[1];
-                        a[3] += (double)(dL_dG * dG_ddelx * ddelx_dx);
-                        a[4] += (double)(dL_dG * dG_ddely * ddely_dy);
-                        a[5] += (double)(-0.5f * gdx * dx * dL_dG);
-                        a[6] += (double)(-0.5f * gdx * dy * dL_dG);
-                        a[7] += (double)(-0.5f * gdy * dy * dL_dG);
-                        a[8] += (double)(G * dL_dalpha);
+                        a[3] = acc_add(a[3], (double)(dL_dG * dG_ddelx * ddelx_dx));
+                        a[4] = acc_add(a[4], (double)(dL_dG * dG_ddely * ddely_dy));
+                        a[5] = acc_add(a[5], (double)(-0.5f * gdx * dx * dL_dG));
+                        a[6] = acc_add(a[6], (double)(-0.5f * gdx * dy * dL_dG));
+                        a[7] = acc_add(a[7], (double)(-0.5f * gdy * dy * dL_dG));
+                        a[8] = acc_add(a[8], (double)(G * dL_dalpha));
                     }
                 }
         }
     }
     double* acc = (double*)calloc((size_t)P * 9, sizeof(double));
     for (long long k = 0; k < b.I; k++)
-        for (int c = 0; c < 9; c++) acc[(size_t)b.inst[k].gid * 9 + c] += iacc[(size_t)k * 9 + c];
+        for (int c = 0; c < 9; c++) {
+            double* d = &acc[(size_t)b.inst[k].gid * 9 + c];
+            *d = acc_add(*d, iacc[(size_t)k * 9 + c]);
+        }
     free(iacc);
     /* preprocess backward for every visible Gaussian */
 #pragma omp parallel for schedule(static)

@@ -180,6 +180,21 @@ def set_exact_tiles(on: bool):
     lib().oracle_set_exact_tiles(int(bool(on)))
 
 
+def set_acc_f32(on: bool):
+    """Backward sums in fp32 (this oracle's order) instead of fp64: the fp32 ordering-noise probe
+    the conditioning-aware gradient checks compare the device against (gs_oracle.c)."""
+    lib().oracle_set_acc_f32(int(bool(on)))
+
+
+def backward_f32_acc(sc: Scene, dL_dpix):
+    """backward() with fp32 accumulation (set_acc_f32), restoring the fp64 default afterwards."""
+    set_acc_f32(True)
+    try:
+        return backward(sc, dL_dpix)
+    finally:
+        set_acc_f32(False)
+
+
 def sh_forward(deg, means, campos, shs):
     P = means.shape[0]
     shs = _f32(shs).reshape(P, -1, 3)

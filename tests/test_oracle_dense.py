@@ -190,3 +190,19 @@ def test_oracle_vs_dense_500_gaussians_clamp_region(oracle, deg, W, H, bgv, mod)
     _close(gr["dmeans3D"], m3.grad.numpy(), name="dmeans3D", **chain)
     # the clamp region's Gaussians carry gradient through the clamped Jacobian too
     assert np.abs(gr["dmeans3D"][clamped & vis]).max() > 0
+
+
+def test_oracle_f32_accumulation_probe(oracle):
+    """oracle.backward_f32_acc (the fp32-order noise probe of the GPU chain checks) changes only the
+    summation precision: the forward is untouched, the fp64 default comes back afterwards, and the
+    two backward answers differ by fp32 rounding only on a well-conditioned scene."""
+    cam, sc = _scene(400, 96, 80, 2, seed=5)
+    osc = _oracle_scene(oracle, cam, sc, np.zeros(3, np.float32))
+    dpix = gs_scenes.dl_dimage(80, 96, seed=6).numpy()
+    g64 = oracle.backward(osc, dpix)
+    g32 = oracle.backward_f32_acc(osc, dpix)
+    again = oracle.backward(osc, dpix)
+    for k in ("dmeans2D", "dopacity", "dmeans3D", "dsh", "dscales", "drotations"):
+        np.testing.assert_array_equal(again[k], g64[k])  # default restored
+        _close(g32[k], g64[k], rtol=1e-4, frac=1e-5, name=k)
+    assert any(not np.array_equal(g32[k], g64[k]) for k in ("dmeans2D", "dsh", "dscales"))
