@@ -70,7 +70,7 @@ def test_gpu_ssim_matches_reference_golden(case, device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(3, 270, 480), (2, 3, 64, 80), (3, 1080, 1920)])
+@pytest.mark.parametrize("shape", [(3, 270, 480), (2, 3, 64, 80), (3, 1080, 1920), (3, 5, 7), (3, 1, 40)])
 def test_gpu_ssim_matches_oracle(shape, device):
     """Including the full 1080p frame of train.py (16x16 tiles, ragged borders)."""
     import gs_loss
@@ -107,7 +107,8 @@ def _oracle_photometric(a0, b0, lam):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape,lam", [((3, 270, 480), 0.2), ((2, 3, 64, 80), 0.2), ((3, 1080, 1920), 0.2),
-                                       ((3, 37, 53), 0.7), ((1, 16, 16), 0.0), ((3, 20, 21), 1.0)])
+                                       ((3, 37, 53), 0.7), ((1, 16, 16), 0.0), ((3, 20, 21), 1.0),
+                                       ((3, 5, 7), 0.2), ((3, 1, 40), 0.2), ((2, 33, 1), 0.5)])
 def test_gpu_photometric_loss_matches_oracle(shape, lam, device):
     """train.py:91-92 fused (gs_loss.photometric_loss) against the fp64 oracle of the same expression:
     value within 2e-6, gradient within 1e-5 relative + 1e-5 x max; pixels with image == gt (L1
