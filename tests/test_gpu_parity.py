@@ -186,6 +186,11 @@ CASES = [
     ("C1_10k_sh0_256", 10_000, 0, 256, 256, 0.0),
     ("ragged_sh1_bg", 3_000, 1, 203, 117, 0.5),
     ("C2_100k_sh3_800", 100_000, 3, 800, 800, 0.0),
+    # degenerate frames: one pixel, one row, one column, smaller than a tile; a single Gaussian
+    ("one_pixel", 16, 0, 1, 1, 0.2),
+    ("one_row", 300, 1, 37, 1, 0.0),
+    ("one_col", 300, 2, 1, 45, 0.3),
+    ("single_gaussian", 1, 3, 33, 17, 0.1),
 ]
 
 
