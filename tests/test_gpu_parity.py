@@ -327,6 +327,16 @@ def test_fast_mode_full_c3_vs_oracle(oracle, device, fast_mode):
     _fast_mode_parity(oracle, device, cam, sc, np.zeros(3, np.float32))
 
 
+@pytest.mark.timeout(600)
+def test_fast_mode_full_c5_vs_oracle(oracle, device, fast_mode):
+    """C5 (bench --workload c5) at full size: 5M Gaussians SH3 at 1920x1080, 21.6M instances, most
+    of them behind saturated pixels (the record cuts and the longest-first order at their extreme),
+    in the default numerics mode against the oracle; same checks as full C3."""
+    cam = gs_scenes.identity_camera(1920, 1080)
+    sc = gs_scenes.random_gaussians(5_000_000, 3, cam=cam, seed=0)
+    _fast_mode_parity(oracle, device, cam, sc, np.zeros(3, np.float32))
+
+
 def test_fast_mode_is_deterministic(device, fast_mode):
     cam = gs_scenes.identity_camera(256, 256)
     sc = gs_scenes.random_gaussians(20000, 3, cam=cam, seed=13)
