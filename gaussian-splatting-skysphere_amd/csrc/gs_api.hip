@@ -272,23 +272,34 @@ static bool queue_order_flags(const uint32_t* counters, hipStream_t st) {
   return false;
 }
 
-int gs_forward_preprocess(int P, int D, int M, const float* background, int W, int H, const float* means3D,
-                          const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
-                          float scale_modifier, const float* rotations, const float* cov3D_precomp,
-                          const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
-                          float tan_fovy, int prefiltered, int* radii_out, void* geom_buffer,
-                          long long* num_rendered_host, int debug, void* stream) {
+// split SH inputs (features_dc + features_rest rows): shs_rest needs SH colours with M >= 2
+static bool validate_split(int M, const float* shs, const float* shs_rest, const float* colors_precomp) {
+  if (!shs_rest) return true;
+  if (!shs || colors_precomp) return set_error("split SH: features_dc and features_rest replace shs (no colours)"), false;
+  if (M < 2) return set_error("split SH: M must be >= 2 (got %d)", M), false;
+  return true;
+}
+
+static int forward_preprocess_impl(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                                   const float* shs, const float* shs_rest, const float* colors_precomp,
+                                   const float* opacities, const float* scales, float scale_modifier,
+                                   const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                                   const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                                   int prefiltered, int* radii_out, void* geom_buffer, long long* num_rendered_host,
+                                   int debug, void* stream) {
   clear_error(debug);
   if (num_rendered_host) *num_rendered_host = 0;
   if (!validate(P, D, M, W, H, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, viewmatrix,
                 projmatrix, campos, background))
     return 1;
+  if (!validate_split(M, shs, shs_rest, colors_precomp)) return 1;
   if (P == 0) return 0;
   if (!radii_out || !geom_buffer || !num_rendered_host) return set_error("missing output pointer"), 1;
   hipStream_t st = (hipStream_t)stream;
   GeomPtrs geo;
   geom_layout((size_t)P, &geo, (char*)geom_buffer);
-  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier};
+  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier,
+                 shs_rest};
   CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, prefiltered);
   // num_rendered is the sum of the per-Gaussian tile counts, known when preprocess ends: read it
   // back through pinned memory behind an event while the GPU goes on with compaction, the depth
@@ -306,6 +317,33 @@ int gs_forward_preprocess(int P, int D, int M, const float* background, int W, i
   if (err & 1u) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
   *num_rendered_host = (long long)I;
   return 0;
+}
+
+int gs_forward_preprocess(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                          const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                          float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                          const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                          float tan_fovy, int prefiltered, int* radii_out, void* geom_buffer,
+                          long long* num_rendered_host, int debug, void* stream) {
+  return forward_preprocess_impl(P, D, M, background, W, H, means3D, shs, nullptr, colors_precomp, opacities, scales,
+                                 scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx,
+                                 tan_fovy, prefiltered, radii_out, geom_buffer, num_rendered_host, debug, stream);
+}
+
+int gs_forward_preprocess_split(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                                const float* shs_dc, const float* shs_rest, const float* opacities,
+                                const float* scales, float scale_modifier, const float* rotations,
+                                const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                                const float* campos, float tan_fovx, float tan_fovy, int prefiltered, int* radii_out,
+                                void* geom_buffer, long long* num_rendered_host, int debug, void* stream) {
+  if (!shs_rest) {
+    clear_error(debug);
+    if (num_rendered_host) *num_rendered_host = 0;
+    return set_error("split SH: features_rest is NULL"), 1;
+  }
+  return forward_preprocess_impl(P, D, M, background, W, H, means3D, shs_dc, shs_rest, nullptr, opacities, scales,
+                                 scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx,
+                                 tan_fovy, prefiltered, radii_out, geom_buffer, num_rendered_host, debug, stream);
 }
 
 int gs_forward_preprocess_views(int K, int P, int D, int M, const float* const* background, const int* image_width,
@@ -427,7 +465,7 @@ long long gs_rasterize_forward(int P, int D, int M, const float* background, int
 }
 
 static int backward_impl(int P, int D, int M, const float* background, int W, int H, const float* means3D,
-                         const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                         const float* shs, const float* shs_rest, const float* colors_precomp, const float* opacities, const float* scales,
                          float scale_modifier, const float* rotations, const float* cov3D_precomp,
                          const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
                          float tan_fovy, const void* geom_buffer, long long num_rendered, const void* binning_buffer,
@@ -440,6 +478,7 @@ static int backward_impl(int P, int D, int M, const float* background, int W, in
   if (!validate(P, D, M, W, H, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, viewmatrix,
                 projmatrix, campos, background, false))
     return 1;
+  if (!validate_split(M, shs, shs_rest, colors_precomp)) return 1;
   if (P == 0) return 0;
   if (!geom_buffer || !binning_buffer || !image_buffer || !dL_dout_color || !grad_buffer)
     return set_error("missing buffer pointer"), 1;
@@ -454,7 +493,8 @@ static int backward_impl(int P, int D, int M, const float* background, int W, in
   geom_layout((size_t)P, &geo, (char*)geom_buffer);
   bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer);
   img_layout(W, H, &img, (char*)image_buffer);
-  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier};
+  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier,
+                 shs_rest};
   float* gradrec = (float*)grad_buffer;
   if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, st);
   // dL_dcov3D is filled whenever the caller passes it: upstream writes it for scale/rotation
@@ -479,7 +519,7 @@ int gs_backward(int P, int D, int M, const float* background, int W, int H, cons
                 float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
                 float* dL_drotations, int debug, void* stream) {
   (void)radii;
-  return backward_impl(P, D, M, background, W, H, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
+  return backward_impl(P, D, M, background, W, H, means3D, shs, nullptr, colors_precomp, opacities, scales, scale_modifier,
                        rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, geom_buffer,
                        num_rendered, binning_buffer, image_buffer, dL_dout_color, grad_buffer, dL_dmeans2D,
                        dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, 0u, nullptr,
@@ -497,11 +537,33 @@ int gs_backward_accumulate(int P, int D, int M, const float* background, int W, 
                            float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
                            unsigned accumulate, void* wait_event, int debug, void* stream) {
   (void)radii;
-  return backward_impl(P, D, M, background, W, H, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
+  return backward_impl(P, D, M, background, W, H, means3D, shs, nullptr, colors_precomp, opacities, scales, scale_modifier,
                        rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, geom_buffer,
                        num_rendered, binning_buffer, image_buffer, dL_dout_color, grad_buffer, dL_dmeans2D,
                        dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, accumulate,
                        wait_event, debug, stream);
+}
+
+int gs_backward_accumulate_split(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                                 const float* shs_dc, const float* shs_rest, const float* opacities,
+                                 const float* scales, float scale_modifier, const float* rotations,
+                                 const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                                 const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                                 const void* geom_buffer, long long num_rendered, const void* binning_buffer,
+                                 const void* image_buffer, const float* dL_dout_color, void* grad_buffer,
+                                 float* dL_dmeans2D, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                                 float* dL_dsh, float* dL_dscales, float* dL_drotations, unsigned accumulate,
+                                 void* wait_event, int debug, void* stream) {
+  (void)radii;
+  if (!shs_rest) {
+    clear_error(debug);
+    return set_error("split SH: features_rest is NULL"), 1;
+  }
+  return backward_impl(P, D, M, background, W, H, means3D, shs_dc, shs_rest, nullptr, opacities, scales,
+                       scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy,
+                       geom_buffer, num_rendered, binning_buffer, image_buffer, dL_dout_color, grad_buffer,
+                       dL_dmeans2D, nullptr, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations,
+                       accumulate, wait_event, debug, stream);
 }
 
 int gs_backward_render(int P, int D, int M, const float* background, int W, int H, const float* viewmatrix,
@@ -716,7 +778,8 @@ int gs_activate_forward(int P, int sh_rest, const float* features_dc, const floa
   clear_error(0);
   if (P < 0 || sh_rest < 0) return set_error("activate: P and sh_rest must be >= 0"), 1;
   if (P == 0) return 0;
-  if (!features_dc || (sh_rest && !features_rest) || !opacity_raw || !scaling_raw || !rotation_raw || !shs ||
+  // shs may be null: only opacity / scales / rotations are activated (split-SH rasterizer inputs)
+  if ((shs && (!features_dc || (sh_rest && !features_rest))) || !opacity_raw || !scaling_raw || !rotation_raw ||
       !opacity || !scales || !rotations)
     return set_error("activate: missing pointer"), 1;
   if (((uintptr_t)rotation_raw | (uintptr_t)rotations | (uintptr_t)shs) & 15)

@@ -940,7 +940,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraAr
 
 // Register variant (GS_PBWD_REG, the default): the lane loads its own SH row (first 3K floats, 16-B loads when
 // the rows allow) and stores dL/dsh the same way; no LDS, so occupancy is set by registers alone.
-template <int DEG>
+template <int DEG, bool SPLIT = false>  // SPLIT: SH rows from g.shs (features_dc) + g.shs_rest
 __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PBWD_WPE) void k_preprocess_bwd_reg(GaussianArgs g, CameraArgs c,
                                                             const uint32_t* __restrict__ tiles,
                                                             const uint8_t* __restrict__ clamped,
@@ -952,8 +952,19 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PBWD_WPE) void k_preprocess_bwd
   const float* src = g.shs + (size_t)i * rowf;
   float* dst = out.dsh + (size_t)i * rowf;
   const bool vec = (KF & 3) == 0 && (rowf & 3) == 0 && ((((uintptr_t)g.shs) | ((uintptr_t)out.dsh)) & 15) == 0;
+  // dL/dsh rows stay [P, M, 3] whether or not the inputs are split
+  const bool vec_out = SPLIT ? (KF & 3) == 0 && (rowf & 3) == 0 && (((uintptr_t)out.dsh) & 15) == 0 : vec;
   float row[KF];
-  if (vec) {
+  if constexpr (SPLIT) {  // split rows: features_dc [P, 1, 3] + features_rest [P, M - 1, 3], 12-B pieces
+    const F3 d = reinterpret_cast<const F3*>(g.shs)[i];
+    row[0] = d.a, row[1] = d.b, row[2] = d.c;
+    const F3* r3 = reinterpret_cast<const F3*>(g.shs_rest + (size_t)i * (rowf - 3));
+#pragma unroll
+    for (int j = 0; j < KF / 3 - 1; j++) {
+      const F3 t = r3[j];
+      row[3 + 3 * j] = t.a, row[4 + 3 * j] = t.b, row[5 + 3 * j] = t.c;
+    }
+  } else if (vec) {
 #pragma unroll
     for (int q = 0; q < KF / 4; q++) {
       const float4 v = reinterpret_cast<const float4*>(src)[q];
@@ -971,7 +982,7 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PBWD_WPE) void k_preprocess_bwd
   }
   preprocess_bwd_one<DEG, true>(i, g, c, tiles, clamped, gsum, out, row);
   if (out.acc & GS_ACC_SH) {  // (uniform) multi-view accumulation: dL/dsh += this view's
-    if (vec) {
+    if (vec_out) {
 #pragma unroll
       for (int q = 0; q < KF / 4; q++) {
         const float4 o = reinterpret_cast<const float4*>(dst)[q];
@@ -984,7 +995,7 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PBWD_WPE) void k_preprocess_bwd
     }
     return;  // coefficients past (D + 1)^2 get + 0
   }
-  if (vec) {
+  if (vec_out) {
 #pragma unroll
     for (int q = 0; q < KF / 4; q++)
       reinterpret_cast<float4*>(dst)[q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
@@ -1257,7 +1268,21 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
               geo.gsum, out);
     return;
   }
-#if GS_PBWD_REG
+  // split SH rows are read by the register variant only
+  if (g.shs_rest) {
+#define GS_PBWD_SPLIT(D)                                                                                        \
+  GS_LAUNCH("preprocess_bwd", (k_preprocess_bwd_reg<D, true>), grid, block, 0, st, g, c, geo.tiles, geo.clamped, \
+            geo.gsum, out)
+    switch (g.D) {
+      case 0: GS_PBWD_SPLIT(0); break;
+      case 1: GS_PBWD_SPLIT(1); break;
+      case 2: GS_PBWD_SPLIT(2); break;
+      default: GS_PBWD_SPLIT(3); break;
+    }
+#undef GS_PBWD_SPLIT
+    return;
+  }
+  if (GS_PBWD_REG) {
   switch (g.D) {
     case 0:
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd_reg<0>, grid, block, 0, st, g, c, geo.tiles, geo.clamped, geo.gsum, out);
@@ -1273,7 +1298,7 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
       break;
   }
   return;
-#endif
+  }
   switch (g.D) {
     case 0:
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<0>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,

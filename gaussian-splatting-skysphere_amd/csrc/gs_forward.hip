@@ -26,12 +26,23 @@ namespace gs {
 // SH -> RGB for one Gaussian, channel-major evaluation order identical to oracle/gs_oracle.c
 // sh_eval_one (reference: /root/reference/utils/sh_utils.py:57-100, +0.5 and clamp_min(0) as
 // /root/reference/gaussian_renderer/__init__.py:77-78).
+// rest != null: split rows (sh = the Gaussian's features_dc row, rest = its features_rest row),
+// read as 12-B pieces; the evaluation is the same.
 template <int DEG>
-__device__ __forceinline__ void sh_to_rgb(const float* __restrict__ sh, int M, float x, float y, float z, float* rgb,
-                                          uint32_t& clamped) {
+__device__ __forceinline__ void sh_to_rgb(const float* __restrict__ sh, const float* __restrict__ rest, int M, float x,
+                                          float y, float z, float* rgb, uint32_t& clamped) {
   constexpr int K = (DEG + 1) * (DEG + 1);
   float s[K * 3];
-  if (((M * 3) & 3) == 0) {
+  if (rest) {
+    const F3 d = *reinterpret_cast<const F3*>(sh);
+    s[0] = d.a, s[1] = d.b, s[2] = d.c;
+    const F3* r3 = reinterpret_cast<const F3*>(rest);
+#pragma unroll
+    for (int j = 0; j < K - 1; j++) {
+      const F3 t = r3[j];
+      s[3 + 3 * j] = t.a, s[4 + 3 * j] = t.b, s[5 + 3 * j] = t.c;
+    }
+  } else if (((M * 3) & 3) == 0) {
     const float4* s4 = reinterpret_cast<const float4*>(sh);
 #pragma unroll
     for (int v = 0; v < (K * 3 + 3) / 4; v++) {
@@ -75,7 +86,10 @@ __device__ __forceinline__ void sh_to_rgb(const float* __restrict__ sh, int M, f
 
 // DEG = -1: colours precomputed by the caller
 // One Gaussian; returns the number of tiles it touches (0 when culled).
-template <int DEG>
+// SPLIT: SH rows from g.shs (features_dc) + g.shs_rest when g.shs_rest is set (a uniform branch:
+// with both row loaders in the kernel the scheduler keeps the split loads where they are used, 91
+// VGPRs; a split-only instantiation hoists them, 130 VGPRs, 75 -> 97 us at C3)
+template <int DEG, bool SPLIT = false>
 __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g, const CameraArgs& c,
                                                    int* __restrict__ radii, float4* __restrict__ splat,
                                                    float4* __restrict__ binrec, uint32_t& dbits,
@@ -128,7 +142,11 @@ __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g,
   } else {
     float dx = px - c.campos[0], dy = py - c.campos[1], dz = pz - c.campos[2];
     float len = sqrtf(dx * dx + dy * dy + dz * dz);
-    sh_to_rgb<(DEG < 0 ? 0 : DEG)>(g.shs + (size_t)i * g.M * 3, g.M, dx / len, dy / len, dz / len, rgb, cl);
+    if (SPLIT && g.shs_rest)
+      sh_to_rgb<(DEG < 0 ? 0 : DEG)>(g.shs + (size_t)i * 3, g.shs_rest + (size_t)i * (g.M - 1) * 3, g.M, dx / len,
+                                     dy / len, dz / len, rgb, cl);
+    else
+      sh_to_rgb<(DEG < 0 ? 0 : DEG)>(g.shs + (size_t)i * g.M * 3, nullptr, g.M, dx / len, dy / len, dz / len, rgb, cl);
   }
   // culling limit of the {alpha >= 1/255} ellipse (render-side work skipping only; never
   // changes a result, see ellipse_meets_rect): q(d) <= 2 ln(255 o), with safety margins
@@ -190,12 +208,56 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess(Gaus
   }
 }
 
+// The split-SH preprocess: k_preprocess's body with the split row loader (preprocess_one SPLIT).
+template <int DEG>
+__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess_split(
+    GaussianArgs g, CameraArgs c, int* __restrict__ radii, float4* __restrict__ splat, float4* __restrict__ binrec,
+    uint32_t* __restrict__ depth_key, uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
+    uint32_t* __restrict__ counters) {
+  __shared__ uint32_t s_sum[4], s_vis[4];
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  uint32_t area = 0, dbits = 0;
+  if (i < g.P) {
+    area = preprocess_one<DEG, true>(i, g, c, radii, splat, binrec, dbits, tiles, clamped, counters);
+    depth_key[i] = area ? dbits : DEPTH_DROP;
+  }
+  uint32_t vis = area ? 1u : 0u;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    area += (uint32_t)__shfl_xor((int)area, d, 64);
+    vis += (uint32_t)__shfl_xor((int)vis, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_sum[threadIdx.x >> 6] = area;
+    s_vis[threadIdx.x >> 6] = vis;
+  }
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+    const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
+    if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(&counters[CNT_NREND]), ((unsigned long long)nv << 32) | tot);
+  }
+}
+
 void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st) {
   (void)hipMemsetAsync(geo.counters, 0, 64, st);
   dim3 grid((g.P + 255) / 256), block(256);
   if (g.colors) {
     GS_LAUNCH("preprocess", k_preprocess<-1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
               geo.clamped, geo.counters);
+    return;
+  }
+  if (g.shs_rest) {  // split SH rows (M >= 2, so D >= 0 applies)
+#define GS_PRE_SPLIT(D)                                                                                        \
+  GS_LAUNCH("preprocess", (k_preprocess_split<D>), grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, \
+            geo.keys_a, geo.tiles, geo.clamped, geo.counters)
+    switch (g.D) {
+      case 0: GS_PRE_SPLIT(0); break;
+      case 1: GS_PRE_SPLIT(1); break;
+      case 2: GS_PRE_SPLIT(2); break;
+      default: GS_PRE_SPLIT(3); break;
+    }
+#undef GS_PRE_SPLIT
     return;
   }
   switch (g.D) {

@@ -55,6 +55,15 @@ struct GaussianArgs {
   const float* rotations;  // [P, 4] or null
   const float* cov3D;      // [P, 6] or null
   float scale_modifier;
+  // split SH rows (gs_forward_preprocess_split / gs_backward_accumulate_split): when set, `shs` is
+  // features_dc [P, 1, 3] and this is features_rest [P, M - 1, 3] (GaussianModel's own tensors,
+  // no concatenated copy); only the single-view preprocess and preprocess backward read it
+  const float* shs_rest = nullptr;
+};
+
+// a 12-B row piece loaded with one global_load_dwordx3 (4-B alignment is enough)
+struct __attribute__((aligned(4))) F3 {
+  float a, b, c;
 };
 
 struct CameraArgs {

@@ -332,7 +332,8 @@ __global__ __launch_bounds__(256) void k_activate_bwd(int P, int feat_blocks, in
 void activate_forward(int P, int rest_w, const float* f_dc, const float* f_rest, const float* o_raw,
                       const float* s_raw, const float* q_raw, float* shs, float* opac, float* scales, float* rots,
                       hipStream_t st) {
-  const uint64_t fe = ((uint64_t)P * (3 + rest_w) + 3) / 4;
+  // shs == null: the SH rows are not concatenated (a split-SH rasterizer call reads f_dc / f_rest)
+  const uint64_t fe = shs ? ((uint64_t)P * (3 + rest_w) + 3) / 4 : 0;
   const int fb = (int)((fe + 255) / 256), gb = (P + 255) / 256;
   GS_LAUNCH("activate_fwd", k_activate_fwd, dim3(fb + gb), dim3(256), 0, st, P, fb, rest_w, f_dc, f_rest, o_raw,
             s_raw, q_raw, shs, opac, scales, rots);

@@ -65,7 +65,7 @@ class _Inputs:
     """Validated, contiguous views of one rasterizer call's tensors."""
 
     def __init__(self, background, means3D, colors, opacity, scales, rotations, cov3D_precomp, viewmatrix,
-                 projmatrix, sh, campos, need_opacity=True):
+                 projmatrix, sh, campos, need_opacity=True, sh_rest=None):
         if means3D.ndimension() != 2 or means3D.size(1) != 3:
             raise RuntimeError("means3D must have dimensions (num_points, 3)")
         _dev_check(means3D, "means3D")
@@ -84,6 +84,15 @@ class _Inputs:
         self.sh = _f32(sh, "sh", d)
         self.campos = _f32(campos, "campos", d, host_ok=True)
         self.M = 0 if self.sh is None else (self.sh.size(1) if self.sh.ndimension() == 3 else self.sh.numel() // max(1, 3 * self.P))
+        # split SH rows (ABI v8): sh is features_dc [P, 1, 3], sh_rest features_rest [P, M - 1, 3]
+        self.sh_rest = _f32(sh_rest, "features_rest", d)
+        if self.sh_rest is not None:
+            if self.sh is None or self.colors is not None:
+                raise RuntimeError("split SH: features_dc and features_rest replace shs (no colors_precomp)")
+            if tuple(self.sh.shape) != (self.P, 1, 3) or self.sh_rest.ndimension() != 3 or tuple(
+                    self.sh_rest.shape[::2]) != (self.P, 3):
+                raise RuntimeError("split SH: expected features_dc [P, 1, 3] and features_rest [P, M - 1, 3]")
+            self.M = 1 + self.sh_rest.size(1)
         if self.P > 0:
             if self.colors is not None and self.colors.numel() != 3 * self.P:
                 raise RuntimeError("colors_precomp must have shape (P, 3)")
@@ -136,11 +145,14 @@ def preprocess_views(backgrounds, means3D, colors, opacity, scales, rotations, s
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, debug, prepared=None):
+                        prefiltered, debug, prepared=None, sh_rest=None):
     """prepared: (num_rendered, radii, geomBuffer) of this call from preprocess_views (the first
-    half already ran); otherwise both halves run here."""
+    half already ran); otherwise both halves run here.  sh_rest: split SH rows (sh is then
+    features_dc [P,1,3], sh_rest features_rest [P,M-1,3]; gs_forward_preprocess_split)."""
     x = _Inputs(background, means3D, colors, opacity, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
-                campos)
+                campos, sh_rest=sh_rest)
+    if prepared is not None and x.sh_rest is not None:
+        raise RuntimeError("split SH rows are not supported with prepared views")
     H, W = int(image_height), int(image_width)
     dev = x.device
     u8 = dict(dtype=torch.uint8, device=dev)
@@ -161,9 +173,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
             radii = torch.empty((x.P,), dtype=torch.int32, device=dev)
             geom = torch.empty((_lib.gs_geom_buffer_bytes(x.P),), **u8)
             nr = ctypes.c_longlong(0)
+            split = x.sh_rest is not None
             _native.check(
-                _lib.gs_forward_preprocess(
-                    x.P, int(degree), x.M, _ptr(x.bg), W, H, _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors),
+                (_lib.gs_forward_preprocess_split if split else _lib.gs_forward_preprocess)(
+                    x.P, int(degree), x.M, _ptr(x.bg), W, H, _ptr(x.means3D), _ptr(x.sh),
+                    _ptr(x.sh_rest) if split else _ptr(x.colors),
                     _ptr(x.opacity), _ptr(x.scales), float(scale_modifier), _ptr(x.rotations), _ptr(x.cov3D),
                     _ptr(x.view), _ptr(x.proj), _ptr(x.campos), float(tan_fovx), float(tan_fovy),
                     int(bool(prefiltered)), _ptr(radii), _ptr(geom), ctypes.byref(nr), int(bool(debug)), st),
@@ -187,16 +201,17 @@ GS_ACC = {n: 1 << k for k, n in enumerate(GRAD_NAMES)}
 
 def backward_impl(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
                   projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R, binningBuffer,
-                  imageBuffer, debug, want_all=True, sinks=None, wait_event=None):
+                  imageBuffer, debug, want_all=True, sinks=None, wait_event=None, sh_rest=None):
     """Shared backward.  With want_all=False the gradients that no autograd input can receive
     (colours when SHs drive the colour, cov3D when scale/rotation drive it, ...) are None and
     not computed.  sinks: {name: (buffer, accumulate)} -- that gradient is written into (or, with
     accumulate, added to) the caller's buffer, which is returned in its place
     (gs_backward_accumulate; multi-view gradient buckets, gs_view_parallel.GradBucket).
     wait_event: torch.cuda.Event the stream waits for before the kernel that writes the gradients
-    (a sink shared with views on other streams)."""
+    (a sink shared with views on other streams).  sh_rest: split SH rows as rasterize_gaussians;
+    the `sh` gradient is then that of the concatenation, [P, M, 3]."""
     x = _Inputs(background, means3D, colors, None, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
-                campos, need_opacity=False)
+                campos, need_opacity=False, sh_rest=sh_rest)
     P, dev = x.P, x.device
     f32 = dict(dtype=torch.float32, device=dev)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
@@ -238,6 +253,18 @@ def backward_impl(background, means3D, radii, colors, scales, rotations, scale_m
     with torch.cuda.device(dev):
         st = _stream(dev)
         grad_scratch = torch.empty((_lib.gs_grad_buffer_bytes(int(R)),), dtype=torch.uint8, device=dev)
+        wait = ctypes.c_void_p(wait_event.cuda_event) if wait_event is not None else None
+        if x.sh_rest is not None:  # split SH rows: SH colours, so no dL/dcolors output
+            _native.check(
+                _lib.gs_backward_accumulate_split(
+                    P, int(degree), M, _ptr(x.bg), W, H, _ptr(x.means3D), _ptr(x.sh), _ptr(x.sh_rest),
+                    _ptr(x.opacity), _ptr(x.scales), float(scale_modifier), _ptr(x.rotations), _ptr(x.cov3D),
+                    _ptr(x.view), _ptr(x.proj), _ptr(x.campos), float(tan_fovx), float(tan_fovy), _ptr(radii),
+                    _ptr(geomBuffer), int(R), _ptr(binningBuffer), _ptr(imageBuffer), _ptr(dpix), _ptr(grad_scratch),
+                    _ptr(o["means2D"]), _ptr(o["opacity"]), _ptr(o["means3D"]), _ptr(o["cov3D"]), _ptr(o["sh"]),
+                    _ptr(o["scales"]), _ptr(o["rotations"]), acc, wait, int(bool(debug)), st),
+                "rasterize_gaussians_backward")
+            return ret
         _native.check(
             _lib.gs_backward_accumulate(
                 P, int(degree), M, _ptr(x.bg), W, H, _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors), _ptr(x.opacity),
@@ -245,8 +272,7 @@ def backward_impl(background, means3D, radii, colors, scales, rotations, scale_m
                 _ptr(x.campos), float(tan_fovx), float(tan_fovy), _ptr(radii), _ptr(geomBuffer), int(R),
                 _ptr(binningBuffer), _ptr(imageBuffer), _ptr(dpix), _ptr(grad_scratch), _ptr(o["means2D"]),
                 _ptr(o["colors"]), _ptr(o["opacity"]), _ptr(o["means3D"]), _ptr(o["cov3D"]), _ptr(o["sh"]),
-                _ptr(o["scales"]), _ptr(o["rotations"]), acc,
-                ctypes.c_void_p(wait_event.cuda_event) if wait_event is not None else None, int(bool(debug)), st),
+                _ptr(o["scales"]), _ptr(o["rotations"]), acc, wait, int(bool(debug)), st),
             "rasterize_gaussians_backward")
     return ret
 

@@ -91,9 +91,9 @@ class GaussianRasterizationSettings(NamedTuple):
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                        raster_settings, prepared=None):
+                        raster_settings, prepared=None, sh_split=None):
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
-                                     cov3Ds_precomp, raster_settings, prepared)
+                                     cov3Ds_precomp, raster_settings, prepared, sh_split)
 
 
 class PreparedView:
@@ -159,15 +159,29 @@ def _run_with_snapshot(fn, args, debug, dump_name, phase):
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings, prepared=None):
+                raster_settings, prepared=None, sh_split=None):
         s = raster_settings
         # the camera matrices arrive transposed (cameras.py:54-56 world_view_transform is a
         # .transpose(0, 1) view); make them contiguous once and reuse them in backward
         view, proj = s.viewmatrix.contiguous(), s.projmatrix.contiguous()
+        sh_rest = None
+        if sh_split is not None:
+            # split SH rows: the kernels read features_dc / features_rest in place; `sh` is only the
+            # [P, M, 3] carrier of the concatenation's gradient (its values are never read)
+            dc, sh_rest = (t.detach() for t in sh_split)
+            if prepared is not None:
+                raise RuntimeError("sh_split: not supported with prepared views")
+            if tuple(sh.shape) != (dc.shape[0], 1 + sh_rest.shape[1], 3):
+                raise RuntimeError("sh_split: shs must be the [P, M, 3] gradient carrier of cat(features_dc, "
+                                   "features_rest)")
+            sh = dc
         args = (s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
                 view, proj, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
                 s.campos, s.prefiltered, s.debug)
-        if prepared is not None:
+        if sh_rest is not None:
+            num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _run_with_snapshot(
+                lambda *a: _C.rasterize_gaussians(*a, sh_rest=sh_rest), args, s.debug, "snapshot_fw.dump", "forward")
+        elif prepared is not None:
             nz = lambda t: None if t is None or t.numel() == 0 else t  # noqa: E731
             tri = prepared.take(s, (means3D, nz(sh), nz(colors_precomp), opacities, nz(scales), nz(rotations),
                                     nz(cov3Ds_precomp)))
@@ -179,6 +193,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
         ctx.matrices = (view, proj)
+        ctx.sh_rest = sh_rest
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the (int) radii output
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
@@ -192,7 +207,7 @@ class _RasterizeGaussians(torch.autograd.Function):
     def backward(ctx, grad_out_color, _grad_radii):
         s = ctx.raster_settings
         if grad_out_color is None:  # the colour output did not reach the loss
-            return (None,) * 10
+            return (None,) * 11
         colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer, imgBuffer = (
             ctx.saved_tensors)
         view, proj = ctx.matrices
@@ -204,6 +219,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         # when every parameter gradient the call needs goes to it: only the per-tile half and
         # dL_dmeans2D run now, the per-Gaussian half later for all of its views in one pass
         deferrer = _deferring_owner(ctx)
+        if deferrer is not None and ctx.sh_rest is not None:
+            raise RuntimeError("sh_split: not supported with a deferring gradient bucket")
         if deferrer is not None:
             dm2 = _C.backward_render(s.bg, view, proj, s.campos, s.tanfovx, s.tanfovy, grad_out_color.contiguous(),
                                      means3D.size(0), s.sh_degree, sh.size(1) if sh.ndimension() == 3 else 0,
@@ -214,7 +231,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                                           degree=s.sh_degree, debug=s.debug),
                                 (view, proj, s.campos, s.tanfovx, s.tanfovy, s.image_width, s.image_height,
                                  geomBuffer))
-            return (None, dm2) + (None,) * 8
+            return (None, dm2) + (None,) * 9
 
         sinks, sunk, owners = {}, set(), []
         for k, name, t, owner in ctx.sinks:
@@ -236,7 +253,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             wait = evs[0] if evs else None
 
         def _bwd(*a):
-            return _C.backward_impl(*a, want_all=False, sinks=sinks, wait_event=wait)
+            return _C.backward_impl(*a, want_all=False, sinks=sinks, wait_event=wait, sh_rest=ctx.sh_rest)
 
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
          grad_rotations) = _run_with_snapshot(_bwd, args, s.debug, "snapshot_bw.dump", "backward")
@@ -244,7 +261,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             if hasattr(o, "written"):
                 o.written(st)
         grads = [grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
-                 grad_rotations, grad_cov3Ds_precomp, None, None]
+                 grad_rotations, grad_cov3Ds_precomp, None, None, None]
         for k in sunk:  # already in the sink's buffer (the tensor's .grad)
             grads[k] = None
         return tuple(grads)
@@ -276,8 +293,12 @@ class GaussianRasterizer(nn.Module):
             return _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
 
     def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
-                cov3D_precomp=None, prepared=None):
-        """prepared: this call's PreparedView from prepare_views (extension; default: none)."""
+                cov3D_precomp=None, prepared=None, sh_split=None):
+        """prepared: this call's PreparedView from prepare_views (extension; default: none).
+        sh_split: (features_dc [P,1,3], features_rest [P,M-1,3]) read in place instead of the
+        concatenated shs (extension, ABI v8: no per-iteration cat); `shs` is then a [P,M,3] tensor
+        whose values are never read and whose .grad receives dL/d cat(features_dc, features_rest)
+        (what FusedAdam.step_activated consumes).  Bit-identical to passing the concatenation."""
         s = self.raster_settings
         if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
             raise Exception("Please provide excatly one of either SHs or precomputed colors!")
@@ -291,4 +312,4 @@ class GaussianRasterizer(nn.Module):
         rotations = empty if rotations is None else rotations
         cov3D_precomp = empty if cov3D_precomp is None else cov3D_precomp
         return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
-                                   s, prepared)
+                                   s, prepared, sh_split)

@@ -67,6 +67,18 @@ SIGNATURES = {
          _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
          ctypes.c_uint, _c_p, _c_i, _c_p],
     ),
+    # ABI v8: features_dc / features_rest in place of shs (and of colors_precomp / dL_dcolors)
+    "gs_forward_preprocess_split": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_f, _c_f, _c_i, _c_p, _c_p, ctypes.POINTER(_c_ll), _c_i, _c_p],
+    ),
+    "gs_backward_accumulate_split": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+         ctypes.c_uint, _c_p, _c_i, _c_p],
+    ),
     "gs_backward_render": (
         _c_i,
         [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_f, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_p,

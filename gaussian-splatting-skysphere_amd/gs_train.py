@@ -246,7 +246,7 @@ def _ptr(t):
 
 class _Activate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, f_dc, f_rest, opacity_raw, scaling_raw, rotation_raw):
+    def forward(ctx, f_dc, f_rest, opacity_raw, scaling_raw, rotation_raw, with_sh=True):
         P = f_dc.shape[0]
         if f_dc.shape[1:] != (1, 3) or f_rest.dim() != 3 or f_rest.shape[0] != P or f_rest.shape[2] != 3:
             raise ValueError(f"activate: expected features_dc [P,1,3] and features_rest [P,K,3], got "
@@ -259,7 +259,8 @@ class _Activate(torch.autograd.Function):
         dc, rest, o, s, q = ins
         K = rest.shape[1]
         dev = dc.device
-        shs = torch.empty((P, 1 + K, 3), dtype=torch.float32, device=dev)
+        # with_sh=False: no concatenated rows (a split-SH rasterizer call reads f_dc / f_rest in place)
+        shs = torch.empty((P, 1 + K, 3), dtype=torch.float32, device=dev) if with_sh else None
         opac = torch.empty(tuple(opacity_raw.shape), dtype=torch.float32, device=dev)
         scales = torch.empty((P, 3), dtype=torch.float32, device=dev)
         rots = torch.empty((P, 4), dtype=torch.float32, device=dev)
@@ -298,12 +299,13 @@ class _Activate(torch.autograd.Function):
         return g_dc, g_rest, g_o, g_s, g_q
 
 
-def activate_values(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw):
+def activate_values(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw, with_sh=True):
     """activate()'s forward only (one launch, no autograd graph): fresh (shs, opacity, scales,
-    rotations) tensors, for a step whose adjoint runs inside FusedAdam.step_activated."""
+    rotations) tensors, for a step whose adjoint runs inside FusedAdam.step_activated.
+    with_sh=False: shs is None (the SH rows go to the rasterizer split, GaussianRasterizer sh_split)."""
     with torch.no_grad():
         return _Activate.forward(_NoCtx(), features_dc, features_rest, opacity_raw, scaling_raw,
-                                 rotation_raw)
+                                 rotation_raw, with_sh)
 
 
 class _NoCtx:

@@ -86,17 +86,32 @@ class TrainModel:
                 torch.exp(self._scaling), torch.nn.functional.normalize(self._rotation))
 
 
-def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | None = None):
+def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | None = None, split_sh: bool = True):
     """gaussian_renderer.render() for the default pipe (SH and covariance in the rasterizer).
     act_leaves (a list): the activated inputs are made autograd leaves (their adjoint then runs in
     FusedAdam.step_activated) and appended to it as (shs, opacity, scales, rotations)."""
-    if act_leaves is not None:
+    sh_split = None
+    if act_leaves is not None and not split_sh:
         acts = gs_train.activate_values(model._features_dc, model._features_rest, model._opacity, model._scaling,
                                         model._rotation)
         for t in acts:
             t.requires_grad_(True)
         act_leaves.extend(acts)
         means3D, (shs, opacity, scales, rotations) = model._xyz, acts
+    elif act_leaves is not None:
+        # the SH rows are read in place by the rasterizer (sh_split): no per-iteration concatenation;
+        # `shs` is the [P, M, 3] carrier of dL/dshs that FusedAdam.step_activated maps back to
+        # features_dc / features_rest
+        _, opacity, scales, rotations = gs_train.activate_values(
+            model._features_dc, model._features_rest, model._opacity, model._scaling, model._rotation, with_sh=False)
+        P, M = model._features_dc.shape[0], 1 + model._features_rest.shape[1]
+        shs = torch.empty((P, M, 3), dtype=torch.float32, device=model._xyz.device)
+        sh_split = (model._features_dc, model._features_rest)
+        acts = (shs, opacity, scales, rotations)
+        for t in acts:
+            t.requires_grad_(True)
+        act_leaves.extend(acts)
+        means3D = model._xyz
     elif fused:
         means3D, shs, opacity, scales, rotations = gs_train.render_inputs(model)
     else:
@@ -106,7 +121,7 @@ def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | N
     screenspace_points = torch.zeros_like(means3D, requires_grad=True)
     image, radii = GaussianRasterizer(raster_settings=settings)(
         means3D=means3D, means2D=screenspace_points, shs=shs, colors_precomp=None, opacities=opacity, scales=scales,
-        rotations=rotations, cov3D_precomp=None)
+        rotations=rotations, cov3D_precomp=None, sh_split=sh_split)
     return image, screenspace_points, radii
 
 
@@ -118,14 +133,14 @@ def _torch_densification_stats(model: TrainModel, viewspace, radii):
 
 
 def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool = True, densify_stats: bool = True,
-               lambda_dssim: float = LAMBDA_DSSIM, fused_adjoint: bool = True) -> torch.Tensor:
+               lambda_dssim: float = LAMBDA_DSSIM, fused_adjoint: bool = True, split_sh: bool = True) -> torch.Tensor:
     """One iteration (module docstring).  Returns the loss tensor (not read back: the reference's
     `loss.item()` for its progress bar, train.py:99, is left to the caller).
     fused_adjoint (with fused): the activation's backward runs inside the Adam update
     (FusedAdam.step_activated), so the raw parameters' gradients are never stored; same floats as
     activate's backward followed by FusedAdam.step, .grad of the activated parameters stays None."""
     acts = [] if (fused and fused_adjoint) else None
-    image, viewspace, radii = render(model, settings, fused, acts)
+    image, viewspace, radii = render(model, settings, fused, acts, split_sh)
     if fused:  # the whole loss expression in one fused forward / backward (gs_loss.photometric_loss)
         loss, Ll1 = gs_loss.photometric_loss(image, gt_image, lambda_dssim)
     else:

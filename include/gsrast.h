@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 7
+#define GSRAST_ABI_VERSION 8
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -159,6 +159,32 @@ int gs_backward_accumulate(int P, int D, int M, const float* background, int ima
                            void* grad_buffer, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
                            float* dL_drotations, unsigned accumulate, void* wait_event, int debug, void* stream);
+
+/* ---- split SH rows (ABI v8, an extension beyond upstream) ----
+ * render() concatenates GaussianModel's features_dc [P,1,3] and features_rest [P,M-1,3] into shs
+ * (gaussian_model.py:99-103) once per iteration.  These variants read the two tensors in place:
+ * shs_dc / shs_rest replace shs (SH colours only; M >= 2 is the coefficient count of the
+ * concatenation); dL_dsh is still the [P,M,3] gradient of the concatenation (what
+ * gs_adam_step_activated's features_dc / features_rest modes read).  Results are bit-identical to
+ * gs_forward_preprocess / gs_backward_accumulate on the concatenated rows.  Every other argument as
+ * there (no dL_dcolors: SH colours). */
+int gs_forward_preprocess_split(int P, int D, int M, const float* background, int image_width, int image_height,
+                                const float* means3D, const float* shs_dc, const float* shs_rest,
+                                const float* opacities, const float* scales, float scale_modifier,
+                                const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                                const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                                int prefiltered, int* radii_out, void* geom_buffer, long long* num_rendered,
+                                int debug, void* stream);
+int gs_backward_accumulate_split(int P, int D, int M, const float* background, int image_width, int image_height,
+                                 const float* means3D, const float* shs_dc, const float* shs_rest,
+                                 const float* opacities, const float* scales, float scale_modifier,
+                                 const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                                 const int* radii, const void* geom_buffer, long long num_rendered,
+                                 const void* binning_buffer, const void* image_buffer, const float* dL_dout_color,
+                                 void* grad_buffer, float* dL_dmeans2D, float* dL_dopacity, float* dL_dmeans3D,
+                                 float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                                 unsigned accumulate, void* wait_event, int debug, void* stream);
 
 /* ---- backward, split for multi-view steps (an extension beyond upstream) ----
  * A view-parallel step renders K views of ONE set of Gaussians into one gradient bucket
@@ -274,7 +300,8 @@ int gs_adam_step_activated(int count, float* const* params_host, const float* co
  * rotations[P,4] = rotation_raw / max(|rotation_raw|, 1e-12).
  * Backward: the adjoints (any of the four dL_d* inputs may be NULL: its outputs are not written);
  * opacity / scales are the forward OUTPUTS, rotation_raw the forward input.  Rotation and shs
- * buffers must be 16-byte aligned. */
+ * buffers must be 16-byte aligned.  shs == NULL (ABI v8): the SH rows are not concatenated (for the
+ * split-SH rasterizer entries); features_dc / features_rest are then not read. */
 int gs_activate_forward(int P, int sh_rest, const float* features_dc, const float* features_rest,
                         const float* opacity_raw, const float* scaling_raw, const float* rotation_raw, float* shs,
                         float* opacity, float* scales, float* rotations, void* stream);

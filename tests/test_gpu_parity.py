@@ -732,3 +732,55 @@ def test_randomized_configurations_vs_oracle(oracle, device, seed):
     gr = oracle.backward(osc, dpix)
     _check_backward(gr, leaves, colors=colors, cov3D=cov, chain_frac=1e-4)
     _check_chain_noise(leaves, gr, oracle.backward_f32_acc(osc, dpix))
+
+
+@pytest.mark.parametrize("deg,M", [(3, 16), (1, 16), (2, 9)])
+def test_sh_split_matches_concatenated_rows(device, fast_mode, deg, M):
+    """GaussianRasterizer(..., sh_split=(features_dc, features_rest)) reads the two tensors in place
+    (gs_forward_preprocess_split / gs_backward_accumulate_split): image, radii and every gradient are
+    bit-identical to the call on cat(features_dc, features_rest), in the default numerics mode; the
+    carrier's .grad is dL/d cat(...), [P, M, 3]."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+
+    W, H = 320, 240
+    cam = gs_scenes.identity_camera(W, H)
+    sc = gs_scenes.random_gaussians(20_000, 3, cam=cam, seed=31)
+    d = sc.to(device)
+    g = torch.Generator().manual_seed(32)
+    shs_full = torch.randn((sc.P, M, 3), generator=g).mul_(0.3).to(device)
+    dc, rest = shs_full[:, :1].contiguous(), shs_full[:, 1:].contiguous()
+    s = gs_scenes.raster_settings_for(cam, deg, bg=torch.tensor([0.1, 0.2, 0.3], device=device), device=device)
+    dpix = gs_scenes.dl_dimage(H, W, seed=33).to(device)
+
+    def run(split):
+        leaves = [t.clone().requires_grad_(True) for t in (d.means3D, d.opacities, d.scales, d.rotations)]
+        m2 = torch.zeros_like(d.means3D, requires_grad=True)
+        shs = (torch.empty((sc.P, M, 3), device=device) if split else shs_full.clone()).requires_grad_(True)
+        img, radii = GaussianRasterizer(s)(means3D=leaves[0], means2D=m2, opacities=leaves[1], shs=shs,
+                                           scales=leaves[2], rotations=leaves[3],
+                                           sh_split=(dc, rest) if split else None)
+        img.backward(dpix)
+        torch.cuda.synchronize()
+        return img.detach(), radii, [t.grad for t in leaves + [m2, shs]]
+
+    a, b = run(False), run(True)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for k, (x, y) in enumerate(zip(a[2], b[2])):
+        assert x.shape == y.shape and torch.equal(x, y), k
+
+
+def test_sh_split_rejects_bad_carriers(device):
+    from diff_gaussian_rasterization import GaussianRasterizer, prepare_views
+
+    cam = gs_scenes.identity_camera(64, 48)
+    sc = gs_scenes.random_gaussians(100, 3, cam=cam, seed=1).to(device)
+    s = gs_scenes.raster_settings_for(cam, 3, device=device)
+    dc, rest = sc.shs[:, :1].contiguous(), sc.shs[:, 1:].contiguous()
+    r = GaussianRasterizer(s)
+    kw = dict(means3D=sc.means3D, means2D=torch.zeros_like(sc.means3D), opacities=sc.opacities, scales=sc.scales,
+              rotations=sc.rotations)
+    with pytest.raises(RuntimeError, match="carrier"):
+        r(shs=torch.empty((100, 9, 3), device=device), sh_split=(dc, rest), **kw)
+    pv = prepare_views([r], sc.means3D, sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    with pytest.raises(RuntimeError, match="prepared"):
+        r(shs=sc.shs, sh_split=(dc, rest), prepared=pv[0], **kw)
