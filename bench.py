@@ -23,18 +23,49 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "gaussian-splatting-skysphere_amd"), ROOT]
 
+# Only torch here: nothing that loads libgsrast.so or touches the GPU may run before the launcher
+# below has decided whether this process is a rank or the parent of N ranks.
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-import gs_scenes  # noqa: E402
-import gs_view_parallel as vp  # noqa: E402
-from diff_gaussian_rasterization import GaussianRasterizer, _C, _native, prepare_views  # noqa: E402
+gs_scenes = vp = GaussianRasterizer = _C = _native = prepare_views = None
+
+
+def _import_product():
+    """The drop-in packages (loads libgsrast.so): imported by the ranks only."""
+    global gs_scenes, vp, GaussianRasterizer, _C, _native, prepare_views
+    import gs_scenes as _s
+    import gs_view_parallel as _vp
+    from diff_gaussian_rasterization import GaussianRasterizer as _R, _C as _c, _native as _n, prepare_views as _p
+
+    gs_scenes, vp, GaussianRasterizer, _C, _native, prepare_views = _s, _vp, _R, _c, _n, _p
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) started without torchrun: start the N ranks as torchrun children
+    (one process per GPU, RCCL) and exit with their status.  The parent has not touched the GPU
+    (only torch is imported); rank 0 prints the JSON line to the inherited stdout."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC on this host driver
+    return subprocess.call(cmd, env=env)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E
 # wave64 VALU issue peak: 256 CUs x 4 SIMD32 x 2.4 GHz / 2 cycles per wave64 instruction
@@ -118,14 +149,42 @@ def main():
     ap.add_argument("--sustain-s", type=float, default=2.0,
                     help="after the timed steps, keep stepping for this long (untimed for `value`) and report "
                          "the sustained rate too")
+    ap.add_argument("--single-view-steps", type=int, default=100,
+                    help="timed iterations of the batch-1 measurement (`single_view`: one view per step, per-view "
+                         "backward, one stream: the shape of train.py's loop); 0 = skip")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, check the process group against --gpus, print one JSON line and exit "
+                         "before any GPU work (tests of the launcher; GS_BENCH_BACKEND=gloo runs it on CPU)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a mislabelled scaling point",
+              file=sys.stderr)
+        sys.exit(2)
     # GS_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU (the
     # driver's multi-GPU runs use RCCL, one rank per GPU)
     backend = os.environ.get("GS_BENCH_BACKEND", "nccl")
+    if args.launch_check:
+        if world > 1:
+            dist.init_process_group(backend)
+            got = dist.get_world_size()
+            dist.barrier()
+        else:
+            got = 1
+        if got != args.gpus:
+            sys.exit(2)
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": got, "backend": backend if world > 1 else None,
+                              "ranks_from": "torchrun env"}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    _import_product()
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     if world > 1:
         if backend == "nccl":
@@ -133,6 +192,7 @@ def main():
         else:
             torch.cuda.set_device(dev)
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus, "process group size != --gpus"
     wl = WORKLOADS[args.workload]
     P, deg, W, H = wl["P"], wl["deg"], wl["W"], wl["H"]
     n_views = wl.get("views", 0)
@@ -142,9 +202,14 @@ def main():
         sc = gs_scenes.random_gaussians(P, deg, seed=0, ball_radius=2.0)
         cam = cams[my_views[0]]
     else:
+        # the rank's K views of a step are K distinct nearby poses of the frustum-filled scene (view
+        # 0 is the C3 identity camera the scene is drawn in; the others are turned by <= 2 degrees and
+        # moved by <= 0.05); ranks draw different poses
         cam = gs_scenes.identity_camera(W, H)
         k_views = max(1, args.views_per_rank)
-        cams, my_views = [cam], [0] * k_views
+        cams = gs_scenes.jittered_cameras(k_views, W, H, seed=7 + rank) if k_views > 1 else [cam]
+        cams[0] = cam
+        my_views = list(range(k_views))
         sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=0)
     settings = gs_scenes.raster_settings_for(cam, deg, device=dev)
     d = sc.to(dev)
@@ -331,6 +396,12 @@ def main():
             render_batched = {"views_per_step": len(rasts), "streams": len(streams),
                               "mpix_s": round(W * H / t_rb / 1e6, 1), "ms_per_view": round(1e3 * t_rb, 4)}
 
+    # batch 1 (train.py's shape, train.py:76-93): one view per step, its whole backward (per-Gaussian
+    # half included, written straight into the .grad bucket) before the next view starts, one stream
+    single = None
+    if args.single_view_steps > 0 and world == 1:
+        single = single_view_bench(bucket, rast, params, dpix, args.single_view_steps, lib)
+
     ms_per_step = 1e3 * elapsed / args.steps
     # whole-job views (= reference train iterations) per second: weak scaling (C1-C3, C5) counts
     # every rank's views; a C4 step is the 8-view batch
@@ -427,6 +498,7 @@ def main():
         "render_mpix_s": round(W * H / t_render / 1e6, 1),
         "render_ms": round(1e3 * t_render, 4),
         "render_batched": render_batched,
+        "single_view": single,
         "num_rendered": int(num_rendered),
         "walked_instances": walked,
         "visible": visible,
@@ -453,6 +525,47 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def single_view_bench(bucket, rast, params, dpix, steps, lib):
+    """Batch-1 rasterizer iterations: zero_grad, one view's forward, its full backward into the
+    gradient bucket (no deferral: the per-Gaussian half runs inside the view's backward), finalize;
+    everything on the current stream.  Returns the rate and a per-kernel breakdown (HIP events on the
+    launch stream, a second pass)."""
+    defers = bucket.defers
+    bucket.defers = False
+
+    def sv_step():
+        bucket.zero_grad()
+        m2 = torch.zeros_like(params[0], requires_grad=True)
+        img, _ = rast(means3D=params[0], means2D=m2, opacities=params[2], shs=params[1], scales=params[3],
+                      rotations=params[4])
+        img.backward(dpix)
+        bucket.finalize()
+
+    try:
+        for _ in range(5):
+            sv_step()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(steps):
+            sv_step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / steps
+        lib.gs_profile_reset()
+        lib.gs_profile_enable(1)
+        for _ in range(steps):
+            sv_step()
+        torch.cuda.synchronize()
+        lib.gs_profile_enable(0)
+        prof = _native.profile_stats()
+    finally:
+        bucket.defers = defers
+    kern = {k: round(1e3 * ms / steps, 2) for k, (ms, n) in sorted(prof.items(), key=lambda kv: -kv[1][0])}
+    return {"what": "one view per step (train.py's batch 1): forward, full backward into the .grad bucket, one "
+                    "stream, no deferral, no overlap between views",
+            "iters_s": round(1.0 / dt, 2), "ms_per_iter": round(1e3 * dt, 4), "steps": steps,
+            "kernel_us_per_iter": kern, "kernel_us_sum": round(sum(kern.values()), 1)}
 
 
 def train_step_bench(sc, cam, deg, dev, steps, densify):

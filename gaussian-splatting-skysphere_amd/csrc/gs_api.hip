@@ -314,7 +314,9 @@ static int forward_preprocess_impl(int P, int D, int M, const float* background,
   check_hip(hipEventSynchronize(rb->ev), "hipEventSynchronize");
   if (t_failed) return 1;
   const uint32_t err = rb->host[CNT_ERR], I = rb->host[CNT_NREND];
-  if (err & 1u) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
+  if (err & ERR_PREFILTERED) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
+  if ((err & ERR_INSTANCES) || (long long)I > GS_MAX_INSTANCES)
+    return set_error("the view has more than %lld (Gaussian, tile) instances", GS_MAX_INSTANCES), 1;
   *num_rendered_host = (long long)I;
   return 0;
 }
@@ -401,8 +403,10 @@ int gs_forward_preprocess_views(int K, int P, int D, int M, const float* const* 
   check_hip(hipEventSynchronize(ev), "hipEventSynchronize");
   if (t_failed) return 1;
   for (int v = 0; v < K; v++) {
-    if (host[8 * v + CNT_ERR] & 1u)
+    if (host[8 * v + CNT_ERR] & ERR_PREFILTERED)
       return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
+    if ((host[8 * v + CNT_ERR] & ERR_INSTANCES) || (long long)host[8 * v + CNT_NREND] > GS_MAX_INSTANCES)
+      return set_error("view %d has more than %lld (Gaussian, tile) instances", v, GS_MAX_INSTANCES), 1;
     num_rendered_host[v] = (long long)host[8 * v + CNT_NREND];
   }
   return 0;
@@ -415,7 +419,7 @@ int gs_forward_render(int P, const float* background, int W, int H, const float*
   clear_error(debug);
   if (P <= 0) return 0;
   if (W <= 0 || H <= 0) return set_error("image size must be positive"), 1;
-  if (num_rendered < 0 || num_rendered > 0xFFFFFFFFll) return set_error("num_rendered out of range"), 1;
+  if (num_rendered < 0 || num_rendered > GS_MAX_INSTANCES) return set_error("num_rendered out of range"), 1;
   if (!geom_buffer || !binning_buffer || !image_buffer || !out_color || !radii)
     return set_error("missing buffer pointer"), 1;
   hipStream_t st = (hipStream_t)stream;
@@ -483,7 +487,7 @@ static int backward_impl(int P, int D, int M, const float* background, int W, in
   if (!geom_buffer || !binning_buffer || !image_buffer || !dL_dout_color || !grad_buffer)
     return set_error("missing buffer pointer"), 1;
   if (!dL_dmeans2D || !dL_dopacity || !dL_dmeans3D) return set_error("missing gradient output pointer"), 1;
-  if (num_rendered < 0 || num_rendered > 0xFFFFFFFFll) return set_error("num_rendered out of range"), 1;
+  if (num_rendered < 0 || num_rendered > GS_MAX_INSTANCES) return set_error("num_rendered out of range"), 1;
   if (accumulate & ~0xFFu) return set_error("accumulate: unknown GS_ACC bits 0x%x", accumulate), 1;
   hipStream_t st = (hipStream_t)stream;
   CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, 0);
@@ -578,7 +582,7 @@ int gs_backward_render(int P, int D, int M, const float* background, int W, int 
   if (!viewmatrix || !projmatrix || !background) return set_error("missing required input pointer"), 1;
   if (!geom_buffer || !binning_buffer || !image_buffer || !dL_dout_color || !grad_buffer)
     return set_error("missing buffer pointer"), 1;
-  if (num_rendered < 0 || num_rendered > 0xFFFFFFFFll) return set_error("num_rendered out of range"), 1;
+  if (num_rendered < 0 || num_rendered > GS_MAX_INSTANCES) return set_error("num_rendered out of range"), 1;
   if (accumulate & ~GS_ACC_MEANS2D) return set_error("accumulate: only GS_ACC_MEANS2D applies here"), 1;
   hipStream_t st = (hipStream_t)stream;
   CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, 0);

@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess(Gaus
   if (threadIdx.x == 0) {
     const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
     const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
-    if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(&counters[CNT_NREND]), ((unsigned long long)nv << 32) | tot);
+    if (tot) add_view_totals(counters, nv, tot);
   }
 }
 
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess_spli
   if (threadIdx.x == 0) {
     const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
     const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
-    if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(&counters[CNT_NREND]), ((unsigned long long)nv << 32) | tot);
+    if (tot) add_view_totals(counters, nv, tot);
   }
 }
 
@@ -310,8 +310,7 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PV_WPE) void k_preprocess_views
     if (threadIdx.x == 0) {
       const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
       const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
-      if (tot)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&geo.counters[CNT_NREND]), ((unsigned long long)nv << 32) | tot);
+      if (tot) add_view_totals(geo.counters, nv, tot);
     }
     lds_barrier();  // s_sum / s_vis are reused by the next view
   }

@@ -77,6 +77,20 @@ struct CameraArgs {
 };
 
 constexpr int CNT_I = 1, CNT_ERR = 2, CNT_NREND = 4, CNT_V = 5, CNT_LB_TILE = 9;
+// error flags in counters[CNT_ERR]: 1 prefiltered cull, 4 look-back timeout, 8 instance count overflow
+constexpr uint32_t ERR_PREFILTERED = 1u, ERR_LOOKBACK = 4u, ERR_INSTANCES = 8u;
+// Largest instance count of one view: the sorts and scans index instances with 32-bit positions
+// (a position plus one sort chunk must stay below 2^32).
+constexpr long long GS_MAX_INSTANCES = (1ll << 31) - 1;
+
+// A preprocess workgroup's totals -> the view's counters: ONE 64-bit add of (V << 32 | I), so the
+// host reads both with one copy.  A carry out of the 32-bit instance field (over 2^32 instances)
+// would land in V: the adding workgroup sees it in the returned word and raises ERR_INSTANCES.
+__device__ __forceinline__ void add_view_totals(uint32_t* counters, uint32_t nv, uint32_t tot) {
+  const unsigned long long old =
+      atomicAdd(reinterpret_cast<unsigned long long*>(&counters[CNT_NREND]), ((unsigned long long)nv << 32) | tot);
+  if ((unsigned long long)(uint32_t)old + tot > 0xFFFFFFFFull) atomicOr(&counters[CNT_ERR], ERR_INSTANCES);
+}
 
 struct GeomPtrs {
   float4* splat;  // 3 per Gaussian: (x, y, cxx, cxy) (cyy, opacity, r, g) (b, depth, cull_lim, -)

@@ -103,6 +103,9 @@ class PreparedView:
 
     def __init__(self, triple, settings, inputs):
         self.triple, self.settings, self.inputs = triple, settings, inputs
+        # autograd version counters: an in-place update between prepare_views and the call (an
+        # optimizer step) would leave the prepared geometry stale
+        self.versions = tuple(None if t is None else t._version for t in inputs)
 
     def take(self, settings, inputs):
         if self.triple is None:
@@ -111,6 +114,9 @@ class PreparedView:
                 (a is None) != (b is None) or (a is not None and (a.data_ptr(), a.shape) != (b.data_ptr(), b.shape))
                 for a, b in zip(inputs, self.inputs)):
             raise RuntimeError("prepare_views: the rasterizer call does not match the prepared view")
+        if any(v is not None and b._version != v for b, v in zip(self.inputs, self.versions)):
+            raise RuntimeError("prepare_views: an input was modified in place after prepare_views (stale prepared "
+                               "view); prepare the views again")
         t, self.triple = self.triple, None
         return t
 
@@ -194,6 +200,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.num_rendered = num_rendered
         ctx.matrices = (view, proj)
         ctx.sh_rest = sh_rest
+        # the split rows are kept outside save_for_backward (they are not inputs of the Function):
+        # their version counters stand in for autograd's in-place check
+        ctx.sh_split_versions = None if sh_rest is None else (sh._version, sh_rest._version)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the (int) radii output
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
@@ -210,6 +219,9 @@ class _RasterizeGaussians(torch.autograd.Function):
             return (None,) * 11
         colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer, imgBuffer = (
             ctx.saved_tensors)
+        if ctx.sh_rest is not None and (sh._version, ctx.sh_rest._version) != ctx.sh_split_versions:
+            raise RuntimeError("sh_split: features_dc or features_rest was modified by an inplace operation between "
+                               "the forward and the backward")
         view, proj = ctx.matrices
         args = (s.bg, means3D, radii, colors_precomp, scales, rotations, s.scale_modifier, cov3Ds_precomp,
                 view, proj, s.tanfovx, s.tanfovy, grad_out_color.contiguous(), sh, s.sh_degree,

@@ -97,6 +97,23 @@ def look_at_camera(position, target, W, H, fovy_deg=60.0, up=(0.0, -1.0, 0.0)) -
     return make_camera(w2c.T, T, W, H, fovy_deg)
 
 
+def jittered_cameras(n, W, H, seed=7, max_angle_deg=2.0, max_shift=0.05, fovy_deg=60.0):
+    """n distinct views around the single-view pose: view 0 is identity_camera, view k > 0 is turned
+    by a random rotation of up to `max_angle_deg` about a random axis and moved by up to `max_shift`
+    along each axis (a batch of nearby training views of one frustum-filled scene)."""
+    rng = np.random.default_rng(seed)
+    cams = [identity_camera(W, H, fovy_deg)]
+    for _ in range(1, n):
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        a = math.radians(max_angle_deg) * rng.uniform(0.5, 1.0)
+        K = np.array([[0.0, -ax[2], ax[1]], [ax[2], 0.0, -ax[0]], [-ax[1], ax[0], 0.0]])
+        w2c = np.eye(3) + math.sin(a) * K + (1.0 - math.cos(a)) * (K @ K)  # Rodrigues
+        T = rng.uniform(-max_shift, max_shift, size=3)
+        cams.append(make_camera(w2c.T, T, W, H, fovy_deg))
+    return cams
+
+
 def circle_cameras(n, radius, W, H, height=0.0, fovy_deg=60.0):
     """C4: n cameras on a circle of `radius` around the origin, looking at the centre."""
     cams = []

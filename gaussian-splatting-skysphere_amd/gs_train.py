@@ -149,8 +149,18 @@ class FusedAdam(torch.optim.Optimizer):
                     continue
                 _check_f32_dense(p, "FusedAdam param")
                 _check_f32_dense(src, "FusedAdam gradient source")
-                if mode == "plain" and src.shape != p.shape:
-                    raise ValueError(f"FusedAdam: grad shape {tuple(src.shape)} != param {tuple(p.shape)}")
+                if mode not in self._MODES:
+                    raise ValueError(f"FusedAdam.step_activated: unknown mode {mode!r}")
+                # the kernel reads the source by the parameter's row count: its shape must match
+                # exactly (a stale carrier from before a densify step would read out of bounds)
+                if mode in ("features_dc", "features_rest"):
+                    want = (p.shape[0], int(sh_coeffs), 3)
+                    if tuple(src.shape) != want:
+                        raise ValueError(f"FusedAdam: {mode} gradient source must be dL/dshs of shape {want}, got "
+                                         f"{tuple(src.shape)}")
+                elif src.shape != p.shape:
+                    raise ValueError(f"FusedAdam: {mode} gradient source shape {tuple(src.shape)} != param "
+                                     f"{tuple(p.shape)}")
                 state = self.state[p]
                 if len(state) == 0:
                     state["step"] = torch.tensor(0.0, dtype=torch.float32)
@@ -335,7 +345,7 @@ _DENS_NAMES = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
 _DENS_ATTRS = ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
 
 
-def densify_and_prune(gaussians, max_grad, min_opacity, extent, max_screen_size, N: int = 2) -> None:
+def densify_and_prune(gaussians, max_grad, min_opacity, extent, max_screen_size, N: int = 2, group=None) -> None:
     """GaussianModel.densify_and_prune (gaussian_model.py:391-403) in three HIP passes.
 
     Same effect on `gaussians` as the reference: the six parameters become new nn.Parameters of
@@ -343,7 +353,13 @@ def densify_and_prune(gaussians, max_grad, min_opacity, extent, max_screen_size,
     Adam moments follow them (zeros for new rows, 'step' kept), the densification stats are re-zeroed,
     and the split draws come from torch.normal with the reference's shapes and order (same RNG
     stream).  Every parameter and moment is rewritten once instead of four times
-    (csrc/gs_densify.hip)."""
+    (csrc/gs_densify.hip).
+
+    View-parallel replicas (a torch.distributed process group of more than one rank, `group` or the
+    default one; gs_view_parallel): every rank draws, then rank 0's split samples are broadcast, so
+    the replicas stay bit-identical (their parameters, moments and reduced statistics already are).
+    A gs_view_parallel.GradBucket that holds the replaced parameters' gradients is rebound to the new
+    parameters."""
     params = [getattr(gaussians, a) for a in _DENS_ATTRS]
     xyz = params[0]
     P = xyz.shape[0]
@@ -380,6 +396,10 @@ def densify_and_prune(gaussians, max_grad, min_opacity, extent, max_screen_size,
                                                  _ptr(stds) if n_split else None, st), "densify stds")
         # the reference's draw (gaussian_model.py:359-360): same shapes, same generator stream
         samples = torch.normal(mean=torch.zeros((stds.size(0), 3), device=dev), std=stds).contiguous()
+        if n_split:
+            import gs_view_parallel
+
+            gs_view_parallel.sync_from_rank0(samples, group)  # replicas: rank 0's draw (no-op alone)
         Pn = tot[0] + tot[1] + N * tot[3]
         groups = {g["name"]: g for g in gaussians.optimizer.param_groups}
         states, outs, m_in, v_in, m_out, v_out = [], [], [], [], [], []
@@ -411,6 +431,15 @@ def densify_and_prune(gaussians, max_grad, min_opacity, extent, max_screen_size,
             ctypes.cast(arr(v_in), ctypes.c_void_p), ctypes.cast(arr(outs), ctypes.c_void_p),
             ctypes.cast(arr(m_out), ctypes.c_void_p), ctypes.cast(arr(v_out), ctypes.c_void_p),
             ctypes.cast((ctypes.c_int * 6)(*widths), ctypes.c_void_p), st), "densify emit")
+    # gradient buckets (gs_view_parallel.GradBucket) that own the old parameters' gradients
+    from diff_gaussian_rasterization import _sink_owner
+
+    owners = []
+    for p in params:
+        o = _sink_owner(p)
+        if o is not None and hasattr(o, "rebind") and all(o is not x for x in owners):
+            owners.append(o)
+    replaced = {}
     # optimizer surgery as cat_tensors_to_optimizer / _prune_optimizer do it
     for i, n in enumerate(_DENS_NAMES):
         grp = groups[n]
@@ -423,6 +452,9 @@ def densify_and_prune(gaussians, max_grad, min_opacity, extent, max_screen_size,
             gaussians.optimizer.state[newp] = stt
         grp["params"][0] = newp
         setattr(gaussians, _DENS_ATTRS[i], newp)
+        replaced[id(old)] = newp
+    for o in owners:
+        o.rebind([replaced.get(id(p), p) for p in o.params])
     gaussians.xyz_gradient_accum = torch.zeros((Pn, 1), device=dev)
     gaussians.denom = torch.zeros((Pn, 1), device=dev)
     gaussians.max_radii2D = torch.zeros((Pn,), device=dev)

@@ -165,6 +165,31 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
     return loss
 
 
+def train_step_views(model: TrainModel, bucket, views, lambda_dssim: float = LAMBDA_DSSIM, densify_stats: bool = True,
+                     average: bool = False):
+    """One view-parallel optimizer step (gs_view_parallel): this rank's views
+    `views` = [(settings, gt_image)] each run render -> L1 + SSIM -> backward with the fused glue,
+    their raw-parameter gradients accumulate in `bucket` (a gs_view_parallel.GradBucket over the six
+    parameters, lazy_zero=False: the activation backward accumulates too), ONE all-reduce sums the
+    bucket over the ranks (every rank holds the same sum), then every rank runs the same Adam step,
+    so the replicas stay bit-identical.  Densification statistics stay per rank until
+    gs_view_parallel.reduce_densify_stats at densify time.  Returns the rank's losses."""
+    bucket.zero_grad()
+    losses = []
+    for settings, gt in views:
+        image, viewspace, radii = render(model, settings, fused=True)
+        loss, _ = gs_loss.photometric_loss(image, gt, lambda_dssim)
+        loss.backward()
+        if densify_stats:
+            with torch.no_grad():
+                gs_train.add_densification_stats(model, viewspace, radii)
+        losses.append(loss)
+    bucket.allreduce(average=average)
+    with torch.no_grad():
+        model.optimizer.step()
+    return losses
+
+
 def synthetic_densify_stats(model: TrainModel, frac: float = 0.05, seed: int = 0,
                             threshold: float = DENSIFY_GRAD_THRESHOLD) -> None:
     """Densification statistics for a densify step on synthetic gradients:
@@ -179,9 +204,10 @@ def synthetic_densify_stats(model: TrainModel, frac: float = 0.05, seed: int = 0
 
 
 def densify(model: TrainModel, extent: float, max_screen_size=20,
-            threshold: float = DENSIFY_GRAD_THRESHOLD) -> None:
+            threshold: float = DENSIFY_GRAD_THRESHOLD, group=None) -> None:
     """train.py:118-120: densify_and_prune(densify_grad_threshold, 0.005, cameras_extent, 20).
     `extent` is scene.cameras_extent (getNerfppNorm's radius, scene/dataset_readers.py:45-66); a
-    single synthetic camera has none, so callers pass one."""
-    gs_train.densify_and_prune(model, threshold, 0.005, extent, max_screen_size)
+    single synthetic camera has none, so callers pass one.  View-parallel replicas: call
+    gs_view_parallel.reduce_densify_stats first; the split draws are synchronised across `group`."""
+    gs_train.densify_and_prune(model, threshold, 0.005, extent, max_screen_size, group=group)
 

@@ -44,9 +44,6 @@ class GradBucket:
     """
 
     def __init__(self, params: Sequence[torch.Tensor], lazy_zero: bool = False, defer: bool = False):
-        from diff_gaussian_rasterization import register_gradient_sink
-
-        self.params = list(params)
         self.lazy_zero = lazy_zero
         # defer=True: a rasterizer backward whose parameter gradients all come here runs only its
         # per-tile half; the per-Gaussian half of all such views runs in ONE pass at finalize() /
@@ -54,26 +51,49 @@ class GradBucket:
         # row written once per step instead of once per view.  Same fp32 sums as without.
         self.defers = defer
         self._deferred = []
+        # stream ordering of the writes into the bucket: the last writer's event and stream (views
+        # rendered on several streams add into one bucket one after another; their forward passes,
+        # sorts and tile backward passes overlap)
+        self._events = {}
+        self._last = None
+        self.params = []
+        self._bind(list(params))
+
+    def _bind(self, params):
+        from diff_gaussian_rasterization import register_gradient_sink
+
+        for p in params:
+            if p.dtype != torch.float32:
+                raise TypeError("GradBucket: float32 parameters only")
+        self.params = params
         self.numel = sum(p.numel() for p in self.params)
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.zeros((self.numel,), dtype=torch.float32, device=dev)
         self.views = {}
         off = 0
         for p in self.params:
-            if p.dtype != torch.float32:
-                raise TypeError("GradBucket: float32 parameters only")
             v = self.flat[off:off + p.numel()].view_as(p)
             off += p.numel()
             p.grad = v
             self.views[id(p)] = v
             register_gradient_sink(p, self)
         self._fresh = {}  # id(p) -> _version of the view at zero_grad (lazy mode: not written yet)
-        # stream ordering of the writes into the bucket: the last writer's event and stream (views
-        # rendered on several streams add into one bucket one after another; their forward passes,
-        # sorts and tile backward passes overlap)
-        self._events = {}
-        self._last = None
         self.zero_grad()
+
+    def rebind(self, params: Sequence[torch.Tensor]) -> None:
+        """Make the bucket the gradient storage of `params` instead (e.g. the new nn.Parameters that
+        densify_and_prune swaps in, with a new Gaussian count): a new flat buffer of the new size,
+        every new .grad a view of it, the old parameters' sinks closed.  gs_train.densify_and_prune
+        calls this for the bucket that owns the replaced parameters."""
+        if self._deferred:
+            raise RuntimeError("GradBucket.rebind: deferred views are pending (finalize / allreduce the step first)")
+        old = self.params
+        self.close()
+        for p in old:
+            if p.grad is self.views.get(id(p)):
+                p.grad = None  # the old tensors keep no view of the old buffer
+        self._events, self._last = {}, None
+        self._bind(list(params))
 
     def close(self):
         from diff_gaussian_rasterization import unregister_gradient_sink
@@ -81,7 +101,20 @@ class GradBucket:
         for p in self.params:
             unregister_gradient_sink(p)
 
+    def _check_bound(self):
+        """Every parameter's .grad must be its bucket view.  optimizer.zero_grad(set_to_none=True)
+        (train.py:128) drops it: it is re-attached here.  Any other tensor in .grad means the
+        gradients would bypass the all-reduce: raise."""
+        for p in self.params:
+            v = self.views[id(p)]
+            if p.grad is None:
+                p.grad = v
+            elif p.grad is not v:
+                raise RuntimeError("GradBucket: a parameter's .grad was replaced by another tensor; its gradient "
+                                   "would bypass the bucket (call rebind() after replacing parameters)")
+
     def zero_grad(self):
+        self._check_bound()
         if self.lazy_zero:
             self._fresh = {id(p): self.views[id(p)]._version for p in self.params}
         else:
@@ -178,6 +211,7 @@ class GradBucket:
         """Run any deferred per-Gaussian backward, zero the views no backward wrote this step (lazy
         mode); then the bucket holds the step's gradient sums (on the current stream: it waits for
         the last write on any stream)."""
+        self._check_bound()
         self.flush()
         self._join()
         for p in self.params:
@@ -192,10 +226,11 @@ class GradBucket:
 
     def allreduce(self, group=None, average: bool = False, async_op: bool = False):
         """Sum (or mean) the gradients across the process group in ONE collective over the flat
-        bucket; the .grad views hold the result afterwards."""
+        bucket; the .grad views hold the result afterwards.  With a process group the collective is
+        issued at every world size (world 1: RCCL's in-place copy), so one code path runs at N = 1..8."""
         flat = self.finalize()
         work = None
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dist.is_available() and dist.is_initialized():
             work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
             if average:
                 if async_op:
@@ -246,6 +281,60 @@ def allreduce_grads(params: Iterable[torch.Tensor], group=None, average: bool = 
         n = p.numel()
         p.grad = flat[off:off + n].view_as(p).clone()
         off += n
+
+
+def replicated_group(group=None):
+    """The process group whose ranks hold replicas of one model (view-parallel training), or None
+    when there is none (no process group, or a world of one)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        return group if group is not None else dist.group.WORLD
+    return None
+
+
+def sync_from_rank0(t: torch.Tensor, group=None) -> torch.Tensor:
+    """Every replica takes rank 0's values of `t` (in place).  Used for random draws that must be
+    the same on every replica, e.g. densify_and_split's split samples
+    (/root/reference/scene/gaussian_model.py:359-360): each rank draws (its generator advances as
+    the reference's does), then rank 0's draw wins."""
+    g = replicated_group(group)
+    if g is not None:
+        dist.broadcast(t, src=dist.get_global_rank(g, 0) if g is not dist.group.WORLD else 0, group=g)
+    return t
+
+
+_DIGEST_MOD = 2147483647  # 2^31 - 1
+
+
+def replica_digest(tensors: Iterable[torch.Tensor]) -> torch.Tensor:
+    """A bitwise digest of `tensors` (int64 [3]: two position-weighted sums of the 32-bit patterns
+    modulo 2^31 - 1, and the element count): two ranks whose tensors differ in any bit get different
+    digests with overwhelming probability.  Exact integer arithmetic on the tensors' device."""
+    s1 = s2 = 0
+    n = 0
+    for t in tensors:
+        b = t.detach().contiguous().view(-1).view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        b = b % _DIGEST_MOD
+        i = torch.arange(b.numel(), dtype=torch.int64, device=b.device) + n
+        w1 = i % 65521 + 1
+        w2 = (i * 40503 + 7) % 65519 + 1
+        s1 = (s1 + int(((b * w1) % _DIGEST_MOD).sum())) % _DIGEST_MOD
+        s2 = (s2 + int(((b * w2) % _DIGEST_MOD).sum())) % _DIGEST_MOD
+        n += b.numel()
+    return torch.tensor([s1, s2, n], dtype=torch.int64)
+
+
+def check_replicas(tensors: Sequence[torch.Tensor], group=None) -> bool:
+    """True when every rank of the group holds bit-identical `tensors` (digest compared with a MIN
+    and a MAX all-reduce).  Always True without a replicated group."""
+    g = replicated_group(group)
+    if g is None:
+        return True
+    d = replica_digest(tensors)
+    dev = tensors[0].device if tensors and tensors[0].is_cuda else torch.device("cpu")
+    lo, hi = d.to(dev).clone(), d.to(dev).clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=g)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=g)
+    return bool(torch.equal(lo, hi))
 
 
 def reduce_densify_stats(xyz_gradient_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,

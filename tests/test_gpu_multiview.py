@@ -70,6 +70,39 @@ def test_two_rank_view_parallel_matches_single_process_sum(tmp_path):
 
 
 @pytest.mark.spawn_first
+def test_two_rank_training_with_densify_keeps_replicas_identical(tmp_path):
+    """View-parallel training across a densify step (2 ranks, gloo, one GPU): train steps through
+    the bucket all-reduce, reduce_densify_stats, densify_and_prune with differently seeded rank
+    generators (rank 0's split draws are broadcast), the bucket rebound to the new parameters, two
+    more steps; every parameter and Adam moment bit-identical across the ranks (replica digest)."""
+    out = tmp_path / "vp_train.txt"
+    env = dict(os.environ, GS_VP_OUT=str(out), HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "vp_train_worker.py"),
+           "gloo2"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, f"workers failed ({r.returncode}):\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    res = out.read_text()
+    print(res)
+    assert res.startswith("OK"), res
+
+
+@pytest.mark.spawn_first
+def test_rccl_world1_bucket_allreduce_equals_single_process(tmp_path):
+    """The RCCL path (torch.distributed backend "nccl" = RCCL on ROCm) at world size 1: the view-
+    parallel train step with its bucket all-reduce issued through RCCL equals the same steps without
+    a process group, bit for bit."""
+    out = tmp_path / "vp_nccl.txt"
+    env = dict(os.environ, GS_VP_OUT=str(out), HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "vp_train_worker.py"), "nccl1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, f"worker failed ({r.returncode}):\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    res = out.read_text()
+    print(res)
+    assert res.startswith("OK"), res
+
+
+@pytest.mark.spawn_first
 def test_concurrent_processes_are_deterministic():
     """Two processes render the 8 C4 views forward + backward on the same GPU at once, four passes
     each; every image and gradient must be bitwise identical across passes.  Sharing the GPU

@@ -115,3 +115,69 @@ def test_lazy_bucket_claim_protocol():
     a.grad = torch.zeros(6)  # replaced by the user: the sink steps aside
     assert b.claim(a) is None
     b.close()
+
+
+def test_bucket_rebind_and_set_to_none():
+    """rebind(): the bucket becomes the gradient storage of new parameters (densify_and_prune swaps
+    in nn.Parameters of a new size); the old ones keep no view.  optimizer.zero_grad(set_to_none=True)
+    drops the views: zero_grad() re-attaches them; a foreign .grad tensor raises."""
+    a = torch.zeros(4, 3, requires_grad=True)
+    c = torch.zeros(4, 1, requires_grad=True)
+    b = vp.GradBucket([a, c])
+    opt = torch.optim.SGD([a, c], lr=0.1)
+    opt.zero_grad(set_to_none=True)
+    assert a.grad is None
+    b.zero_grad()
+    assert a.grad.data_ptr() == b.flat.data_ptr()
+    (a.sum() * 2).backward()
+    assert torch.all(b.flat[:12] == 2)
+    a2 = torch.zeros(7, 3, requires_grad=True)
+    b.rebind([a2, c])
+    assert b.numel == 7 * 3 + 4 and a.grad is None
+    assert a2.grad.data_ptr() == b.flat.data_ptr() and c.grad.data_ptr() == b.flat.data_ptr() + 21 * 4
+    (a2.sum() + 3 * c.sum()).backward()
+    assert torch.all(a2.grad == 1) and torch.all(c.grad == 3)
+    c.grad = torch.ones(4, 1)
+    with pytest.raises(RuntimeError, match="replaced"):
+        b.zero_grad()
+    b.close()
+
+
+def test_replica_digest_sees_one_bit():
+    x = torch.randn(1000)
+    y = x.clone()
+    assert torch.equal(vp.replica_digest([x]), vp.replica_digest([y]))
+    y.view(torch.int32)[517] ^= 1  # one ulp
+    assert not torch.equal(vp.replica_digest([x]), vp.replica_digest([y]))
+    z = x.clone()
+    z[3], z[4] = x[4], x[3]  # same values, other positions
+    assert not torch.equal(vp.replica_digest([x]), vp.replica_digest([z]))
+
+
+def _sync_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = torch.full((5, 3), float(rank + 1))
+        vp.sync_from_rank0(t)
+        same = vp.check_replicas([t])
+        u = torch.full((4,), float(rank))
+        differ = vp.check_replicas([u])
+        out_q.put((rank, t.numpy(), same, differ))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sync_from_rank0_and_check_replicas_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sync_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, t, same, differ in res:
+        assert (t == 1.0).all() and same and not differ
