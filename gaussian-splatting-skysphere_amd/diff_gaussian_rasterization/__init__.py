@@ -171,6 +171,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         # .transpose(0, 1) view); make them contiguous once and reuse them in backward
         view, proj = s.viewmatrix.contiguous(), s.projmatrix.contiguous()
         sh_rest = None
+        sh_input = sh  # the autograd input (with sh_split: the gradient carrier; its sink owner receives dL/dshs)
         if sh_split is not None:
             # split SH rows: the kernels read features_dc / features_rest in place; `sh` is only the
             # [P, M, 3] carrier of the concatenation's gradient (its values are never read)
@@ -207,7 +208,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii)
-        inputs = (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
+        inputs = (means3D, means2D, sh_input, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
         ctx.sinks = [(k, name, inputs[k], _sink_owner(inputs[k])) for k, name in _SINK_INPUTS
                      if _sink_owner(inputs[k]) is not None] if _SINKS else []
         return color, radii
