@@ -152,6 +152,12 @@ def main():
     ap.add_argument("--single-view-steps", type=int, default=100,
                     help="timed iterations of the batch-1 measurement (`single_view`: one view per step, per-view "
                          "backward, one stream: the shape of train.py's loop); 0 = skip")
+    ap.add_argument("--c4-views-per-rank", type=int, default=0,
+                    help="C4 weak scaling: every rank renders this many views of a ring of N x K cameras per step "
+                         "(default 0: the 8 ring views of BASELINE config 4 sharded over the ranks, strong scaling)")
+    ap.add_argument("--allreduce-chunks", type=int, default=4,
+                    help="N > 1: the deferred per-Gaussian pass runs in this many Gaussian-row ranges and each "
+                         "range's gradient rows are all-reduced (RCCL, side stream) as soon as they are written")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, check the process group against --gpus, print one JSON line and exit "
                          "before any GPU work (tests of the launcher; GS_BENCH_BACKEND=gloo runs it on CPU)")
@@ -196,6 +202,8 @@ def main():
     wl = WORKLOADS[args.workload]
     P, deg, W, H = wl["P"], wl["deg"], wl["W"], wl["H"]
     n_views = wl.get("views", 0)
+    if n_views and args.c4_views_per_rank > 0:
+        n_views = world * args.c4_views_per_rank  # weak C4: K views per rank on a ring of N x K cameras
     if n_views:  # C4: ball scene seen from a ring of cameras; this rank's share of the views
         cams = gs_scenes.circle_cameras(n_views, 6.0, W, H)
         my_views = vp.shard_views(n_views, rank, world)
@@ -223,15 +231,17 @@ def main():
     # producer here, so the step's first backward overwrites and the others add (lazy zeroing)
     # defer: the per-Gaussian half of the backward runs once for all of the step's views (at
     # finalize / allreduce) instead of once per view (--no-defer: per view)
-    bucket = vp.GradBucket(params, lazy_zero=True, defer=not args.no_defer)
+    bucket = vp.GradBucket(params, lazy_zero=True, defer=not args.no_defer,
+                           chunks=args.allreduce_chunks if world > 1 else 1)
 
     streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
 
     def view_fn(r, pre=None):
         def run():
             # a fresh screen-space carrier per render, as the reference's render() makes
-            # (gaussian_renderer/__init__.py:24); its gradient is not kept here
-            m2 = torch.zeros_like(params[0], requires_grad=True)
+            # (gaussian_renderer/__init__.py:24); the rasterizer never reads its values (only its
+            # .grad is written), so it is not zero-filled; its gradient is not kept here
+            m2 = torch.empty_like(params[0], requires_grad=True)
             img, _ = r(means3D=params[0], means2D=m2, opacities=params[2], shs=params[1], scales=params[3],
                        rotations=params[4], prepared=pre)
             img.backward(dpix)
@@ -485,7 +495,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if n_views else "weak",
+        "scaling": "strong" if (n_views and args.c4_views_per_rank <= 0) else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded; SURVEY.md §8d distribution)",
@@ -494,7 +504,8 @@ def main():
                    "render_exp2": "exact-polynomial" if os.environ.get("GSRAST_EXACT_EXP", "0") not in ("", "0")
                    else "hardware v_exp_f32",
                    "parallelism": f"view-parallel dp{world}" +
-                   (" + RCCL all-reduce of 59 f32/Gaussian" if world > 1 else "")},
+                   (f" + RCCL all-reduce of 59 f32/Gaussian in {bucket.chunks} row chunks overlapped with the "
+                    "per-Gaussian pass" if world > 1 else "")},
         "render_mpix_s": round(W * H / t_render / 1e6, 1),
         "render_ms": round(1e3 * t_render, 4),
         "render_batched": render_batched,
@@ -537,7 +548,7 @@ def single_view_bench(bucket, rast, params, dpix, steps, lib):
 
     def sv_step():
         bucket.zero_grad()
-        m2 = torch.zeros_like(params[0], requires_grad=True)
+        m2 = torch.empty_like(params[0], requires_grad=True)  # values never read (gradient carrier)
         img, _ = rast(means3D=params[0], means2D=m2, opacities=params[2], shs=params[1], scales=params[3],
                       rotations=params[4])
         img.backward(dpix)

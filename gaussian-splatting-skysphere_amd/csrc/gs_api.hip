@@ -202,11 +202,26 @@ size_t gs_grad_buffer_bytes(long long num_rendered) {
   return align_up((size_t)(num_rendered > 0 ? num_rendered : 1) * GRAD_REC * sizeof(float));
 }
 
-// Per-thread, per-device pinned readback word block + event (reused call after call: a call
-// waits on its event before returning, so the slot is free again when the next call starts).
+// Pinned, device-mapped host words: kernels store into them directly (vector stores through the
+// device pointer), so a readback costs no copy launch.
+static bool mapped_words(size_t bytes, uint32_t** host, uint32_t** dev) {
+  void* p = nullptr;
+  void* d = nullptr;
+  if (!check_hip(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc")) return false;
+  if (!check_hip(hipHostGetDevicePointer(&d, p, 0), "hipHostGetDevicePointer")) return false;
+  memset(p, 0, bytes);
+  *host = (uint32_t*)p;
+  *dev = (uint32_t*)d;
+  return true;
+}
+
+// Per-thread, per-device readback words + events (reused call after call: a call waits on its
+// events before returning, so the slot is free again when the next call starts).  View v's
+// totals land in words [8 v, 8 v + 4): instances low / high, V, error flags (CounterFinalize).
 struct ReadbackSlot {
-  uint32_t* host = nullptr;  // [0, 8): counters after preprocess
-  hipEvent_t ev = nullptr;   // preprocess done (num_rendered readable)
+  uint32_t* host = nullptr;
+  uint32_t* dev = nullptr;
+  hipEvent_t ev[FUSED_MAX_VIEWS] = {};  // view v's totals written (the first depth-sort histogram launch)
 };
 static ReadbackSlot* readback_slot() {
   static thread_local ReadbackSlot slots[64];
@@ -215,61 +230,90 @@ static ReadbackSlot* readback_slot() {
   if (dev < 0 || dev >= 64) return set_error("device ordinal out of range"), nullptr;
   ReadbackSlot& s = slots[dev];
   if (!s.host) {
-    void* p = nullptr;
-    if (!check_hip(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc")) return nullptr;
-    if (!check_hip(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate")) return nullptr;
-    s.host = (uint32_t*)p;
+    if (!mapped_words(32 * FUSED_MAX_VIEWS, &s.host, &s.dev)) return nullptr;
+    for (int v = 0; v < FUSED_MAX_VIEWS; v++)
+      if (!check_hip(hipEventCreateWithFlags(&s.ev[v], hipEventDisableTiming), "hipEventCreate")) return nullptr;
   }
   return &s;
 }
 
+// view v's instance count from its readback words; false (error set) for an invalid view
+static bool read_view_totals(const uint32_t* w, int v, int views, long long* num_rendered) {
+  const uint32_t err = w[3];
+  const unsigned long long I = (unsigned long long)w[1] << 32 | w[0];
+  if (err & ERR_PREFILTERED) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), false;
+  if ((err & ERR_INSTANCES) || I > (unsigned long long)GS_MAX_INSTANCES) {
+    if (views > 1) return set_error("view %d has %llu (Gaussian, tile) instances, more than %lld", v, I, GS_MAX_INSTANCES), false;
+    return set_error("the view has %llu (Gaussian, tile) instances, more than %lld", I, GS_MAX_INSTANCES), false;
+  }
+  *num_rendered = (long long)I;
+  return true;
+}
+
 // Error flags of the last forward's sorts / scans, per device (not per thread: the backward of a
-// forward runs on the autograd engine's device thread).  gs_forward_render queues their readback
-// behind an event; the next forward or backward call on the device checks them (bit 4: a look-back
-// wait ran out) once its own launches are queued or before it starts, so no host wait idles the GPU.
+// forward runs on the autograd engine's device thread).  Each gs_forward_render's render kernel
+// stores them into one of two pinned words (alternating), behind an event; once its own launches
+// are queued, the forward checks the previous forward's word, and the next backward or forward
+// call checks this one (ERR_LOOKBACK: a look-back wait ran out), so no host wait idles the GPU.
 struct OrderFlags {
   std::mutex mu;
-  uint32_t* host = nullptr;  // counters after the forward's binning
-  hipEvent_t ev = nullptr;
-  bool pending = false;
+  uint32_t* host = nullptr;  // words 0 and 16: the ordering error flags of alternate forwards
+  uint32_t* dev = nullptr;   // device pointer of `host`
+  hipEvent_t ev[2] = {};
+  unsigned long long seq = 0;   // forwards queued so far
+  long long pending = -1;       // the queued forward whose flags are not checked yet
 };
 static OrderFlags g_order[64];
 
-// true: failed (error set)
-static bool check_order_flags() {
+static OrderFlags* order_flags() {
   int dev = 0;
-  if (!check_hip(hipGetDevice(&dev), "hipGetDevice") || dev < 0 || dev >= 64) return true;
-  OrderFlags& o = g_order[dev];
-  std::lock_guard<std::mutex> lk(o.mu);
-  if (!o.pending) return false;
-  o.pending = false;
-  if (!check_hip(hipEventSynchronize(o.ev), "hipEventSynchronize")) return true;
-  if (o.host[CNT_ERR] & 4u) {
+  if (!check_hip(hipGetDevice(&dev), "hipGetDevice")) return nullptr;
+  if (dev < 0 || dev >= 64) return set_error("device ordinal out of range"), nullptr;
+  return &g_order[dev];
+}
+
+// check the pending forward's flags (waits for its render kernel); true: failed (error set)
+static bool check_order_flags_locked(OrderFlags& o) {
+  if (o.pending < 0) return false;
+  const int k = (int)(o.pending & 1);
+  o.pending = -1;
+  if (!check_hip(hipEventSynchronize(o.ev[k]), "hipEventSynchronize")) return true;
+  if (o.host[16 * k] & ERR_LOOKBACK) {
     set_error("forward ordering: a look-back wait of the offsets scan or a one-sweep sort timed out "
               "(the instance list of that forward is invalid)");
     return true;
   }
   return false;
 }
+static bool check_order_flags() {
+  OrderFlags* o = order_flags();
+  if (!o) return true;
+  std::lock_guard<std::mutex> lk(o->mu);
+  return check_order_flags_locked(*o);
+}
 
-// queue the readback of this forward's ordering flags (after checking the previous forward's)
-static bool queue_order_flags(const uint32_t* counters, hipStream_t st) {
-  if (check_order_flags()) return true;
-  int dev = 0;
-  if (!check_hip(hipGetDevice(&dev), "hipGetDevice") || dev < 0 || dev >= 64) return true;
-  OrderFlags& o = g_order[dev];
-  std::lock_guard<std::mutex> lk(o.mu);
-  if (!o.host) {
-    void* p = nullptr;
-    if (!check_hip(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc")) return true;
-    if (!check_hip(hipEventCreateWithFlags(&o.ev, hipEventDisableTiming), "hipEventCreate")) return true;
-    o.host = (uint32_t*)p;
+// the device word this forward's render kernel stores its ordering flags into; null on error
+static uint32_t* order_flags_word() {
+  OrderFlags* o = order_flags();
+  if (!o) return nullptr;
+  std::lock_guard<std::mutex> lk(o->mu);
+  if (!o->host) {
+    if (!mapped_words(128, &o->host, &o->dev)) return nullptr;
+    for (int k = 0; k < 2; k++)
+      if (!check_hip(hipEventCreateWithFlags(&o->ev[k], hipEventDisableTiming), "hipEventCreate")) return nullptr;
   }
-  if (!check_hip(hipMemcpyAsync(o.host, counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)") ||
-      !check_hip(hipEventRecord(o.ev, st), "hipEventRecord"))
-    return true;
-  o.pending = true;
-  return false;
+  return o->dev + 16 * (o->seq & 1);
+}
+// the render kernel that stores this forward's flags is queued on `st`: record its event, then
+// check the previous forward's flags (its word is reused by the next forward)
+static bool queue_order_flags(hipStream_t st) {
+  OrderFlags* o = order_flags();
+  if (!o) return true;
+  std::lock_guard<std::mutex> lk(o->mu);
+  if (!check_hip(hipEventRecord(o->ev[o->seq & 1], st), "hipEventRecord")) return true;
+  const bool failed = check_order_flags_locked(*o);
+  o->pending = (long long)o->seq++;
+  return failed;
 }
 
 // split SH inputs (features_dc + features_rest rows): shs_rest needs SH colours with M >= 2
@@ -301,24 +345,18 @@ static int forward_preprocess_impl(int P, int D, int M, const float* background,
   GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier,
                  shs_rest};
   CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, prefiltered);
-  // num_rendered is the sum of the per-Gaussian tile counts, known when preprocess ends: read it
-  // back through pinned memory behind an event while the GPU goes on with compaction, the depth
-  // sort and the instance offsets, so the host round trip overlaps device work.
+  // num_rendered is the sum of the per-Gaussian tile counts, known when the first depth-sort
+  // histogram launch has summed the preprocess workgroups' totals: that launch stores it straight
+  // into pinned memory, and the host waits for it while the GPU goes on with the depth sort and
+  // the instance offsets, so the host round trip overlaps device work.
   ReadbackSlot* rb = readback_slot();
   if (!rb) return 1;
   if (check_order_flags()) return 1;  // an earlier forward's look-back waits
   fwd_preprocess(g, c, radii_out, geo, st);
-  check_hip(hipMemcpyAsync(rb->host, geo.counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
-  check_hip(hipEventRecord(rb->ev, st), "hipEventRecord");
-  fwd_order(P, geo, st);
-  check_hip(hipEventSynchronize(rb->ev), "hipEventSynchronize");
+  fwd_order(P, geo, st, rb->dev, rb->ev[0]);
+  check_hip(hipEventSynchronize(rb->ev[0]), "hipEventSynchronize");
   if (t_failed) return 1;
-  const uint32_t err = rb->host[CNT_ERR], I = rb->host[CNT_NREND];
-  if (err & ERR_PREFILTERED) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
-  if ((err & ERR_INSTANCES) || (long long)I > GS_MAX_INSTANCES)
-    return set_error("the view has more than %lld (Gaussian, tile) instances", GS_MAX_INSTANCES), 1;
-  *num_rendered_host = (long long)I;
-  return 0;
+  return read_view_totals(rb->host, 0, 1, num_rendered_host) ? 0 : 1;
 }
 
 int gs_forward_preprocess(int P, int D, int M, const float* background, int W, int H, const float* means3D,
@@ -379,36 +417,24 @@ int gs_forward_preprocess_views(int K, int P, int D, int M, const float* const* 
     pv.radii[v] = radii_out[v];
     geom_layout((size_t)P, &pv.geo[v], (char*)geom_buffer[v]);
   }
-  static thread_local uint32_t* host = nullptr;  // pinned: K x 8 counters
-  static thread_local hipEvent_t ev = nullptr, ev_pre = nullptr;
-  if (!host) {
-    void* p = nullptr;
-    if (!check_hip(hipHostMalloc(&p, 32 * FUSED_MAX_VIEWS, hipHostMallocDefault), "hipHostMalloc")) return 1;
-    if (!check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate")) return 1;
-    if (!check_hip(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming), "hipEventCreate")) return 1;
-    host = (uint32_t*)p;
-  }
+  ReadbackSlot* rb = readback_slot();
+  if (!rb) return 1;
+  static thread_local hipEvent_t ev_pre = nullptr;
+  if (!ev_pre && !check_hip(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming), "hipEventCreate")) return 1;
   if (check_order_flags()) return 1;  // an earlier forward's look-back waits
   fwd_preprocess_views(g, pv, st);
-  for (int v = 0; v < K; v++)
-    check_hip(hipMemcpyAsync(host + 8 * v, pv.geo[v].counters, 24, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(counters)");
-  check_hip(hipEventRecord(ev, st), "hipEventRecord");
-  // each view's ordering on its own stream (view_streams[v], or `stream`), after the preprocess
+  // each view's ordering on its own stream (view_streams[v], or `stream`), after the preprocess;
+  // its first histogram launch stores the view's totals into readback words [8 v, 8 v + 4)
   check_hip(hipEventRecord(ev_pre, st), "hipEventRecord");
   for (int v = 0; v < K; v++) {
     hipStream_t vs = view_streams && view_streams[v] ? (hipStream_t)view_streams[v] : st;
     if (vs != st) check_hip(hipStreamWaitEvent(vs, ev_pre, 0), "hipStreamWaitEvent");
-    fwd_order(P, pv.geo[v], vs);
+    fwd_order(P, pv.geo[v], vs, rb->dev + 8 * v, rb->ev[v]);
   }
-  check_hip(hipEventSynchronize(ev), "hipEventSynchronize");
+  for (int v = 0; v < K; v++) check_hip(hipEventSynchronize(rb->ev[v]), "hipEventSynchronize");
   if (t_failed) return 1;
-  for (int v = 0; v < K; v++) {
-    if (host[8 * v + CNT_ERR] & ERR_PREFILTERED)
-      return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), 1;
-    if ((host[8 * v + CNT_ERR] & ERR_INSTANCES) || (long long)host[8 * v + CNT_NREND] > GS_MAX_INSTANCES)
-      return set_error("view %d has more than %lld (Gaussian, tile) instances", v, GS_MAX_INSTANCES), 1;
-    num_rendered_host[v] = (long long)host[8 * v + CNT_NREND];
-  }
+  for (int v = 0; v < K; v++)
+    if (!read_view_totals(rb->host + 8 * v, v, K, &num_rendered_host[v])) return 1;
   return 0;
 }
 
@@ -430,12 +456,15 @@ int gs_forward_render(int P, const float* background, int W, int H, const float*
   geom_layout((size_t)P, &geo, (char*)geom_buffer);
   bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer);
   img_layout(W, H, &img, (char*)image_buffer);
-  fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
-  fwd_render(c, geo, bin, img, out_color, st);
   // the look-back waits of the offsets scan and of the one-sweep sorts (never expected to run out:
-  // the waited-for workgroups are running) leave error bit 4; its readback rides behind an event
-  // that the next backward or forward call of this thread checks, so no host wait idles the device
-  if (!t_failed && queue_order_flags(geo.counters, st)) return 1;
+  // the waited-for workgroups are running) leave ERR_LOOKBACK; the render kernel stores the flags
+  // into pinned memory, behind an event that the next backward or forward call checks, so no host
+  // wait idles the device
+  uint32_t* flags_word = order_flags_word();
+  if (!flags_word) return 1;
+  fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
+  fwd_render(c, geo, bin, img, out_color, st, flags_word);
+  if (!t_failed && queue_order_flags(st)) return 1;
   return t_failed ? 1 : 0;
 }
 
@@ -600,16 +629,18 @@ int gs_backward_render(int P, int D, int M, const float* background, int W, int 
   return t_failed ? 1 : 0;
 }
 
-int gs_backward_gaussians(int P, int D, int M, const float* means3D, const float* shs, const float* colors_precomp,
-                          const float* scales, float scale_modifier, const float* rotations,
-                          const float* cov3D_precomp, int num_views, const gs_view_grad* views, float* dL_dcolors,
-                          float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
-                          float* dL_dscales, float* dL_drotations, unsigned accumulate, void* wait_event, int debug,
-                          void* stream) {
+static int backward_gaussians_impl(int P, int first, int count, int D, int M, const float* means3D, const float* shs,
+                                   const float* colors_precomp, const float* scales, float scale_modifier,
+                                   const float* rotations, const float* cov3D_precomp, int num_views,
+                                   const gs_view_grad* views, float* dL_dcolors, float* dL_dopacity,
+                                   float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                                   float* dL_drotations, unsigned accumulate, void* wait_event, int debug,
+                                   void* stream) {
   clear_error(debug);
   if (P < 0) return set_error("P must be >= 0"), 1;
+  if (first < 0 || count < 0 || (long long)first + count > P) return set_error("Gaussian range out of bounds"), 1;
   if (num_views < 0 || (num_views > 0 && !views)) return set_error("bad view list"), 1;
-  if (P == 0 || num_views == 0) return 0;
+  if (P == 0 || count == 0 || num_views == 0) return 0;
   if (!means3D) return set_error("missing required input pointer"), 1;
   if ((shs == nullptr) == (colors_precomp == nullptr))
     return set_error("Please provide excatly one of either SHs or precomputed colors!"), 1;
@@ -627,7 +658,13 @@ int gs_backward_gaussians(int P, int D, int M, const float* means3D, const float
   }
   hipStream_t st = (hipStream_t)stream;
   if (wait_event && !check_hip(hipStreamWaitEvent(st, (hipEvent_t)wait_event, 0), "hipStreamWaitEvent")) return 1;
-  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, nullptr, scales, rotations, cov3D_precomp, scale_modifier};
+  // the range [first, first + count) as a P = count problem: every per-Gaussian array is row-indexed,
+  // so the rows' pointers are offset by `first` (the geom buffers keep their P-row layout)
+  const size_t f = (size_t)first;
+  auto off = [f](const float* p, size_t w) { return p ? p + f * w : nullptr; };
+  auto offw = [f](float* p, size_t w) { return p ? p + f * w : nullptr; };
+  GaussianArgs g{count, D, M, off(means3D, 3), off(shs, 3 * (size_t)M), off(colors_precomp, 3), nullptr,
+                 off(scales, 3), off(rotations, 4), off(cov3D_precomp, 6), scale_modifier};
   // passes of up to FUSED_MAX_VIEWS views; the later passes add to what the earlier wrote
   for (int v0 = 0; v0 < num_views; v0 += FUSED_MAX_VIEWS) {
     FusedViews fv;
@@ -638,16 +675,38 @@ int gs_backward_gaussians(int P, int D, int M, const float* means3D, const float
       geom_layout((size_t)P, &geo, (char*)w.geom_buffer);
       fv.v[k].c = make_camera(nullptr, w.image_width, w.image_height, w.viewmatrix, w.projmatrix, w.campos,
                               w.tan_fovx, w.tan_fovy, 0);
-      fv.v[k].tiles = geo.tiles;
-      fv.v[k].clamped = geo.clamped;
-      fv.v[k].gsum = geo.gsum;
+      fv.v[k].tiles = geo.tiles + f;
+      fv.v[k].clamped = geo.clamped + f;
+      fv.v[k].gsum = geo.gsum + f * GRAD_REC;
     }
-    GradOut out{nullptr, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, shs ? dL_dsh : nullptr,
-                cov3D_precomp ? nullptr : dL_dscales, cov3D_precomp ? nullptr : dL_drotations,
-                v0 == 0 ? accumulate : 0xFFu};
+    GradOut out{nullptr, offw(dL_dcolors, 3), offw(dL_dopacity, 1), offw(dL_dmeans3D, 3), offw(dL_dcov3D, 6),
+                shs ? offw(dL_dsh, 3 * (size_t)M) : nullptr, cov3D_precomp ? nullptr : offw(dL_dscales, 3),
+                cov3D_precomp ? nullptr : offw(dL_drotations, 4), v0 == 0 ? accumulate : 0xFFu};
     bwd_gaussians(g, fv, out, st);
   }
   return t_failed ? 1 : 0;
+}
+
+int gs_backward_gaussians(int P, int D, int M, const float* means3D, const float* shs, const float* colors_precomp,
+                          const float* scales, float scale_modifier, const float* rotations,
+                          const float* cov3D_precomp, int num_views, const gs_view_grad* views, float* dL_dcolors,
+                          float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                          float* dL_dscales, float* dL_drotations, unsigned accumulate, void* wait_event, int debug,
+                          void* stream) {
+  return backward_gaussians_impl(P, 0, P, D, M, means3D, shs, colors_precomp, scales, scale_modifier, rotations,
+                                 cov3D_precomp, num_views, views, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+                                 dL_dsh, dL_dscales, dL_drotations, accumulate, wait_event, debug, stream);
+}
+
+int gs_backward_gaussians_range(int P, int first, int count, int D, int M, const float* means3D, const float* shs,
+                                const float* colors_precomp, const float* scales, float scale_modifier,
+                                const float* rotations, const float* cov3D_precomp, int num_views,
+                                const gs_view_grad* views, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                                float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                                unsigned accumulate, void* wait_event, int debug, void* stream) {
+  return backward_gaussians_impl(P, first, count, D, M, means3D, shs, colors_precomp, scales, scale_modifier,
+                                 rotations, cov3D_precomp, num_views, views, dL_dcolors, dL_dopacity, dL_dmeans3D,
+                                 dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, accumulate, wait_event, debug, stream);
 }
 
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,

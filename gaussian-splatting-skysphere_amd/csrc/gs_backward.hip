@@ -86,6 +86,9 @@ constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x
 #ifndef GS_BWD_PREFETCH
 #define GS_BWD_PREFETCH 1
 #endif
+#ifndef GS_BWD_ABLATE
+#define GS_BWD_ABLATE 0  // timing-only builds (wrong gradients): 1 no wave reduction, 2 no commit, 3 no walk
+#endif
 #ifndef GS_BWD_HALFROW
 #define GS_BWD_HALFROW 1  // 0: row sums (4 DPP steps) with one writer lane per row
 #endif
@@ -209,7 +212,17 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) GS_WPE_ATTR(GS_BWD_WPE) v
     s[7] = __builtin_fmaf(w4.x, dy.x, w4.y * dy.y);
     T = Tn;
     U = pk_fma(Cd, dch, U);
-#if GS_BWD_HALFROW
+#if GS_BWD_ABLATE == 1  // timing only: no wave reduction
+    float d = s[(lane >> 3) & 7], d8 = s[8];
+    asm volatile("" ::"v"(d), "v"(d8));
+    if ((lane & 7) == 0) {
+      uint32_t eo = j * ACC_STRIDE;
+      asm volatile("" : "+s"(eo));
+      lds_float* acc = acc_lane + eo;
+      acc[0] = d;
+      acc[8] = d8;
+    }
+#elif GS_BWD_HALFROW
     float d, d8;
     wave_sum9_halfrows(s, hi8, d, d8);
     asm volatile("" ::"v"(d), "v"(d8));
@@ -354,6 +367,9 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) GS_WPE_ATTR(GS_BWD_WPE) v
 #pragma unroll 1
     for (int g = 0; g < BWD_GROUPS; g++) {
       uint64_t m = uniform_u64(s_mask[g][wid]);
+#if GS_BWD_ABLATE == 3  // timing only: staging and flush, no walk
+      m = 0;
+#endif
       // entries no pixel of this wave reaches (e >= wave_last) sit at the low bits: drop them
       const int jmin = (int)n_eff - (int)wave_last - (int)base - g * 64;  // j - 64 g >= jmin
       if (jmin > 0) m &= jmin >= 64 ? 0ull : ~((1ull << jmin) - 1ull);
@@ -390,7 +406,11 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) GS_WPE_ATTR(GS_BWD_WPE) v
           }
         }
 #endif
+#if GS_BWD_ABLATE == 2  // timing only: evaluation and test, no commit
+        if (__ballot(v.cA || v.cB) != 0) asm volatile("" ::"v"(v.oG.x), "v"(v.oG.y));
+#else
         if (__ballot(v.cA || v.cB) != 0) apply(j, v, xr);
+#endif
       }
 #endif
     }

@@ -94,13 +94,13 @@ __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g,
                                                    int* __restrict__ radii, float4* __restrict__ splat,
                                                    float4* __restrict__ binrec, uint32_t& dbits,
                                                    uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
-                                                   uint32_t* __restrict__ counters) {
+                                                   bool& culled_prefiltered) {
   radii[i] = 0;
   tiles[i] = 0;
   const float px = g.means3D[3 * i + 0], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
   const float3v pv = xf43(c.view, px, py, pz);
   if (pv.z <= 0.2f) {
-    if (c.prefiltered) atomicOr(&counters[CNT_ERR], 1u);
+    culled_prefiltered = c.prefiltered != 0;  // upstream raises "Point is filtered although prefiltered is set"
     return 0;
   }
   const float* P = c.proj;
@@ -173,24 +173,13 @@ __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g,
   return count;
 }
 
-// The workgroup's tile total (num_rendered, read back by the host as soon as this kernel is done
-// while the ordering kernels run) and its count of Gaussians with instances (V) go to
-// counters[CNT_NREND] / [CNT_V] by one 64-bit atomic add.  depth_key[i] is the depth's bits for those and DEPTH_DROP for every other
-// Gaussian: the first depth-sort pass drops them, which is the visibility compaction.
-template <int DEG>
-__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
-                                                    float4* __restrict__ splat, float4* __restrict__ binrec,
-                                                    uint32_t* __restrict__ depth_key,
-                                                    uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
-                                                    uint32_t* __restrict__ counters) {
+
+// The workgroup's tile total and count of Gaussians with instances (+ a prefiltered cull) -> its
+// WgTotals slot; the first depth-sort histogram launch sums the slots (CounterFinalize).
+__device__ __forceinline__ void workgroup_totals(uint32_t area, bool culled, WgTotals* wg) {
   __shared__ uint32_t s_sum[4], s_vis[4];
-  const int i = blockIdx.x * 256 + (int)threadIdx.x;
-  uint32_t area = 0, dbits = 0;
-  if (i < g.P) {
-    area = preprocess_one<DEG>(i, g, c, radii, splat, binrec, dbits, tiles, clamped, counters);
-    depth_key[i] = area ? dbits : DEPTH_DROP;
-  }
   uint32_t vis = area ? 1u : 0u;
+  const uint64_t cm = __ballot(culled);
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     area += (uint32_t)__shfl_xor((int)area, d, 64);
@@ -198,14 +187,37 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess(Gaus
   }
   if ((threadIdx.x & 63) == 0) {
     s_sum[threadIdx.x >> 6] = area;
-    s_vis[threadIdx.x >> 6] = vis;
+    s_vis[threadIdx.x >> 6] = vis | (cm ? 0x80000000u : 0u);
   }
   lds_barrier();
   if (threadIdx.x == 0) {
     const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-    const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
-    if (tot) add_view_totals(counters, nv, tot);
+    const uint32_t v4 = s_vis[0] | s_vis[1] | s_vis[2] | s_vis[3];
+    const uint32_t nv = (s_vis[0] & 0x7FFFFFFFu) + (s_vis[1] & 0x7FFFFFFFu) + (s_vis[2] & 0x7FFFFFFFu) +
+                        (s_vis[3] & 0x7FFFFFFFu);
+    store_wg_totals(wg, nv, tot, (v4 >> 31) != 0);
   }
+}
+
+// The workgroup's tile total (num_rendered, read back by the host right after the first depth-sort
+// histogram launch while the ordering kernels run) and its count of Gaussians with instances (V)
+// go to its WgTotals slot (workgroup_totals).  depth_key[i] is the depth's bits for those and
+// DEPTH_DROP for every other Gaussian: the first depth-sort pass drops them, which is the
+// visibility compaction.
+template <int DEG>
+__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
+                                                    float4* __restrict__ splat, float4* __restrict__ binrec,
+                                                    uint32_t* __restrict__ depth_key,
+                                                    uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
+                                                    WgTotals* __restrict__ wg) {
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  uint32_t area = 0, dbits = 0;
+  bool culled = false;
+  if (i < g.P) {
+    area = preprocess_one<DEG>(i, g, c, radii, splat, binrec, dbits, tiles, clamped, culled);
+    depth_key[i] = area ? dbits : DEPTH_DROP;
+  }
+  workgroup_totals(area, culled, wg);
 }
 
 // The split-SH preprocess: k_preprocess's body with the split row loader (preprocess_one SPLIT).
@@ -213,44 +225,28 @@ template <int DEG>
 __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess_split(
     GaussianArgs g, CameraArgs c, int* __restrict__ radii, float4* __restrict__ splat, float4* __restrict__ binrec,
     uint32_t* __restrict__ depth_key, uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
-    uint32_t* __restrict__ counters) {
-  __shared__ uint32_t s_sum[4], s_vis[4];
+    WgTotals* __restrict__ wg) {
   const int i = blockIdx.x * 256 + (int)threadIdx.x;
   uint32_t area = 0, dbits = 0;
+  bool culled = false;
   if (i < g.P) {
-    area = preprocess_one<DEG, true>(i, g, c, radii, splat, binrec, dbits, tiles, clamped, counters);
+    area = preprocess_one<DEG, true>(i, g, c, radii, splat, binrec, dbits, tiles, clamped, culled);
     depth_key[i] = area ? dbits : DEPTH_DROP;
   }
-  uint32_t vis = area ? 1u : 0u;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    area += (uint32_t)__shfl_xor((int)area, d, 64);
-    vis += (uint32_t)__shfl_xor((int)vis, d, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    s_sum[threadIdx.x >> 6] = area;
-    s_vis[threadIdx.x >> 6] = vis;
-  }
-  lds_barrier();
-  if (threadIdx.x == 0) {
-    const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-    const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
-    if (tot) add_view_totals(counters, nv, tot);
-  }
+  workgroup_totals(area, culled, wg);
 }
 
 void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st) {
-  (void)hipMemsetAsync(geo.counters, 0, 64, st);
   dim3 grid((g.P + 255) / 256), block(256);
   if (g.colors) {
     GS_LAUNCH("preprocess", k_preprocess<-1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
-              geo.clamped, geo.counters);
+              geo.clamped, geo.wg_tot);
     return;
   }
   if (g.shs_rest) {  // split SH rows (M >= 2, so D >= 0 applies)
 #define GS_PRE_SPLIT(D)                                                                                        \
   GS_LAUNCH("preprocess", (k_preprocess_split<D>), grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, \
-            geo.keys_a, geo.tiles, geo.clamped, geo.counters)
+            geo.keys_a, geo.tiles, geo.clamped, geo.wg_tot)
     switch (g.D) {
       case 0: GS_PRE_SPLIT(0); break;
       case 1: GS_PRE_SPLIT(1); break;
@@ -263,19 +259,19 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
   switch (g.D) {
     case 0:
       GS_LAUNCH("preprocess", k_preprocess<0>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
-                geo.clamped, geo.counters);
+                geo.clamped, geo.wg_tot);
       break;
     case 1:
       GS_LAUNCH("preprocess", k_preprocess<1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
-                geo.clamped, geo.counters);
+                geo.clamped, geo.wg_tot);
       break;
     case 2:
       GS_LAUNCH("preprocess", k_preprocess<2>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
-                geo.clamped, geo.counters);
+                geo.clamped, geo.wg_tot);
       break;
     default:
       GS_LAUNCH("preprocess", k_preprocess<3>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
-                geo.clamped, geo.counters);
+                geo.clamped, geo.wg_tot);
       break;
   }
 }
@@ -283,41 +279,25 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
 // K views in one launch: every lane runs the single-view preprocess of its Gaussian for each
 // camera in turn (preprocess_one, so each view's outputs are bit-identical to its own launch);
 // the Gaussian's inputs come from HBM once, the later views read them from the caches.  The
-// per-view workgroup totals go to each view's counters as in k_preprocess.
+// per-view workgroup totals go to each view's WgTotals slots as in k_preprocess.
 template <int DEG>
 __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PV_WPE) void k_preprocess_views(GaussianArgs g, PreViews pv) {
-  __shared__ uint32_t s_sum[4], s_vis[4];
   const int i = blockIdx.x * 256 + (int)threadIdx.x;
   for (int v = 0; v < pv.K; v++) {
     const GeomPtrs& geo = pv.geo[v];
     uint32_t area = 0, dbits = 0;
+    bool culled = false;
     if (i < g.P) {
       area = preprocess_one<DEG>(i, g, pv.c[v], pv.radii[v], geo.splat, geo.binrec, dbits, geo.tiles, geo.clamped,
-                                 geo.counters);
+                                 culled);
       geo.keys_a[i] = area ? dbits : DEPTH_DROP;
     }
-    uint32_t vis = area ? 1u : 0u;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      area += (uint32_t)__shfl_xor((int)area, d, 64);
-      vis += (uint32_t)__shfl_xor((int)vis, d, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      s_sum[threadIdx.x >> 6] = area;
-      s_vis[threadIdx.x >> 6] = vis;
-    }
-    lds_barrier();
-    if (threadIdx.x == 0) {
-      const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-      const uint32_t nv = s_vis[0] + s_vis[1] + s_vis[2] + s_vis[3];
-      if (tot) add_view_totals(geo.counters, nv, tot);
-    }
-    lds_barrier();  // s_sum / s_vis are reused by the next view
+    workgroup_totals(area, culled, geo.wg_tot);
+    lds_barrier();  // workgroup_totals' LDS is reused by the next view
   }
 }
 
 void fwd_preprocess_views(const GaussianArgs& g, const PreViews& pv, hipStream_t st) {
-  for (int v = 0; v < pv.K; v++) (void)hipMemsetAsync(pv.geo[v].counters, 0, 64, st);
   dim3 grid((g.P + 255) / 256), block(256);
   if (g.colors) {
     GS_LAUNCH("preprocess_views", k_preprocess_views<-1>, grid, block, 0, st, g, pv);
@@ -366,8 +346,73 @@ struct DstOffsets {
 #ifndef GS_DEPTH_SORT_BLOCKS
 #define GS_DEPTH_SORT_BLOCKS 4096  // workgroups per depth-sort pass (sort_plan)
 #endif
-void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
+// The extra workgroup of the first depth-sort histogram launch: the view's totals from the preprocess
+// workgroups' WgTotals (64-bit instance sum: an overflow of the 32-bit instance positions is seen
+// exactly), written to the view's counters (which need no zeroing beforehand: every counter the
+// later kernels read is set here) and to the host's readback words (host: a device-visible pointer
+// into pinned host memory, or null): [0] instances low, [1] high, [2] V, [3] error flags.
+struct CounterFinalize {
+  static constexpr bool active = true;
+  const WgTotals* wg;
+  uint32_t nwg;
+  uint32_t* counters;
+  uint32_t* host;
+  __device__ void operator()() const {
+    __shared__ uint32_t s_lo[4], s_hi[4], s_v[4], s_e[4];
+    unsigned long long si = 0;
+    uint32_t sv = 0, se = 0;
+    for (uint32_t k = threadIdx.x; k < nwg; k += SORT_THREADS) {
+      const WgTotals t = wg[k];
+      si += t.inst;
+      sv += t.vis & 0x7FFFFFFFu;
+      se |= t.vis >> 31;
+    }
+    uint32_t lo = (uint32_t)si, hi = (uint32_t)(si >> 32);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint32_t olo = (uint32_t)__shfl_xor((int)lo, d, 64), ohi = (uint32_t)__shfl_xor((int)hi, d, 64);
+      const unsigned long long a = ((unsigned long long)hi << 32 | lo) + ((unsigned long long)ohi << 32 | olo);
+      lo = (uint32_t)a;
+      hi = (uint32_t)(a >> 32);
+      sv += (uint32_t)__shfl_xor((int)sv, d, 64);
+      se |= (uint32_t)__shfl_xor((int)se, d, 64);
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s_lo[w] = lo, s_hi[w] = hi, s_v[w] = sv, s_e[w] = se;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      unsigned long long I = 0;
+      uint32_t V = 0, e = 0;
+      for (int k = 0; k < SORT_THREADS / 64; k++) {
+        I += (unsigned long long)s_hi[k] << 32 | s_lo[k];
+        V += s_v[k];
+        e |= s_e[k];
+      }
+      const uint32_t err = (e ? ERR_PREFILTERED : 0u) | (I > (unsigned long long)GS_MAX_INSTANCES ? ERR_INSTANCES : 0u);
+      counters[CNT_NREND] = (uint32_t)I;
+      counters[CNT_V] = V;
+      counters[CNT_ERR] = err;
+      counters[CNT_I] = 0u;
+      counters[CNT_LB_TILE] = 0u;
+      if (host) {
+        host[0] = (uint32_t)I;
+        host[1] = (uint32_t)(I >> 32);
+        host[2] = V;
+        host[3] = err;
+      }
+    }
+  }
+};
+
+void fwd_order(int P, const GeomPtrs& geo, hipStream_t st, uint32_t* host_counts, hipEvent_t counts_ready) {
   const uint32_t n = (uint32_t)P;
+  // the first depth-sort pass's counts, with the view's totals finalised by block 0 (the host
+  // waits for this launch only: the rest of the ordering overlaps its readback)
+  const SortPlan sp = sort_plan(n, GS_DEPTH_SORT_BLOCKS);
+  GS_LAUNCH("radix_hist", k_radix_hist<CounterFinalize>, dim3(sp.nb + 1), dim3(SORT_THREADS), 0, st, geo.keys_a, nullptr,
+            n, 0, radix_first_bits(32), sp.chunk, sp.nb, geo.sort_scratch, true,
+            CounterFinalize{geo.wg_tot, (n + 255) / 256, geo.counters, host_counts});
+  if (counts_ready) (void)hipEventRecord(counts_ready, st);
   // depth sort of the Gaussians with instances: the first pass reads all P keys in index order
   // and drops the DEPTH_DROP ones (compaction), the later passes sort the V survivors.
   if (lb_tiles(n) <= LB_STATIC_MAX) {
@@ -375,8 +420,8 @@ void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
     // tile ids); it gathers each rank's tile count (the gather is cheaper here than carrying the
     // counts through the four sort passes)
     radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
-                     geo.sort_scratch, st, /*drop_first=*/true, false, nullptr, nullptr, nullptr, nullptr,
-                     GS_DEPTH_SORT_BLOCKS);
+                     geo.sort_scratch, st, /*drop_first=*/true, /*hist0_ready=*/true, nullptr, nullptr, nullptr,
+                     nullptr, GS_DEPTH_SORT_BLOCKS);
     scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid, n}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
                       &geo.counters[CNT_V], n, geo.lb_status, &geo.counters[CNT_LB_TILE], &geo.counters[CNT_I],
                       &geo.counters[CNT_ERR], st);
@@ -385,7 +430,8 @@ void fwd_order(int P, const GeomPtrs& geo, hipStream_t st) {
     // the first pass), and the 3-launch scan reads them in depth order, coalesced (C5, 5M: the
     // per-rank gather and the ticketed look-back took 197 us)
     radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
-                     geo.sort_scratch, st, /*drop_first=*/true, false, geo.tiles, geo.rtiles_a, geo.rtiles_b);
+                     geo.sort_scratch, st, /*drop_first=*/true, /*hist0_ready=*/true, geo.tiles, geo.rtiles_a,
+                     geo.rtiles_b, nullptr, GS_DEPTH_SORT_BLOCKS);
     scan_exclusive(SrcArray{geo.tiles_by_rank}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
                    &geo.counters[CNT_V], n, geo.scan_partial, &geo.counters[CNT_I], st);
   }
@@ -741,8 +787,10 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
                                                          float4* __restrict__ inst_splat, float* __restrict__ out,
                                                          float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                          uint32_t* __restrict__ tile_max, ImgPtrs img,
-                                                         const uint32_t* __restrict__ err) {
+                                                         const uint32_t* __restrict__ err,
+                                                         uint32_t* __restrict__ err_host) {
   __shared__ float4 s_ent[3 * GS_BLOCK];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && err_host) err_host[0] = *err;
   __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[4][GS_BLOCK + 2 * FWD_ILP];  // per quadrant wave: byte offsets
   const uint32_t tile = blockIdx.x;
@@ -824,7 +872,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
                                                      float4* __restrict__ inst_splat, float* __restrict__ out,
                                                      float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                      uint32_t* __restrict__ tile_max, ImgPtrs img,
-                                                     const uint32_t* __restrict__ err) {
+                                                     const uint32_t* __restrict__ err, uint32_t* __restrict__ err_host) {
   __shared__ float4 s_ent[3 * FWDQ_NB];
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
   const uint32_t b = blockIdx.x;
@@ -833,6 +881,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   const int wid = (int)((b >> 3) & 3);
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int lane = threadIdx.x;
+  // the ordering's error flags (final once the binning kernels are done) -> the host's readback word
+  if (b == 0 && lane == 0 && err_host) err_host[0] = *err;
   const QuadPix q = quad_pixel(tx, ty, wid, lane);
   const bool inside = q.px < c.W && q.py < c.H;
   const uint2 range = ranges[tile];
@@ -901,28 +951,28 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
 #define GS_FWD_WAVE 1
 #endif
 void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
-                hipStream_t st) {
+                hipStream_t st, uint32_t* err_host) {
   const int tiles = c.gx * c.gy;
   if (GS_FWD_WAVE) {
     const int blocks = (int)xcd_span((uint32_t)tiles) * 32;
     if (exact_exp())
       GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
                 GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-                &geo.counters[CNT_ERR]);
+                &geo.counters[CNT_ERR], err_host);
     else
       GS_LAUNCH("render_fwd", k_render_fwd_q<false>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
                 GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-                &geo.counters[CNT_ERR]);
+                &geo.counters[CNT_ERR], err_host);
     return;
   }
   if (exact_exp())
     GS_LAUNCH("render_fwd", k_render_fwd<true>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
               GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-                &geo.counters[CNT_ERR]);
+                &geo.counters[CNT_ERR], err_host);
   else
     GS_LAUNCH("render_fwd", k_render_fwd<false>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
               GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-                &geo.counters[CNT_ERR]);
+                &geo.counters[CNT_ERR], err_host);
 }
 
 // ------------------------------------------------------------------------------------------

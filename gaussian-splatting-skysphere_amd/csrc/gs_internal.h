@@ -83,13 +83,16 @@ constexpr uint32_t ERR_PREFILTERED = 1u, ERR_LOOKBACK = 4u, ERR_INSTANCES = 8u;
 // (a position plus one sort chunk must stay below 2^32).
 constexpr long long GS_MAX_INSTANCES = (1ll << 31) - 1;
 
-// A preprocess workgroup's totals -> the view's counters: ONE 64-bit add of (V << 32 | I), so the
-// host reads both with one copy.  A carry out of the 32-bit instance field (over 2^32 instances)
-// would land in V: the adding workgroup sees it in the returned word and raises ERR_INSTANCES.
-__device__ __forceinline__ void add_view_totals(uint32_t* counters, uint32_t nv, uint32_t tot) {
-  const unsigned long long old =
-      atomicAdd(reinterpret_cast<unsigned long long*>(&counters[CNT_NREND]), ((unsigned long long)nv << 32) | tot);
-  if ((unsigned long long)(uint32_t)old + tot > 0xFFFFFFFFull) atomicOr(&counters[CNT_ERR], ERR_INSTANCES);
+// A preprocess workgroup's totals: its instance count and its count of Gaussians with instances
+// (bit 31: a Gaussian was culled although `prefiltered` is set), stored per workgroup (no atomics,
+// no zeroing).  The first depth-sort histogram launch sums them in 64-bit (k_radix_hist<true>),
+// writes the view's counters and copies them to the host's readback words.
+struct WgTotals {
+  uint32_t inst;  // tiles touched by the workgroup's Gaussians (<= 256 x tiles of the image)
+  uint32_t vis;   // Gaussians with instances | ERR_PREFILTERED << 31
+};
+__device__ __forceinline__ void store_wg_totals(WgTotals* wg, uint32_t nv, uint32_t tot, bool culled_prefiltered) {
+  wg[blockIdx.x] = WgTotals{tot, nv | (culled_prefiltered ? 0x80000000u : 0u)};
 }
 
 struct GeomPtrs {
@@ -106,11 +109,12 @@ struct GeomPtrs {
   uint32_t* scan_partial;
   uint64_t* lb_status;  // look-back scan status words (lb_tiles(P))
   uint32_t* sort_scratch;
-  // [1] instances I (offsets scan), [2] error flags (1 prefiltered cull, 4 look-back timeout),
-  // [4] / [5] num_rendered / V (Gaussians with instances) summed by preprocess as ONE 64-bit
-  // word (one same-address atomic per workgroup), [9] look-back tile counter (offsets scan)
+  // [1] instances I (offsets scan), [2] error flags (ERR_*), [4] / [5] num_rendered / V
+  // (Gaussians with instances) from the preprocess workgroups' WgTotals (CounterFinalize, the first
+  // depth-sort histogram launch), [9] look-back tile counter (offsets scan)
   uint32_t* counters;
   uint32_t* sorted_gid;  // = vals_a or vals_b after the depth sort
+  WgTotals* wg_tot;      // per preprocess workgroup (ceil(P / 256))
 };
 
 inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
@@ -133,6 +137,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
   size_t o_lb = take((size_t)lb_tiles(Pn) * 8);
   size_t o_ss = take(sort_scratch_words(Pn) * 4);
   size_t o_cnt = take(64);
+  size_t o_wg = take(((Pn + 255) / 256) * sizeof(WgTotals));
   if (out && base) {
     out->splat = (float4*)(base + o_splat);
     out->binrec = (float4*)(base + o_bin);
@@ -152,6 +157,7 @@ inline size_t geom_layout(size_t P, GeomPtrs* out, char* base) {
     out->lb_status = (uint64_t*)(base + o_lb);
     out->sort_scratch = (uint32_t*)(base + o_ss);
     out->counters = (uint32_t*)(base + o_cnt);
+    out->wg_tot = (WgTotals*)(base + o_wg);
     out->sorted_gid = (radix_passes(32) % 2 == 0) ? out->vals_a : out->vals_b;
   }
   return off;
@@ -325,11 +331,15 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
 
 // ---- stages (gs_forward.hip / gs_backward.hip) ----
 void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st);
-void fwd_order(int P, const GeomPtrs& geo, hipStream_t st);  // compaction, depth sort, instance offsets
+// compaction, depth sort, instance offsets; the view's totals are finalised by the first histogram
+// launch (written to host_counts when given: [I lo, I hi, V, err]), after which counts_ready is recorded
+void fwd_order(int P, const GeomPtrs& geo, hipStream_t st, uint32_t* host_counts = nullptr,
+               hipEvent_t counts_ready = nullptr);
 void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const GeomPtrs& geo, const BinPtrs& bin,
              const ImgPtrs& img, hipStream_t st);
+// err_host (device-visible pinned host word, or null): the ordering's error flags, copied by the render
 void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
-                hipStream_t st);
+                hipStream_t st, uint32_t* err_host = nullptr);
 void mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
                   hipStream_t st);
 void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,

@@ -359,12 +359,25 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits
   return peers;
 }
 
-static __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys,
-                                                                     const uint32_t* n_dev, uint32_t n_max,
-                                                                     int shift, int bits, uint32_t chunk,
-                                                                     uint32_t nb, uint32_t* __restrict__ hist,
-                                                                     bool drop) {
+// Fin: work of one extra workgroup (blockIdx nb, all 256 threads; the launch then has nb + 1
+// workgroups) beside the counting ones, e.g. the forward's counter finalisation in the first
+// depth-sort pass (gs_forward.hip CounterFinalize); NoFin: none.
+struct NoFin {
+  static constexpr bool active = false;
+  __device__ void operator()() const {}
+};
+template <class Fin = NoFin>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, const uint32_t* n_dev,
+                                                             uint32_t n_max, int shift, int bits, uint32_t chunk,
+                                                             uint32_t nb, uint32_t* __restrict__ hist, bool drop,
+                                                             Fin fin = Fin()) {
   __shared__ uint32_t h[RADIX];
+  if constexpr (Fin::active) {
+    if (blockIdx.x == nb) {  // (uniform) the extra workgroup runs beside the counting ones
+      fin();
+      return;
+    }
+  }
   const uint32_t n = resolve_n(n_dev, n_max);
   h[threadIdx.x] = 0;
   lds_barrier();
@@ -579,8 +592,8 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
     // keys_in0: the first pass reads its keys from there (kept), not from keys_a
     const uint32_t* kin_p = (shift == 0 && keys_in0) ? keys_in0 : kin;
     if (!(hist0_ready && shift == 0))
-      GS_LAUNCH("radix_hist", k_radix_hist, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin_p, nd, n_max, shift, bits,
-                p.chunk, p.nb, hist, drop);
+      GS_LAUNCH("radix_hist", k_radix_hist<NoFin>, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin_p, nd, n_max, shift,
+                bits, p.chunk, p.nb, hist, drop, NoFin());
     GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX), dim3(SORT_THREADS), 0, st, hist, p.nb, row_total);
     const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
     if (aux0) {

@@ -304,11 +304,12 @@ def backward_render(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fo
 
 
 def backward_gaussians(means3D, sh, colors, scales, rotations, cov3D_precomp, scale_modifier, degree, views, outs,
-                       accumulate, wait_event=None, debug=False):
+                       accumulate, wait_event=None, debug=False, first=0, count=None):
     """Per-Gaussian half of the backward for several views at once (gs_backward_gaussians).
     views: [(viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, W, H, geomBuffer)] in order (each
     after its backward_render); outs: {name: buffer} for colors / opacity / means3D / cov3D / sh /
-    scales / rotations (absent: not produced); accumulate: GS_ACC bits of the first view."""
+    scales / rotations (absent: not produced); accumulate: GS_ACC bits of the first view.
+    first / count: only the Gaussians [first, first + count) (gs_backward_gaussians_range)."""
     x = _Inputs(None, means3D, colors, None, scales, rotations, cov3D_precomp, views[0][0],
                 views[0][1], sh, views[0][2], need_opacity=False)
     P, dev = x.P, x.device
@@ -326,14 +327,16 @@ def backward_gaussians(means3D, sh, colors, scales, rotations, cov3D_precomp, sc
     for n, t in o.items():
         if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev):
             raise RuntimeError(f"backward_gaussians: {n} output must be a contiguous float32 tensor on {dev}")
+    count = P - int(first) if count is None else int(count)
     with torch.cuda.device(dev):
         _native.check(
-            _lib.gs_backward_gaussians(
-                P, int(degree), x.M, _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors), _ptr(x.scales), float(scale_modifier),
-                _ptr(x.rotations), _ptr(x.cov3D), len(views), arr, _ptr(o["colors"]), _ptr(o["opacity"]),
-                _ptr(o["means3D"]), _ptr(o["cov3D"]), _ptr(o["sh"]), _ptr(o["scales"]), _ptr(o["rotations"]),
-                int(accumulate), ctypes.c_void_p(wait_event.cuda_event) if wait_event is not None else None,
-                int(bool(debug)), _stream(dev)),
+            _lib.gs_backward_gaussians_range(
+                P, int(first), count, int(degree), x.M, _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors), _ptr(x.scales),
+                float(scale_modifier), _ptr(x.rotations), _ptr(x.cov3D), len(views), arr, _ptr(o["colors"]),
+                _ptr(o["opacity"]), _ptr(o["means3D"]), _ptr(o["cov3D"]), _ptr(o["sh"]), _ptr(o["scales"]),
+                _ptr(o["rotations"]), int(accumulate),
+                ctypes.c_void_p(wait_event.cuda_event) if wait_event is not None else None, int(bool(debug)),
+                _stream(dev)),
             "rasterize_gaussians_backward (per-Gaussian half)")
 
 

@@ -140,13 +140,32 @@ def prepare_views(rasterizers, means3D, opacities, shs=None, colors_precomp=None
     with torch.no_grad():
         tri = _C.preprocess_views([s.bg for s in ss], means3D.detach(), e(colors_precomp).detach(), opacities.detach(),
                                   e(scales).detach(), e(rotations).detach(), s0.scale_modifier,
-                                  e(cov3D_precomp).detach(), [s.viewmatrix.contiguous() for s in ss],
-                                  [s.projmatrix.contiguous() for s in ss], [s.tanfovx for s in ss],
+                                  e(cov3D_precomp).detach(), [_contiguous_matrix(s.viewmatrix) for s in ss],
+                                  [_contiguous_matrix(s.projmatrix) for s in ss], [s.tanfovx for s in ss],
                                   [s.tanfovy for s in ss], [s.image_height for s in ss], [s.image_width for s in ss],
                                   e(shs).detach(), s0.sh_degree, [s.campos for s in ss], s0.prefiltered, s0.debug,
                                   streams)
     inputs = (means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp)
     return [PreparedView(t, s, inputs) for t, s in zip(tri, ss)]
+
+
+_CONTIG: dict = {}  # id(camera tensor) -> (weakref, _version, contiguous copy)
+
+
+def _contiguous_matrix(t: torch.Tensor) -> torch.Tensor:
+    """t.contiguous() for the camera matrices, memoised per source tensor and version.  The
+    reference's Camera keeps world_view_transform / full_proj_transform as transposed views
+    (scene/cameras.py:54-56), so every render() would otherwise copy both (one copy launch each)."""
+    if t.is_contiguous():
+        return t
+    e = _CONTIG.get(id(t))
+    if e is not None and e[0]() is t and e[1] == t._version:
+        return e[2]
+    c = t.contiguous()
+    if len(_CONTIG) > 256:
+        _CONTIG.clear()
+    _CONTIG[id(t)] = (weakref.ref(t), t._version, c)
+    return c
 
 
 def _run_with_snapshot(fn, args, debug, dump_name, phase):
@@ -169,7 +188,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         s = raster_settings
         # the camera matrices arrive transposed (cameras.py:54-56 world_view_transform is a
         # .transpose(0, 1) view); make them contiguous once and reuse them in backward
-        view, proj = s.viewmatrix.contiguous(), s.projmatrix.contiguous()
+        view, proj = _contiguous_matrix(s.viewmatrix), _contiguous_matrix(s.projmatrix)
         sh_rest = None
         sh_input = sh  # the autograd input (with sh_split: the gradient carrier; its sink owner receives dL/dshs)
         if sh_split is not None:

@@ -89,6 +89,12 @@ SIGNATURES = {
         [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_i, ctypes.POINTER(ViewGrad), _c_p, _c_p,
          _c_p, _c_p, _c_p, _c_p, _c_p, ctypes.c_uint, _c_p, _c_i, _c_p],
     ),
+    # ABI v9: the per-Gaussian half for the Gaussians [first, first + count)
+    "gs_backward_gaussians_range": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_i, ctypes.POINTER(ViewGrad), _c_p,
+         _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, ctypes.c_uint, _c_p, _c_i, _c_p],
+    ),
     "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),
     "gs_knn_mean_dist2": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p]),

@@ -116,9 +116,9 @@ def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | N
         means3D, shs, opacity, scales, rotations = gs_train.render_inputs(model)
     else:
         means3D, shs, opacity, scales, rotations = model.torch_render_inputs()
-    # __init__.py:26 (zeros_like(...) + 0, then retain_grad): the same zero gradient carrier as a leaf,
-    # one fill launch instead of two
-    screenspace_points = torch.zeros_like(means3D, requires_grad=True)
+    # __init__.py:26 (zeros_like(...) + 0, then retain_grad): the screen-space gradient carrier as a
+    # leaf; the rasterizer never reads its values (only its .grad is written), so no fill launch
+    screenspace_points = torch.empty_like(means3D, requires_grad=True)
     image, radii = GaussianRasterizer(raster_settings=settings)(
         means3D=means3D, means2D=screenspace_points, shs=shs, colors_precomp=None, opacities=opacity, scales=scales,
         rotations=rotations, cov3D_precomp=None, sh_split=sh_split)

@@ -43,8 +43,14 @@ class GradBucket:
     the bucket (one memset) and every write accumulates.
     """
 
-    def __init__(self, params: Sequence[torch.Tensor], lazy_zero: bool = False, defer: bool = False):
+    def __init__(self, params: Sequence[torch.Tensor], lazy_zero: bool = False, defer: bool = False,
+                 chunks: int = 1):
         self.lazy_zero = lazy_zero
+        # chunks > 1 (with defer): allreduce() runs the deferred per-Gaussian pass in `chunks`
+        # Gaussian-row ranges and starts each range's all-reduce (its rows of every parameter) on a
+        # side stream as soon as that range is written, so the collective overlaps the pass
+        self.chunks = max(1, int(chunks))
+        self._comm = None
         # defer=True: a rasterizer backward whose parameter gradients all come here runs only its
         # per-tile half; the per-Gaussian half of all such views runs in ONE pass at finalize() /
         # allreduce() (gs_backward_gaussians): every Gaussian's inputs are read and its gradient
@@ -172,10 +178,9 @@ class GradBucket:
         sunk = [(name, t) for k, name, t, o in ctx.sinks if o is self and ctx.needs_input_grad[k] and k != 1]
         self._deferred.append((inputs, view, ev, sunk))
 
-    def flush(self):
-        """Run the pending views' per-Gaussian backward in one pass on the current stream."""
-        if not self._deferred:
-            return
+    def _claim_deferred(self):
+        """Join the pending views' streams and claim the outputs of their per-Gaussian pass:
+        (inputs, views, outs, accumulate bits)."""
         from diff_gaussian_rasterization import _C
 
         inputs = self._deferred[0][0]
@@ -191,12 +196,19 @@ class GradBucket:
                                    "the deferred backward ran")
             outs[name], accumulate = claim
             acc |= _C.GS_ACC[name] if accumulate else 0
-        views = [d[1] for d in self._deferred]
+        return inputs, [d[1] for d in self._deferred], outs, acc
+
+    def _deferred_pass(self, inputs, views, outs, acc, first=0, count=None):
+        from diff_gaussian_rasterization import _C
+
         _C.backward_gaussians(inputs["means3D"], inputs["sh"], inputs["colors"], inputs["scales"],
                               inputs["rotations"], inputs["cov3D"], inputs["scale_modifier"], inputs["degree"],
-                              views, outs, acc, debug=inputs["debug"])
+                              views, outs, acc, debug=inputs["debug"], first=first, count=count)
+
+    def _retire_deferred(self, inputs, views):
         # the views' buffers were allocated on their own streams: keep them out of reuse there until
         # this stream's pass is done
+        cur = torch.cuda.current_stream(self.flat.device)
         for v in views:
             for t in (v[0], v[1], v[2], v[7]):
                 if isinstance(t, torch.Tensor) and t.is_cuda:
@@ -207,13 +219,15 @@ class GradBucket:
         self.written(cur)
         self._deferred = []
 
-    def finalize(self):
-        """Run any deferred per-Gaussian backward, zero the views no backward wrote this step (lazy
-        mode); then the bucket holds the step's gradient sums (on the current stream: it waits for
-        the last write on any stream)."""
-        self._check_bound()
-        self.flush()
-        self._join()
+    def flush(self):
+        """Run the pending views' per-Gaussian backward in one pass on the current stream."""
+        if not self._deferred:
+            return
+        inputs, views, outs, acc = self._claim_deferred()
+        self._deferred_pass(inputs, views, outs, acc)
+        self._retire_deferred(inputs, views)
+
+    def _zero_unwritten(self):
         for p in self.params:
             ver = self._fresh.pop(id(p), None)
             if ver is not None:
@@ -222,12 +236,75 @@ class GradBucket:
                     raise RuntimeError("GradBucket(lazy_zero=True): a gradient view was accumulated into without "
                                        "a rasterizer write in the step")
                 v.zero_()
+
+    def finalize(self):
+        """Run any deferred per-Gaussian backward, zero the views no backward wrote this step (lazy
+        mode); then the bucket holds the step's gradient sums (on the current stream: it waits for
+        the last write on any stream)."""
+        self._check_bound()
+        self.flush()
+        self._join()
+        self._zero_unwritten()
         return self.flat
+
+    def _chunk_rows(self):
+        """Gaussian-row count of the chunked all-reduce, or None (every parameter must have the
+        deferred inputs' row count)."""
+        if self.chunks <= 1 or not self._deferred or not (dist.is_available() and dist.is_initialized()):
+            return None
+        P = self._deferred[0][0]["means3D"].shape[0]
+        if P < self.chunks or any(p.dim() == 0 or p.shape[0] != P for p in self.params):
+            return None
+        return P
+
+    def _allreduce_chunked(self, P, group):
+        """The deferred per-Gaussian pass in self.chunks row ranges on the current stream; after each
+        range, its rows of every parameter gradient are all-reduced on a side stream (one coalesced
+        group with RCCL), so the collectives overlap the remaining ranges' pass.  The current stream
+        then waits for every collective."""
+        self._check_bound()
+        inputs, views, outs, acc = self._claim_deferred()
+        self._zero_unwritten()  # views no backward writes this step, before any collective reads them
+        cur = torch.cuda.current_stream(self.flat.device)
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(self.flat.device)
+        comm = self._comm
+        coalesce = dist.get_backend(group) == "nccl"
+        bounds = [P * c // self.chunks for c in range(self.chunks + 1)]
+        works = []
+        for c in range(self.chunks):
+            b, e = bounds[c], bounds[c + 1]
+            self._deferred_pass(inputs, views, outs, acc, first=b, count=e - b)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            comm.wait_event(ev)
+            with torch.cuda.stream(comm):
+                rows = [p.grad[b:e] for p in self.params]
+                if coalesce:
+                    with dist._coalescing_manager(group, device=self.flat.device, async_ops=True) as cm:
+                        for t in rows:
+                            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+                    works.append(cm)
+                else:
+                    works += [dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True) for t in rows]
+        self._retire_deferred(inputs, views)
+        for w in works:
+            w.wait()  # the current stream waits for the collective
+        cur.wait_stream(comm)
+        self.written(cur)
 
     def allreduce(self, group=None, average: bool = False, async_op: bool = False):
         """Sum (or mean) the gradients across the process group in ONE collective over the flat
         bucket; the .grad views hold the result afterwards.  With a process group the collective is
-        issued at every world size (world 1: RCCL's in-place copy), so one code path runs at N = 1..8."""
+        issued at every world size (world 1: RCCL's in-place copy), so one code path runs at N = 1..8.
+        With chunks > 1 and a deferred pass pending, the all-reduce runs in row chunks overlapped with
+        that pass (same sums: every element is reduced once, in the same rank order)."""
+        P = self._chunk_rows()
+        if P is not None:
+            self._allreduce_chunked(P, group)
+            if average:
+                self.flat.div_(dist.get_world_size(group))
+            return None if async_op else self.flat
         flat = self.finalize()
         work = None
         if dist.is_available() and dist.is_initialized():

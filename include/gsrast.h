@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 8
+#define GSRAST_ABI_VERSION 9
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -219,6 +219,19 @@ int gs_backward_gaussians(int P, int D, int M, const float* means3D, const float
                           float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
                           float* dL_dscales, float* dL_drotations, unsigned accumulate, void* wait_event, int debug,
                           void* stream);
+
+/* gs_backward_gaussians_range (ABI v9): gs_backward_gaussians for the Gaussians [first, first +
+ *   count) of the P only (every pointer is the whole-array one; the views' geom buffers are laid
+ *   out for P).  A view-parallel step runs the per-Gaussian half in Gaussian-range chunks and
+ *   starts each chunk's gradient all-reduce as soon as that chunk is written (gs_view_parallel
+ *   GradBucket chunks); the union of the chunks equals one whole-range call, bit for
+ *   bit (every Gaussian's arithmetic is independent of the others). */
+int gs_backward_gaussians_range(int P, int first, int count, int D, int M, const float* means3D, const float* shs,
+                                const float* colors_precomp, const float* scales, float scale_modifier,
+                                const float* rotations, const float* cov3D_precomp, int num_views,
+                                const gs_view_grad* views, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                                float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                                unsigned accumulate, void* wait_event, int debug, void* stream);
 
 /* ---- mark_visible: present[P] (uint8 0/1), near-plane test ---- */
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

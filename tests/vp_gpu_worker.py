@@ -22,11 +22,11 @@ N_VIEWS, P, W, H = 8, 1_000_000, 1920, 1080
 NAMES = ("means3D", "shs", "opacities", "scales", "rotations")
 
 
-def render_views(d, cams, views, dev):
+def render_views(d, cams, views, dev, chunks=1):
     params = [d.means3D.clone().requires_grad_(True), d.shs.clone().requires_grad_(True),
               d.opacities.clone().requires_grad_(True), d.scales.clone().requires_grad_(True),
               d.rotations.clone().requires_grad_(True)]
-    bucket = vp.GradBucket(params, lazy_zero=True, defer=True)
+    bucket = vp.GradBucket(params, lazy_zero=True, defer=True, chunks=chunks)
     bucket.zero_grad()
     for v in views:
         rast = GaussianRasterizer(gs_scenes.raster_settings_for(cams[v], 3, device=dev))
@@ -45,10 +45,19 @@ def main():
     cams = gs_scenes.circle_cameras(N_VIEWS, 6.0, W, H)
     d = gs_scenes.random_gaussians(P, 3, seed=0, ball_radius=2.0).to(dev)
     mine = vp.shard_views(N_VIEWS, rank, world)
+    # the chunked all-reduce (per-Gaussian pass in 3 row ranges, each range's rows all-reduced as
+    # soon as they are written) must give the one-shot bucket's sums bit for bit
+    c_params, c_bucket = render_views(d, cams, mine, dev, chunks=3)
+    c_bucket.allreduce()
+    torch.cuda.synchronize()
+    chunk_flat = c_bucket.flat.clone()
+    c_bucket.close()
+    del c_params, c_bucket
     params, bucket = render_views(d, cams, mine, dev)
     ptrs = [p.grad.data_ptr() for p in params]
     bucket.allreduce()
     torch.cuda.synchronize()
+    chunked_equal = bool(torch.equal(chunk_flat, bucket.flat))
     msg = None
     if rank == 0:
         assert ptrs == [p.grad.data_ptr() for p in params]
@@ -62,9 +71,10 @@ def main():
             scale = float(ref.abs().max())
             bad = (got - ref).abs() > 1e-5 * ref.abs() + 1e-5 * scale
             nbad = int(bad.sum())
-            ok = ok and nbad == 0 and scale > 0
+            ok = ok and nbad == 0 and scale > 0 and chunked_equal
             lines.append(f"{name}: max|ref| {scale:.3e} max|d| {float((got - ref).abs().max()):.3e} beyond tol {nbad}")
-        msg = ("OK " if ok else "FAIL ") + f"views/rank {len(mine)}; " + "; ".join(lines)
+        msg = ("OK " if ok else "FAIL ") + f"views/rank {len(mine)}; chunked all-reduce equal {chunked_equal}; " + \
+            "; ".join(lines)
         with open(os.environ["GS_VP_OUT"], "w") as f:
             f.write(msg + "\n")
     dist.barrier()

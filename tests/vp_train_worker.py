@@ -120,12 +120,41 @@ def nccl1():
     got = run()
     dist.all_reduce = orig
     same = all(torch.equal(a, b) for a, b in zip(ref, got))
+    # the chunked all-reduce (RCCL coalesced groups per Gaussian-row range, on a side stream,
+    # overlapping the deferred per-Gaussian pass) against the bucket's one-shot finalize
+    chunk_same = chunked_vs_finalize(sc, settings, dev)
     backend = dist.get_backend()
     dist.destroy_process_group()
-    ok = same and len(calls) == 2 and backend == "nccl"
-    msg = ("OK " if ok else "FAIL ") + f"backend {backend}; all-reduces {len(calls)}; bitwise equal to no-group {same}"
+    ok = same and len(calls) == 2 and backend == "nccl" and chunk_same
+    msg = ("OK " if ok else "FAIL ") + (f"backend {backend}; all-reduces {len(calls)}; bitwise equal to no-group "
+                                        f"{same}; chunked all-reduce equal to finalize {chunk_same}")
     with open(os.environ["GS_VP_OUT"], "w") as f:
         f.write(msg + "\n")
+
+
+def chunked_vs_finalize(sc, settings, dev):
+    import gs_scenes
+    import gs_view_parallel as vp
+    from diff_gaussian_rasterization import GaussianRasterizer
+
+    d = sc.to(dev)
+
+    def run(chunks, reduce):
+        params = [t.clone().requires_grad_(True) for t in (d.means3D, d.shs, d.opacities, d.scales, d.rotations)]
+        b = vp.GradBucket(params, lazy_zero=True, defer=True, chunks=chunks)
+        b.zero_grad()
+        for v, s in enumerate(settings[:3]):
+            m2 = torch.empty_like(params[0], requires_grad=True)
+            img, _ = GaussianRasterizer(s)(means3D=params[0], means2D=m2, opacities=params[2], shs=params[1],
+                                           scales=params[3], rotations=params[4])
+            img.backward(gs_scenes.dl_dimage(H, W, seed=70 + v).to(dev))
+        b.allreduce() if reduce else b.finalize()
+        torch.cuda.synchronize()
+        out = b.flat.clone()
+        b.close()
+        return out
+
+    return bool(torch.equal(run(4, True), run(1, False)))
 
 
 if __name__ == "__main__":
