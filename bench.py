@@ -158,6 +158,9 @@ def main():
     ap.add_argument("--allreduce-chunks", type=int, default=4,
                     help="N > 1: the deferred per-Gaussian pass runs in this many Gaussian-row ranges and each "
                          "range's gradient rows are all-reduced (RCCL, side stream) as soon as they are written")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="skip the HIP-graph measurement (the same step with bounded binning buffers, captured "
+                         "once into a torch.cuda.CUDAGraph and replayed; N = 1)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, check the process group against --gpus, print one JSON line and exit "
                          "before any GPU work (tests of the launcher; GS_BENCH_BACKEND=gloo runs it on CPU)")
@@ -412,6 +415,12 @@ def main():
     if args.single_view_steps > 0 and world == 1:
         single = single_view_bench(bucket, rast, params, dpix, args.single_view_steps, lib)
 
+    # the same steps captured into HIP graphs (bounded binning buffers: no host wait in the forward)
+    graphs = None
+    if world == 1 and not args.no_graph:
+        graphs = graph_bench(bucket, rasts, params, dpix, streams, fused_front, step, args.steps,
+                             args.single_view_steps, len(my_views))
+
     ms_per_step = 1e3 * elapsed / args.steps
     # whole-job views (= reference train iterations) per second: weak scaling (C1-C3, C5) counts
     # every rank's views; a C4 step is the 8-view batch
@@ -510,6 +519,7 @@ def main():
         "render_ms": round(1e3 * t_render, 4),
         "render_batched": render_batched,
         "single_view": single,
+        "graph": graphs,
         "num_rendered": int(num_rendered),
         "walked_instances": walked,
         "visible": visible,
@@ -577,6 +587,97 @@ def single_view_bench(bucket, rast, params, dpix, steps, lib):
                     "stream, no deferral, no overlap between views",
             "iters_s": round(1.0 / dt, 2), "ms_per_iter": round(1e3 * dt, 4), "steps": steps,
             "kernel_us_per_iter": kern, "kernel_us_sum": round(sum(kern.values()), 1)}
+
+
+def graph_bench(bucket, rasts, params, dpix, streams, fused_front, eager_step, steps, sv_steps, k_views,
+                headroom=1.10):
+    """The timed step and the batch-1 step, each captured once into a HIP graph
+    (torch.cuda.CUDAGraph) and replayed.  Their forwards are bounded (binning_capacity = each
+    view's measured instance count x `headroom`): nothing in the step waits on the host, so the
+    whole step -- fused front, both streams, backwards, deferred per-Gaussian pass -- is one graph
+    launch.  The replays are checked bit for bit against the eager step, and the bounded status
+    (no view over its capacity) after the timed replays."""
+    from diff_gaussian_rasterization import bounded_status
+
+    # instance counts of the step's views (eager, read back) -> capacities
+    pre = prepare_views(rasts, params[0], params[2], shs=params[1], scales=params[3], rotations=params[4])
+    caps = [int(p.triple[0] * headroom) + 4096 for p in pre]
+    del pre
+    bounded_status()
+
+    def run_graph(fn, n_rep, ref_fn):
+        ref_fn()  # the eager (read-back) step: the reference bucket
+        torch.cuda.synchronize()
+        ref = bucket.flat.clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                fn()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        bucket.flat.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        same = bool(torch.equal(bucket.flat, ref))
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(n_rep):
+            g.replay()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / n_rep
+        del g
+        return dt, same
+
+    def step_bounded():
+        bucket.zero_grad()
+        if fused_front:
+            pv = prepare_views(rasts, params[0], params[2], shs=params[1], scales=params[3], rotations=params[4],
+                               streams=[streams[k % len(streams)] for k in range(len(rasts))], binning_capacity=caps)
+            fns = [(lambda r=r, p=p: _view_bwd(r, params, dpix, prepared=p)) for r, p in zip(rasts, pv)]
+        else:
+            fns = [(lambda r=r, c=c: _view_bwd(r, params, dpix, cap=c)) for r, c in zip(rasts, caps)]
+        vp.run_views(fns, streams)
+        bucket.finalize()
+
+    out = {"what": "the timed step and the batch-1 step as HIP graphs: bounded binning buffers (measured "
+                   f"instances x {headroom} + 4096), captured once, replayed",
+           "capacities": caps}
+    dt, same = run_graph(step_bounded, steps, eager_step)
+    out["step"] = {"iters_s": round(k_views / dt, 2), "ms_per_step": round(1e3 * dt, 4), "bitwise_equal_eager": same}
+    if sv_steps > 0:
+        defers = bucket.defers
+        bucket.defers = False
+
+        def sv(cap):
+            bucket.zero_grad()
+            _view_bwd(rasts[0], params, dpix, cap=cap)
+            bucket.finalize()
+
+        try:
+            dt1, same1 = run_graph(lambda: sv(caps[0]), sv_steps, lambda: sv(None))
+        finally:
+            bucket.defers = defers
+        out["single_view"] = {"iters_s": round(1.0 / dt1, 2), "ms_per_iter": round(1e3 * dt1, 4),
+                              "bitwise_equal_eager": same1}
+    try:
+        bounded_status()
+        out["capacity_exceeded"] = False
+    except RuntimeError as e:  # a view outgrew its capacity: the replays' results are invalid
+        out["capacity_exceeded"] = str(e)
+    return out
+
+
+def _view_bwd(r, params, dpix, prepared=None, cap=None):
+    m2 = torch.empty_like(params[0], requires_grad=True)
+    img, _ = r(means3D=params[0], means2D=m2, opacities=params[2], shs=params[1], scales=params[3],
+               rotations=params[4], prepared=prepared, binning_capacity=cap)
+    img.backward(dpix)
 
 
 def train_step_bench(sc, cam, deg, dev, steps, densify):

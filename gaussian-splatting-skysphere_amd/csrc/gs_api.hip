@@ -302,6 +302,9 @@ static uint32_t* order_flags_word() {
     for (int k = 0; k < 2; k++)
       if (!check_hip(hipEventCreateWithFlags(&o->ev[k], hipEventDisableTiming), "hipEventCreate")) return nullptr;
   }
+  // the render stores nonzero flags only: clear the word (its previous forward, two back, was checked
+  // when the one after it was queued)
+  o->host[16 * (o->seq & 1)] = 0u;
   return o->dev + 16 * (o->seq & 1);
 }
 // the render kernel that stores this forward's flags is queued on `st`: record its event, then
@@ -314,6 +317,46 @@ static bool queue_order_flags(hipStream_t st) {
   const bool failed = check_order_flags_locked(*o);
   o->pending = (long long)o->seq++;
   return failed;
+}
+
+// Status of bounded forwards (gs_forward_bounded), per device: pinned words the kernels store into
+// only when a view has error flags -- [0] the preprocess totals' flags (CounterFinalize) with [1], [2]
+// that view's instance count, [4] the ordering flags (render kernel) -- so no event, no host wait
+// and nothing per call (HIP-graph capturable).  gs_bounded_status reads and clears them.
+struct BoundedStatus {
+  std::mutex mu;
+  uint32_t* host = nullptr;
+  uint32_t* dev = nullptr;
+};
+static BoundedStatus g_bounded[64];
+static BoundedStatus* bounded_status() {
+  int dev = 0;
+  if (!check_hip(hipGetDevice(&dev), "hipGetDevice")) return nullptr;
+  if (dev < 0 || dev >= 64) return set_error("device ordinal out of range"), nullptr;
+  BoundedStatus& b = g_bounded[dev];
+  std::lock_guard<std::mutex> lk(b.mu);
+  if (!b.host && !mapped_words(64, &b.host, &b.dev)) return nullptr;
+  return &b;
+}
+// flags of the bounded forwards since the last read (0: none), and the instance count of a view that
+// raised them; clears them
+static uint32_t take_bounded_status(BoundedStatus* b, long long* instances) {
+  std::lock_guard<std::mutex> lk(b->mu);
+  volatile uint32_t* w = b->host;
+  const uint32_t f = w[0] | w[4];
+  if (instances) *instances = f ? (long long)((unsigned long long)w[2] << 32 | w[1]) : 0;
+  if (f) w[0] = 0u, w[1] = 0u, w[2] = 0u, w[4] = 0u;
+  return f;
+}
+static bool bounded_status_error(uint32_t f, long long inst) {
+  if (f & ERR_PREFILTERED) return set_error("Point is filtered although prefiltered is set. This shouldn't happen!"), true;
+  if (f & (ERR_CAPACITY | ERR_INSTANCES))
+    return set_error("bounded forward: a view had %lld (Gaussian, tile) instances, more than its binning capacity "
+                     "(its image and gradients are invalid; rerun with a larger capacity)", inst), true;
+  if (f & ERR_LOOKBACK)
+    return set_error("bounded forward: a look-back wait of the offsets scan or a one-sweep sort timed out "
+                     "(the instance list of that forward is invalid)"), true;
+  return false;
 }
 
 // split SH inputs (features_dc + features_rest rows): shs_rest needs SH colours with M >= 2
@@ -386,21 +429,35 @@ int gs_forward_preprocess_split(int P, int D, int M, const float* background, in
                                  tan_fovy, prefiltered, radii_out, geom_buffer, num_rendered_host, debug, stream);
 }
 
-int gs_forward_preprocess_views(int K, int P, int D, int M, const float* const* background, const int* image_width,
-                                const int* image_height, const float* means3D, const float* shs,
-                                const float* colors_precomp, const float* opacities, const float* scales,
-                                float scale_modifier, const float* rotations, const float* cov3D_precomp,
-                                const float* const* viewmatrix, const float* const* projmatrix,
-                                const float* const* campos, const float* tan_fovx, const float* tan_fovy,
-                                int prefiltered, int* const* radii_out, void* const* geom_buffer,
-                                long long* num_rendered_host, int debug, void* stream, void* const* view_streams) {
+// The K views' depth sorts as one set of launches (contiguous geometry buffers); GSRAST_BATCH_VIEWS=0
+// in the environment runs them view by view on the views' streams (A/B runs; the Python layer then
+// also bins the views one by one)
+static bool batch_views() {
+  static const bool on = [] {
+    const char* e = getenv("GSRAST_BATCH_VIEWS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// capacity (bounded, gs_forward_preprocess_views_bounded): per-view binning capacities; the counts
+// are not read back (num_rendered_host unused), a view over its capacity leaves the sticky flag
+static int preprocess_views_impl(int K, int P, int D, int M, const float* const* background, const int* image_width,
+                                 const int* image_height, const float* means3D, const float* shs,
+                                 const float* colors_precomp, const float* opacities, const float* scales,
+                                 float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                 const float* const* viewmatrix, const float* const* projmatrix,
+                                 const float* const* campos, const float* tan_fovx, const float* tan_fovy,
+                                 int prefiltered, int* const* radii_out, void* const* geom_buffer,
+                                 long long* num_rendered_host, const long long* capacity, int debug, void* stream,
+                                 void* const* view_streams) {
   clear_error(debug);
   if (K <= 0 || K > FUSED_MAX_VIEWS) return set_error("views: 1 to 8 per call"), 1;
   if (!background || !image_width || !image_height || !viewmatrix || !projmatrix || !campos || !tan_fovx ||
-      !tan_fovy || !radii_out || !geom_buffer || !num_rendered_host)
+      !tan_fovy || !radii_out || !geom_buffer || (!num_rendered_host && !capacity))
     return set_error("missing per-view argument array"), 1;
   for (int v = 0; v < K; v++) {
-    num_rendered_host[v] = 0;
+    if (num_rendered_host) num_rendered_host[v] = 0;
+    if (capacity && (capacity[v] < 0 || capacity[v] > GS_MAX_INSTANCES)) return set_error("capacity out of range"), 1;
     if (!validate(P, D, M, image_width[v], image_height[v], means3D, shs, colors_precomp, opacities, scales, rotations,
                   cov3D_precomp, viewmatrix[v], projmatrix[v], campos[v], background[v]))
       return 1;
@@ -417,31 +474,100 @@ int gs_forward_preprocess_views(int K, int P, int D, int M, const float* const* 
     pv.radii[v] = radii_out[v];
     geom_layout((size_t)P, &pv.geo[v], (char*)geom_buffer[v]);
   }
-  ReadbackSlot* rb = readback_slot();
-  if (!rb) return 1;
-  static thread_local hipEvent_t ev_pre = nullptr;
-  if (!ev_pre && !check_hip(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming), "hipEventCreate")) return 1;
-  if (check_order_flags()) return 1;  // an earlier forward's look-back waits
-  fwd_preprocess_views(g, pv, st);
-  // each view's ordering on its own stream (view_streams[v], or `stream`), after the preprocess;
-  // its first histogram launch stores the view's totals into readback words [8 v, 8 v + 4)
-  check_hip(hipEventRecord(ev_pre, st), "hipEventRecord");
-  for (int v = 0; v < K; v++) {
-    hipStream_t vs = view_streams && view_streams[v] ? (hipStream_t)view_streams[v] : st;
-    if (vs != st) check_hip(hipStreamWaitEvent(vs, ev_pre, 0), "hipStreamWaitEvent");
-    fwd_order(P, pv.geo[v], vs, rb->dev + 8 * v, rb->ev[v]);
+  // (bounded: no readback slot, the views' flags go to the sticky words)
+  ReadbackSlot* rb = capacity ? nullptr : readback_slot();
+  if (!capacity && !rb) return 1;
+  BoundedStatus* bs = capacity ? bounded_status() : nullptr;
+  if (capacity && !bs) return 1;
+  if (bs) {
+    long long inst = 0;
+    if (bounded_status_error(take_bounded_status(bs, &inst), inst)) return 1;  // an earlier bounded forward
   }
-  for (int v = 0; v < K; v++) check_hip(hipEventSynchronize(rb->ev[v]), "hipEventSynchronize");
+  // one fork event per thread and slot of a ring: a captured step may hold several forks
+  static thread_local hipEvent_t ev_pre[4] = {};
+  static thread_local unsigned ev_next = 0;
+  hipEvent_t& fork = ev_pre[ev_next++ & 3];
+  if (!fork && !check_hip(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "hipEventCreate")) return 1;
+  if (!capacity && check_order_flags()) return 1;  // an earlier forward's look-back waits
+  uint32_t cap32[FUSED_MAX_VIEWS];
+  for (int v = 0; v < K; v++) cap32[v] = capacity ? (uint32_t)capacity[v] : 0xFFFFFFFFu;
+  // geometry buffers at one stride (slices of one allocation, as prepare_views makes them): the K
+  // orderings run as one set of launches on `stream` (blockIdx.y = view), every view's totals
+  // stored by the first histogram launch into readback words [8 v, 8 v + 4)
+  const ptrdiff_t vstride = K > 1 ? (char*)geom_buffer[1] - (char*)geom_buffer[0] : 0;
+  bool batched = batch_views() && K > 1 && vstride >= (ptrdiff_t)gs_geom_buffer_bytes(P) && vstride % 256 == 0;
+  for (int v = 2; v < K && batched; v++) batched = (char*)geom_buffer[v] == (char*)geom_buffer[0] + v * vstride;
+  fwd_preprocess_views(g, pv, st);
+  if (batched) {
+    fwd_order(P, pv.geo[0], st, capacity ? nullptr : rb->dev, capacity ? nullptr : rb->ev[0], cap32,
+              capacity ? bs->dev : nullptr, K, (uint64_t)vstride);
+    // the views' later kernels run on their streams, after the orderings
+    check_hip(hipEventRecord(fork, st), "hipEventRecord");
+    for (int v = 0; v < K; v++) {
+      hipStream_t vs = view_streams && view_streams[v] ? (hipStream_t)view_streams[v] : st;
+      if (vs != st) check_hip(hipStreamWaitEvent(vs, fork, 0), "hipStreamWaitEvent");
+    }
+  } else {
+    // each view's ordering on its own stream (view_streams[v], or `stream`), after the preprocess
+    check_hip(hipEventRecord(fork, st), "hipEventRecord");
+    for (int v = 0; v < K; v++) {
+      hipStream_t vs = view_streams && view_streams[v] ? (hipStream_t)view_streams[v] : st;
+      if (vs != st) check_hip(hipStreamWaitEvent(vs, fork, 0), "hipStreamWaitEvent");
+      if (capacity)
+        fwd_order(P, pv.geo[v], vs, nullptr, nullptr, &cap32[v], bs->dev);
+      else
+        fwd_order(P, pv.geo[v], vs, rb->dev + 8 * v, rb->ev[v]);
+    }
+  }
+  if (capacity) return t_failed ? 1 : 0;
+  for (int v = 0; v < (batched ? 1 : K); v++) check_hip(hipEventSynchronize(rb->ev[v]), "hipEventSynchronize");
   if (t_failed) return 1;
   for (int v = 0; v < K; v++)
     if (!read_view_totals(rb->host + 8 * v, v, K, &num_rendered_host[v])) return 1;
   return 0;
 }
 
-int gs_forward_render(int P, const float* background, int W, int H, const float* viewmatrix, const float* projmatrix,
-                      const float* campos, float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
-                      long long num_rendered, void* binning_buffer, void* image_buffer, float* out_color, int debug,
-                      void* stream) {
+int gs_forward_preprocess_views(int K, int P, int D, int M, const float* const* background, const int* image_width,
+                                const int* image_height, const float* means3D, const float* shs,
+                                const float* colors_precomp, const float* opacities, const float* scales,
+                                float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                const float* const* viewmatrix, const float* const* projmatrix,
+                                const float* const* campos, const float* tan_fovx, const float* tan_fovy,
+                                int prefiltered, int* const* radii_out, void* const* geom_buffer,
+                                long long* num_rendered_host, int debug, void* stream, void* const* view_streams) {
+  if (!num_rendered_host) {
+    clear_error(debug);
+    return set_error("missing per-view argument array"), 1;
+  }
+  return preprocess_views_impl(K, P, D, M, background, image_width, image_height, means3D, shs, colors_precomp,
+                               opacities, scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix,
+                               campos, tan_fovx, tan_fovy, prefiltered, radii_out, geom_buffer, num_rendered_host,
+                               nullptr, debug, stream, view_streams);
+}
+
+int gs_forward_preprocess_views_bounded(int K, int P, int D, int M, const float* const* background,
+                                        const int* image_width, const int* image_height, const float* means3D,
+                                        const float* shs, const float* colors_precomp, const float* opacities,
+                                        const float* scales, float scale_modifier, const float* rotations,
+                                        const float* cov3D_precomp, const float* const* viewmatrix,
+                                        const float* const* projmatrix, const float* const* campos,
+                                        const float* tan_fovx, const float* tan_fovy, int prefiltered,
+                                        int* const* radii_out, void* const* geom_buffer, const long long* capacity,
+                                        int debug, void* stream, void* const* view_streams) {
+  if (!capacity) {
+    clear_error(debug);
+    return set_error("missing capacity array"), 1;
+  }
+  return preprocess_views_impl(K, P, D, M, background, image_width, image_height, means3D, shs, colors_precomp,
+                               opacities, scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix,
+                               campos, tan_fovx, tan_fovy, prefiltered, radii_out, geom_buffer, nullptr, capacity,
+                               debug, stream, view_streams);
+}
+
+static int forward_render_impl(int P, const float* background, int W, int H, const float* viewmatrix,
+                               const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                               const int* radii, void* geom_buffer, long long num_rendered, void* binning_buffer,
+                               void* image_buffer, float* out_color, bool bounded, int debug, void* stream) {
   clear_error(debug);
   if (P <= 0) return 0;
   if (W <= 0 || H <= 0) return set_error("image size must be positive"), 1;
@@ -460,12 +586,151 @@ int gs_forward_render(int P, const float* background, int W, int H, const float*
   // the waited-for workgroups are running) leave ERR_LOOKBACK; the render kernel stores the flags
   // into pinned memory, behind an event that the next backward or forward call checks, so no host
   // wait idles the device
-  uint32_t* flags_word = order_flags_word();
+  // (bounded: the sticky word, nothing recorded or checked here)
+  BoundedStatus* bs = bounded ? bounded_status() : nullptr;
+  uint32_t* flags_word = bounded ? (bs ? bs->dev + 4 : nullptr) : order_flags_word();
   if (!flags_word) return 1;
   fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
   fwd_render(c, geo, bin, img, out_color, st, flags_word);
-  if (!t_failed && queue_order_flags(st)) return 1;
+  if (!bounded && !t_failed && queue_order_flags(st)) return 1;
   return t_failed ? 1 : 0;
+}
+
+int gs_forward_bin_views(int K, int P, int W, int H, void* const* geom_buffer, const long long* num_rendered,
+                         void* const* binning_buffer, void* const* image_buffer, int debug, void* stream,
+                         void* const* view_streams) {
+  clear_error(debug);
+  if (K <= 0 || K > FUSED_MAX_VIEWS) return set_error("views: 1 to 8 per call"), 1;
+  if (P < 0) return set_error("P must be >= 0"), 1;
+  if (W <= 0 || H <= 0) return set_error("image size must be positive"), 1;
+  if (!geom_buffer || !num_rendered || !binning_buffer || !image_buffer) return set_error("missing per-view array"), 1;
+  if (P == 0) return 0;
+  long long I = 0;
+  for (int v = 0; v < K; v++) {
+    if (!geom_buffer[v] || !binning_buffer[v] || !image_buffer[v]) return set_error("view %d: missing buffer", v), 1;
+    if (num_rendered[v] < 0 || num_rendered[v] > GS_MAX_INSTANCES) return set_error("num_rendered out of range"), 1;
+    I = num_rendered[v] > I ? num_rendered[v] : I;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  CameraArgs c = make_camera(nullptr, W, H, nullptr, nullptr, nullptr, 1.0f, 1.0f, 0);
+  // every view's buffers at one stride per kind (slices of one allocation each)
+  auto stride_of = [&](void* const* b, size_t min_bytes, uint64_t* out) {
+    const ptrdiff_t d = K > 1 ? (char*)b[1] - (char*)b[0] : 0;
+    if (K > 1 && (d < (ptrdiff_t)min_bytes || d % 256 != 0)) return false;
+    for (int v = 2; v < K; v++)
+      if ((char*)b[v] != (char*)b[0] + v * d) return false;
+    *out = (uint64_t)d;
+    return true;
+  };
+  uint64_t gs = 0, bs = 0, is = 0;
+  if (!stride_of(geom_buffer, gs_geom_buffer_bytes(P), &gs) ||
+      !stride_of(binning_buffer, gs_binning_buffer_bytes(I, W, H), &bs) ||
+      !stride_of(image_buffer, gs_image_buffer_bytes(W, H), &is))
+    return set_error("bin_views: each kind of buffer must be K slices of one allocation, one stride apart, each "
+                     "sized for the largest num_rendered"), 1;
+  GeomPtrs geo;
+  BinPtrs bin;
+  ImgPtrs img;
+  geom_layout((size_t)P, &geo, (char*)geom_buffer[0]);
+  bin_layout((size_t)I, c.gx * c.gy, &bin, (char*)binning_buffer[0]);
+  img_layout(W, H, &img, (char*)image_buffer[0]);
+  fwd_bin_views(K, P, (uint32_t)I, c, geo, bin, img, gs, bs, is, st);
+  // the views' renders run on their streams, after the binning
+  static thread_local hipEvent_t ev_bin[4] = {};
+  static thread_local unsigned ev_next = 0;
+  hipEvent_t& done = ev_bin[ev_next++ & 3];
+  if (!done && !check_hip(hipEventCreateWithFlags(&done, hipEventDisableTiming), "hipEventCreate")) return 1;
+  check_hip(hipEventRecord(done, st), "hipEventRecord");
+  for (int v = 0; v < K; v++) {
+    hipStream_t vs = view_streams && view_streams[v] ? (hipStream_t)view_streams[v] : st;
+    if (vs != st) check_hip(hipStreamWaitEvent(vs, done, 0), "hipStreamWaitEvent");
+  }
+  return t_failed ? 1 : 0;
+}
+
+int gs_forward_render_binned(int P, const float* background, int W, int H, const float* viewmatrix,
+                             const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                             void* geom_buffer, long long num_rendered, void* binning_buffer, void* image_buffer,
+                             float* out_color, int bounded, int debug, void* stream) {
+  clear_error(debug);
+  if (P <= 0) return 0;
+  if (W <= 0 || H <= 0) return set_error("image size must be positive"), 1;
+  if (num_rendered < 0 || num_rendered > GS_MAX_INSTANCES) return set_error("num_rendered out of range"), 1;
+  if (!geom_buffer || !binning_buffer || !image_buffer || !out_color) return set_error("missing buffer pointer"), 1;
+  hipStream_t st = (hipStream_t)stream;
+  CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, 0);
+  GeomPtrs geo;
+  BinPtrs bin;
+  ImgPtrs img;
+  geom_layout((size_t)P, &geo, (char*)geom_buffer);
+  bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer);
+  img_layout(W, H, &img, (char*)image_buffer);
+  BoundedStatus* bst = bounded ? bounded_status() : nullptr;
+  uint32_t* flags_word = bounded ? (bst ? bst->dev + 4 : nullptr) : order_flags_word();
+  if (!flags_word) return 1;
+  fwd_render(c, geo, bin, img, out_color, st, flags_word);
+  if (!bounded && !t_failed && queue_order_flags(st)) return 1;
+  return t_failed ? 1 : 0;
+}
+
+int gs_forward_render(int P, const float* background, int W, int H, const float* viewmatrix, const float* projmatrix,
+                      const float* campos, float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
+                      long long num_rendered, void* binning_buffer, void* image_buffer, float* out_color, int debug,
+                      void* stream) {
+  return forward_render_impl(P, background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii,
+                             geom_buffer, num_rendered, binning_buffer, image_buffer, out_color, false, debug, stream);
+}
+
+int gs_forward_render_bounded(int P, const float* background, int W, int H, const float* viewmatrix,
+                              const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                              const int* radii, void* geom_buffer, long long capacity, void* binning_buffer,
+                              void* image_buffer, float* out_color, int debug, void* stream) {
+  return forward_render_impl(P, background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii,
+                             geom_buffer, capacity, binning_buffer, image_buffer, out_color, true, debug, stream);
+}
+
+int gs_forward_bounded(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                       const float* shs, const float* shs_rest, const float* colors_precomp, const float* opacities,
+                       const float* scales, float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                       const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                       float tan_fovy, int prefiltered, int* radii_out, void* geom_buffer, long long capacity,
+                       void* binning_buffer, void* image_buffer, float* out_color, int debug, void* stream) {
+  clear_error(debug);
+  if (!validate(P, D, M, W, H, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, viewmatrix,
+                projmatrix, campos, background))
+    return 1;
+  if (!validate_split(M, shs, shs_rest, colors_precomp)) return 1;
+  if (P == 0) return 0;
+  if (capacity < 0 || capacity > GS_MAX_INSTANCES) return set_error("capacity out of range"), 1;
+  if (!radii_out || !geom_buffer || !binning_buffer || !image_buffer || !out_color)
+    return set_error("missing buffer pointer"), 1;
+  BoundedStatus* bs = bounded_status();
+  if (!bs) return 1;
+  long long inst = 0;
+  if (bounded_status_error(take_bounded_status(bs, &inst), inst)) return 1;  // an earlier bounded forward
+  hipStream_t st = (hipStream_t)stream;
+  GeomPtrs geo;
+  geom_layout((size_t)P, &geo, (char*)geom_buffer);
+  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier,
+                 shs_rest};
+  CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, prefiltered);
+  fwd_preprocess(g, c, radii_out, geo, st);
+  const uint32_t cap32 = (uint32_t)capacity;
+  fwd_order(P, geo, st, nullptr, nullptr, &cap32, bs->dev);
+  if (t_failed) return 1;
+  return forward_render_impl(P, background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii_out,
+                             geom_buffer, capacity, binning_buffer, image_buffer, out_color, true, debug, stream);
+}
+
+int gs_bounded_status(unsigned* flags, long long* instances) {
+  clear_error(0);
+  BoundedStatus* bs = bounded_status();
+  if (!bs) return 1;
+  long long inst = 0;
+  const uint32_t f = take_bounded_status(bs, &inst);
+  if (flags) *flags = f;
+  if (instances) *instances = inst;
+  return bounded_status_error(f, inst) ? 1 : 0;
 }
 
 long long gs_rasterize_forward(int P, int D, int M, const float* background, int W, int H, const float* means3D,

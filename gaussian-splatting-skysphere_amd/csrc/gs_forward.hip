@@ -356,8 +356,15 @@ struct CounterFinalize {
   const WgTotals* wg;
   uint32_t nwg;
   uint32_t* counters;
-  uint32_t* host;
-  __device__ void operator()() const {
+  uint32_t* host;    // view v's words at host + 8 v
+  uint32_t* sticky;  // pinned host words for a view with error flags (gs_forward_bounded), or null
+  uint64_t vstride;  // bytes between the views' geometry buffers (batched launch)
+  uint32_t cap[FUSED_MAX_VIEWS];  // the views' binning capacities
+  __device__ void operator()(uint32_t v) const {
+    const WgTotals* wg = vptr(this->wg, vstride);
+    uint32_t* counters = vptr(this->counters, vstride);
+    uint32_t* host = this->host ? this->host + 8 * v : nullptr;
+    const uint32_t cap = this->cap[v];
     __shared__ uint32_t s_lo[4], s_hi[4], s_v[4], s_e[4];
     unsigned long long si = 0;
     uint32_t sv = 0, se = 0;
@@ -388,7 +395,8 @@ struct CounterFinalize {
         V += s_v[k];
         e |= s_e[k];
       }
-      const uint32_t err = (e ? ERR_PREFILTERED : 0u) | (I > (unsigned long long)GS_MAX_INSTANCES ? ERR_INSTANCES : 0u);
+      const uint32_t err = (e ? ERR_PREFILTERED : 0u) | (I > (unsigned long long)GS_MAX_INSTANCES ? ERR_INSTANCES : 0u) |
+                           (I > (unsigned long long)cap ? ERR_CAPACITY : 0u);
       counters[CNT_NREND] = (uint32_t)I;
       counters[CNT_V] = V;
       counters[CNT_ERR] = err;
@@ -400,38 +408,61 @@ struct CounterFinalize {
         host[2] = V;
         host[3] = err;
       }
+      if (sticky && err) {
+        sticky[0] = err;
+        sticky[1] = (uint32_t)I;
+        sticky[2] = (uint32_t)(I >> 32);
+      }
     }
   }
 };
 
-void fwd_order(int P, const GeomPtrs& geo, hipStream_t st, uint32_t* host_counts, hipEvent_t counts_ready) {
+void fwd_scan(int P, const GeomPtrs& geo, hipStream_t st);
+
+void fwd_order(int P, const GeomPtrs& geo, hipStream_t st, uint32_t* host_counts, hipEvent_t counts_ready,
+               const uint32_t* cap, uint32_t* sticky, int views, uint64_t vstride) {
   const uint32_t n = (uint32_t)P;
-  // the first depth-sort pass's counts, with the view's totals finalised by block 0 (the host
-  // waits for this launch only: the rest of the ordering overlaps its readback)
+  // the first depth-sort pass's counts, with each view's totals finalised by an extra workgroup
+  // (the host waits for this launch only: the rest of the ordering overlaps its readback)
   const SortPlan sp = sort_plan(n, GS_DEPTH_SORT_BLOCKS);
-  GS_LAUNCH("radix_hist", k_radix_hist<CounterFinalize>, dim3(sp.nb + 1), dim3(SORT_THREADS), 0, st, geo.keys_a, nullptr,
-            n, 0, radix_first_bits(32), sp.chunk, sp.nb, geo.sort_scratch, true,
-            CounterFinalize{geo.wg_tot, (n + 255) / 256, geo.counters, host_counts});
+  CounterFinalize fin{geo.wg_tot, (n + 255) / 256, geo.counters, host_counts, sticky, vstride, {}};
+  for (int v = 0; v < FUSED_MAX_VIEWS; v++) fin.cap[v] = cap && v < views ? cap[v] : 0xFFFFFFFFu;
+  GS_LAUNCH("radix_hist", k_radix_hist<CounterFinalize>, dim3(sp.nb + 1, views), dim3(SORT_THREADS), 0, st,
+            geo.keys_a, nullptr, n, 0, radix_first_bits(32), sp.chunk, sp.nb, geo.sort_scratch, true, vstride, fin);
   if (counts_ready) (void)hipEventRecord(counts_ready, st);
   // depth sort of the Gaussians with instances: the first pass reads all P keys in index order
-  // and drops the DEPTH_DROP ones (compaction), the later passes sort the V survivors.
+  // and drops the DEPTH_DROP ones (compaction), the later passes sort the V survivors; every
+  // view's passes in one set of launches (blockIdx.y = view)
   if (lb_tiles(n) <= LB_STATIC_MAX) {
-    // up to 1M Gaussians: the offsets scan is one look-back launch whose grid is resident (static
-    // tile ids); it gathers each rank's tile count (the gather is cheaper here than carrying the
-    // counts through the four sort passes)
     radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
                      geo.sort_scratch, st, /*drop_first=*/true, /*hist0_ready=*/true, nullptr, nullptr, nullptr,
-                     nullptr, GS_DEPTH_SORT_BLOCKS);
-    scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid, n}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
-                      &geo.counters[CNT_V], n, geo.lb_status, &geo.counters[CNT_LB_TILE], &geo.counters[CNT_I],
-                      &geo.counters[CNT_ERR], st);
+                     nullptr, GS_DEPTH_SORT_BLOCKS, views, vstride);
   } else {
     // larger scenes: the tile counts travel with the keys through the sort (read in index order by
     // the first pass), and the 3-launch scan reads them in depth order, coalesced (C5, 5M: the
     // per-rank gather and the ticketed look-back took 197 us)
     radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
                      geo.sort_scratch, st, /*drop_first=*/true, /*hist0_ready=*/true, geo.tiles, geo.rtiles_a,
-                     geo.rtiles_b, nullptr, GS_DEPTH_SORT_BLOCKS);
+                     geo.rtiles_b, nullptr, GS_DEPTH_SORT_BLOCKS, views, vstride);
+  }
+  for (int v = 0; v < views; v++) {
+    GeomPtrs g = geo;
+    if (v) geom_layout((size_t)P, &g, (char*)geo.splat + (uint64_t)v * vstride);
+    fwd_scan(P, g, st);
+  }
+}
+
+// instance offsets in depth order (+ the duplicate's block owner table), after the depth sort
+void fwd_scan(int P, const GeomPtrs& geo, hipStream_t st) {
+  const uint32_t n = (uint32_t)P;
+  if (lb_tiles(n) <= LB_STATIC_MAX) {
+    // up to 1M Gaussians: one look-back launch whose grid is resident (static tile ids); it
+    // gathers each rank's tile count (cheaper here than carrying the counts through the four sort
+    // passes)
+    scan_exclusive_lb(SrcTilesByRank{geo.tiles, geo.sorted_gid, n}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
+                      &geo.counters[CNT_V], n, geo.lb_status, &geo.counters[CNT_LB_TILE], &geo.counters[CNT_I],
+                      &geo.counters[CNT_ERR], st);
+  } else {
     scan_exclusive(SrcArray{geo.tiles_by_rank}, DstOffsets{geo.offsets, geo.dup_first, geo.counters, n},
                    &geo.counters[CNT_V], n, geo.scan_partial, &geo.counters[CNT_I], st);
   }
@@ -455,7 +486,7 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, const uint32_t* _
                                                    uint32_t* __restrict__ tile_keys,
                                                    uint32_t* __restrict__ presort_gid) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-  if (s >= P || s >= counters[CNT_V] || (counters[CNT_ERR] & 4u)) return;  // (timed-out sort: write nothing)
+  if (s >= P || s >= counters[CNT_V] || (counters[CNT_ERR] & ERR_INVALID)) return;  // (invalid list: write nothing)
   const uint32_t gid = sorted_gid[s];
   uint32_t off = offsets[s];
   // (a timed-out offsets scan only under-estimates offsets: every write stays below I)
@@ -484,11 +515,17 @@ constexpr int DUP_ITEMS = DUP_SLOTS / DUP_THREADS;
 // 8 consecutive slots on distinct banks
 __device__ __forceinline__ uint32_t own_idx(uint32_t i) { return i + (i >> 3); }
 
+// Views (blockIdx.y): view v's geometry / binning / image arrays lie v * gs / bs / is bytes further.
 __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     uint32_t I, const uint32_t* __restrict__ counters, const uint32_t* __restrict__ dup_first,
     const uint32_t* __restrict__ sorted_gid, const uint32_t* __restrict__ offsets,
     const float4* __restrict__ binrec, int gx, int gy, uint32_t* __restrict__ tile_keys,
-    uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges, uint32_t* __restrict__ hist0, uint32_t mask0) {
+    uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges, uint32_t* __restrict__ hist0, uint32_t mask0,
+    uint32_t* __restrict__ n_copy, uint64_t gs, uint64_t bs, uint64_t is) {
+  counters = vptr(counters, gs), dup_first = vptr(dup_first, gs), sorted_gid = vptr(sorted_gid, gs);
+  offsets = vptr(offsets, gs), binrec = vptr(binrec, gs);
+  tile_keys = vptr(tile_keys, bs), presort_gid = vptr(presort_gid, bs), hist0 = vptr(hist0, bs);
+  n_copy = vptr(n_copy, bs), ranges = vptr(ranges, is);
   __shared__ uint32_t s_own[DUP_SLOTS + DUP_SLOTS / 8];  // (slot + 1) << 16 | segment at segment starts
   // per row segment: (tile id of its first slot) - (that slot), mod 2^32 (the slot may precede the
   // block), so slot k of the segment has key base + k; one table instead of two keeps the LDS at
@@ -503,12 +540,15 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   const uint32_t tiles = (uint32_t)(gx * gy);
   for (uint32_t t = b * DUP_THREADS + tid; t < tiles; t += gridDim.x * DUP_THREADS) ranges[t] = make_uint2(0u, 0u);
   const uint32_t V = counters[CNT_V];
+  // I: the binning buffer's capacity (= the count, unless the buffer was sized ahead of it)
+  I = min(I, counters[CNT_NREND]);
+  if (b == 0 && tid == 0) n_copy[0] = I;  // for the tile sort and k_ranges (kernels after this one)
   const uint32_t k0 = b * DUP_SLOTS;
-  const uint32_t k1 = min(k0 + DUP_SLOTS, I);
-  if (counters[CNT_ERR] & 4u) {
-    // a look-back wait of the depth sort or the offsets scan timed out (the host raises at its next
-    // call): the owner table is not valid, so fill the block's slots with a safe placeholder --
-    // tile 0, Gaussian 0 -- that keeps every later kernel in bounds instead of following it
+  const uint32_t k1 = k0 < I ? min(k0 + DUP_SLOTS, I) : k0;
+  if (counters[CNT_ERR] & ERR_INVALID) {
+    // a look-back wait of the depth sort or the offsets scan timed out, or the instances exceed the
+    // buffer (the host raises at its next call): the owner table is not valid, so fill the block's
+    // slots with a safe placeholder -- tile 0, Gaussian 0 -- that keeps every later kernel in bounds
     const uint32_t g0 = 0u;
     for (uint32_t k = k0 + tid; k < k1; k += DUP_THREADS) {
       tile_keys[k] = 0u;
@@ -517,6 +557,10 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     if (hist0) {
       hist0[(size_t)tid * gridDim.x + b] = tid == 0 ? k1 - k0 : 0u;
     }
+    return;
+  }
+  if (k1 == k0) {  // past the count (a buffer sized ahead of it): no slots
+    if (hist0) hist0[(size_t)tid * gridDim.x + b] = 0u;
     return;
   }
   const uint32_t s_lo = dup_first[b];
@@ -593,10 +637,14 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
 }
 
 // tile ranges over the sorted instance list, 4 instances per lane
-__global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __restrict__ tile, uint2* __restrict__ ranges,
-                                                uint32_t* __restrict__ sched, uint32_t sched_words, uint32_t tiles) {
+__global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __restrict__ n_dev,
+                                                const uint32_t* __restrict__ tile, uint2* __restrict__ ranges,
+                                                uint32_t* __restrict__ sched, uint32_t sched_words, uint32_t tiles,
+                                                uint64_t bs, uint64_t is) {
+  n_dev = vptr(n_dev, bs), tile = vptr(tile, bs), ranges = vptr(ranges, is), sched = vptr(sched, is);
   // clear the render's per-tile completion counters and length buckets (k_render_fwd* epilogue)
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sched_words; i += gridDim.x * 256) sched[i] = 0u;
+  I = min(I, *n_dev);  // the capacity I, or the count when below it
   const uint32_t k0 = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (k0 >= I) return;
   uint32_t t[6];
@@ -624,34 +672,55 @@ __global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __re
 
 void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const GeomPtrs& geo, const BinPtrs& bin,
              const ImgPtrs& img, hipStream_t st) {
+  (void)radii;
+  fwd_bin_views(1, P, I, c, geo, bin, img, 0, 0, 0, st);
+}
+
+void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
+                   const ImgPtrs& img, uint64_t gs, uint64_t bs, uint64_t is, hipStream_t st) {
   const int tiles = c.gx * c.gy;
-  if (I == 0) {
-    (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
-    (void)hipMemsetAsync(img.tile_done, 0,
-                         sizeof(uint64_t) * (size_t)tiles + sizeof(uint32_t) * (ORDER_GROUPS * ORDER_BUCKETS + 1), st);
+  const uint32_t sched_words = 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS + 1u;
+  if (I == 0 || !dup_balanced(I, (uint32_t)P)) {
+    // no instances (capacity 0), or more than DUP_SLOTS per Gaussian on average: view by view
+    for (int v = 0; v < views; v++) {
+      GeomPtrs g;
+      BinPtrs bb;
+      ImgPtrs im;
+      geom_layout((size_t)P, &g, (char*)geo.splat + (uint64_t)v * gs);
+      bin_layout((size_t)I, tiles, &bb, (char*)bin.keys_a + (uint64_t)v * bs);
+      img_layout(c.W, c.H, &im, (char*)img.ranges + (uint64_t)v * is);
+      if (I == 0) {
+        (void)hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
+        (void)hipMemsetAsync(im.tile_done, 0, sizeof(uint32_t) * sched_words, st);
+        continue;
+      }
+      (void)hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
+      GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, g.counters,
+                g.sorted_gid, g.offsets, g.binrec, c.gx, bb.slot_tile, bb.presort_gid);
+      radix_sort_pairs(bb.keys_a, bb.vals_a, bb.keys_b, bb.vals_b, true, &g.counters[CNT_NREND], I, tile_bits(tiles),
+                       bb.sort_scratch, st, false, false, GS_SORT_GID ? bb.presort_gid : nullptr, bb.aux_a,
+                       bb.presort_gid, bb.slot_tile, GS_TILE_SORT_BLOCKS);
+      GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, &g.counters[CNT_NREND],
+                bb.sorted_tile, im.ranges, (uint32_t*)im.tile_done, sched_words, (uint32_t)tiles, 0ull, 0ull);
+    }
     return;
   }
   const int tbits = tile_bits(tiles);
-  bool hist0 = false;
-  if (dup_balanced(I, (uint32_t)P)) {
-    // one duplicate block per sort tile: the duplicate also counts the first sort pass's digits
-    hist0 = sort_plan(I, GS_TILE_SORT_BLOCKS).chunk == DUP_SLOTS;
-    GS_LAUNCH("duplicate", k_duplicate_lb, dim3((I + DUP_SLOTS - 1) / DUP_SLOTS), dim3(DUP_THREADS), 0, st, I,
-              geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy,
-              bin.slot_tile, bin.presort_gid, img.ranges, hist0 ? bin.sort_scratch : nullptr,
-              (1u << radix_first_bits(tbits)) - 1u);
-  } else {
-    (void)hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
-    GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
-              geo.sorted_gid, geo.offsets, geo.binrec, c.gx, bin.slot_tile, bin.presort_gid);
-  }
+  // one duplicate block per sort tile: the duplicate also counts the first sort pass's digits; it
+  // copies each view's bounded count into its binning buffer (bin.count) for the sort and ranges
+  const bool hist0 = sort_plan(I, GS_TILE_SORT_BLOCKS).chunk == DUP_SLOTS;
+  GS_LAUNCH("duplicate", k_duplicate_lb, dim3((I + DUP_SLOTS - 1) / DUP_SLOTS, views), dim3(DUP_THREADS), 0, st, I,
+            geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy, bin.slot_tile,
+            bin.presort_gid, img.ranges, hist0 ? bin.sort_scratch : nullptr, (1u << radix_first_bits(tbits)) - 1u,
+            bin.count, gs, bs, is);
   // GS_SORT_GID: the Gaussian ids travel with the slots (aux stream): the renders then read
-  // point_gid contiguously instead of gathering presort_gid[slot]
-  radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, nullptr, I, tbits, bin.sort_scratch, st,
+  // point_gid contiguously instead of gathering presort_gid[slot].  The device count bounds the
+  // sort (I is the buffers' capacity, which may exceed it).
+  radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, bin.count, I, tbits, bin.sort_scratch, st,
                    false, hist0, GS_SORT_GID ? bin.presort_gid : nullptr, bin.aux_a, bin.presort_gid, bin.slot_tile,
-                   GS_TILE_SORT_BLOCKS);
-  GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.sorted_tile, img.ranges,
-            (uint32_t*)img.tile_done, 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS + 1u, (uint32_t)tiles);
+                   GS_TILE_SORT_BLOCKS, views, bs);
+  GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024, views), dim3(256), 0, st, I, bin.count, bin.sorted_tile,
+            img.ranges, (uint32_t*)img.tile_done, sched_words, (uint32_t)tiles, bs, is);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -790,7 +859,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
                                                          const uint32_t* __restrict__ err,
                                                          uint32_t* __restrict__ err_host) {
   __shared__ float4 s_ent[3 * GS_BLOCK];
-  if (blockIdx.x == 0 && threadIdx.x == 0 && err_host) err_host[0] = *err;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && err_host && *err) err_host[0] = *err;
   __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[4][GS_BLOCK + 2 * FWD_ILP];  // per quadrant wave: byte offsets
   const uint32_t tile = blockIdx.x;
@@ -801,7 +870,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
   const bool inside = q.px < c.W && q.py < c.H;
   const uint2 range = ranges[tile];
   // a sort / scan look-back that timed out (reported by the host) leaves no valid list: render none
-  const uint32_t n = (*err & 4u) ? 0u : range.y - range.x;
+  const uint32_t n = (*err & ERR_INVALID) ? 0u : range.y - range.x;
   const char* ent = reinterpret_cast<const char*>(s_ent);
   FwdPix px;
   px.done = __builtin_amdgcn_ballot_w64(!inside);
@@ -882,12 +951,12 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int lane = threadIdx.x;
   // the ordering's error flags (final once the binning kernels are done) -> the host's readback word
-  if (b == 0 && lane == 0 && err_host) err_host[0] = *err;
+  if (b == 0 && lane == 0 && err_host && *err) err_host[0] = *err;
   const QuadPix q = quad_pixel(tx, ty, wid, lane);
   const bool inside = q.px < c.W && q.py < c.H;
   const uint2 range = ranges[tile];
   // a sort / scan look-back that timed out (reported by the host) leaves no valid list: render none
-  const uint32_t n = (*err & 4u) ? 0u : range.y - range.x;
+  const uint32_t n = (*err & ERR_INVALID) ? 0u : range.y - range.x;
   const char* ent = reinterpret_cast<const char*>(s_ent);
   const float qx = (float)(tx * GS_TILE + 8 * (wid & 1)), qy = (float)(ty * GS_TILE + 8 * (wid >> 1));
   FwdPix px;

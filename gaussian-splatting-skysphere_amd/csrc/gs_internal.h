@@ -66,6 +66,86 @@ struct __attribute__((aligned(4))) F3 {
   float a, b, c;
 };
 
+// Coalesced staging of a workgroup's 256 degree-3 SH rows (48 floats each) into LDS, row stride
+// SH_STAGE_ROW floats (16-B aligned rows, conflict-free 16-B lane reads), for the preprocess
+// backward (k_preprocess_bwd_stage): the block of rows is contiguous in HBM, so it is read with 16-B loads, every load in
+// flight before the LDS stores -- instead of one lane-strided 192-B row per lane, each load
+// instruction touching 64 cache lines.  SPLIT: features_dc's block (12 B per Gaussian, g.shs) and
+// features_rest's (180 B, g.shs_rest) are each contiguous; their 16-B pieces straddle rows and are
+// stored as dwords.  Needs 16-B aligned bases.  The caller puts a barrier after it.
+constexpr int SH_STAGE_ROW = 52;
+template <bool SPLIT>
+__device__ __forceinline__ void stage_sh_rows48(const GaussianArgs& g, int i0, int nG, float* s_rows) {
+  constexpr int KF = 48, Q = KF / 4;
+  const int t = (int)threadIdx.x;
+  if constexpr (SPLIT) {
+    constexpr int RF = KF - 3, RQ = (256 * RF + 1023) / 1024;  // features_rest float4 per thread (12)
+    const float* rest = g.shs_rest + (size_t)i0 * RF;
+    const int nf = nG * RF, n4 = nf >> 2;
+    float4 v[RQ];
+#pragma unroll
+    for (int q = 0; q < RQ; q++) {
+      const int f = t + 256 * q;
+      v[q] = f < n4 ? reinterpret_cast<const float4*>(rest)[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float* dc = g.shs + (size_t)i0 * 3;
+    float4 d4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int nd4 = (nG * 3) >> 2;
+    if (t < nd4) d4 = reinterpret_cast<const float4*>(dc)[t];
+#pragma unroll
+    for (int q = 0; q < RQ; q++) {
+      const int f = t + 256 * q;
+      if (f < n4) {
+        const float e4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int e = 4 * f + j, r = e / RF;
+          s_rows[r * SH_STAGE_ROW + 3 + (e - r * RF)] = e4[j];
+        }
+      }
+    }
+    if (t < nd4) {
+      const float e4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int e = 4 * t + j, r = e / 3;
+        s_rows[r * SH_STAGE_ROW + (e - 3 * r)] = e4[j];
+      }
+    }
+    // tails of a partial last block (float counts that are not multiples of 4)
+    if (t < nf - 4 * n4) {
+      const int e = 4 * n4 + t, r = e / RF;
+      s_rows[r * SH_STAGE_ROW + 3 + (e - r * RF)] = rest[e];
+    }
+    if (t < nG * 3 - 4 * nd4) {
+      const int e = 4 * nd4 + t, r = e / 3;
+      s_rows[r * SH_STAGE_ROW + (e - 3 * r)] = dc[e];
+    }
+  } else {
+    const float4* src4 = reinterpret_cast<const float4*>(g.shs + (size_t)i0 * KF);
+    const int n4 = nG * Q;
+    float4 v[Q];
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const int f = t + 256 * q;
+      v[q] = f < n4 ? src4[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const int f = t + 256 * q;
+      if (f < n4) {
+        const int r = f / Q;
+        *reinterpret_cast<float4*>(&s_rows[r * SH_STAGE_ROW + 4 * (f - r * Q)]) = v[q];
+      }
+    }
+  }
+}
+// launch condition of the staged kernels: degree 3, M == 16, 16-B aligned row bases
+inline bool sh_stage_ok(const GaussianArgs& g) {
+  return g.D == 3 && g.M == 16 && g.shs && !g.colors &&
+         ((((uintptr_t)g.shs) | ((uintptr_t)g.shs_rest)) & 15) == 0;
+}
+
 struct CameraArgs {
   const float* view;    // 16, device
   const float* proj;    // 16, device
@@ -77,8 +157,12 @@ struct CameraArgs {
 };
 
 constexpr int CNT_I = 1, CNT_ERR = 2, CNT_NREND = 4, CNT_V = 5, CNT_LB_TILE = 9;
-// error flags in counters[CNT_ERR]: 1 prefiltered cull, 4 look-back timeout, 8 instance count overflow
-constexpr uint32_t ERR_PREFILTERED = 1u, ERR_LOOKBACK = 4u, ERR_INSTANCES = 8u;
+// error flags in counters[CNT_ERR]: 1 prefiltered cull, 4 look-back timeout, 8 instance count overflow,
+// 16 more instances than the binning buffer's capacity (gs_forward_bounded)
+constexpr uint32_t ERR_PREFILTERED = 1u, ERR_LOOKBACK = 4u, ERR_INSTANCES = 8u, ERR_CAPACITY = 16u;
+// flags under which the instance list is not valid: the binning kernels write placeholders that
+// keep every later kernel in bounds, the renders composite nothing, the record sums are zero
+constexpr uint32_t ERR_INVALID = ERR_LOOKBACK | ERR_CAPACITY;
 // Largest instance count of one view: the sorts and scans index instances with 32-bit positions
 // (a position plus one sort chunk must stay below 2^32).
 constexpr long long GS_MAX_INSTANCES = (1ll << 31) - 1;
@@ -176,6 +260,8 @@ struct BinPtrs {
                          // first pass reads it and writes keys_b)
   float4* inst_splat;    // GS_INST_REC: the 48-B splat record of every instance the forward staged, by
                          // list position (the backward streams it instead of gathering slot -> id -> splat)
+  uint32_t* count;       // [0]: the view's instance count bounded by the buffer's capacity (the duplicate
+                         // writes it; the tile sort and k_ranges read it from this buffer)
 };
 
 // Occupancy requests (amdgpu_waves_per_eu) for register-limited kernels; 0 = the compiler's choice.
@@ -221,7 +307,9 @@ inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base) {
   size_t o_pg = take(In * 4), o_st = take(In * 4), o_ax = take(GS_SORT_GID ? In * 4 : 0);
   size_t o_ss = take(sort_scratch_words(In) * 4);
   size_t o_is = take(GS_INST_REC ? In * 48 : 0);
+  size_t o_cn = take(64);
   if (out && base) {
+    out->count = (uint32_t*)(base + o_cn);
     out->inst_splat = GS_INST_REC ? (float4*)(base + o_is) : nullptr;
     out->keys_a = (uint32_t*)(base + o_ka);
     out->vals_a = (uint32_t*)(base + o_va);
@@ -332,12 +420,22 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
 // ---- stages (gs_forward.hip / gs_backward.hip) ----
 void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st);
 // compaction, depth sort, instance offsets; the view's totals are finalised by the first histogram
-// launch (written to host_counts when given: [I lo, I hi, V, err]), after which counts_ready is recorded
+// launch (written to host_counts when given: [I lo, I hi, V, err]), after which counts_ready is recorded.
+// cap: the binning buffer's instance capacity (more instances: ERR_CAPACITY); sticky (pinned host
+// words, or null): a view with error flags stores them into sticky[0] and its count into [1], [2].
+// views > 1: the orderings of `views` views at once, view v's geometry buffer lying v * vstride
+// bytes after geo's (slices of one allocation); cap[v] per view (null: unbounded), host_counts + 8 v
 void fwd_order(int P, const GeomPtrs& geo, hipStream_t st, uint32_t* host_counts = nullptr,
-               hipEvent_t counts_ready = nullptr);
+               hipEvent_t counts_ready = nullptr, const uint32_t* cap = nullptr, uint32_t* sticky = nullptr,
+               int views = 1, uint64_t vstride = 0);
 void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const GeomPtrs& geo, const BinPtrs& bin,
              const ImgPtrs& img, hipStream_t st);
-// err_host (device-visible pinned host word, or null): the ordering's error flags, copied by the render
+// the binning of `views` views of one image size at once: view v's geometry / binning / image
+// buffers lie v * {geo,bin,img}_stride bytes after geo's / bin's / img's (I: the largest capacity)
+void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
+                   const ImgPtrs& img, uint64_t geo_stride, uint64_t bin_stride, uint64_t img_stride, hipStream_t st);
+// err_host (device-visible pinned host word, or null): the ordering's error flags, stored by the render
+// when nonzero (the host clears the word before it hands it out)
 void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
                 hipStream_t st, uint32_t* err_host = nullptr);
 void mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,

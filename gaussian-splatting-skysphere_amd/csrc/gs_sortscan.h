@@ -348,6 +348,18 @@ inline size_t sort_scratch_words(uint64_t n_max) {
   return hist + RADIX + 16;
 }
 
+// View batching: one launch sorts the same-shaped arrays of several views (blockIdx.y = view) whose
+// buffers lie `vstride` bytes apart (the views' geometry buffers are slices of one allocation).
+// vptr(p): this workgroup's view's copy of p (null stays null).
+template <class T>
+__device__ __forceinline__ T* vptr(T* p, uint64_t vstride) {
+  return p ? (T*)((char*)p + (uint64_t)blockIdx.y * vstride) : p;
+}
+template <class T>
+__device__ __forceinline__ const T* vptr(const T* p, uint64_t vstride) {
+  return p ? (const T*)((const char*)p + (uint64_t)blockIdx.y * vstride) : p;
+}
+
 // lanes of this wave whose `bits`-bit digit equals mine (valid lanes only)
 __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits) {
   uint64_t peers = __ballot(valid);
@@ -362,22 +374,24 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int bits
 // Fin: work of one extra workgroup (blockIdx nb, all 256 threads; the launch then has nb + 1
 // workgroups) beside the counting ones, e.g. the forward's counter finalisation in the first
 // depth-sort pass (gs_forward.hip CounterFinalize); NoFin: none.
+// Fin::operator()(view) runs for each view of a batched launch (blockIdx.y).
 struct NoFin {
   static constexpr bool active = false;
-  __device__ void operator()() const {}
+  __device__ void operator()(uint32_t) const {}
 };
 template <class Fin = NoFin>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, const uint32_t* n_dev,
                                                              uint32_t n_max, int shift, int bits, uint32_t chunk,
                                                              uint32_t nb, uint32_t* __restrict__ hist, bool drop,
-                                                             Fin fin = Fin()) {
+                                                             uint64_t vstride, Fin fin = Fin()) {
   __shared__ uint32_t h[RADIX];
   if constexpr (Fin::active) {
     if (blockIdx.x == nb) {  // (uniform) the extra workgroup runs beside the counting ones
-      fin();
+      fin(blockIdx.y);
       return;
     }
   }
+  keys = vptr(keys, vstride), n_dev = vptr(n_dev, vstride), hist = vptr(hist, vstride);
   const uint32_t n = resolve_n(n_dev, n_max);
   h[threadIdx.x] = 0;
   lds_barrier();
@@ -405,8 +419,10 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __r
 // Row scan of the [digit][block] histogram: workgroup d turns row d into exclusive per-block
 // offsets (within digit d) and writes the row total; the scatter adds the digit base itself.
 static __global__ __launch_bounds__(SORT_THREADS) void k_radix_rowscan(uint32_t* __restrict__ hist, uint32_t nb,
-                                                                        uint32_t* __restrict__ row_total) {
+                                                                        uint32_t* __restrict__ row_total,
+                                                                        uint64_t vstride) {
   __shared__ uint32_t sh[4];
+  hist = vptr(hist, vstride), row_total = vptr(row_total, vstride);
   uint32_t* row = hist + (size_t)blockIdx.x * nb;
   uint32_t carry = 0;
   for (uint32_t base = 0; base < nb; base += SORT_THREADS * 4) {
@@ -447,7 +463,7 @@ __global__ __launch_bounds__(SORT_THREADS) GS_SCATTER_ATTR void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, uint32_t chunk,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ row_total, bool drop,
-    const uint32_t* __restrict__ aux_in, uint32_t* __restrict__ aux_out) {
+    const uint32_t* __restrict__ aux_in, uint32_t* __restrict__ aux_out, uint64_t vstride) {
   __shared__ uint32_t s_base[RADIX];      // global position of the next key of each digit
   __shared__ uint32_t s_wcnt[4][RADIX];   // per-wave running counts -> per-wave exclusive prefix
   __shared__ uint32_t s_loc[RADIX];       // digit offsets inside the tile (for the LDS reorder)
@@ -456,6 +472,9 @@ __global__ __launch_bounds__(SORT_THREADS) GS_SCATTER_ATTR void k_radix_scatter(
   __shared__ uint32_t s_key[SORT_TILE];
   __shared__ uint32_t s_val[SORT_TILE];
   __shared__ uint32_t s_aux[AUX ? SORT_TILE : 1];
+  keys_in = vptr(keys_in, vstride), vals_in = vptr(vals_in, vstride), keys_out = vptr(keys_out, vstride);
+  vals_out = vptr(vals_out, vstride), n_dev = vptr(n_dev, vstride), hist = vptr(hist, vstride);
+  row_total = vptr(row_total, vstride), aux_in = vptr(aux_in, vstride), aux_out = vptr(aux_out, vstride);
   const uint32_t n = resolve_n(n_dev, n_max);
   const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   {
@@ -546,10 +565,10 @@ template <bool AUX>
 static inline void launch_scatter(int bits, uint32_t nb, hipStream_t st, const uint32_t* kin, const uint32_t* vin,
                                   uint32_t* kout, uint32_t* vout, const uint32_t* nd, uint32_t n_max, int shift,
                                   uint32_t chunk, const uint32_t* hist, const uint32_t* row_total, bool drop,
-                                  const uint32_t* ain, uint32_t* aout) {
-#define GS_SCATTER(B)                                                                                             \
-  GS_LAUNCH("radix_scatter", (k_radix_scatter<AUX, B>), dim3(nb), dim3(SORT_THREADS), 0, st, kin, vin, kout, vout, \
-            nd, n_max, shift, chunk, nb, hist, row_total, drop, ain, aout)
+                                  const uint32_t* ain, uint32_t* aout, int views, uint64_t vstride) {
+#define GS_SCATTER(B)                                                                                       \
+  GS_LAUNCH("radix_scatter", (k_radix_scatter<AUX, B>), dim3(nb, views), dim3(SORT_THREADS), 0, st, kin, vin, \
+            kout, vout, nd, n_max, shift, chunk, nb, hist, row_total, drop, ain, aout, vstride)
   switch (bits) {
     case 8: GS_SCATTER(8); break;
     case 7: GS_SCATTER(7); break;
@@ -569,12 +588,15 @@ static inline void launch_scatter(int bits, uint32_t nb, hipStream_t st, const u
 // hist0_ready: the caller already wrote the first pass's [digit][block] counts into scratch.
 // drop_first: the first pass reads n_max keys (host count) and drops those equal to DEPTH_DROP;
 // the later passes then sort the *n_dev survivors.  Otherwise every pass sorts n (n_dev / n_max).
+// views / vstride: `views` such sorts at once, view v's arrays (every pointer argument) lying
+// v * vstride bytes after view 0's.
 static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b,
                                     bool vals_identity, const uint32_t* n_dev, uint32_t n_max, int end_bit,
                                     uint32_t* scratch, hipStream_t st, bool drop_first = false,
                                     bool hist0_ready = false, const uint32_t* aux0 = nullptr,
                                     uint32_t* aux_a = nullptr, uint32_t* aux_b = nullptr,
-                                    const uint32_t* keys_in0 = nullptr, uint32_t max_blocks = SORT_MAX_BLOCKS) {
+                                    const uint32_t* keys_in0 = nullptr, uint32_t max_blocks = SORT_MAX_BLOCKS,
+                                    int views = 1, uint64_t vstride = 0) {
   SortPlan p = sort_plan(n_max, max_blocks);
   uint32_t* hist = scratch;
   const size_t hist_n = (size_t)RADIX * p.nb;
@@ -592,18 +614,19 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
     // keys_in0: the first pass reads its keys from there (kept), not from keys_a
     const uint32_t* kin_p = (shift == 0 && keys_in0) ? keys_in0 : kin;
     if (!(hist0_ready && shift == 0))
-      GS_LAUNCH("radix_hist", k_radix_hist<NoFin>, dim3(p.nb), dim3(SORT_THREADS), 0, st, kin_p, nd, n_max, shift,
-                bits, p.chunk, p.nb, hist, drop, NoFin());
-    GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX), dim3(SORT_THREADS), 0, st, hist, p.nb, row_total);
+      GS_LAUNCH("radix_hist", k_radix_hist<NoFin>, dim3(p.nb, views), dim3(SORT_THREADS), 0, st, kin_p, nd, n_max,
+                shift, bits, p.chunk, p.nb, hist, drop, vstride, NoFin());
+    GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX, views), dim3(SORT_THREADS), 0, st, hist, p.nb, row_total,
+              vstride);
     const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
     if (aux0) {
       launch_scatter<true>(bits, p.nb, st, kin_p, vsrc, kout, vout, nd, n_max, shift, p.chunk, hist, row_total, drop, ain,
-                           aout);
+                           aout, views, vstride);
       ain = aout;
       aout = aout == aux_a ? aux_b : aux_a;
     } else {
       launch_scatter<false>(bits, p.nb, st, kin_p, vsrc, kout, vout, nd, n_max, shift, p.chunk, hist, row_total, drop,
-                            nullptr, nullptr);
+                            nullptr, nullptr, views, vstride);
     }
     uint32_t* t;
     t = kin; kin = kout; kout = t;

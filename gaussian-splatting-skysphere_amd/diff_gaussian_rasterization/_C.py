@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -105,11 +106,13 @@ class _Inputs:
 
 def preprocess_views(backgrounds, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                      viewmatrices, projmatrices, tan_fovx, tan_fovy, image_heights, image_widths, sh, degree, campos,
-                     prefiltered, debug, streams=None):
+                     prefiltered, debug, streams=None, capacities=None):
     """First half of K views' forwards in one preprocess launch (gs_forward_preprocess_views):
-    returns [(num_rendered, radii, geomBuffer)] per view, each what rasterize_gaussians computes for
-    that camera before its binning; view k's depth ordering is enqueued on streams[k] (default:
-    the current stream).  Pass each view's triple to rasterize_gaussians(..., prepared=)."""
+    returns [(num_rendered, radii, geomBuffer, bounded)] per view, each what rasterize_gaussians
+    computes for that camera before its binning; view k's depth ordering is enqueued on streams[k]
+    (default: the current stream).  Pass each view's tuple to rasterize_gaussians(..., prepared=).
+    capacities: K binning capacities -- nothing is read back (gs_forward_preprocess_views_bounded),
+    num_rendered is the capacity and the view's render is bounded (gs_forward_render_bounded)."""
     K = len(viewmatrices)
     if not 1 <= K <= 8:
         raise RuntimeError("preprocess_views: 1 to 8 views per call")
@@ -118,17 +121,26 @@ def preprocess_views(backgrounds, means3D, colors, opacity, scales, rotations, s
     x, dev = xs[0], xs[0].device
     u8 = dict(dtype=torch.uint8, device=dev)
     radii = [torch.empty((x.P,), dtype=torch.int32, device=dev) for _ in range(K)]
-    geoms = [torch.empty((_lib.gs_geom_buffer_bytes(x.P) if x.P else 0,), **u8) for _ in range(K)]
+    # the views' geometry buffers are slices of one allocation (one stride apart): the library then
+    # runs the K depth sorts as one set of launches
+    gb = _lib.gs_geom_buffer_bytes(x.P) if x.P else 0
+    geom_all = torch.empty((K * gb,), **u8)
+    geoms = [geom_all[k * gb:(k + 1) * gb] for k in range(K)]
     if x.P == 0:
-        return [(0, r, g) for r, g in zip(radii, geoms)]
+        return [(0, r, g, False) for r, g in zip(radii, geoms)]
+    if capacities is not None and len(capacities) != K:
+        raise RuntimeError("preprocess_views: one capacity per view")
     arr = lambda ts: (ctypes.c_void_p * K)(*[t.data_ptr() if t is not None else None for t in ts])  # noqa: E731
     nr = (ctypes.c_longlong * K)()
     vst = None
     if streams is not None:
         vst = (ctypes.c_void_p * K)(*[s.cuda_stream for s in streams])
+    if capacities is not None:
+        for k, c in enumerate(capacities):
+            nr[k] = int(c)
     with torch.cuda.device(dev):
         _native.check(
-            _lib.gs_forward_preprocess_views(
+            (_lib.gs_forward_preprocess_views if capacities is None else _lib.gs_forward_preprocess_views_bounded)(
                 K, x.P, int(degree), x.M, arr([y.bg for y in xs]), (ctypes.c_int * K)(*[int(w) for w in image_widths]),
                 (ctypes.c_int * K)(*[int(h) for h in image_heights]), _ptr(x.means3D), _ptr(x.sh), _ptr(x.colors),
                 _ptr(x.opacity), _ptr(x.scales), float(scale_modifier), _ptr(x.rotations), _ptr(x.cov3D),
@@ -136,23 +148,60 @@ def preprocess_views(backgrounds, means3D, colors, opacity, scales, rotations, s
                 (ctypes.c_float * K)(*[float(t) for t in tan_fovx]), (ctypes.c_float * K)(*[float(t) for t in tan_fovy]),
                 int(bool(prefiltered)), arr(radii), arr(geoms), nr, int(bool(debug)), _stream(dev), vst),
             "preprocess_views")
+    bounded = capacities is not None
+    out = [(int(nr[k]), radii[k], geoms[k], bounded) for k in range(K)]
+    W0, H0 = int(image_widths[0]), int(image_heights[0])
+    if os.environ.get("GSRAST_BATCH_VIEWS", "1") != "0" and all(
+            int(w) == W0 and int(h) == H0 for w, h in zip(image_widths, image_heights)):
+        # the K views' binning (duplicate, tile sort, ranges) as one set of launches: every binning
+        # buffer is a slice of one allocation, sized for the largest count, which then stands for
+        # every view's num_rendered (buffer layout, backward scratch)
+        I = max(int(nr[k]) for k in range(K))
+        bb, ib = _lib.gs_binning_buffer_bytes(I, W0, H0), _lib.gs_image_buffer_bytes(W0, H0)
+        bin_all, img_all = torch.empty((K * bb,), **u8), torch.empty((K * ib,), **u8)
+        bins = [bin_all[k * bb:(k + 1) * bb] for k in range(K)]
+        imgs = [img_all[k * ib:(k + 1) * ib] for k in range(K)]
+        with torch.cuda.device(dev):
+            _native.check(_lib.gs_forward_bin_views(K, x.P, W0, H0, arr(geoms), nr, arr(bins), arr(imgs),
+                                                    int(bool(debug)), _stream(dev), vst), "preprocess_views (binning)")
+        out = [(I, radii[k], geoms[k], bounded, bins[k], imgs[k]) for k in range(K)]
     if streams is not None:  # the buffers are used on the views' streams
         for k, s in enumerate(streams):
-            radii[k].record_stream(s)
-            geoms[k].record_stream(s)
-    return [(int(nr[k]), radii[k], geoms[k]) for k in range(K)]
+            for t in out[k][1:]:
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(s)
+    return out
+
+
+# instance count of the last forward that read it back (bounded forwards do not): a base for a
+# binning capacity (last_num_rendered())
+_LAST_NUM_RENDERED = [0]
+
+
+def bounded_status():
+    """(flags, instances) that bounded forwards left on the current device since the last call
+    (gs_bounded_status; clears them).  Raises RuntimeError when a flag is set."""
+    flags, inst = ctypes.c_uint(0), ctypes.c_longlong(0)
+    rc = _lib.gs_bounded_status(ctypes.byref(flags), ctypes.byref(inst))
+    if rc != 0:
+        raise RuntimeError(f"bounded forward: {_native.last_error()}")
+    return int(flags.value), int(inst.value)
 
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, debug, prepared=None, sh_rest=None):
+                        prefiltered, debug, prepared=None, sh_rest=None, capacity=None):
     """prepared: (num_rendered, radii, geomBuffer) of this call from preprocess_views (the first
     half already ran); otherwise both halves run here.  sh_rest: split SH rows (sh is then
-    features_dc [P,1,3], sh_rest features_rest [P,M-1,3]; gs_forward_preprocess_split)."""
+    features_dc [P,1,3], sh_rest features_rest [P,M-1,3]; gs_forward_preprocess_split).
+    capacity: the binning buffer is sized for that many instances and the whole forward is
+    enqueued without a host wait (gs_forward_bounded); the returned num_rendered is the capacity."""
     x = _Inputs(background, means3D, colors, opacity, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
                 campos, sh_rest=sh_rest)
     if prepared is not None and x.sh_rest is not None:
         raise RuntimeError("split SH rows are not supported with prepared views")
+    if prepared is not None and capacity is not None:
+        raise RuntimeError("a binning capacity is not supported with prepared views")
     H, W = int(image_height), int(image_width)
     dev = x.device
     u8 = dict(dtype=torch.uint8, device=dev)
@@ -163,12 +212,42 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                 torch.empty((0,), **u8), torch.empty((0,), **u8), torch.empty((0,), **u8))
     # every pixel of the image and every radius is written by the kernels
     out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+    if capacity is not None:
+        capacity = int(capacity)
+        radii = torch.empty((x.P,), dtype=torch.int32, device=dev)
+        geom = torch.empty((_lib.gs_geom_buffer_bytes(x.P),), **u8)
+        binning = torch.empty((_lib.gs_binning_buffer_bytes(capacity, W, H),), **u8)
+        img = torch.empty((_lib.gs_image_buffer_bytes(W, H),), **u8)
+        split = x.sh_rest is not None
+        with torch.cuda.device(dev):
+            _native.check(
+                _lib.gs_forward_bounded(
+                    x.P, int(degree), x.M, _ptr(x.bg), W, H, _ptr(x.means3D), _ptr(x.sh), _ptr(x.sh_rest),
+                    _ptr(x.colors), _ptr(x.opacity), _ptr(x.scales), float(scale_modifier), _ptr(x.rotations),
+                    _ptr(x.cov3D), _ptr(x.view), _ptr(x.proj), _ptr(x.campos), float(tan_fovx), float(tan_fovy),
+                    int(bool(prefiltered)), _ptr(radii), _ptr(geom), capacity, _ptr(binning), _ptr(img),
+                    _ptr(out_color), int(bool(debug)), _stream(dev)),
+                "rasterize_gaussians (bounded)")
+        return capacity, out_color, radii, geom, binning, img
     with torch.cuda.device(dev):
         st = _stream(dev)
+        bounded = False
         if prepared is not None:
-            num_rendered, radii, geom = prepared
+            num_rendered, radii, geom = prepared[:3]
+            bounded = len(prepared) > 3 and prepared[3]
             if radii.numel() != x.P or geom.numel() != _lib.gs_geom_buffer_bytes(x.P):
                 raise RuntimeError("rasterize_gaussians: the prepared view does not match these inputs")
+            if len(prepared) > 4:  # binned with the other prepared views: the compositing only
+                binning, img = prepared[4], prepared[5]
+                if img.numel() != _lib.gs_image_buffer_bytes(W, H):
+                    raise RuntimeError("rasterize_gaussians: the prepared view was binned for another image size")
+                _native.check(
+                    _lib.gs_forward_render_binned(
+                        x.P, _ptr(x.bg), W, H, _ptr(x.view), _ptr(x.proj), _ptr(x.campos), float(tan_fovx),
+                        float(tan_fovy), _ptr(geom), num_rendered, _ptr(binning), _ptr(img), _ptr(out_color),
+                        int(bool(bounded)), int(bool(debug)), st),
+                    "rasterize_gaussians (render)")
+                return num_rendered, out_color, radii, geom, binning, img
         else:
             radii = torch.empty((x.P,), dtype=torch.int32, device=dev)
             geom = torch.empty((_lib.gs_geom_buffer_bytes(x.P),), **u8)
@@ -183,10 +262,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                     int(bool(prefiltered)), _ptr(radii), _ptr(geom), ctypes.byref(nr), int(bool(debug)), st),
                 "rasterize_gaussians (preprocess)")
             num_rendered = int(nr.value)
+            _LAST_NUM_RENDERED[0] = num_rendered
         binning = torch.empty((_lib.gs_binning_buffer_bytes(num_rendered, W, H),), **u8)
         img = torch.empty((_lib.gs_image_buffer_bytes(W, H),), **u8)
         _native.check(
-            _lib.gs_forward_render(
+            (_lib.gs_forward_render_bounded if bounded else _lib.gs_forward_render)(
                 x.P, _ptr(x.bg), W, H, _ptr(x.view), _ptr(x.proj), _ptr(x.campos), float(tan_fovx), float(tan_fovy),
                 _ptr(radii), _ptr(geom), num_rendered, _ptr(binning), _ptr(img), _ptr(out_color),
                 int(bool(debug)), st),

@@ -30,7 +30,8 @@ import torch.nn as nn
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "cpu_deep_copy_tuple",
-           "register_gradient_sink", "unregister_gradient_sink", "prepare_views"]
+           "register_gradient_sink", "unregister_gradient_sink", "prepare_views", "last_num_rendered",
+           "bounded_status"]
 
 # ------------------------------------------------------------------------------------------
 # Gradient sinks (an extension beyond the upstream API, used by gs_view_parallel.GradBucket).
@@ -91,9 +92,30 @@ class GaussianRasterizationSettings(NamedTuple):
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                        raster_settings, prepared=None, sh_split=None):
+                        raster_settings, prepared=None, sh_split=None, binning_capacity=None):
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
-                                     cov3Ds_precomp, raster_settings, prepared, sh_split)
+                                     cov3Ds_precomp, raster_settings, prepared, sh_split, binning_capacity)
+
+
+# ------------------------------------------------------------------------------------------
+# Bounded forwards (an extension beyond the upstream API, ABI v10).  Upstream reads num_rendered
+# back to size its binning buffer, one host wait per forward.  With `binning_capacity=N` the
+# buffer is sized for N instances ahead of time and the forward is enqueued without any host
+# wait, event or allocation inside the library, so a training step can be captured into a
+# HIP graph (torch.cuda.CUDAGraph).  Outputs are bit-identical while the view's instance count
+# fits; a view that exceeds N leaves a sticky flag (its outputs invalid, all accesses in bounds)
+# that the next bounded forward raises, or bounded_status() reports.  last_num_rendered() is the
+# count of the last forward that read it back, a base for N.
+# ------------------------------------------------------------------------------------------
+def last_num_rendered() -> int:
+    return _C._LAST_NUM_RENDERED[0]
+
+
+def bounded_status():
+    """(flags, instances) left by bounded forwards on the current device since the last call
+    (cleared); raises RuntimeError if one exceeded its capacity, culled a prefiltered point or
+    timed out.  Covers the forwards whose kernels ran: call it after a synchronisation."""
+    return _C.bounded_status()
 
 
 class PreparedView:
@@ -122,13 +144,15 @@ class PreparedView:
 
 
 def prepare_views(rasterizers, means3D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
-                  cov3D_precomp=None, streams=None):
+                  cov3D_precomp=None, streams=None, binning_capacity=None):
     """Run the first half of the forward (preprocess, depth order, instance offsets) of several
     views of the same Gaussians at once: one preprocess launch reads every Gaussian's inputs once
     for all cameras (gs_forward_preprocess_views) and one host wait returns every view's instance
     count.  Returns one PreparedView per rasterizer, to pass as `prepared=` to that rasterizer's
     call with the same tensors; view k's ordering runs on streams[k] (its call must run there).
-    The rasterizers must share sh_degree, scale_modifier, prefiltered and debug."""
+    The rasterizers must share sh_degree, scale_modifier, prefiltered and debug.
+    binning_capacity (one int, or one per view): bounded views -- no instance count is read back,
+    each view's binning buffer is sized for its capacity (see bounded_status())."""
     ss = [r.raster_settings for r in rasterizers]
     s0 = ss[0]
     for s in ss[1:]:
@@ -137,6 +161,10 @@ def prepare_views(rasterizers, means3D, opacities, shs=None, colors_precomp=None
             raise ValueError("prepare_views: the views must share sh_degree, scale_modifier, prefiltered, debug")
     empty = torch.Tensor([])
     e = lambda t: empty if t is None else t  # noqa: E731
+    caps = None
+    if binning_capacity is not None:
+        caps = ([int(binning_capacity)] * len(ss) if isinstance(binning_capacity, int)
+                else [int(c) for c in binning_capacity])
     with torch.no_grad():
         tri = _C.preprocess_views([s.bg for s in ss], means3D.detach(), e(colors_precomp).detach(), opacities.detach(),
                                   e(scales).detach(), e(rotations).detach(), s0.scale_modifier,
@@ -144,7 +172,7 @@ def prepare_views(rasterizers, means3D, opacities, shs=None, colors_precomp=None
                                   [_contiguous_matrix(s.projmatrix) for s in ss], [s.tanfovx for s in ss],
                                   [s.tanfovy for s in ss], [s.image_height for s in ss], [s.image_width for s in ss],
                                   e(shs).detach(), s0.sh_degree, [s.campos for s in ss], s0.prefiltered, s0.debug,
-                                  streams)
+                                  streams, caps)
     inputs = (means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp)
     return [PreparedView(t, s, inputs) for t, s in zip(tri, ss)]
 
@@ -184,7 +212,7 @@ def _run_with_snapshot(fn, args, debug, dump_name, phase):
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings, prepared=None, sh_split=None):
+                raster_settings, prepared=None, sh_split=None, binning_capacity=None):
         s = raster_settings
         # the camera matrices arrive transposed (cameras.py:54-56 world_view_transform is a
         # .transpose(0, 1) view); make them contiguous once and reuse them in backward
@@ -204,9 +232,12 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
                 view, proj, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
                 s.campos, s.prefiltered, s.debug)
-        if sh_rest is not None:
+        if prepared is not None and binning_capacity is not None:
+            raise RuntimeError("binning_capacity: not supported with prepared views")
+        if sh_rest is not None or binning_capacity is not None:
             num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _run_with_snapshot(
-                lambda *a: _C.rasterize_gaussians(*a, sh_rest=sh_rest), args, s.debug, "snapshot_fw.dump", "forward")
+                lambda *a: _C.rasterize_gaussians(*a, sh_rest=sh_rest, capacity=binning_capacity), args, s.debug,
+                "snapshot_fw.dump", "forward")
         elif prepared is not None:
             nz = lambda t: None if t is None or t.numel() == 0 else t  # noqa: E731
             tri = prepared.take(s, (means3D, nz(sh), nz(colors_precomp), opacities, nz(scales), nz(rotations),
@@ -236,7 +267,7 @@ class _RasterizeGaussians(torch.autograd.Function):
     def backward(ctx, grad_out_color, _grad_radii):
         s = ctx.raster_settings
         if grad_out_color is None:  # the colour output did not reach the loss
-            return (None,) * 11
+            return (None,) * 12
         colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer, imgBuffer = (
             ctx.saved_tensors)
         if ctx.sh_rest is not None and (sh._version, ctx.sh_rest._version) != ctx.sh_split_versions:
@@ -263,7 +294,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                                           degree=s.sh_degree, debug=s.debug),
                                 (view, proj, s.campos, s.tanfovx, s.tanfovy, s.image_width, s.image_height,
                                  geomBuffer))
-            return (None, dm2) + (None,) * 9
+            return (None, dm2) + (None,) * 10
 
         sinks, sunk, owners = {}, set(), []
         for k, name, t, owner in ctx.sinks:
@@ -293,7 +324,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             if hasattr(o, "written"):
                 o.written(st)
         grads = [grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
-                 grad_rotations, grad_cov3Ds_precomp, None, None, None]
+                 grad_rotations, grad_cov3Ds_precomp, None, None, None, None]
         for k in sunk:  # already in the sink's buffer (the tensor's .grad)
             grads[k] = None
         return tuple(grads)
@@ -325,8 +356,10 @@ class GaussianRasterizer(nn.Module):
             return _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
 
     def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
-                cov3D_precomp=None, prepared=None, sh_split=None):
+                cov3D_precomp=None, prepared=None, sh_split=None, binning_capacity=None):
         """prepared: this call's PreparedView from prepare_views (extension; default: none).
+        binning_capacity: size the binning buffer for that many instances and run the forward
+        without a host wait (extension, ABI v10; see bounded_status()).
         sh_split: (features_dc [P,1,3], features_rest [P,M-1,3]) read in place instead of the
         concatenated shs (extension, ABI v8: no per-iteration cat); `shs` is then a [P,M,3] tensor
         whose values are never read and whose .grad receives dL/d cat(features_dc, features_rest)
@@ -344,4 +377,4 @@ class GaussianRasterizer(nn.Module):
         rotations = empty if rotations is None else rotations
         cov3D_precomp = empty if cov3D_precomp is None else cov3D_precomp
         return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
-                                   s, prepared, sh_split)
+                                   s, prepared, sh_split, binning_capacity)

@@ -95,6 +95,28 @@ SIGNATURES = {
         [_c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_i, ctypes.POINTER(ViewGrad), _c_p,
          _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, ctypes.c_uint, _c_p, _c_i, _c_p],
     ),
+    # ABI v10: the whole forward without a host wait (binning buffer sized ahead) and its sticky status
+    "gs_forward_bounded": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_f, _c_f, _c_i, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_i, _c_p],
+    ),
+    "gs_bounded_status": (_c_i, [ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(_c_ll)]),
+    "gs_forward_preprocess_views_bounded": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_p, _c_p, _c_i, _c_p, _c_p, ctypes.POINTER(_c_ll), _c_i, _c_p, _c_p],
+    ),
+    "gs_forward_render_bounded": (
+        _c_i,
+        [_c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_f, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_i, _c_p],
+    ),
+    # ABI v11: the binning of K prepared views in one set of launches, then each view's compositing
+    "gs_forward_bin_views": (_c_i, [_c_i, _c_i, _c_i, _c_i, _c_p, ctypes.POINTER(_c_ll), _c_p, _c_p, _c_i, _c_p, _c_p]),
+    "gs_forward_render_binned": (
+        _c_i,
+        [_c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_f, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_i, _c_i, _c_p],
+    ),
     "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),
     "gs_knn_mean_dist2": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p]),

@@ -19,6 +19,9 @@
  *                                                  train.py:93, fused into the last kernel)
  *   gs_mark_visible                            <-  _C.mark_visible(...)
  *   gs_forward_preprocess_views                <-  (extension) the first half of K views' forwards
+ *   gs_forward_bounded / gs_bounded_status     <-  (extension) _C.rasterize_gaussians with the
+ *                                                  binning buffer sized ahead (no host wait,
+ *                                                  HIP-graph capturable)
  *   gs_knn_mean_dist2                          <-  simple_knn._C.distCUDA2(points)
  *                                                  (/root/reference/scene/gaussian_model.py:20,134)
  *   gs_ssim_forward / gs_ssim_backward         <-  utils.loss_utils.ssim(img1, img2)
@@ -56,7 +59,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 9
+#define GSRAST_ABI_VERSION 11
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -102,6 +105,65 @@ int gs_forward_render(int P, const float* background, int image_width, int image
                       const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
                       float tan_fovy, const int* radii, void* geom_buffer, long long num_rendered,
                       void* binning_buffer, void* image_buffer, float* out_color, int debug, void* stream);
+
+/* ---- forward in one call without a host wait (bounded binning buffer) ----
+ * Both halves of gs_forward_preprocess + gs_forward_render, enqueued without reading num_rendered
+ * back: the caller sizes binning_buffer for `capacity` instances (gs_binning_buffer_bytes(capacity,
+ * W, H)) and passes capacity wherever num_rendered goes afterwards (gs_backward*: num_rendered and
+ * gs_grad_buffer_bytes).  The instance count on the device drives every kernel, so outputs are
+ * bit-identical to the two-call forward whenever the count fits.  A view with more instances than
+ * `capacity` (or a prefiltered cull, or a timed-out look-back) leaves a sticky per-device flag, its
+ * image and gradients invalid (zero records, nothing composited, every access in bounds): the next
+ * gs_forward_bounded fails with the message, and gs_bounded_status reads / clears it.  Nothing
+ * here synchronises, records events or allocates, so a step of bounded forwards and their backwards
+ * can be captured into a HIP graph.  shs_rest: split SH rows as gs_forward_preprocess_split
+ * (shs = features_dc), or NULL. */
+int gs_forward_bounded(int P, int D, int M, const float* background, int image_width, int image_height,
+                       const float* means3D, const float* shs, const float* shs_rest, const float* colors_precomp,
+                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                       const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                       const float* campos, float tan_fovx, float tan_fovy, int prefiltered, int* radii_out,
+                       void* geom_buffer, long long capacity, void* binning_buffer, void* image_buffer,
+                       float* out_color, int debug, void* stream);
+/* The bounded forms of the two-call forward: gs_forward_preprocess_views without the readback
+ * (capacity: K binning capacities; nothing waits), then gs_forward_render_bounded per view with
+ * that view's capacity in place of num_rendered.  Same sticky status as gs_forward_bounded. */
+int gs_forward_preprocess_views_bounded(int K, int P, int D, int M, const float* const* background,
+                                        const int* image_width, const int* image_height, const float* means3D,
+                                        const float* shs, const float* colors_precomp, const float* opacities,
+                                        const float* scales, float scale_modifier, const float* rotations,
+                                        const float* cov3D_precomp, const float* const* viewmatrix,
+                                        const float* const* projmatrix, const float* const* campos,
+                                        const float* tan_fovx, const float* tan_fovy, int prefiltered,
+                                        int* const* radii_out, void* const* geom_buffer, const long long* capacity,
+                                        int debug, void* stream, void* const* view_streams);
+int gs_forward_render_bounded(int P, const float* background, int image_width, int image_height,
+                              const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                              float tan_fovy, const int* radii, void* geom_buffer, long long capacity,
+                              void* binning_buffer, void* image_buffer, float* out_color, int debug, void* stream);
+/* Flags (*flags: 1 prefiltered cull, 4 look-back timeout, 8 / 16 more instances than 2^31 - 1 /
+ * than the capacity) that bounded forwards left on the current device since the last call, with the
+ * instance count of a view that raised them (*instances); clears them.  Returns non-zero (message in
+ * gs_last_error) when a flag is set.  Only forwards whose kernels have run are seen: call it after
+ * a synchronisation point to cover every forward before it. */
+int gs_bounded_status(unsigned* flags, long long* instances);
+
+/* ---- the binning of K prepared views at once (ABI v11) ----
+ * After gs_forward_preprocess_views(_bounded): duplicate + tile sort + tile ranges of all K views as
+ * one set of launches on `stream` (each view's count on the device bounds its part), then each view
+ * stream waits for them.  Each kind of buffer (geometry, binning, image) must be K slices of one
+ * allocation, one stride apart; every binning slice sized for the largest num_rendered[v]
+ * (gs_binning_buffer_bytes(max, W, H)), which is then the num_rendered of every view afterwards
+ * (gs_forward_render_binned, backward, gs_grad_buffer_bytes).  All views share W x H. */
+int gs_forward_bin_views(int K, int P, int image_width, int image_height, void* const* geom_buffer,
+                         const long long* num_rendered, void* const* binning_buffer, void* const* image_buffer,
+                         int debug, void* stream, void* const* view_streams);
+/* The compositing of one binned view (gs_forward_render without its binning); bounded: the view
+ * came from gs_forward_preprocess_views_bounded (flags to the sticky status). */
+int gs_forward_render_binned(int P, const float* background, int image_width, int image_height,
+                             const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                             float tan_fovy, void* geom_buffer, long long num_rendered, void* binning_buffer,
+                             void* image_buffer, float* out_color, int bounded, int debug, void* stream);
 
 /* ---- one-call forward with an upstream-style allocator callback ----
  * alloc(ctx, which, bytes) returns a device pointer of >= bytes (which: 0 geometry, 1 binning,

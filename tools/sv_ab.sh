@@ -11,7 +11,7 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][0])
 k = d["kernels"]
 top = " ".join(f"{n}={v}" for n, v in list(k.items())[:6])
-print(f"{d['tag']:14s} {d['iters_s']:7.1f} it/s {d['ms']:.4f} ms | {top}")
+print(f"{d['tag']:14s} {d['mode']:9s} {d['iters_s']:7.1f} it/s {d['ms']:.4f} ms ksum {d['ksum_us']} | {top}")
 PY
   done
 done
