@@ -430,16 +430,27 @@ def main():
     # per-kernel breakdown + roofline of the dominant kernel
     k_local = len(my_views)
     acc_frac = (k_local - 1) / k_local  # preprocess_bwd launches that add into the bucket
+    # views per launch of the sort / binning kernels: with the fused front the library runs the K
+    # views' depth sorts (P <= 2M) and binnings (<= 8M instances per view) as one set of launches
+    batched = (fused_front and os.environ.get("GSRAST_BATCH_VIEWS", "1") != "0" and P <= (2 << 20)
+               and num_rendered <= (8 << 20))
+    per_launch_views = {k: (k_local if batched else 1)
+                        for k in ("radix_scatter", "radix_hist", "radix_rowscan", "duplicate", "ranges")}
+
+    def kb(name):  # algorithmic bytes of one launch of `name`
+        b = kernel_bytes(name, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac, k_local)
+        return b * per_launch_views.get(name, 1) if b else b
+
     kernels = {}
     for name, (ms, n) in prof.items():
         per_launch_ms = ms / max(n, 1)
-        b = kernel_bytes(name, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac, k_local)
+        b = kb(name)
         kernels[name] = dict(total_ms_per_step=round(ms / args.steps, 4), launches_per_step=round(n / args.steps, 2),
                              avg_us=round(1e3 * per_launch_ms, 2),
                              algo_GBs=(round(b / (per_launch_ms * 1e-3) / 1e9, 1) if b else None))
     dom = max(kernels, key=lambda k: kernels[k]["total_ms_per_step"])
     dom_avg_ms = kernels[dom]["avg_us"] / 1e3
-    dom_bytes = kernel_bytes(dom, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac, k_local)
+    dom_bytes = kb(dom)
     achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9 if dom_bytes else None
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -464,7 +475,7 @@ def main():
                                     frac=round(vi / (dom_avg_ms * 1e-3) / VALU_PEAK_IPS, 4))
     # whole-step algorithmic bytes (P*a_G + I*a_I + Npix*a_px), per view: every kernel's
     # bytes per launch times its launches per step, over the step's views
-    step_bytes = sum((kernel_bytes(k, P, visible, num_rendered, M, W, H, tiles, walked, acc_frac, k_local) or 0)
+    step_bytes = sum((kb(k) or 0)
                      * v["launches_per_step"] for k, v in kernels.items()) / k_local
     ms_per_view = ms_per_step / k_local
     step_roofline = dict(algo_bytes_per_view=int(step_bytes), ms_per_view=round(ms_per_view, 4),

@@ -135,9 +135,19 @@ static bool validate(int P, int D, int M, int W, int H, const float* means3D, co
 // ------------------------------------------------------------------------------------------
 // debug export kernel
 // ------------------------------------------------------------------------------------------
-__global__ void k_export_list(uint32_t I, const uint32_t* point_list, const uint32_t* ids, uint32_t* out) {
+// entries past the list's device count (a bounded buffer's capacity, or the instances the depth
+// slabs skipped) are not written by the forward: exported as ~0 (no gather through them)
+__global__ void k_export_list(uint32_t I, const uint32_t* counters, const uint32_t* point_list, const uint32_t* ids,
+                              uint32_t* out) {
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k < I) out[k] = GS_SORT_GID ? ids[k] : ids[point_list[k]];
+  if (k >= I) return;
+  const uint32_t n = min(I, counters[CNT_I]);
+  if (k >= n) {
+    out[k] = 0xFFFFFFFFu;
+    return;
+  }
+  const uint32_t s = GS_SORT_GID ? k : point_list[k];
+  out[k] = s < I ? ids[s] : 0xFFFFFFFFu;
 }
 __global__ void k_export_splat(int P, const float4* splat, float* xy, float* co, float* rgb, float* depth) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -166,6 +176,26 @@ __global__ void k_export_splat(int P, const float4* splat, float* xy, float* co,
 using namespace gs;
 
 namespace gs {
+static std::atomic<int> g_slabs{-1};  // -1: not yet read from GSRAST_SLABS (0 off, 1 by size, 2 always)
+int slab_setting() {
+  int v = g_slabs.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("GSRAST_SLABS");
+    v = e ? atoi(e) : 0;  // off: at C5 they measured 488-504 it/s against 497-509 without
+    v = v < 0 ? 0 : (v > 2 ? 2 : v);
+    g_slabs.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+// the near slab's share of the instances, in 1/64ths (GSRAST_SLAB_NEAR64, default 16: a quarter)
+uint32_t slab_target(size_t I) {
+  static const uint32_t n64 = [] {
+    const char* e = getenv("GSRAST_SLAB_NEAR64");
+    int v = e ? atoi(e) : 16;
+    return (uint32_t)(v < 1 ? 1 : (v > 63 ? 63 : v));
+  }();
+  return (uint32_t)(((uint64_t)I * n64) >> 6);
+}
 static std::atomic<int> g_exact_exp{-1};  // -1: not yet read from GSRAST_EXACT_EXP
 bool exact_exp() {
   int v = g_exact_exp.load(std::memory_order_relaxed);
@@ -199,7 +229,8 @@ size_t gs_binning_buffer_bytes(long long num_rendered, int W, int H) {
 }
 size_t gs_image_buffer_bytes(int W, int H) { return img_layout(W, H, nullptr, nullptr); }
 size_t gs_grad_buffer_bytes(long long num_rendered) {
-  return align_up((size_t)(num_rendered > 0 ? num_rendered : 1) * GRAD_REC * sizeof(float));
+  const size_t R = (size_t)(num_rendered > 0 ? num_rendered : 1);
+  return align_up(R * GRAD_REC * sizeof(float) + sumrec_extra_bytes(R));
 }
 
 // Pinned, device-mapped host words: kernels store into them directly (vector stores through the
@@ -432,6 +463,12 @@ int gs_forward_preprocess_split(int P, int D, int M, const float* background, in
 // The K views' depth sorts as one set of launches (contiguous geometry buffers); GSRAST_BATCH_VIEWS=0
 // in the environment runs them view by view on the views' streams (A/B runs; the Python layer then
 // also bins the views one by one)
+#ifndef GS_BATCH_ORDER_MAX
+#define GS_BATCH_ORDER_MAX (2 << 20)
+#endif
+#ifndef GS_BATCH_BIN_MAX
+#define GS_BATCH_BIN_MAX (8u << 20)  // instances per view up to which gs_forward_bin_views batches
+#endif
 static bool batch_views() {
   static const bool on = [] {
     const char* e = getenv("GSRAST_BATCH_VIEWS");
@@ -495,7 +532,10 @@ static int preprocess_views_impl(int K, int P, int D, int M, const float* const*
   // orderings run as one set of launches on `stream` (blockIdx.y = view), every view's totals
   // stored by the first histogram launch into readback words [8 v, 8 v + 4)
   const ptrdiff_t vstride = K > 1 ? (char*)geom_buffer[1] - (char*)geom_buffer[0] : 0;
-  bool batched = batch_views() && K > 1 && vstride >= (ptrdiff_t)gs_geom_buffer_bytes(P) && vstride % 256 == 0;
+  // (up to GS_BATCH_ORDER_MAX Gaussians: larger sorts fill the GPU on their own, and view by view
+  // on the views' streams they overlap the other views' render kernels)
+  bool batched = batch_views() && K > 1 && P <= GS_BATCH_ORDER_MAX && vstride >= (ptrdiff_t)gs_geom_buffer_bytes(P) &&
+                 vstride % 256 == 0;
   for (int v = 2; v < K && batched; v++) batched = (char*)geom_buffer[v] == (char*)geom_buffer[0] + v * vstride;
   fwd_preprocess_views(g, pv, st);
   if (batched) {
@@ -579,8 +619,9 @@ static int forward_render_impl(int P, const float* background, int W, int H, con
   GeomPtrs geo;
   BinPtrs bin;
   ImgPtrs img;
+  SlabPtrs slab;
   geom_layout((size_t)P, &geo, (char*)geom_buffer);
-  bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer);
+  bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer, &slab);
   img_layout(W, H, &img, (char*)image_buffer);
   // the look-back waits of the offsets scan and of the one-sweep sorts (never expected to run out:
   // the waited-for workgroups are running) leave ERR_LOOKBACK; the render kernel stores the flags
@@ -590,8 +631,12 @@ static int forward_render_impl(int P, const float* background, int W, int H, con
   BoundedStatus* bs = bounded ? bounded_status() : nullptr;
   uint32_t* flags_word = bounded ? (bs ? bs->dev + 4 : nullptr) : order_flags_word();
   if (!flags_word) return 1;
-  fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
-  fwd_render(c, geo, bin, img, out_color, st, flags_word);
+  if (slab_mode((size_t)num_rendered, c.gx * c.gy)) {
+    fwd_bin_render_slabs(P, (uint32_t)num_rendered, c, geo, bin, slab, img, out_color, st, flags_word);
+  } else {
+    fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
+    fwd_render(c, geo, bin, img, out_color, st, flags_word);
+  }
   if (!bounded && !t_failed && queue_order_flags(st)) return 1;
   return t_failed ? 1 : 0;
 }
@@ -622,6 +667,9 @@ int gs_forward_bin_views(int K, int P, int W, int H, void* const* geom_buffer, c
     *out = (uint64_t)d;
     return true;
   };
+  if (slab_mode((size_t)I, c.gx * c.gy))
+    return set_error("bin_views: views of this size bin in depth slabs, view by view (gs_binning_slabs; use "
+                     "gs_forward_render)"), 1;
   uint64_t gs = 0, bs = 0, is = 0;
   if (!stride_of(geom_buffer, gs_geom_buffer_bytes(P), &gs) ||
       !stride_of(binning_buffer, gs_binning_buffer_bytes(I, W, H), &bs) ||
@@ -631,6 +679,18 @@ int gs_forward_bin_views(int K, int P, int W, int H, void* const* geom_buffer, c
   GeomPtrs geo;
   BinPtrs bin;
   ImgPtrs img;
+  if (!batch_views() || I > (long long)GS_BATCH_BIN_MAX) {
+    // large views: each view's binning on its own stream, where it overlaps the other views'
+    // render kernels (a batched sort of K large views would serialise in front of them)
+    for (int v = 0; v < K; v++) {
+      hipStream_t vs = view_streams && view_streams[v] ? (hipStream_t)view_streams[v] : st;
+      geom_layout((size_t)P, &geo, (char*)geom_buffer[v]);
+      bin_layout((size_t)I, c.gx * c.gy, &bin, (char*)binning_buffer[v]);
+      img_layout(W, H, &img, (char*)image_buffer[v]);
+      fwd_bin_views(1, P, (uint32_t)I, c, geo, bin, img, 0, 0, 0, vs);
+    }
+    return t_failed ? 1 : 0;
+  }
   geom_layout((size_t)P, &geo, (char*)geom_buffer[0]);
   bin_layout((size_t)I, c.gx * c.gy, &bin, (char*)binning_buffer[0]);
   img_layout(W, H, &img, (char*)image_buffer[0]);
@@ -659,6 +719,7 @@ int gs_forward_render_binned(int P, const float* background, int W, int H, const
   if (!geom_buffer || !binning_buffer || !image_buffer || !out_color) return set_error("missing buffer pointer"), 1;
   hipStream_t st = (hipStream_t)stream;
   CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, 0);
+  if (slab_mode((size_t)num_rendered, c.gx * c.gy)) return set_error("render_binned: a depth-slab view (gs_binning_slabs)"), 1;
   GeomPtrs geo;
   BinPtrs bin;
   ImgPtrs img;
@@ -802,7 +863,7 @@ static int backward_impl(int P, int D, int M, const float* background, int W, in
               accumulate};
   // the gradient outputs may be shared with views on other streams: order only this last kernel
   if (wait_event && !check_hip(hipStreamWaitEvent(st, (hipEvent_t)wait_event, 0), "hipStreamWaitEvent")) return 1;
-  bwd_preprocess(g, c, geo, bin, img, gradrec, num_rendered > 0, out, st);
+  bwd_preprocess(g, c, geo, bin, img, gradrec, (uint32_t)num_rendered, num_rendered > 0, out, st);
   // the forward's ordering flags, now that this backward's kernels are queued
   if (!t_failed && check_order_flags()) return 1;
   return t_failed ? 1 : 0;
@@ -889,7 +950,7 @@ int gs_backward_render(int P, int D, int M, const float* background, int W, int 
   GaussianArgs g{P, D, M, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1.0f};
   float* gradrec = (float*)grad_buffer;
   if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, st);
-  bwd_records(g, geo, bin, img, gradrec, num_rendered > 0, dL_dmeans2D, accumulate, st);
+  bwd_records(g, geo, bin, img, gradrec, (uint32_t)num_rendered, num_rendered > 0, dL_dmeans2D, accumulate, st);
   if (!t_failed && check_order_flags()) return 1;
   return t_failed ? 1 : 0;
 }
@@ -999,6 +1060,17 @@ unsigned gs_debug_set_scan_spin_limit(unsigned limit) {
 }
 
 /* ---- numerics mode of the render loops ---- */
+int gs_set_slabs(int mode) {
+  const int prev = slab_setting();
+  g_slabs.store(mode < 0 ? 0 : (mode > 2 ? 2 : mode), std::memory_order_relaxed);
+  return prev;
+}
+
+int gs_binning_slabs(long long num_rendered, int W, int H) {
+  const int tiles = ((W + GS_TILE - 1) / GS_TILE) * ((H + GS_TILE - 1) / GS_TILE);
+  return num_rendered > 0 && slab_mode((size_t)num_rendered, tiles) ? 1 : 0;
+}
+
 int gs_set_exact_exp(int exact) {
   const int prev = exact_exp() ? 1 : 0;
   gs::g_exact_exp.store(exact ? 1 : 0, std::memory_order_relaxed);
@@ -1237,7 +1309,8 @@ int gs_debug_export(int P, int W, int H, long long num_rendered, const void* geo
   img_layout(W, H, &img, (char*)image_buffer);
   if (point_list && num_rendered > 0)
     GS_LAUNCH("export_list", k_export_list, dim3((unsigned)((num_rendered + 255) / 256)), dim3(256), 0, st,
-              (uint32_t)num_rendered, bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, point_list);
+              (uint32_t)num_rendered, geo.counters, bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid,
+              point_list);
   if (ranges) check_hip(hipMemcpyAsync(ranges, img.ranges, sizeof(uint2) * gx * gy, hipMemcpyDeviceToDevice, st), "copy");
   if (xy || conic_opacity || rgb || depth)
     GS_LAUNCH("export_splat", k_export_splat, dim3((P + 255) / 256), dim3(256), 0, st, P, geo.splat, xy, conic_opacity,

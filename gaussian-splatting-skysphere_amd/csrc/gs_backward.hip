@@ -529,6 +529,9 @@ void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& 
 #ifndef GS_SUMREC_WAVES
 #define GS_SUMREC_WAVES 4
 #endif
+#ifndef GS_SUMREC_ABLATE
+#define GS_SUMREC_ABLATE 0  // timing-only builds (wrong sums): 1 no record loads, 2 no scan, 3 no cut test
+#endif
 constexpr int SUMREC_WAVES = GS_SUMREC_WAVES;
 // one step of the segmented wave scan: v += (shifted v) when the shifted lane has the same owner
 // (owners are carried +1 so a lane without a source (0) never matches)
@@ -590,10 +593,25 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
       const uint32_t kn = base + 64 + lane;
 #pragma unroll
       for (int c = 0; c < GRAD_REC; c++) vn[c] = 0.0f;
+#if GS_SUMREC_ABLATE == 1  // timing only: no record loads
+      const bool h = kn < S1 && kn < tile_cut[slot_tile[kn]];
+      if (h) vn[0] = 1.0f;
+#elif GS_SUMREC_ABLATE == 3  // timing only: no cut test (every slot's record loaded)
+      const bool h = kn < S1;
+      if (h) load_rec(gradrec + (size_t)kn * GRAD_REC, vn);
+#else
       const bool h = kn < S1 && kn < tile_cut[slot_tile[kn]];
       if (h) load_rec(gradrec + (size_t)kn * GRAD_REC, vn);
+#endif
       hn = __ballot(h);
     }
+#if GS_SUMREC_ABLATE == 2  // timing only: no segmented scan / accumulation
+    if (hc) {
+      asm volatile("" ::"v"(v[0]), "v"(v[4]), "v"(v[8]));
+      jbase += (uint32_t)__popcll(__ballot(my_off >= base && my_off < base + 64));
+      continue;
+    }
+#endif
     if (hc == 0) {
       // no record in the chunk (every slot behind its tile's walk, as for most of a dense
       // scene's instances): only count the owners that start in it
@@ -631,6 +649,143 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
 #pragma unroll
     for (int c = 0; c < GRAD_REC; c++) gsum[gid * GRAD_REC + c] = (float)s_acc[wid][lane][c];
   }
+}
+
+// Slot-parallel record sums (GS_SUMREC_SLOTS=1; off by default: at C3 it measured 65 us against the
+// rank-parallel kernel's 56-62 us per view, the per-chunk partials and the join costing more than the
+// parallelism gained).  k_sum_records gives a wave 64
+// depth ranks and sweeps their records chunk after chunk: a chain of dependent loads per chunk
+// (slot -> tile -> cut -> record) with only V / 64 waves to hide it.  Here wave c takes the
+// instance slots [64 c, 64 c + 64) -- I / 64 independent waves: each slot's owner comes from the
+// duplicate's presort_gid (a Gaussian's slots are contiguous), the chunk's records are summed per
+// owner with the same segmented DPP scan, and an owner that lies inside the chunk is written
+// directly.  An owner that spans chunks leaves its per-chunk fp32 partials (head, whole chunks,
+// tail); k_sum_records_join adds them in chunk order in fp64.  Deterministic; the same sums as
+// k_sum_records up to where the chunk boundaries fall (fp32 partials, fp64 accumulation).
+#ifndef GS_SUMREC_SLOTS
+#define GS_SUMREC_SLOTS 0
+#endif
+constexpr uint32_t SR_IN = 1u, SR_OUT = 2u, SR_WHOLE = 4u;  // chunk flags
+// scratch after the records: per chunk two partials (9 f32: [0] its first owner's part when that
+// owner began in an earlier chunk, [1] its last owner's part when that owner continues) + flags
+inline size_t sumrec_chunks(size_t R) { return (R + 63) / 64; }
+size_t sumrec_extra_bytes(size_t R) {
+  if (!GS_SUMREC_SLOTS) return 0;
+  const size_t n = sumrec_chunks(R);
+  return n * 2 * GRAD_REC * sizeof(float) + n * sizeof(uint32_t);
+}
+
+__global__ __launch_bounds__(256) void k_sum_records_slots(const uint32_t* __restrict__ counters,
+                                                           const uint32_t* __restrict__ presort_gid,
+                                                           const uint32_t* __restrict__ slot_tile,
+                                                           const uint32_t* __restrict__ tile_cut,
+                                                           const uint32_t* __restrict__ cut_max,
+                                                           const float* __restrict__ gradrec, float* __restrict__ gsum,
+                                                           float* __restrict__ part, uint32_t* __restrict__ flags,
+                                                           uint32_t R, uint32_t P) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);  // chunk of this wave
+  if (counters[CNT_ERR] & ERR_INVALID) {
+    // the forward's instance list is invalid (reported by the host): no valid records, zero sums
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < P; i += gridDim.x * 256)
+      for (int k = 0; k < GRAD_REC; k++) gsum[(size_t)i * GRAD_REC + k] = 0.0f;
+    return;
+  }
+  const uint32_t I = min(counters[CNT_I], R);
+  const uint32_t k0 = c * 64;
+  if (k0 >= I) return;  // wave-uniform; no workgroup barrier in this kernel
+  const uint32_t k = k0 + lane;
+  const bool valid = k < I;
+  const uint32_t gid = valid ? presort_gid[k] : 0xFFFFFFFFu;
+  // records exist below the slot's tile cut (and below the largest cut)
+  const bool has = valid && k < *cut_max && k < tile_cut[slot_tile[k]];
+  float v[GRAD_REC];
+#pragma unroll
+  for (int q = 0; q < GRAD_REC; q++) v[q] = 0.0f;
+  if (has) load_rec(gradrec + (size_t)k * GRAD_REC, v);
+  // neighbours across the chunk edges (same owner: the owner spans chunks)
+  const uint32_t before = k0 > 0 ? presort_gid[k0 - 1] : 0xFFFFFFFEu;
+  const uint32_t after = k0 + 64 < I ? presort_gid[k0 + 64] : 0xFFFFFFFEu;
+  const uint32_t own1 = valid ? gid + 1 : 0;
+  if (__ballot(has)) {  // (uniform) a chunk without records (behind every walk) only writes zeros
+    seg_scan_step<0x111, 0xF>(v, own1);  // row_shr:1
+    seg_scan_step<0x112, 0xF>(v, own1);  // row_shr:2
+    seg_scan_step<0x114, 0xF>(v, own1);  // row_shr:4
+    seg_scan_step<0x118, 0xF>(v, own1);  // row_shr:8
+    seg_scan_step<0x142, 0xA>(v, own1);  // row_bcast:15 -> rows 1, 3
+    seg_scan_step<0x143, 0xC>(v, own1);  // row_bcast:31 -> rows 2, 3
+  }
+  const uint32_t gid_first = (uint32_t)__shfl((int)gid, 0, 64);
+  const uint32_t nv = min(64u, I - k0);
+  const uint32_t gid_last = (uint32_t)__shfl((int)gid, (int)nv - 1, 64);
+  const bool in = before == gid_first, out = after == gid_last;
+  const uint32_t next = lane + 1 < nv ? (uint32_t)__shfl_down((int)gid, 1, 64) : 0xFFFFFFFDu;
+  const bool end = valid && next != gid;  // last slot of its owner within the chunk
+  if (end) {
+    const bool first_seg = gid == gid_first, last_seg = lane + 1 == nv;
+    if ((first_seg && in) || (last_seg && out)) {
+      // a part of an owner that spans chunks: [0] the continued first owner (also when it fills the
+      // whole chunk and continues), [1] the last owner that begins here and continues
+      float* pp = part + ((size_t)c * 2 + ((first_seg && in) ? 0 : 1)) * GRAD_REC;
+#pragma unroll
+      for (int q = 0; q < GRAD_REC; q++) pp[q] = v[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < GRAD_REC; q++) gsum[(size_t)gid * GRAD_REC + q] = v[q];
+    }
+  }
+  if (lane == 0) flags[c] = (in ? SR_IN : 0u) | (out ? SR_OUT : 0u) | (gid_first == gid_last ? SR_WHOLE : 0u);
+}
+
+// One lane per chunk whose first owner began in an earlier chunk and ends here: that owner's parts,
+// head chunk first, summed in fp64.
+__global__ __launch_bounds__(256) void k_sum_records_join(const uint32_t* __restrict__ counters,
+                                                          const uint32_t* __restrict__ presort_gid,
+                                                          const float* __restrict__ part,
+                                                          const uint32_t* __restrict__ flags,
+                                                          float* __restrict__ gsum, uint32_t R) {
+  if (counters[CNT_ERR] & ERR_INVALID) return;
+  const uint32_t I = min(counters[CNT_I], R);
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if ((size_t)c * 64 >= I) return;
+  const uint32_t f = flags[c];
+  // the owner's tail is here unless it fills this chunk and continues
+  if (!(f & SR_IN) || ((f & SR_WHOLE) && (f & SR_OUT))) return;
+  uint32_t h = c;  // the head chunk: back over the whole chunks the owner fills
+  do {
+    h--;
+  } while ((flags[h] & SR_WHOLE) && (flags[h] & SR_IN));
+  // head: the owner begins there as its last owner ([1]); the later chunks hold it first ([0])
+  double acc[GRAD_REC];
+  const float* ph = part + ((size_t)h * 2 + 1) * GRAD_REC;
+#pragma unroll
+  for (int q = 0; q < GRAD_REC; q++) acc[q] = (double)ph[q];
+  for (uint32_t j = h + 1; j <= c; j++) {
+    const float* pj = part + (size_t)j * 2 * GRAD_REC;
+#pragma unroll
+    for (int q = 0; q < GRAD_REC; q++) acc[q] += (double)pj[q];
+  }
+  const size_t gid = presort_gid[(size_t)c * 64];
+#pragma unroll
+  for (int q = 0; q < GRAD_REC; q++) gsum[gid * GRAD_REC + q] = (float)acc[q];
+}
+
+static void launch_sum_records(const GaussianArgs& g, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
+                               float* gradrec, uint32_t R, hipStream_t st) {
+  if (GS_SUMREC_SLOTS) {
+    const uint32_t nch = (uint32_t)sumrec_chunks(R);
+    float* part = gradrec + (size_t)R * GRAD_REC;
+    uint32_t* fl = reinterpret_cast<uint32_t*>(part + (size_t)nch * 2 * GRAD_REC);
+    GS_LAUNCH("sum_records", k_sum_records_slots, dim3((nch + 3) / 4), dim3(256), 0, st, geo.counters,
+              bin.presort_gid, bin.slot_tile, img.tile_cut, img.cut_max, gradrec, geo.gsum, part, fl, R,
+              (uint32_t)g.P);
+    GS_LAUNCH("sum_records_join", k_sum_records_join, dim3((nch + 255) / 256), dim3(256), 0, st, geo.counters,
+              bin.presort_gid, part, fl, geo.gsum, R);
+    return;
+  }
+  GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
+            dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
+            img.cut_max, gradrec, geo.gsum, (uint32_t)g.P);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1319,25 +1474,19 @@ __global__ __launch_bounds__(256) void k_mean2d_grad(int P, const uint32_t* __re
 }
 
 void bwd_records(const GaussianArgs& g, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* gradrec,
-                 bool have_records, float* dmean2D, uint32_t acc, hipStream_t st) {
+                 uint32_t R, bool have_records, float* dmean2D, uint32_t acc, hipStream_t st) {
   if (g.P <= 0) return;
-  if (have_records)
-    GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
-              dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
-              img.cut_max, gradrec, geo.gsum, (uint32_t)g.P);
+  if (have_records) launch_sum_records(g, geo, bin, img, gradrec, R, st);
   if (dmean2D)
     GS_LAUNCH("mean2d_grad", k_mean2d_grad, dim3((g.P + 255) / 256), dim3(256), 0, st, g.P, geo.tiles, geo.gsum,
               dmean2D, acc);
 }
 
 void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
-                    const ImgPtrs& img, float* gradrec,
+                    const ImgPtrs& img, float* gradrec, uint32_t R,
                     bool have_records, const GradOut& out, hipStream_t st) {
   if (g.P <= 0) return;
-  if (have_records)
-    GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
-              dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
-              img.cut_max, gradrec, geo.gsum, (uint32_t)g.P);
+  if (have_records) launch_sum_records(g, geo, bin, img, gradrec, R, st);
   dim3 grid((g.P + 255) / 256), block(256);
   const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
   const size_t lds = sh ? (size_t)256 * (3 * g.M + 1) * sizeof(float) : 0;

@@ -179,8 +179,12 @@ __device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
 template <class Src, class Dst>
 __global__ __launch_bounds__(LB_THREADS) void k_scan_lb(Src src, Dst dst, const uint32_t* n_dev, uint32_t n_max,
                                                         uint64_t* __restrict__ status, uint32_t* tile_counter,
-                                                        uint32_t epoch, uint32_t* total_out, uint32_t* err_flag,
+                                                        uint32_t epoch, const uint32_t* epoch_seq,
+                                                        uint32_t* total_out, uint32_t* err_flag,
                                                         uint32_t spin_limit) {
+  // epoch_seq: a device word advanced once per forward before this launch -- a HIP graph replays
+  // the host epoch unchanged, and the previous replay's status words must not match this one's
+  if (epoch_seq) epoch = ((epoch + *epoch_seq) % ((1u << 30) - 1u)) + 1u;
   __shared__ uint32_t sh[4];
   __shared__ uint32_t s_tile, s_excl;
   // Tile ids: with a grid every CU can hold at once (LB_STATIC_MAX workgroups, a quarter of the
@@ -271,13 +275,15 @@ __global__ __launch_bounds__(LB_THREADS) void k_scan_lb(Src src, Dst dst, const 
 uint32_t next_scan_epoch();  // host: a fresh non-zero epoch per call (gs_api.hip)
 uint32_t scan_spin_limit();  // host: LB_SPIN_LIMIT unless a test lowered it (gs_api.hip)
 
-// host: one-launch scan.  status needs lb_tiles(n_max) u64; *tile_counter must be 0.
+// host: one-launch scan.  status needs lb_tiles(n_max) u64; *tile_counter must be 0; epoch_seq (or
+// null) is a device word that changes between calls a HIP graph may replay.
 template <class Src, class Dst>
 inline void scan_exclusive_lb(Src src, Dst dst, const uint32_t* n_dev, uint32_t n_max, uint64_t* status,
-                              uint32_t* tile_counter, uint32_t* total_out, uint32_t* err_flag, hipStream_t st) {
+                              uint32_t* tile_counter, uint32_t* total_out, uint32_t* err_flag, hipStream_t st,
+                              const uint32_t* epoch_seq, const char* name = "scan_lb") {
   const uint32_t tiles = lb_tiles(n_max);
-  GS_LAUNCH("scan_lb", (k_scan_lb<Src, Dst>), dim3(tiles), dim3(LB_THREADS), 0, st, src, dst, n_dev, n_max, status,
-            tile_counter, next_scan_epoch(), total_out, err_flag, scan_spin_limit());
+  GS_LAUNCH(name, (k_scan_lb<Src, Dst>), dim3(tiles), dim3(LB_THREADS), 0, st, src, dst, n_dev, n_max, status,
+            tile_counter, next_scan_epoch(), epoch_seq, total_out, err_flag, scan_spin_limit());
 }
 
 // simple functors

@@ -159,6 +159,23 @@ def test_bounded_view_parallel_step_replays_in_a_hip_graph(device, front):
         for a, b in zip(imgs, ref_imgs):
             assert torch.equal(a, b)
         bucket.flat.fill_(float("nan"))
+    # new parameter values between replays: the look-back scans' epochs advance on the device (the
+    # counter finalize's sequence word), so no status word of the previous replay is taken as this one's
+    gen = torch.Generator(device=device).manual_seed(77)
+    for _ in range(2):
+        with torch.no_grad():
+            for t, amp in zip(p[:3], (0.01, 0.05, 0.05)):  # means, SH, opacities (the counts stay below cap)
+                t.add_(amp * torch.randn(t.shape, device=device, generator=gen))
+        step(None)
+        torch.cuda.synchronize()
+        ref_flat = bucket.flat.clone()
+        ref_imgs = [t.clone() for t in imgs]
+        bucket.flat.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(bucket.flat, ref_flat)
+        for a, b in zip(imgs, ref_imgs):
+            assert torch.equal(a, b)
     assert bounded_status() == (0, 0)
     del graph
     bucket.close()
