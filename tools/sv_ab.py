@@ -23,6 +23,7 @@ ap.add_argument("--steps", type=int, default=100)
 ap.add_argument("--tag", default="")
 ap.add_argument("--bounded", action="store_true", help="bounded forwards (capacity = measured count x 1.1 + 4096)")
 ap.add_argument("--graph", action="store_true", help="bounded, and the step captured into a HIP graph")
+ap.add_argument("--no-prof", action="store_true", help="skip the per-kernel event pass (for an external profiler)")
 a = ap.parse_args()
 P, deg, W, H = WL[a.workload]
 dev = torch.device("cuda:0")
@@ -76,6 +77,9 @@ dt = (time.perf_counter() - t) / a.steps
 if cap is not None:
     bounded_status()  # raises if a view outgrew its capacity
     step = eager_step  # (per-kernel events: eager launches)
+if a.no_prof:
+    print(json.dumps({"tag": a.tag, "iters_s": round(1 / dt, 1), "ms": round(1e3 * dt, 4)}))
+    sys.exit(0)
 lib = _native.load()
 lib.gs_profile_reset()
 lib.gs_profile_enable(1)
