@@ -14,6 +14,9 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); parity tests through the C ABI")
     config.addinivalue_line("markers", "spawn_first: starts child processes on the GPU; runs before any other test, "
                                        "while this process has not touched the GPU")
+    # autograd accumulating one leaf's gradient from backwards on several streams (multi-stream
+    # views without a GradBucket): an error, not a warning, so no test relies on it
+    config.addinivalue_line("filterwarnings", "error:The AccumulateGrad node's stream does not match:UserWarning")
 
 
 def pytest_collection_modifyitems(config, items):

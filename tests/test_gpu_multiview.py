@@ -418,8 +418,15 @@ def test_prepared_views_equal_single_view_calls(device):
     rasts = [GaussianRasterizer(gs_scenes.raster_settings_for(c, 3, device=device)) for c in cams]
     dpix = gs_scenes.dl_dimage(H, W, seed=4, scale=1.0).to(device)
 
+    import gs_view_parallel as vp
+
     def run(prepared):
         leaves = [t.clone().requires_grad_(True) for t in (sc.means3D, sc.shs, sc.opacities, sc.scales, sc.rotations)]
+        # views on two streams write the leaves' gradients through a GradBucket (the rasterizer's
+        # gradient sink, ordered across the streams by the bucket), not through autograd's
+        # per-leaf accumulation, whose node would be shared between the streams
+        bucket = vp.GradBucket(leaves)
+        bucket.zero_grad()
         sts = [torch.cuda.Stream(device) for _ in range(2)]
         pre = (prepare_views(rasts, leaves[0], leaves[2], shs=leaves[1], scales=leaves[3], rotations=leaves[4],
                              streams=[sts[k % 2] for k in range(len(rasts))]) if prepared else [None] * len(rasts))
@@ -436,8 +443,11 @@ def test_prepared_views_equal_single_view_calls(device):
                 outs.append((img.detach().clone(), radii.clone(), m2.grad.clone()))
         for st in sts:
             main.wait_stream(st)
+        bucket.finalize()
         torch.cuda.synchronize()
-        return outs, [t.grad.clone() for t in leaves]
+        grads = [t.grad.clone() for t in leaves]
+        bucket.close()
+        return outs, grads
 
     a_out, a_grad = run(False)
     b_out, b_grad = run(True)
