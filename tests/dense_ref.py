@@ -50,12 +50,12 @@ def quat_R(q):
     ], -2)
 
 
-def render(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, bg, shs=None, deg=0, colors=None,
-           scales=None, rots=None, cov3D=None, mod=1.0):
-    """Returns (image [3, H, W], radii [P]).  All inputs double precision recommended."""
+def _prep(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, shs=None, deg=0, colors=None,
+          scales=None, rots=None, cov3D=None, mod=1.0):
+    """The per-Gaussian half (projection, EWA covariance, conic, radius, colour, tile rectangle)."""
     dt = means3D.dtype
     P = means3D.shape[0]
-    ones = torch.ones((P, 1), dtype=dt)
+    ones = torch.ones((P, 1), dtype=dt, device=means3D.device)
     ph = torch.cat([means3D, ones], 1)
     p_view = ph @ view
     p_hom = ph @ proj
@@ -93,7 +93,7 @@ def render(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, b
         disc = torch.clamp(mid * mid - det, min=0.1)
         lam = torch.maximum(mid + disc.sqrt(), mid - disc.sqrt())
         radius = torch.ceil(3 * lam.sqrt())
-    pix = ((ndc + 1) * torch.tensor([W, H], dtype=dt) - 1) * 0.5
+    pix = ((ndc + 1) * torch.tensor([W, H], dtype=dt, device=means3D.device) - 1) * 0.5
     if colors is None:
         d = means3D - campos[None]
         d = d / d.norm(dim=1, keepdim=True)
@@ -109,7 +109,19 @@ def render(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, b
         y1 = torch.clamp(((py_ + radius + 15) / 16).trunc(), 0, gy)
         visible = (tz > 0.2) & (det != 0) & ((x1 - x0) * (y1 - y0) > 0)
         radii = torch.where(visible, radius, torch.zeros_like(radius)).to(torch.int32)
-        order = [int(i) for i in torch.argsort(tz, stable=True) if visible[i]]
+        srt = torch.argsort(tz, stable=True)
+        order = srt[visible[srt]].tolist()
+    return dict(pix=pix, conic=conic, rgb=rgb, tz=tz, x0=x0, y0=y0, x1=x1, y1=y1, radii=radii, order=order)
+
+
+def render(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, bg, shs=None, deg=0, colors=None,
+           scales=None, rots=None, cov3D=None, mod=1.0):
+    """Returns (image [3, H, W], radii [P]).  All inputs double precision recommended."""
+    dt = means3D.dtype
+    q = _prep(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, shs, deg, colors, scales, rots,
+              cov3D, mod)
+    pix, conic, rgb, x0, y0, x1, y1, radii, order = (q[k] for k in ("pix", "conic", "rgb", "x0", "y0", "x1", "y1",
+                                                                     "radii", "order"))
     ys, xs = torch.meshgrid(torch.arange(H, dtype=dt), torch.arange(W, dtype=dt), indexing="ij")
     xs, ys = xs.reshape(-1), ys.reshape(-1)
     txi, tyi = (xs // 16), (ys // 16)
@@ -134,3 +146,49 @@ def render(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, b
         Tr = torch.where(ok, Tr * (1 - alpha), Tr)
     img = C + Tr[None] * bg[:, None]
     return img.reshape(3, H, W), radii
+
+
+def render_local(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, bg, shs=None, deg=0,
+                 colors=None, scales=None, rots=None, cov3D=None, mod=1.0, flag_rel=1e-5):
+    """The same function as render(), composited Gaussian by Gaussian over the pixels of its tile
+    rectangle only (gathers / index_add into the flat image), so it runs on a GPU at thousands of
+    Gaussians.  Also returns a bool [H, W] map of the pixels where some tested decision lies within
+    `flag_rel` (relative) of its threshold -- alpha vs 1/255, the tested T vs 1e-4 -- or power within
+    1e-6 of 0: there an fp32 evaluation may decide the other way."""
+    dt, dev = means3D.dtype, means3D.device
+    q = _prep(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, shs, deg, colors, scales, rots,
+              cov3D, mod)
+    pix, conic, rgb, x0, y0, x1, y1, radii, order = (q[k] for k in ("pix", "conic", "rgb", "x0", "y0", "x1", "y1",
+                                                                     "radii", "order"))
+    npx = W * H
+    Tr = torch.ones(npx, dtype=dt, device=dev)
+    C = torch.zeros((3, npx), dtype=dt, device=dev)
+    done = torch.zeros(npx, dtype=torch.bool, device=dev)
+    flag = torch.zeros(npx, dtype=torch.bool, device=dev)
+    rect = torch.stack([x0, y0, x1, y1], 1).to(torch.int64).cpu()
+    for i in order:
+        rx0, ry0, rx1, ry1 = (int(v) for v in rect[i])
+        xs = torch.arange(16 * rx0, min(16 * rx1, W), device=dev)
+        ys = torch.arange(16 * ry0, min(16 * ry1, H), device=dev)
+        yy, xx = torch.meshgrid(ys, xs, indexing="ij")
+        idx = (yy * W + xx).reshape(-1)
+        dx, dy = pix[i, 0] - xx.reshape(-1).to(dt), pix[i, 1] - yy.reshape(-1).to(dt)
+        power = -0.5 * (conic[i, 0] * dx * dx + conic[i, 2] * dy * dy) - conic[i, 1] * dx * dy
+        a_raw = opac[i] * torch.exp(power)
+        alpha = a_raw - torch.clamp(a_raw.detach() - 0.99, min=0.0)   # min(0.99, .), straight-through grad
+        Ti = Tr[idx]
+        with torch.no_grad():
+            live = ~done[idx]
+            ok = live & (power <= 0) & (alpha >= 1.0 / 255.0)
+            test_T = Ti * (1 - alpha)
+            stop = ok & (test_T < 1e-4)
+            near = live & (((alpha - 1.0 / 255.0).abs() <= flag_rel / 255.0) | (power.abs() <= 1e-6)
+                           | (ok & ((test_T - 1e-4).abs() <= flag_rel * 1e-4)))
+            flag[idx] |= near
+            ok = ok & ~stop
+            done[idx] |= stop
+        okf = ok.to(dt)
+        C = C.index_add(1, idx, rgb[i][:, None] * (alpha * Ti * okf)[None])
+        Tr = Tr.index_put((idx,), torch.where(ok, Ti * (1 - alpha), Ti))
+    img = C + Tr[None] * bg[:, None]
+    return img.reshape(3, H, W), radii, flag.reshape(H, W)

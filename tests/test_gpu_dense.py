@@ -1,0 +1,125 @@
+"""GPU parity against an independent reference: the HIP path (fp32, the library's default numerics)
+against tests/dense_ref.py -- a dense PyTorch restatement of the spec in
+fp64, differentiated by autograd, composited Gaussian by Gaussian over each tile rectangle on the
+same GPU (dense_ref.render_local) -- at thousands of Gaussians.  Neither the C oracle nor the
+kernels' hand-derived backward enter this comparison.
+
+Where a decision of the per-pixel loop sits at its threshold (alpha vs 1/255, the tested T vs 1e-4,
+power vs 0) fp32 and fp64 may decide differently; the reference flags those pixels (relative 1e-5
+of the threshold) and they are left out of the image check, and every Gaussian whose tile rectangle
+covers a flagged pixel -- or whose fp32 radius differs from the fp64 one, which moves its rectangle --
+is left out of the gradient checks.  The counts are bounded and printed.  Bounds: the image and the
+opacity and SH gradients 1e-5 * |ref| + 1e-5 * max|ref|.  The screen-position gradient and the
+covariance chain behind it (means2D, means3D, scales, rotations) sum terms with cancellation over
+hundreds of pixels, each term carrying the T recovered by repeated division, so fp32 itself moves
+them by about 1e-5 of their max: they get 1e-5 * |ref| + 1e-4 * max|ref| (the bound
+tests/test_gpu_parity.py uses for the chain against the oracle) and, as the conditioning check, a
+max deviation within 4x that of the same dense reference evaluated in fp32 (one other valid fp32
+order), plus 1e-5 of the max."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import dense_ref
+import gs_scenes
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def _check(got, ref, name, keep, frac=RTOL):
+    got = got.detach().double().cpu().numpy()[keep]
+    ref = ref.detach().double().cpu().numpy()[keep]
+    scale = float(np.abs(ref).max(initial=0.0))
+    d = np.abs(got - ref)
+    bad = d > RTOL * np.abs(ref) + frac * scale
+    print(f"{name}: max|d| {d.max(initial=0.0):.3e}  max|ref| {scale:.3e}")
+    assert not bad.any(), f"{name}: {int(bad.sum())}/{bad.size} beyond tol, max|d| {d.max():.3e}, max|ref| {scale:.3e}"
+
+
+CASES = [(2000, 3, 192, 128, 0.0, 41, None), (6000, 2, 320, 200, 0.3, 42, None),
+         # deeper overlap (scales up to 0.08): long walks, T-stop decisions
+         (12000, 3, 400, 256, 0.0, 43, (0.01, 0.08))]
+
+
+@pytest.mark.parametrize("P,deg,W,H,bgv,seed,scale_range", CASES,
+                         ids=["2k_sh3_192x128", "6k_sh2_320x200_bg", "12k_sh3_400x256_deep"])
+def test_hip_vs_dense_autograd_reference(device, P, deg, W, H, bgv, seed, scale_range):
+    from diff_gaussian_rasterization import GaussianRasterizer
+
+    cam = gs_scenes.identity_camera(W, H)
+    kw = {} if scale_range is None else {"scale_range": scale_range}
+    sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=seed, **kw)
+    dpix = gs_scenes.dl_dimage(H, W, seed=seed + 1, scale=1.0).to(device)
+    bg = torch.full((3,), bgv, device=device)
+
+    # the HIP path, fp32, as the reference adapter calls it
+    s = gs_scenes.raster_settings_for(cam, deg, bg=bg, device=device)
+    d = sc.to(device)
+    hip = {k: getattr(d, k).clone().requires_grad_(True) for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    hip["means2D"] = torch.zeros_like(hip["means3D"], requires_grad=True)
+    img, radii = GaussianRasterizer(s)(means3D=hip["means3D"], means2D=hip["means2D"], opacities=hip["opacities"],
+                                       shs=hip["shs"], scales=hip["scales"], rotations=hip["rotations"])
+    (img * dpix).sum().backward()
+
+    # the dense fp64 reference on the same GPU, gradients by autograd
+    f = torch.float64
+    ref = {k: getattr(d, k).to(f).clone().requires_grad_(True) for k in ("means3D", "opacities", "shs", "scales",
+                                                                          "rotations")}
+    ref["means2D"] = torch.zeros((P, 3), dtype=f, device=device, requires_grad=True)
+    rimg, rradii, flag = dense_ref.render_local(
+        ref["means3D"], ref["means2D"], ref["opacities"], cam.world_view_transform.to(device, f),
+        cam.full_proj_transform.to(device, f), cam.camera_center.to(device, f), math.tan(cam.FoVx / 2),
+        math.tan(cam.FoVy / 2), W, H, bg.to(f), shs=ref["shs"], deg=deg, scales=ref["scales"], rots=ref["rotations"])
+    (rimg * dpix.to(f)).sum().backward()
+    # the same reference in fp32: what fp32 alone does to each gradient on this scene
+    r32 = {k: getattr(d, k).clone().requires_grad_(True) for k in ("means3D", "opacities", "shs", "scales",
+                                                                   "rotations")}
+    r32["means2D"] = torch.zeros((P, 3), device=device, requires_grad=True)
+    img32, _, _ = dense_ref.render_local(
+        r32["means3D"], r32["means2D"], r32["opacities"], cam.world_view_transform.to(device),
+        cam.full_proj_transform.to(device), cam.camera_center.to(device), math.tan(cam.FoVx / 2),
+        math.tan(cam.FoVy / 2), W, H, bg, shs=r32["shs"], deg=deg, scales=r32["scales"], rots=r32["rotations"])
+    (img32 * dpix).sum().backward()
+    torch.cuda.synchronize()
+
+    # Gaussians whose radius (and so tile rectangle) differs between fp32 and fp64
+    rdiff = (radii.cpu() != rradii.cpu()).numpy()
+    assert rdiff.mean() <= 1e-3, f"{int(rdiff.sum())} radii differ"
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    fl = flag.cpu().numpy()
+    # tile rectangles (fp64 radii)
+    with torch.no_grad():
+        q = dense_ref._prep(ref["means3D"], ref["means2D"], ref["opacities"], cam.world_view_transform.to(device, f),
+                            cam.full_proj_transform.to(device, f), cam.camera_center.to(device, f),
+                            math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), W, H, shs=ref["shs"], deg=deg,
+                            scales=ref["scales"], rots=ref["rotations"])
+    rect = torch.stack([q["x0"], q["y0"], q["x1"], q["y1"]], 1).to(torch.int64).cpu().numpy()
+    # a Gaussian whose radius differs composites into a rectangle up to one tile wider in fp32
+    for i in np.nonzero(rdiff)[0]:
+        x0, y0, x1, y1 = rect[i]
+        fl[max(16 * y0 - 16, 0):16 * y1 + 16, max(16 * x0 - 16, 0):16 * x1 + 16] = True
+    tflag = np.zeros((gy, gx), bool)
+    for ty in range(gy):
+        for tx in range(gx):
+            tflag[ty, tx] = fl[16 * ty:16 * ty + 16, 16 * tx:16 * tx + 16].any()
+    touched = np.array([tflag[y0:y1, x0:x1].any() for x0, y0, x1, y1 in rect])
+    keep_g = ~(touched | rdiff)
+    keep_px = ~fl
+    print(f"\n[dense] flagged pixels {int(fl.sum())}/{fl.size}, excluded Gaussians {int((~keep_g).sum())}/{P}")
+    assert fl.mean() <= 0.02 and keep_g.mean() >= 0.9
+
+    _check(img.permute(1, 2, 0), rimg.permute(1, 2, 0), "image", keep_px)
+    for k in ("opacities", "shs"):
+        _check(hip[k].grad, ref[k].grad, f"d{k}", keep_g)
+    for k in ("means2D", "means3D", "scales", "rotations"):
+        _check(hip[k].grad, ref[k].grad, f"d{k}", keep_g, frac=1e-4)
+        g = hip[k].grad.detach().double().cpu().numpy()[keep_g]
+        r = ref[k].grad.detach().double().cpu().numpy()[keep_g]
+        n = r32[k].grad.detach().double().cpu().numpy()[keep_g]
+        d_gpu, d_32, scale = np.abs(g - r).max(initial=0.0), np.abs(n - r).max(initial=0.0), np.abs(r).max(initial=0.0)
+        print(f"  d{k}: max|hip - f64| {d_gpu:.3e}  max|dense f32 - f64| {d_32:.3e}  ({d_gpu / scale:.2e} of max)")
+        assert d_gpu <= 4.0 * d_32 + RTOL * scale, (k, d_gpu, d_32, scale)

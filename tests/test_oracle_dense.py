@@ -206,3 +206,28 @@ def test_oracle_f32_accumulation_probe(oracle):
         np.testing.assert_array_equal(again[k], g64[k])  # default restored
         _close(g32[k], g64[k], rtol=1e-4, frac=1e-5, name=k)
     assert any(not np.array_equal(g32[k], g64[k]) for k in ("dmeans2D", "dsh", "dscales"))
+
+
+def test_dense_local_compositor_equals_dense():
+    """dense_ref.render_local (the rect-local compositor the GPU test runs at thousands of Gaussians)
+    is the same function as dense_ref.render: image and every autograd gradient agree to fp64
+    round-off on a small scene."""
+    cam, sc = _scene(60, 70, 45, 3, seed=5)
+    d = torch.float64
+    outs = []
+    for fn in (dense_ref.render, dense_ref.render_local):
+        m3 = sc.means3D.to(d).requires_grad_(True)
+        op = sc.opacities.to(d).requires_grad_(True)
+        shs = sc.shs.to(d).requires_grad_(True)
+        scl = sc.scales.to(d).requires_grad_(True)
+        rot = sc.rotations.to(d).requires_grad_(True)
+        m2 = torch.zeros((60, 3), dtype=d, requires_grad=True)
+        res = fn(m3, m2, op, cam.world_view_transform.to(d), cam.full_proj_transform.to(d), cam.camera_center.to(d),
+                 math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), 70, 45, torch.full((3,), 0.2, dtype=d), shs=shs,
+                 deg=3, scales=scl, rots=rot)
+        img = res[0]
+        dpix = gs_scenes.dl_dimage(45, 70, seed=9, scale=1.0).to(d)
+        (img * dpix).sum().backward()
+        outs.append([img.detach(), m3.grad, m2.grad, op.grad, shs.grad, scl.grad, rot.grad])
+    for a, b in zip(*outs):
+        assert torch.allclose(a, b, rtol=1e-10, atol=1e-13)
