@@ -9,13 +9,13 @@ power vs 0) fp32 and fp64 may decide differently; the reference flags those pixe
 of the threshold) and they are left out of the image check, and every Gaussian whose tile rectangle
 covers a flagged pixel -- or whose fp32 radius differs from the fp64 one, which moves its rectangle --
 is left out of the gradient checks.  The counts are bounded and printed.  Bounds: the image and the
-opacity and SH gradients 1e-5 * |ref| + 1e-5 * max|ref|.  The screen-position gradient and the
-covariance chain behind it (means2D, means3D, scales, rotations) sum terms with cancellation over
-hundreds of pixels, each term carrying the T recovered by repeated division, so fp32 itself moves
-them by about 1e-5 of their max: they get 1e-5 * |ref| + 1e-4 * max|ref| (the bound
-tests/test_gpu_parity.py uses for the chain against the oracle) and, as the conditioning check, a
-max deviation within 4x that of the same dense reference evaluated in fp32 (one other valid fp32
-order), plus 1e-5 of the max."""
+opacity and colour (SH or precomputed) gradients 1e-5 * |ref| + 1e-5 * max|ref|.  The
+screen-position gradient and the covariance chain behind it (means2D, means3D, scales, rotations,
+cov3D) sum terms with cancellation over hundreds of pixels, each term carrying the T recovered by
+repeated division, so fp32 itself moves them by about 1e-5 of their max: they get 1e-5 * |ref| +
+1e-4 * max|ref| (the bound tests/test_gpu_parity.py uses for the chain against the oracle) and, as
+the conditioning check, a max deviation within 4x that of the same dense reference evaluated in
+fp32 (one other valid fp32 order), plus 1e-5 of the max."""
 import math
 
 import numpy as np
@@ -28,6 +28,7 @@ import gs_scenes
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5
+CHAIN = ("means2D", "means3D", "scales", "rotations", "cov3D")
 
 
 def _check(got, ref, name, keep, frac=RTOL):
@@ -40,49 +41,34 @@ def _check(got, ref, name, keep, frac=RTOL):
     assert not bad.any(), f"{name}: {int(bad.sum())}/{bad.size} beyond tol, max|d| {d.max():.3e}, max|ref| {scale:.3e}"
 
 
-CASES = [(2000, 3, 192, 128, 0.0, 41, None), (6000, 2, 320, 200, 0.3, 42, None),
-         # deeper overlap (scales up to 0.08): long walks, T-stop decisions
-         (12000, 3, 400, 256, 0.0, 43, (0.01, 0.08))]
+def _dense(cam, leaves, W, H, bg, deg, mod, dtype, device):
+    """dense_ref.render_local on copies of `leaves` in `dtype` (their grads by autograd)."""
+    t = {k: v.detach().to(dtype).clone().requires_grad_(True) for k, v in leaves.items()}
+    res = dense_ref.render_local(
+        t["means3D"], t["means2D"], t["opacities"], cam.world_view_transform.to(device, dtype),
+        cam.full_proj_transform.to(device, dtype), cam.camera_center.to(device, dtype), math.tan(cam.FoVx / 2),
+        math.tan(cam.FoVy / 2), W, H, bg.to(dtype), shs=t.get("shs"), deg=deg, colors=t.get("colors"),
+        scales=t.get("scales"), rots=t.get("rotations"), cov3D=t.get("cov3D"), mod=mod)
+    return t, res
 
 
-@pytest.mark.parametrize("P,deg,W,H,bgv,seed,scale_range", CASES,
-                         ids=["2k_sh3_192x128", "6k_sh2_320x200_bg", "12k_sh3_400x256_deep"])
-def test_hip_vs_dense_autograd_reference(device, P, deg, W, H, bgv, seed, scale_range):
+def _run_and_compare(cam, leaves, W, H, bg, deg=0, mod=1.0, seed=0, device=None):
     from diff_gaussian_rasterization import GaussianRasterizer
 
-    cam = gs_scenes.identity_camera(W, H)
-    kw = {} if scale_range is None else {"scale_range": scale_range}
-    sc = gs_scenes.random_gaussians(P, deg, cam=cam, seed=seed, **kw)
+    P = leaves["means3D"].shape[0]
     dpix = gs_scenes.dl_dimage(H, W, seed=seed + 1, scale=1.0).to(device)
-    bg = torch.full((3,), bgv, device=device)
-
     # the HIP path, fp32, as the reference adapter calls it
-    s = gs_scenes.raster_settings_for(cam, deg, bg=bg, device=device)
-    d = sc.to(device)
-    hip = {k: getattr(d, k).clone().requires_grad_(True) for k in ("means3D", "opacities", "shs", "scales", "rotations")}
-    hip["means2D"] = torch.zeros_like(hip["means3D"], requires_grad=True)
+    s = gs_scenes.raster_settings_for(cam, deg, bg=bg, scale_modifier=mod, device=device)
+    hip = {k: v.detach().clone().requires_grad_(True) for k, v in leaves.items()}
+    kw = {"shs": hip.get("shs"), "colors_precomp": hip.get("colors"), "scales": hip.get("scales"),
+          "rotations": hip.get("rotations"), "cov3D_precomp": hip.get("cov3D")}
     img, radii = GaussianRasterizer(s)(means3D=hip["means3D"], means2D=hip["means2D"], opacities=hip["opacities"],
-                                       shs=hip["shs"], scales=hip["scales"], rotations=hip["rotations"])
+                                       **{k: v for k, v in kw.items() if v is not None})
     (img * dpix).sum().backward()
-
-    # the dense fp64 reference on the same GPU, gradients by autograd
-    f = torch.float64
-    ref = {k: getattr(d, k).to(f).clone().requires_grad_(True) for k in ("means3D", "opacities", "shs", "scales",
-                                                                          "rotations")}
-    ref["means2D"] = torch.zeros((P, 3), dtype=f, device=device, requires_grad=True)
-    rimg, rradii, flag = dense_ref.render_local(
-        ref["means3D"], ref["means2D"], ref["opacities"], cam.world_view_transform.to(device, f),
-        cam.full_proj_transform.to(device, f), cam.camera_center.to(device, f), math.tan(cam.FoVx / 2),
-        math.tan(cam.FoVy / 2), W, H, bg.to(f), shs=ref["shs"], deg=deg, scales=ref["scales"], rots=ref["rotations"])
-    (rimg * dpix.to(f)).sum().backward()
-    # the same reference in fp32: what fp32 alone does to each gradient on this scene
-    r32 = {k: getattr(d, k).clone().requires_grad_(True) for k in ("means3D", "opacities", "shs", "scales",
-                                                                   "rotations")}
-    r32["means2D"] = torch.zeros((P, 3), device=device, requires_grad=True)
-    img32, _, _ = dense_ref.render_local(
-        r32["means3D"], r32["means2D"], r32["opacities"], cam.world_view_transform.to(device),
-        cam.full_proj_transform.to(device), cam.camera_center.to(device), math.tan(cam.FoVx / 2),
-        math.tan(cam.FoVy / 2), W, H, bg, shs=r32["shs"], deg=deg, scales=r32["scales"], rots=r32["rotations"])
+    # the dense reference on the same GPU, fp64 (the reference) and fp32 (what fp32 alone does)
+    ref, (rimg, rradii, flag) = _dense(cam, leaves, W, H, bg, deg, mod, torch.float64, device)
+    (rimg * dpix.double()).sum().backward()
+    r32, (img32, _, _) = _dense(cam, leaves, W, H, bg, deg, mod, torch.float32, device)
     (img32 * dpix).sum().backward()
     torch.cuda.synchronize()
 
@@ -91,12 +77,13 @@ def test_hip_vs_dense_autograd_reference(device, P, deg, W, H, bgv, seed, scale_
     assert rdiff.mean() <= 1e-3, f"{int(rdiff.sum())} radii differ"
     gx, gy = (W + 15) // 16, (H + 15) // 16
     fl = flag.cpu().numpy()
-    # tile rectangles (fp64 radii)
     with torch.no_grad():
+        f = torch.float64
         q = dense_ref._prep(ref["means3D"], ref["means2D"], ref["opacities"], cam.world_view_transform.to(device, f),
                             cam.full_proj_transform.to(device, f), cam.camera_center.to(device, f),
-                            math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), W, H, shs=ref["shs"], deg=deg,
-                            scales=ref["scales"], rots=ref["rotations"])
+                            math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2), W, H, shs=ref.get("shs"), deg=deg,
+                            colors=ref.get("colors"), scales=ref.get("scales"), rots=ref.get("rotations"),
+                            cov3D=ref.get("cov3D"), mod=mod)
     rect = torch.stack([q["x0"], q["y0"], q["x1"], q["y1"]], 1).to(torch.int64).cpu().numpy()
     # a Gaussian whose radius differs composites into a rectangle up to one tile wider in fp32
     for i in np.nonzero(rdiff)[0]:
@@ -108,14 +95,14 @@ def test_hip_vs_dense_autograd_reference(device, P, deg, W, H, bgv, seed, scale_
             tflag[ty, tx] = fl[16 * ty:16 * ty + 16, 16 * tx:16 * tx + 16].any()
     touched = np.array([tflag[y0:y1, x0:x1].any() for x0, y0, x1, y1 in rect])
     keep_g = ~(touched | rdiff)
-    keep_px = ~fl
     print(f"\n[dense] flagged pixels {int(fl.sum())}/{fl.size}, excluded Gaussians {int((~keep_g).sum())}/{P}")
     assert fl.mean() <= 0.02 and keep_g.mean() >= 0.9
 
-    _check(img.permute(1, 2, 0), rimg.permute(1, 2, 0), "image", keep_px)
-    for k in ("opacities", "shs"):
-        _check(hip[k].grad, ref[k].grad, f"d{k}", keep_g)
-    for k in ("means2D", "means3D", "scales", "rotations"):
+    _check(img.permute(1, 2, 0), rimg.permute(1, 2, 0), "image", ~fl)
+    for k in hip:
+        if k not in CHAIN:
+            _check(hip[k].grad, ref[k].grad, f"d{k}", keep_g)
+            continue
         _check(hip[k].grad, ref[k].grad, f"d{k}", keep_g, frac=1e-4)
         g = hip[k].grad.detach().double().cpu().numpy()[keep_g]
         r = ref[k].grad.detach().double().cpu().numpy()[keep_g]
@@ -123,3 +110,46 @@ def test_hip_vs_dense_autograd_reference(device, P, deg, W, H, bgv, seed, scale_
         d_gpu, d_32, scale = np.abs(g - r).max(initial=0.0), np.abs(n - r).max(initial=0.0), np.abs(r).max(initial=0.0)
         print(f"  d{k}: max|hip - f64| {d_gpu:.3e}  max|dense f32 - f64| {d_32:.3e}  ({d_gpu / scale:.2e} of max)")
         assert d_gpu <= 4.0 * d_32 + RTOL * scale, (k, d_gpu, d_32, scale)
+
+
+CASES = [(2000, 3, 192, 128, 0.0, 41, None), (6000, 2, 320, 200, 0.3, 42, None),
+         # deeper overlap (scales up to 0.08): long walks, T-stop decisions
+         (12000, 3, 400, 256, 0.0, 43, (0.01, 0.08))]
+
+
+@pytest.mark.parametrize("P,deg,W,H,bgv,seed,scale_range", CASES,
+                         ids=["2k_sh3_192x128", "6k_sh2_320x200_bg", "12k_sh3_400x256_deep"])
+def test_hip_vs_dense_autograd_reference(device, P, deg, W, H, bgv, seed, scale_range):
+    cam = gs_scenes.identity_camera(W, H)
+    kw = {} if scale_range is None else {"scale_range": scale_range}
+    d = gs_scenes.random_gaussians(P, deg, cam=cam, seed=seed, **kw).to(device)
+    leaves = {k: getattr(d, k) for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    leaves["means2D"] = torch.zeros_like(d.means3D)
+    _run_and_compare(cam, leaves, W, H, torch.full((3,), bgv, device=device), deg=deg, seed=seed, device=device)
+
+
+def test_hip_vs_dense_precomputed_colors_and_cov3d(device):
+    """colors_precomp and cov3D_precomp (upper-triangular xx, xy, xz, yy, yz, zz) instead of SH and
+    scale / rotation, a coloured background."""
+    W, H, P = 256, 160, 4000
+    cam = gs_scenes.identity_camera(W, H)
+    d = gs_scenes.random_gaussians(P, 0, cam=cam, seed=44).to(device)
+    g = torch.Generator(device=device).manual_seed(45)
+    with torch.no_grad():
+        R = dense_ref.quat_R(d.rotations)
+        L = R * d.scales[:, None, :]
+        S = L @ L.transpose(1, 2)
+        cov = torch.stack([S[:, 0, 0], S[:, 0, 1], S[:, 0, 2], S[:, 1, 1], S[:, 1, 2], S[:, 2, 2]], 1).contiguous()
+    leaves = dict(means3D=d.means3D, means2D=torch.zeros_like(d.means3D), opacities=d.opacities,
+                  colors=torch.rand((P, 3), device=device, generator=g), cov3D=cov)
+    _run_and_compare(cam, leaves, W, H, torch.tensor([0.1, 0.2, 0.3], device=device), seed=44, device=device)
+
+
+def test_hip_vs_dense_scale_modifier(device):
+    """scale_modifier 0.7 on SH1 rows."""
+    W, H, P = 256, 160, 4000
+    cam = gs_scenes.identity_camera(W, H)
+    d = gs_scenes.random_gaussians(P, 1, cam=cam, seed=46).to(device)
+    leaves = {k: getattr(d, k) for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    leaves["means2D"] = torch.zeros_like(d.means3D)
+    _run_and_compare(cam, leaves, W, H, torch.zeros(3, device=device), deg=1, mod=0.7, seed=46, device=device)
