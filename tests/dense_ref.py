@@ -149,12 +149,13 @@ def render(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, b
 
 
 def render_local(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, bg, shs=None, deg=0,
-                 colors=None, scales=None, rots=None, cov3D=None, mod=1.0, flag_rel=1e-5):
+                 colors=None, scales=None, rots=None, cov3D=None, mod=1.0, flag_rel=1e-5, flag_T_rel=None):
     """The same function as render(), composited Gaussian by Gaussian over the pixels of its tile
     rectangle only (gathers / index_add into the flat image), so it runs on a GPU at thousands of
     Gaussians.  Also returns a bool [H, W] map of the pixels where some tested decision lies within
-    `flag_rel` (relative) of its threshold -- alpha vs 1/255, the tested T vs 1e-4 -- or power within
-    1e-6 of 0: there an fp32 evaluation may decide the other way."""
+    `flag_rel` (relative) of its threshold -- alpha vs 1/255, the tested T vs 1e-4 (`flag_T_rel`
+    if given) -- or power within 1e-6 of 0: there an fp32 evaluation may decide the other way."""
+    flag_T_rel = flag_rel if flag_T_rel is None else flag_T_rel
     dt, dev = means3D.dtype, means3D.device
     q = _prep(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W, H, shs, deg, colors, scales, rots,
               cov3D, mod)
@@ -183,7 +184,7 @@ def render_local(means3D, means2D, opac, view, proj, campos, tanfovx, tanfovy, W
             test_T = Ti * (1 - alpha)
             stop = ok & (test_T < 1e-4)
             near = live & (((alpha - 1.0 / 255.0).abs() <= flag_rel / 255.0) | (power.abs() <= 1e-6)
-                           | (ok & ((test_T - 1e-4).abs() <= flag_rel * 1e-4)))
+                           | (ok & ((test_T - 1e-4).abs() <= flag_T_rel * 1e-4)))
             flag[idx] |= near
             ok = ok & ~stop
             done[idx] |= stop

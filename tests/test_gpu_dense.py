@@ -6,16 +6,17 @@ kernels' hand-derived backward enter this comparison.
 
 Where a decision of the per-pixel loop sits at its threshold (alpha vs 1/255, the tested T vs 1e-4,
 power vs 0) fp32 and fp64 may decide differently; the reference flags those pixels (relative 1e-5
-of the threshold) and they are left out of the image check, and every Gaussian whose tile rectangle
-covers a flagged pixel -- or whose fp32 radius differs from the fp64 one, which moves its rectangle --
-is left out of the gradient checks.  The counts are bounded and printed.  Bounds: the image and the
+of the threshold) and they are left out of the image check; the backward runs with dL/dpix zeroed
+there (a pixel with dL/dpix = 0 adds nothing to any gradient, whatever it decided), and a Gaussian
+whose fp32 radius differs from the fp64 one (which moves its rectangle) is left out of the gradient
+checks.  The counts are bounded and printed.  Bounds: the image and the
 opacity and colour (SH or precomputed) gradients 1e-5 * |ref| + 1e-5 * max|ref|.  The
 screen-position gradient and the covariance chain behind it (means2D, means3D, scales, rotations,
 cov3D) sum terms with cancellation over hundreds of pixels, each term carrying the T recovered by
 repeated division, so fp32 itself moves them by about 1e-5 of their max: they get 1e-5 * |ref| +
-1e-4 * max|ref| (the bound tests/test_gpu_parity.py uses for the chain against the oracle) and, as
-the conditioning check, a max deviation within 4x that of the same dense reference evaluated in
-fp32 (one other valid fp32 order), plus 1e-5 of the max."""
+1e-4 * max|ref| (the bound tests/test_gpu_parity.py uses for the chain against the oracle) and,
+as the conditioning check, a max deviation within 4x that of the same
+dense reference evaluated in fp32 (one other valid fp32 order), plus 1e-5 of the max."""
 import math
 
 import numpy as np
@@ -41,18 +42,20 @@ def _check(got, ref, name, keep, frac=RTOL):
     assert not bad.any(), f"{name}: {int(bad.sum())}/{bad.size} beyond tol, max|d| {d.max():.3e}, max|ref| {scale:.3e}"
 
 
-def _dense(cam, leaves, W, H, bg, deg, mod, dtype, device):
+def _dense(cam, leaves, W, H, bg, deg, mod, dtype, device, flag_rel=1e-5, flag_T_rel=None):
     """dense_ref.render_local on copies of `leaves` in `dtype` (their grads by autograd)."""
     t = {k: v.detach().to(dtype).clone().requires_grad_(True) for k, v in leaves.items()}
     res = dense_ref.render_local(
         t["means3D"], t["means2D"], t["opacities"], cam.world_view_transform.to(device, dtype),
         cam.full_proj_transform.to(device, dtype), cam.camera_center.to(device, dtype), math.tan(cam.FoVx / 2),
         math.tan(cam.FoVy / 2), W, H, bg.to(dtype), shs=t.get("shs"), deg=deg, colors=t.get("colors"),
-        scales=t.get("scales"), rots=t.get("rotations"), cov3D=t.get("cov3D"), mod=mod)
+        scales=t.get("scales"), rots=t.get("rotations"), cov3D=t.get("cov3D"), mod=mod, flag_rel=flag_rel,
+        flag_T_rel=flag_T_rel)
     return t, res
 
 
-def _run_and_compare(cam, leaves, W, H, bg, deg=0, mod=1.0, seed=0, device=None):
+def _run_and_compare(cam, leaves, W, H, bg, deg=0, mod=1.0, seed=0, device=None, chain_frac=1e-4, flag_rel=1e-5,
+                     flag_T_rel=None, noise_check=True):
     from diff_gaussian_rasterization import GaussianRasterizer
 
     P = leaves["means3D"].shape[0]
@@ -64,18 +67,14 @@ def _run_and_compare(cam, leaves, W, H, bg, deg=0, mod=1.0, seed=0, device=None)
           "rotations": hip.get("rotations"), "cov3D_precomp": hip.get("cov3D")}
     img, radii = GaussianRasterizer(s)(means3D=hip["means3D"], means2D=hip["means2D"], opacities=hip["opacities"],
                                        **{k: v for k, v in kw.items() if v is not None})
-    (img * dpix).sum().backward()
     # the dense reference on the same GPU, fp64 (the reference) and fp32 (what fp32 alone does)
-    ref, (rimg, rradii, flag) = _dense(cam, leaves, W, H, bg, deg, mod, torch.float64, device)
-    (rimg * dpix.double()).sum().backward()
+    ref, (rimg, rradii, flag) = _dense(cam, leaves, W, H, bg, deg, mod, torch.float64, device, flag_rel,
+                                       flag_T_rel)
     r32, (img32, _, _) = _dense(cam, leaves, W, H, bg, deg, mod, torch.float32, device)
-    (img32 * dpix).sum().backward()
-    torch.cuda.synchronize()
 
     # Gaussians whose radius (and so tile rectangle) differs between fp32 and fp64
     rdiff = (radii.cpu() != rradii.cpu()).numpy()
     assert rdiff.mean() <= 1e-3, f"{int(rdiff.sum())} radii differ"
-    gx, gy = (W + 15) // 16, (H + 15) // 16
     fl = flag.cpu().numpy()
     with torch.no_grad():
         f = torch.float64
@@ -89,27 +88,31 @@ def _run_and_compare(cam, leaves, W, H, bg, deg=0, mod=1.0, seed=0, device=None)
     for i in np.nonzero(rdiff)[0]:
         x0, y0, x1, y1 = rect[i]
         fl[max(16 * y0 - 16, 0):16 * y1 + 16, max(16 * x0 - 16, 0):16 * x1 + 16] = True
-    tflag = np.zeros((gy, gx), bool)
-    for ty in range(gy):
-        for tx in range(gx):
-            tflag[ty, tx] = fl[16 * ty:16 * ty + 16, 16 * tx:16 * tx + 16].any()
-    touched = np.array([tflag[y0:y1, x0:x1].any() for x0, y0, x1, y1 in rect])
-    keep_g = ~(touched | rdiff)
-    print(f"\n[dense] flagged pixels {int(fl.sum())}/{fl.size}, excluded Gaussians {int((~keep_g).sum())}/{P}")
-    assert fl.mean() <= 0.02 and keep_g.mean() >= 0.9
+    print(f"\n[dense] flagged pixels {int(fl.sum())}/{fl.size}, radii differing {int(rdiff.sum())}/{P}")
+    assert fl.mean() <= 0.02
+    # the backward runs with dL/dpix zeroed at the flagged pixels: a pixel with dL/dpix = 0 adds
+    # nothing to any gradient, so a decision that fp32 and fp64 take differently there changes none
+    keep_px = torch.from_numpy(~fl).to(device)
+    dpm = dpix * keep_px[None]
+    (img * dpm).sum().backward()
+    (rimg * dpm.double()).sum().backward()
+    (img32 * dpm).sum().backward()
+    torch.cuda.synchronize()
+    keep_g = ~rdiff
 
     _check(img.permute(1, 2, 0), rimg.permute(1, 2, 0), "image", ~fl)
     for k in hip:
         if k not in CHAIN:
             _check(hip[k].grad, ref[k].grad, f"d{k}", keep_g)
             continue
-        _check(hip[k].grad, ref[k].grad, f"d{k}", keep_g, frac=1e-4)
+        _check(hip[k].grad, ref[k].grad, f"d{k}", keep_g, frac=chain_frac)
         g = hip[k].grad.detach().double().cpu().numpy()[keep_g]
         r = ref[k].grad.detach().double().cpu().numpy()[keep_g]
         n = r32[k].grad.detach().double().cpu().numpy()[keep_g]
         d_gpu, d_32, scale = np.abs(g - r).max(initial=0.0), np.abs(n - r).max(initial=0.0), np.abs(r).max(initial=0.0)
         print(f"  d{k}: max|hip - f64| {d_gpu:.3e}  max|dense f32 - f64| {d_32:.3e}  ({d_gpu / scale:.2e} of max)")
-        assert d_gpu <= 4.0 * d_32 + RTOL * scale, (k, d_gpu, d_32, scale)
+        if noise_check:
+            assert d_gpu <= 4.0 * d_32 + RTOL * scale, (k, d_gpu, d_32, scale)
 
 
 CASES = [(2000, 3, 192, 128, 0.0, 41, None), (6000, 2, 320, 200, 0.3, 42, None),
@@ -153,3 +156,29 @@ def test_hip_vs_dense_scale_modifier(device):
     leaves = {k: getattr(d, k) for k in ("means3D", "opacities", "shs", "scales", "rotations")}
     leaves["means2D"] = torch.zeros_like(d.means3D)
     _run_and_compare(cam, leaves, W, H, torch.zeros(3, device=device), deg=1, mod=0.7, seed=46, device=device)
+
+
+def test_hip_vs_dense_large_and_needle_splats(device):
+    """tests/test_gpu_parity.py's large-splat scene with needles (one axis / 60): 60 splats spanning
+    dozens of tiles among 3000 small ones.
+    The forward decisions are less well conditioned here too: a needle's falloff is a quadratic form
+    with large, nearly cancelling conic terms (power carries ~1e-4 relative fp32 error), and the
+    large splats are opaque (alpha up to the 0.99 clamp, where one ulp of alpha is 1e-5 of 1 - alpha,
+    so T drifts ~1e-4 relative along a walk): alpha decisions within 2e-4 and T-stop decisions
+    within 1e-3 (relative) of their thresholds are flagged.  Every Gaussian, needles included, is
+    held to the fixed bounds -- for the covariance chain the 2e-3 of max that the oracle test gives
+    needles (measured: means3D / scales 5e-5 / 8e-5, rotations 5e-4 of max); the 4x-of-dense-fp32
+    check is left out here: the kernels follow
+    upstream's covariance-backward formulas, whose fp32 conditioning on needles differs from that of
+    the autograd graph the dense fp32 run differentiates (against the oracle's own fp32 order they
+    stay within 4x, tests/test_gpu_parity.py::test_needle_splats_conditioning)."""
+    W, H = 640, 360
+    cam = gs_scenes.identity_camera(W, H)
+    small = gs_scenes.random_gaussians(3000, 2, cam=cam, seed=21)
+    big = gs_scenes.random_gaussians(60, 2, cam=cam, seed=22, scale_range=(0.3, 1.5), z_range=(2.0, 4.0))
+    big.scales[::3, 0] /= 60.0
+    d = gs_scenes.concat_scenes(small, big).to(device)
+    leaves = {k: getattr(d, k) for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    leaves["means2D"] = torch.zeros_like(d.means3D)
+    _run_and_compare(cam, leaves, W, H, torch.tensor([0.1, 0.2, 0.3], device=device), deg=2, seed=23, device=device,
+                     flag_rel=2e-4, flag_T_rel=1e-3, chain_frac=2e-3, noise_check=False)
