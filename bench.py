@@ -524,8 +524,9 @@ def main():
                    "render_exp2": "exact-polynomial" if os.environ.get("GSRAST_EXACT_EXP", "0") not in ("", "0")
                    else "hardware v_exp_f32",
                    "parallelism": f"view-parallel dp{world}" +
-                   (f" + RCCL all-reduce of 59 f32/Gaussian in {bucket.chunks} row chunks overlapped with the "
-                    "per-Gaussian pass" if world > 1 else "")},
+                   (f" + {'RCCL' if backend == 'nccl' else backend} all-reduce of 59 f32/Gaussian in "
+                    f"{bucket.chunks} row chunks overlapped with the per-Gaussian pass" if world > 1 else ""),
+                   "backend": backend if world > 1 else None},
         "render_mpix_s": round(W * H / t_render / 1e6, 1),
         "render_ms": round(1e3 * t_render, 4),
         "render_batched": render_batched,

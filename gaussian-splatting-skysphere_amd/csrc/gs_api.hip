@@ -135,8 +135,8 @@ static bool validate(int P, int D, int M, int W, int H, const float* means3D, co
 // ------------------------------------------------------------------------------------------
 // debug export kernel
 // ------------------------------------------------------------------------------------------
-// entries past the list's device count (a bounded buffer's capacity, or the instances the depth
-// slabs skipped) are not written by the forward: exported as ~0 (no gather through them)
+// entries past the list's device count (past a bounded buffer's capacity) are not written by the
+// forward: exported as ~0 (no gather through them)
 __global__ void k_export_list(uint32_t I, const uint32_t* counters, const uint32_t* point_list, const uint32_t* ids,
                               uint32_t* out) {
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
@@ -176,26 +176,6 @@ __global__ void k_export_splat(int P, const float4* splat, float* xy, float* co,
 using namespace gs;
 
 namespace gs {
-static std::atomic<int> g_slabs{-1};  // -1: not yet read from GSRAST_SLABS (0 off, 1 by size, 2 always)
-int slab_setting() {
-  int v = g_slabs.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("GSRAST_SLABS");
-    v = e ? atoi(e) : 0;  // off: at C5 they measured 488-504 it/s against 497-509 without
-    v = v < 0 ? 0 : (v > 2 ? 2 : v);
-    g_slabs.store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
-// the near slab's share of the instances, in 1/64ths (GSRAST_SLAB_NEAR64, default 16: a quarter)
-uint32_t slab_target(size_t I) {
-  static const uint32_t n64 = [] {
-    const char* e = getenv("GSRAST_SLAB_NEAR64");
-    int v = e ? atoi(e) : 16;
-    return (uint32_t)(v < 1 ? 1 : (v > 63 ? 63 : v));
-  }();
-  return (uint32_t)(((uint64_t)I * n64) >> 6);
-}
 static std::atomic<int> g_exact_exp{-1};  // -1: not yet read from GSRAST_EXACT_EXP
 bool exact_exp() {
   int v = g_exact_exp.load(std::memory_order_relaxed);
@@ -281,18 +261,21 @@ static bool read_view_totals(const uint32_t* w, int v, int views, long long* num
   return true;
 }
 
-// Error flags of the last forward's sorts / scans, per device (not per thread: the backward of a
+// Error flags of the last forwards' sorts / scans, per device (not per thread: the backward of a
 // forward runs on the autograd engine's device thread).  Each gs_forward_render's render kernel
-// stores them into one of two pinned words (alternating), behind an event; once its own launches
-// are queued, the forward checks the previous forward's word, and the next backward or forward
-// call checks this one (ERR_LOOKBACK: a look-back wait ran out), so no host wait idles the GPU.
+// stores them into a pinned word of a small ring, behind an event; once its own launches are
+// queued, a forward checks the forwards queued before it, and the next backward or forward call
+// checks this one (ERR_LOOKBACK: a look-back wait ran out), so no host wait idles the GPU.
+// A forward reserves its word and its sequence number in one critical section; reusing a word
+// first checks the forward that last held it, so concurrent host threads never share or drop one.
+constexpr int ORDER_RING = 8;
 struct OrderFlags {
   std::mutex mu;
-  uint32_t* host = nullptr;  // words 0 and 16: the ordering error flags of alternate forwards
+  uint32_t* host = nullptr;  // words 16 k (k < ORDER_RING): the ordering error flags of forward seq % ORDER_RING
   uint32_t* dev = nullptr;   // device pointer of `host`
-  hipEvent_t ev[2] = {};
-  unsigned long long seq = 0;   // forwards queued so far
-  long long pending = -1;       // the queued forward whose flags are not checked yet
+  hipEvent_t ev[ORDER_RING] = {};
+  int state[ORDER_RING] = {};  // 0 free, 1 reserved (render not queued yet), 2 queued, not checked
+  unsigned long long seq = 0;  // forwards that reserved a word so far
 };
 static OrderFlags g_order[64];
 
@@ -303,11 +286,10 @@ static OrderFlags* order_flags() {
   return &g_order[dev];
 }
 
-// check the pending forward's flags (waits for its render kernel); true: failed (error set)
-static bool check_order_flags_locked(OrderFlags& o) {
-  if (o.pending < 0) return false;
-  const int k = (int)(o.pending & 1);
-  o.pending = -1;
+// check ring slot k's queued forward (waits for its render kernel); true: failed (error set)
+static bool check_order_slot_locked(OrderFlags& o, int k) {
+  if (o.state[k] != 2) return false;
+  o.state[k] = 0;
   if (!check_hip(hipEventSynchronize(o.ev[k]), "hipEventSynchronize")) return true;
   if (o.host[16 * k] & ERR_LOOKBACK) {
     set_error("forward ordering: a look-back wait of the offsets scan or a one-sweep sort timed out "
@@ -316,38 +298,62 @@ static bool check_order_flags_locked(OrderFlags& o) {
   }
   return false;
 }
+// every queued forward's flags
 static bool check_order_flags() {
   OrderFlags* o = order_flags();
   if (!o) return true;
   std::lock_guard<std::mutex> lk(o->mu);
-  return check_order_flags_locked(*o);
+  bool failed = false;
+  for (int k = 0; k < ORDER_RING; k++) failed |= check_order_slot_locked(*o, k);
+  return failed;
 }
 
-// the device word this forward's render kernel stores its ordering flags into; null on error
-static uint32_t* order_flags_word() {
+// The device word this forward's render kernel stores its ordering flags into, and (*seq_out) the
+// forward's sequence number; null on error.
+static uint32_t* order_flags_word(unsigned long long* seq_out) {
   OrderFlags* o = order_flags();
   if (!o) return nullptr;
   std::lock_guard<std::mutex> lk(o->mu);
   if (!o->host) {
-    if (!mapped_words(128, &o->host, &o->dev)) return nullptr;
-    for (int k = 0; k < 2; k++)
+    if (!mapped_words(16 * ORDER_RING, &o->host, &o->dev)) return nullptr;
+    for (int k = 0; k < ORDER_RING; k++)
       if (!check_hip(hipEventCreateWithFlags(&o->ev[k], hipEventDisableTiming), "hipEventCreate")) return nullptr;
   }
-  // the render stores nonzero flags only: clear the word (its previous forward, two back, was checked
-  // when the one after it was queued)
-  o->host[16 * (o->seq & 1)] = 0u;
-  return o->dev + 16 * (o->seq & 1);
+  const unsigned long long q = o->seq;
+  const int k = (int)(q % ORDER_RING);
+  if (o->state[k] == 1) return set_error("more than %d forwards queueing at once on one device", ORDER_RING), nullptr;
+  if (check_order_slot_locked(*o, k)) return nullptr;  // the word's previous forward
+  o->seq++;
+  o->state[k] = 1;
+  *seq_out = q;
+  // the render stores nonzero flags only: clear the word
+  o->host[16 * k] = 0u;
+  return o->dev + 16 * k;
 }
-// the render kernel that stores this forward's flags is queued on `st`: record its event, then
-// check the previous forward's flags (its word is reused by the next forward)
-static bool queue_order_flags(hipStream_t st) {
+// the render kernel that stores forward `q`'s flags is queued on `st`: record its event, then
+// check the forwards queued before it
+static bool queue_order_flags(hipStream_t st, unsigned long long q) {
   OrderFlags* o = order_flags();
   if (!o) return true;
   std::lock_guard<std::mutex> lk(o->mu);
-  if (!check_hip(hipEventRecord(o->ev[o->seq & 1], st), "hipEventRecord")) return true;
-  const bool failed = check_order_flags_locked(*o);
-  o->pending = (long long)o->seq++;
+  const int k = (int)(q % ORDER_RING);
+  if (!check_hip(hipEventRecord(o->ev[k], st), "hipEventRecord")) {
+    o->state[k] = 0;
+    return true;
+  }
+  o->state[k] = 2;
+  bool failed = false;
+  for (int j = 0; j < ORDER_RING; j++)
+    if (j != k) failed |= check_order_slot_locked(*o, j);
   return failed;
+}
+// a forward that reserved a word and failed before queueing its render gives the word back
+static void release_order_word(unsigned long long q) {
+  OrderFlags* o = order_flags();
+  if (!o) return;
+  std::lock_guard<std::mutex> lk(o->mu);
+  const int k = (int)(q % ORDER_RING);
+  if (o->state[k] == 1) o->state[k] = 0;
 }
 
 // Status of bounded forwards (gs_forward_bounded), per device: pinned words the kernels store into
@@ -373,10 +379,13 @@ static BoundedStatus* bounded_status() {
 // raised them; clears them
 static uint32_t take_bounded_status(BoundedStatus* b, long long* instances) {
   std::lock_guard<std::mutex> lk(b->mu);
-  volatile uint32_t* w = b->host;
-  const uint32_t f = w[0] | w[4];
-  if (instances) *instances = f ? (long long)((unsigned long long)w[2] << 32 | w[1]) : 0;
-  if (f) w[0] = 0u, w[1] = 0u, w[2] = 0u, w[4] = 0u;
+  uint32_t* w = b->host;
+  // take and clear each flag word in one atomic exchange: a bounded kernel still in flight that
+  // stores its flags between a read and a clear would otherwise lose them (the count words are
+  // only meaningful beside a flag, so they are taken after the flags)
+  const uint32_t f = __atomic_exchange_n(&w[0], 0u, __ATOMIC_ACQ_REL) | __atomic_exchange_n(&w[4], 0u, __ATOMIC_ACQ_REL);
+  const uint32_t lo = __atomic_exchange_n(&w[1], 0u, __ATOMIC_ACQ_REL), hi = __atomic_exchange_n(&w[2], 0u, __ATOMIC_ACQ_REL);
+  if (instances) *instances = f ? (long long)((unsigned long long)hi << 32 | lo) : 0;
   return f;
 }
 static bool bounded_status_error(uint32_t f, long long inst) {
@@ -619,9 +628,8 @@ static int forward_render_impl(int P, const float* background, int W, int H, con
   GeomPtrs geo;
   BinPtrs bin;
   ImgPtrs img;
-  SlabPtrs slab;
   geom_layout((size_t)P, &geo, (char*)geom_buffer);
-  bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer, &slab);
+  bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer);
   img_layout(W, H, &img, (char*)image_buffer);
   // the look-back waits of the offsets scan and of the one-sweep sorts (never expected to run out:
   // the waited-for workgroups are running) leave ERR_LOOKBACK; the render kernel stores the flags
@@ -629,15 +637,15 @@ static int forward_render_impl(int P, const float* background, int W, int H, con
   // wait idles the device
   // (bounded: the sticky word, nothing recorded or checked here)
   BoundedStatus* bs = bounded ? bounded_status() : nullptr;
-  uint32_t* flags_word = bounded ? (bs ? bs->dev + 4 : nullptr) : order_flags_word();
+  unsigned long long oseq = 0;
+  uint32_t* flags_word = bounded ? (bs ? bs->dev + 4 : nullptr) : order_flags_word(&oseq);
   if (!flags_word) return 1;
-  if (slab_mode((size_t)num_rendered, c.gx * c.gy)) {
-    fwd_bin_render_slabs(P, (uint32_t)num_rendered, c, geo, bin, slab, img, out_color, st, flags_word);
-  } else {
-    fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
-    fwd_render(c, geo, bin, img, out_color, st, flags_word);
+  fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
+  fwd_render(c, geo, bin, img, out_color, st, flags_word);
+  if (!bounded) {
+    if (t_failed) release_order_word(oseq);
+    else if (queue_order_flags(st, oseq)) return 1;
   }
-  if (!bounded && !t_failed && queue_order_flags(st)) return 1;
   return t_failed ? 1 : 0;
 }
 
@@ -667,9 +675,6 @@ int gs_forward_bin_views(int K, int P, int W, int H, void* const* geom_buffer, c
     *out = (uint64_t)d;
     return true;
   };
-  if (slab_mode((size_t)I, c.gx * c.gy))
-    return set_error("bin_views: views of this size bin in depth slabs, view by view (gs_binning_slabs; use "
-                     "gs_forward_render)"), 1;
   uint64_t gs = 0, bs = 0, is = 0;
   if (!stride_of(geom_buffer, gs_geom_buffer_bytes(P), &gs) ||
       !stride_of(binning_buffer, gs_binning_buffer_bytes(I, W, H), &bs) ||
@@ -719,7 +724,6 @@ int gs_forward_render_binned(int P, const float* background, int W, int H, const
   if (!geom_buffer || !binning_buffer || !image_buffer || !out_color) return set_error("missing buffer pointer"), 1;
   hipStream_t st = (hipStream_t)stream;
   CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, 0);
-  if (slab_mode((size_t)num_rendered, c.gx * c.gy)) return set_error("render_binned: a depth-slab view (gs_binning_slabs)"), 1;
   GeomPtrs geo;
   BinPtrs bin;
   ImgPtrs img;
@@ -727,10 +731,14 @@ int gs_forward_render_binned(int P, const float* background, int W, int H, const
   bin_layout((size_t)num_rendered, c.gx * c.gy, &bin, (char*)binning_buffer);
   img_layout(W, H, &img, (char*)image_buffer);
   BoundedStatus* bst = bounded ? bounded_status() : nullptr;
-  uint32_t* flags_word = bounded ? (bst ? bst->dev + 4 : nullptr) : order_flags_word();
+  unsigned long long oseq = 0;
+  uint32_t* flags_word = bounded ? (bst ? bst->dev + 4 : nullptr) : order_flags_word(&oseq);
   if (!flags_word) return 1;
   fwd_render(c, geo, bin, img, out_color, st, flags_word);
-  if (!bounded && !t_failed && queue_order_flags(st)) return 1;
+  if (!bounded) {
+    if (t_failed) release_order_word(oseq);
+    else if (queue_order_flags(st, oseq)) return 1;
+  }
   return t_failed ? 1 : 0;
 }
 
@@ -1060,17 +1068,6 @@ unsigned gs_debug_set_scan_spin_limit(unsigned limit) {
 }
 
 /* ---- numerics mode of the render loops ---- */
-int gs_set_slabs(int mode) {
-  const int prev = slab_setting();
-  g_slabs.store(mode < 0 ? 0 : (mode > 2 ? 2 : mode), std::memory_order_relaxed);
-  return prev;
-}
-
-int gs_binning_slabs(long long num_rendered, int W, int H) {
-  const int tiles = ((W + GS_TILE - 1) / GS_TILE) * ((H + GS_TILE - 1) / GS_TILE);
-  return num_rendered > 0 && slab_mode((size_t)num_rendered, tiles) ? 1 : 0;
-}
-
 int gs_set_exact_exp(int exact) {
   const int prev = exact_exp() ? 1 : 0;
   gs::g_exact_exp.store(exact ? 1 : 0, std::memory_order_relaxed);

@@ -440,6 +440,280 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) GS_WPE_ATTR(GS_BWD_WPE) v
 
 }
 
+// ------------------------------------------------------------------------------------------
+// Tile-wave backward (round 4, the default): ONE wave64 per tile, four pixel slots per lane.
+//
+// Lane l owns pixel (l & 7, l >> 3) of each 8x8 quadrant k of the tile (slot k).  A staged entry
+// carries the set of quadrants its alpha >= 1/255 ellipse meets (the forward's per-quadrant cull)
+// and the walk evaluates and commits only those slots: the C3 oracle study
+// (tools/bwd_layout_stats.py, profiles/r04_bwd_layout_stats_c3.txt) puts the pixel slots
+// evaluated per walked entry at 143 (quadrant slots) against 193 for the two 8x16 half waves of
+// k_render_bwd, and the nine per-entry sums are reduced over the wave ONCE per tile entry (0.86
+// reductions per walked entry instead of 1.36).  The lane's slots are pre-summed in registers
+// (one FMA per term and slot).  One wave per workgroup: staging, walk and flush need no workgroup
+// barrier, and every lane stages (and later flushes) one entry of a 64-entry batch, keeping that
+// entry's raw conic, opacity and slot in its registers.
+// Same per-pixel recurrence and decisions as k_render_bwd (and as the forward); only the order in
+// which a tile entry's per-pixel terms are summed differs.
+// ------------------------------------------------------------------------------------------
+#ifndef GS_BWD_TW
+#define GS_BWD_TW 1
+#endif
+#ifndef GS_BWDT_MINW
+#define GS_BWDT_MINW 1
+#endif
+#ifndef GS_BWDT_CENTRED
+#define GS_BWDT_CENTRED 1  // 0: moments about the splat mean summed in fp32 (k_render_bwd's form)
+#endif
+
+struct BwdSlot {
+  float T, U, d0, d1, d2;
+  uint32_t last;
+};
+
+// one slot's evaluation + commit for one entry; s[] accumulates the lane's slot terms
+template <bool EXACT>
+__device__ __forceinline__ bool bwd_slot(BwdSlot& q, float pfx, float pfy, float ux, float uy, const float4 xr,
+                                         const float4 co, float bl, uint32_t e, float* s) {
+  const float dx = xr.x - pfx, dy = xr.y - pfy;
+  const float pw = falloff_log2(co, dx, dy);  // log2(e) * power
+  const float oG = co.w * exp2_m<EXACT>(pw);
+  // same decision as the forward (k_render_fwd_q): alpha = min(0.99, o G) >= 1/255 <=> o G >= 1/255
+  const bool con = e < q.last && (!EXACT || pw <= 0.0f) && oG >= 1.0f / 255.0f;
+  // a non-contributing pixel runs as an o G = 0 entry: T and U pass through unchanged bit for bit
+  const float oGm = con ? oG : 0.0f;
+  const float ae = __builtin_amdgcn_fmed3f(oGm, 0.0f, 0.99f);
+  const float omA = 1.0f - ae;
+  float inv = __builtin_amdgcn_rcpf(omA);
+  if constexpr (EXACT) inv = __builtin_fmaf(inv, __builtin_fmaf(-omA, inv, 1.0f), inv);
+  const float Tn = q.T * inv;
+  const float dch = ae * Tn;
+  const float Cd = __builtin_fmaf(bl, q.d2, __builtin_fmaf(xr.w, q.d1, xr.z * q.d0));
+  const float dLa = __builtin_fmaf(Tn, Cd, -(q.U * inv));
+  const float qq = oGm * dLa;  // dL/dG G = o G dL/dalpha (not gated by the 0.99 clamp)
+  s[0] = __builtin_fmaf(dch, q.d0, s[0]);
+  s[1] = __builtin_fmaf(dch, q.d1, s[1]);
+  s[2] = __builtin_fmaf(dch, q.d2, s[2]);
+  // moments of q about the tile centre (ux, uy = pixel - centre, |.| <= 7.5, exact): small terms,
+  // turned into the moments about the splat mean in fp64 at the flush (see k_render_bwd_tw)
+  const float mx = GS_BWDT_CENTRED ? ux : dx, my = GS_BWDT_CENTRED ? uy : dy;
+  const float qx = qq * mx, qy = qq * my;
+  s[3] = s[3] + qx;
+  s[4] = s[4] + qy;
+  s[5] = __builtin_fmaf(qx, mx, s[5]);
+  s[6] = __builtin_fmaf(qx, my, s[6]);
+  s[7] = __builtin_fmaf(qy, my, s[7]);
+  s[8] = s[8] + qq;
+  q.T = Tn;
+  q.U = __builtin_fmaf(Cd, dch, q.U);
+  return con;
+}
+
+template <bool EXACT>
+__global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c, const uint2* __restrict__ ranges,
+                                                                    const uint32_t* __restrict__ point_list,
+                                                                    const uint32_t* __restrict__ point_gid,
+                                                                    const float4* __restrict__ splat,
+                                                                    const float* __restrict__ final_T,
+                                                                    const uint32_t* __restrict__ n_contrib,
+                                                                    const uint32_t* __restrict__ tile_max,
+                                                                    const uint32_t* __restrict__ tile_order,
+                                                                    const float* __restrict__ dL_dpix,
+                                                                    float* __restrict__ gradrec) {
+  __shared__ float4 s_xy[64];  // (x, y, r, g)
+  __shared__ float4 s_co[64];  // falloff coefficients + opacity (fall_coefs)
+  __shared__ float s_bl[64];   // b
+  __shared__ __attribute__((aligned(16))) float s_acc[64][16];
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(tile_order ? tile_order[blockIdx.x] : blockIdx.x);
+  if (tile == ~0u) return;  // a hole of the XCD-group launch order
+  const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
+  const int lane = threadIdx.x;
+  const uint2 range = ranges[tile];
+  const uint32_t n = range.y - range.x;
+  // per-quadrant largest n_contrib (the forward's quadrant waves): slot k's walk ends there
+  const uint4 qm = reinterpret_cast<const uint4*>(tile_max)[tile];
+  const uint32_t qlast[4] = {min(qm.x, n), min(qm.y, n), min(qm.z, n), min(qm.w, n)};
+  const uint32_t n_eff = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
+  if (n_eff == 0) return;  // no instance walked: no records (k_sum_records reads none below a cut of 0)
+
+  const size_t HW = (size_t)c.W * c.H;
+  const int qx0 = tx * GS_TILE + (lane & 7), qy0 = ty * GS_TILE + (lane >> 3);
+  BwdSlot p[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int px = qx0 + 8 * (k & 1), py = qy0 + 8 * (k >> 1);
+    const bool in = px < c.W && py < c.H;
+    const size_t pix = in ? (size_t)py * c.W + px : 0;
+    const float Tf = in ? final_T[pix] : 0.0f;
+    p[k].T = Tf;
+    p[k].last = in ? n_contrib[pix] : 0u;
+    p[k].d0 = in ? dL_dpix[pix] : 0.0f;
+    p[k].d1 = in ? dL_dpix[HW + pix] : 0.0f;
+    p[k].d2 = in ? dL_dpix[2 * HW + pix] : 0.0f;
+    // U = S + T_final bg . dL/dpix (see k_render_bwd)
+    p[k].U = Tf * (c.bg[0] * p[k].d0 + c.bg[1] * p[k].d1 + c.bg[2] * p[k].d2);
+  }
+  const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
+  const float pfx0 = (float)qx0, pfy0 = (float)qy0;
+  const float ux0 = (float)(lane & 7) - 7.5f, uy0 = (float)(lane >> 3) - 7.5f;  // slot 0 pixel - tile centre
+  using lds_float = __attribute__((address_space(3))) float;
+  // writer lanes 16 r + 8 h: s[r + 4 h] at slot r + 4 h, their s8 partial at slot 8 + r + 4 h
+  lds_float* const acc_lane = (lds_float*)(&s_acc[0][(lane >> 4) + 4 * ((lane >> 3) & 1)]);
+  const bool hi8 = (lane & 8) != 0;
+
+  // staging pipeline (one entry per lane): while batch k is walked, the splat records of batch
+  // k + 1, the ids of batch k + 2 and (ids by slot) the slots of batch k + 3 are in flight.
+  // Batch k's entry of lane t sits at list position range.x + e0 - 64 k, e0 = n_eff - 1 - t.
+  const int32_t e0 = (int32_t)n_eff - 1 - lane;
+  const uint32_t* const plist = point_list + range.x;
+  uint32_t slot_c = 0, S1 = 0, G1 = 0, S2 = 0;
+  float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pd = pa;
+  if (e0 >= 0) {
+    slot_c = plist[e0];
+    const uint32_t g0 = GS_SORT_GID ? point_gid[range.x + e0] : point_gid[slot_c];
+    pa = splat[3 * g0], pb = splat[3 * g0 + 1], pd = splat[3 * g0 + 2];
+  }
+  if (e0 - 64 >= 0) {
+    S1 = plist[e0 - 64];
+    G1 = GS_SORT_GID ? point_gid[range.x + e0 - 64] : point_gid[S1];
+  }
+  if (!GS_SORT_GID && e0 - 128 >= 0) S2 = plist[e0 - 128];
+
+  for (uint32_t base = 0; base < n_eff; base += 64) {
+    const uint32_t cnt = min(64u, n_eff - base);
+    // stage: lane t holds entry t of the batch (walk order: back to front)
+    const bool mine = (uint32_t)lane < cnt;
+    const uint32_t slot = slot_c;
+    const float ccx = pa.z, ccy = pa.w, ccz = pb.x, cop = pb.y;  // raw conic + opacity (flush)
+    uint32_t qmask = 0;
+    if (mine) {
+      s_xy[lane] = make_float4(pa.x, pa.y, pb.z, pb.w);
+      s_co[lane] = fall_coefs(pa.z, pa.w, pb.x, pb.y);
+      s_bl[lane] = pd.x;
+      qmask = quadrant_mask(pa.x, pa.y, pa.z, pa.w, pb.x, pd.z, tx, ty);
+    }
+    // issue the next batch's splat loads, the ids after it and (ids by slot) the slots after those
+    const int32_t e1 = e0 - (int32_t)(base + 64);
+    if (e1 >= 0) {
+      slot_c = S1;
+      pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
+    }
+    if (e1 - 64 >= 0) {
+      if (GS_SORT_GID) {
+        S1 = plist[e1 - 64];
+        G1 = point_gid[range.x + e1 - 64];
+      } else {
+        S1 = S2;
+        G1 = point_gid[S2];
+      }
+    }
+    if (!GS_SORT_GID && e1 - 128 >= 0) S2 = plist[e1 - 128];
+    // per-slot entry sets; entries no pixel of quadrant k reaches (e >= qlast[k]) sit at the low bits
+    uint64_t M[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint64_t mk = __ballot((qmask >> k) & 1u);
+      const int jmin = (int)n_eff - (int)qlast[k] - (int)base;  // entry j reaches quadrant k iff j >= jmin
+      if (jmin > 0) mk &= jmin >= 64 ? 0ull : ~((1ull << jmin) - 1ull);
+      M[k] = mk;
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint64_t m = (M[0] | M[1]) | (M[2] | M[3]);
+    uint64_t wrote = 0;
+#pragma unroll 1
+    while (m) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      const float4 xr = s_xy[j], co = s_co[j];
+      const float bl = s_bl[j];
+      const uint32_t e = n_eff - 1 - (base + j);
+      float s[GRAD_REC];
+#pragma unroll
+      for (int t = 0; t < GRAD_REC; t++) s[t] = 0.0f;
+      bool con = false;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if ((M[k] >> j) & 1ull)
+          con |= bwd_slot<EXACT>(p[k], pfx0 + (float)(8 * (k & 1)), pfy0 + (float)(8 * (k >> 1)),
+                                 ux0 + (float)(8 * (k & 1)), uy0 + (float)(8 * (k >> 1)), xr, co, bl, e, s);
+      if (__ballot(con) != 0) {
+        wrote |= 1ull << j;
+        float d, d8;
+        wave_sum9_halfrows(s, hi8, d, d8);
+        asm volatile("" ::"v"(d), "v"(d8));
+        if ((lane & 7) == 0) {
+          uint32_t eo = j * 16;
+          asm volatile("" : "+s"(eo));
+          lds_float* acc = acc_lane + eo;
+          acc[0] = d;
+          acc[8] = d8;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // flush: lane t stores the record of its entry (zeros for an entry no pixel took)
+    if (mine) {
+      float S[GRAD_REC];
+      if ((wrote >> lane) & 1ull) {
+        const float4 a0 = *reinterpret_cast<const float4*>(&s_acc[lane][0]);
+        const float4 a1 = *reinterpret_cast<const float4*>(&s_acc[lane][4]);
+        const float4 a2 = *reinterpret_cast<const float4*>(&s_acc[lane][8]);
+        const float4 a3 = *reinterpret_cast<const float4*>(&s_acc[lane][12]);
+        S[0] = a0.x, S[1] = a0.y, S[2] = a0.z, S[3] = a0.w, S[4] = a1.x, S[5] = a1.y, S[6] = a1.z, S[7] = a1.w;
+        S[8] = ((a2.x + a2.y) + (a2.z + a2.w)) + ((a3.x + a3.y) + (a3.z + a3.w));
+      } else {
+#pragma unroll
+        for (int t = 0; t < GRAD_REC; t++) S[t] = 0.0f;
+      }
+      // S3..S7 are the moments of q = o G dL/dalpha about the tile centre; with D = mean - centre
+      // (dx = D.x - ux): sum q dx = D.x S8 - S3, sum q dx^2 = D.x^2 S8 - 2 D.x S3 + S5, ... in fp64,
+      // one rounding to the record (the conic gradient of a long splat is a small difference of
+      // large moments: rounding them term by term in fp32 is what the covariance chain amplifies)
+#if !GS_BWDT_CENTRED
+      Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)slot * GRAD_REC);
+      r[0] = Rec3{S[0], S[1], S[2]};
+      r[1] = Rec3{-ddelx_dx * (ccx * S[3] + ccy * S[4]), -ddely_dy * (ccz * S[4] + ccy * S[3]), -0.5f * S[5]};
+      r[2] = Rec3{-0.5f * S[6], -0.5f * S[7], S[8] != 0.0f ? S[8] / cop : 0.0f};
+#elif GS_BWDT_CENTRED == 2
+      // the same in fp32 with FMAs: its roundings are of the size of the record's own final rounding
+      const float2 mxy = *reinterpret_cast<const float2*>(&s_xy[lane]);
+      const float Dx = mxy.x - ((float)(tx * GS_TILE) + 7.5f), Dy = mxy.y - ((float)(ty * GS_TILE) + 7.5f);
+      const float q0 = S[8], qx = S[3], qy = S[4];
+      const float m1x = __builtin_fmaf(Dx, q0, -qx), m1y = __builtin_fmaf(Dy, q0, -qy);
+      const float m2xx = __builtin_fmaf(Dx, __builtin_fmaf(Dx, q0, -2.0f * qx), S[5]);
+      const float m2xy = __builtin_fmaf(Dx, __builtin_fmaf(Dy, q0, -qy), __builtin_fmaf(-Dy, qx, S[6]));
+      const float m2yy = __builtin_fmaf(Dy, __builtin_fmaf(Dy, q0, -2.0f * qy), S[7]);
+      Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)slot * GRAD_REC);
+      r[0] = Rec3{S[0], S[1], S[2]};
+      r[1] = Rec3{-ddelx_dx * (ccx * m1x + ccy * m1y), -ddely_dy * (ccz * m1y + ccy * m1x), -0.5f * m2xx};
+      r[2] = Rec3{-0.5f * m2xy, -0.5f * m2yy, S[8] != 0.0f ? S[8] / cop : 0.0f};
+#else
+      const float2 mxy = *reinterpret_cast<const float2*>(&s_xy[lane]);
+      // the tile centre is formed here (from scalars), not kept in four VGPRs across the walk
+      int ox = tx * GS_TILE, oy = ty * GS_TILE;
+      asm volatile("" : "+s"(ox), "+s"(oy));
+      const double Dx = (double)mxy.x - ((double)ox + 7.5), Dy = (double)mxy.y - ((double)oy + 7.5), q0 = S[8];
+      // (scheduling barriers keep the fp64 temporaries of one output from living beside the next's)
+      const float m1x = (float)__builtin_fma(Dx, q0, -(double)S[3]), m1y = (float)__builtin_fma(Dy, q0, -(double)S[4]);
+      __builtin_amdgcn_sched_barrier(0);
+      const float m2xx = (float)__builtin_fma(Dx, __builtin_fma(Dx, q0, -2.0 * (double)S[3]), (double)S[5]);
+      __builtin_amdgcn_sched_barrier(0);
+      const float m2xy = (float)__builtin_fma(Dx, __builtin_fma(Dy, q0, -(double)S[4]),
+                                              __builtin_fma(-Dy, (double)S[3], (double)S[6]));
+      __builtin_amdgcn_sched_barrier(0);
+      const float m2yy = (float)__builtin_fma(Dy, __builtin_fma(Dy, q0, -2.0 * (double)S[4]), (double)S[7]);
+      __builtin_amdgcn_sched_barrier(0);
+      Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)slot * GRAD_REC);
+      r[0] = Rec3{S[0], S[1], S[2]};
+      r[1] = Rec3{-ddelx_dx * (ccx * m1x + ccy * m1y), -ddely_dy * (ccz * m1y + ccy * m1x), -0.5f * m2xx};
+      // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
+      r[2] = Rec3{-0.5f * m2xy, -0.5f * m2yy, S[8] != 0.0f ? S[8] / cop : 0.0f};
+#endif
+    }
+    __builtin_amdgcn_wave_barrier();  // the next batch overwrites the staged entries
+  }
+}
+
 // Longest-first launch order for the backward.  A tile's walk is as long as its largest
 // n_contrib (the forward's per-quadrant maxima), which varies ~10x across an image, and dense
 // tiles sit together: in index order the last workgroups to start include heavy ones and the
@@ -505,6 +779,17 @@ void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& 
   GS_LAUNCH("tile_order", k_tile_order, dim3((slots + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
             img.len_hist, img.tile_brank, (uint32_t)c.gx, (uint32_t)c.gy, order, img.tile_max, img.ranges,
             bin.point_list, img.tile_cut, img.cut_max);
+  if (GS_BWD_TW) {
+    if (exact_exp())
+      GS_LAUNCH("render_bwd", k_render_bwd_tw<true>, dim3(slots), dim3(64), 0, st, c, img.ranges, bin.point_list,
+                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max,
+                order, dL_dpix, gradrec);
+    else
+      GS_LAUNCH("render_bwd", k_render_bwd_tw<false>, dim3(slots), dim3(64), 0, st, c, img.ranges, bin.point_list,
+                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max,
+                order, dL_dpix, gradrec);
+    return;
+  }
   if (exact_exp())
     GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(slots), dim3(BWD_THREADS), 0, st, c, img.ranges,
               bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, img.final_T, img.n_contrib, img.tile_max, order,

@@ -522,7 +522,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
     const uint32_t* __restrict__ sorted_gid, const uint32_t* __restrict__ offsets,
     const float4* __restrict__ binrec, int gx, int gy, uint32_t* __restrict__ tile_keys,
     uint32_t* __restrict__ presort_gid, uint2* __restrict__ ranges, uint32_t* __restrict__ hist0, uint32_t mask0,
-    uint32_t* __restrict__ n_copy, uint64_t gs, uint64_t bs, uint64_t is, int near_word = -1) {
+    uint32_t* __restrict__ n_copy, uint64_t gs, uint64_t bs, uint64_t is) {
   counters = vptr(counters, gs), dup_first = vptr(dup_first, gs), sorted_gid = vptr(sorted_gid, gs);
   offsets = vptr(offsets, gs), binrec = vptr(binrec, gs);
   tile_keys = vptr(tile_keys, bs), presort_gid = vptr(presort_gid, bs), hist0 = vptr(hist0, bs);
@@ -543,10 +543,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   const uint32_t V = counters[CNT_V];
   // I: the binning buffer's capacity (= the count, unless the buffer was sized ahead of it)
   I = min(I, counters[CNT_NREND]);
-  // the slots the tile sort takes: all of them, or (near_word, the depth slabs) the near slab's
-  // counters[CNT_SLAB_IA] -- the slot arrays are written for every slot either way
-  const uint32_t n_out = near_word >= 0 ? min(I, counters[near_word]) : I;
-  if (b == 0 && tid == 0) n_copy[0] = n_out;  // for the tile sort and k_ranges (kernels after this one)
+  if (b == 0 && tid == 0) n_copy[0] = I;  // for the tile sort and k_ranges (kernels after this one)
   const uint32_t k0 = b * DUP_SLOTS;
   const uint32_t k1 = k0 < I ? min(k0 + DUP_SLOTS, I) : k0;
   if (counters[CNT_ERR] & ERR_INVALID) {
@@ -559,7 +556,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
       presort_gid[k] = g0;
     }
     if (hist0) {
-      hist0[(size_t)tid * gridDim.x + b] = tid == 0 ? min(k1, n_out) - min(k0, n_out) : 0u;
+      hist0[(size_t)tid * gridDim.x + b] = tid == 0 ? k1 - k0 : 0u;
     }
     return;
   }
@@ -629,7 +626,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
       const uint32_t key = s_seg_base[o] + k;
       tile_keys[k] = key;
       presort_gid[k] = s_seg_gid[o];
-      if (hist0 && k < n_out) atomicAdd(&s_hist[key & mask0], 1u);  // counts only: order-free
+      if (hist0) atomicAdd(&s_hist[key & mask0], 1u);  // counts only: order-free
     }
   }
   // the tile sort's first-pass digit counts of this block's slots (its sort tile is the same 2048
@@ -725,192 +722,6 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
                    GS_TILE_SORT_BLOCKS, views, bs);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024, views), dim3(256), 0, st, I, bin.count, bin.sorted_tile,
             img.ranges, (uint32_t*)img.tile_done, sched_words, (uint32_t)tiles, bs, is);
-}
-
-// ------------------------------------------------------------------------------------------
-// depth slabs (slab_mode): most instances of a deep scene lie behind pixels that have already
-// stopped (C5: 1.55M of 21.6M are walked), yet the duplicate, the tile sort, the ranges and the
-// record sums scale with all of them.  The near slab -- the depth ranks whose instances start
-// below I / 4 -- is binned and rendered first, saving each pixel's state; the far slab is then
-// binned only into tiles with a pixel still running, the two sorted lists are merged per tile
-// (near entries first, both in depth order) into the view's point_list, and the render resumes
-// from the saved state at each tile's first far entry.  Per pixel the entries and their order are
-// those of the full list up to where the pixel stops, so every output is unchanged; the backward
-// sees one list as always, and every instance keeps its one-list slot (the skipped ones have no
-// record, as they would have none after the one-list walk).
-// ------------------------------------------------------------------------------------------
-// the near slab's instance count I_A (the offset of the first rank whose instances start at or past
-// `target`) and the far slab's slot count; also clears the far ranges and the saturation bits
-__global__ __launch_bounds__(256) void k_slab_split(uint32_t* __restrict__ counters,
-                                                    const uint32_t* __restrict__ offsets, uint32_t target,
-                                                    uint32_t Icap, uint2* __restrict__ ranges_b,
-                                                    uint32_t* __restrict__ qbits, uint32_t tiles) {
-  for (uint32_t t = threadIdx.x; t < tiles; t += 256) ranges_b[t] = make_uint2(0u, 0u);
-  for (uint32_t w = threadIdx.x; w < (tiles + 7) / 8; w += 256) qbits[w] = 0u;
-  if (threadIdx.x != 0) return;
-  const uint32_t V = counters[CNT_V], I = min(counters[CNT_I], Icap);
-  uint32_t lo = 0, hi = V;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (offsets[mid] >= target) hi = mid;
-    else lo = mid + 1;
-  }
-  const uint32_t IA = min(lo < V ? offsets[lo] : I, I);
-  counters[CNT_SLAB_IA] = IA;
-  counters[CNT_SLAB_NF] = I - IA;
-}
-
-// a tile's four quadrant bits (qbits: 4 bits per tile, set by the near slab's render for each
-// quadrant whose pixels all stopped)
-__device__ __forceinline__ bool tile_saturated(const uint32_t* qbits, uint32_t t) {
-  return ((qbits[t >> 3] >> (4u * (t & 7u))) & 0xFu) == 0xFu;
-}
-
-// the far slab's sort entries: a stream compaction over its slots [I_A, I) (slot order = depth
-// order within each tile) keeping those whose tile still has a running pixel -- key tile, value
-// slot.  Every slot keeps its one-list number, and the slot arrays the record sums read (slot ->
-// tile, slot -> Gaussian) were written for all of them by the duplicate, so the backward's record
-// sums group the same slots as the one-list forward's (bit-identical gradients).
-// Workgroup b takes far slots [b FC_SLOTS, (b + 1) FC_SLOTS) as FC_ITEMS rows of 256 (row k, lane
-// l: slot k 256 + l -- each row one coalesced load); a slot's rank is the kept slots of the earlier
-// rows plus those of its row before it (ballots per wave, one LDS prefix over rows x waves).
-// k_far_count writes the workgroups' kept counts, k_scan_partials turns them into bases (and the
-// total I_B), k_far_compact writes the entries.
-// The saturation bits are staged in LDS (16 KB: up to 32768 tiles; larger images read them from
-// global memory).
-constexpr int FC_ITEMS = 16;
-constexpr uint32_t FC_SLOTS = 256u * FC_ITEMS;
-constexpr uint32_t FC_BITS_LDS = 4096;
-__device__ __forceinline__ const uint32_t* far_bits(const uint32_t* __restrict__ qbits, uint32_t tiles,
-                                                    uint32_t* s_bits) {
-  const uint32_t nw = (tiles + 7) / 8;
-  if (nw > FC_BITS_LDS) return qbits;
-  for (uint32_t i = threadIdx.x; i < nw; i += 256) s_bits[i] = qbits[i];
-  lds_barrier();
-  return s_bits;
-}
-__device__ __forceinline__ void far_flags(const uint32_t* __restrict__ counters, const uint32_t* __restrict__ slot_tile,
-                                          const uint32_t* bits, uint32_t tiles, uint32_t t[FC_ITEMS],
-                                          bool keep[FC_ITEMS]) {
-  const uint32_t IA = counters[CNT_SLAB_IA], NF = counters[CNT_SLAB_NF];
-  const uint32_t i0 = blockIdx.x * FC_SLOTS + threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < FC_ITEMS; k++) {
-    const uint32_t i = i0 + (uint32_t)k * 256u;
-    t[k] = i < NF ? slot_tile[IA + i] : tiles;
-  }
-#pragma unroll
-  for (int k = 0; k < FC_ITEMS; k++) keep[k] = t[k] < tiles && !tile_saturated(bits, t[k]);
-}
-
-__global__ __launch_bounds__(256) void k_far_count(const uint32_t* __restrict__ counters,
-                                                   const uint32_t* __restrict__ slot_tile,
-                                                   const uint32_t* __restrict__ qsat, uint32_t tiles,
-                                                   uint32_t* __restrict__ partial) {
-  __shared__ uint32_t s_w[4];
-  __shared__ uint32_t s_bits[FC_BITS_LDS];
-  uint32_t t[FC_ITEMS];
-  bool keep[FC_ITEMS];
-  far_flags(counters, slot_tile, far_bits(qsat, tiles, s_bits), tiles, t, keep);
-  uint32_t n = 0;
-#pragma unroll
-  for (int k = 0; k < FC_ITEMS; k++) n += (uint32_t)__popcll(__ballot(keep[k]));
-  if (__lane_id() == 0) s_w[threadIdx.x >> 6] = n;
-  lds_barrier();
-  if (threadIdx.x == 0) partial[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-}
-
-__global__ __launch_bounds__(256) void k_far_compact(const uint32_t* __restrict__ counters,
-                                                     const uint32_t* __restrict__ slot_tile,
-                                                     const uint32_t* __restrict__ qsat, uint32_t tiles,
-                                                     const uint32_t* __restrict__ partial, uint32_t* __restrict__ keys,
-                                                     uint32_t* __restrict__ slots) {
-  __shared__ uint32_t s_cnt[FC_ITEMS * 4];
-  __shared__ uint32_t s_bits[FC_BITS_LDS];
-  uint32_t t[FC_ITEMS];
-  bool keep[FC_ITEMS];
-  far_flags(counters, slot_tile, far_bits(qsat, tiles, s_bits), tiles, t, keep);
-  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
-  uint64_t m[FC_ITEMS];
-#pragma unroll
-  for (int k = 0; k < FC_ITEMS; k++) {
-    m[k] = __ballot(keep[k]);
-    if (lane == 0) s_cnt[k * 4 + w] = (uint32_t)__popcll(m[k]);
-  }
-  lds_barrier();
-  // exclusive prefix over (row, wave) in slot order: lane j of wave 0 holds entry j
-  if (w == 0) {
-    const uint32_t c = s_cnt[lane];
-    const uint32_t incl = wave_incl_scan(c);
-    s_cnt[lane] = incl - c;
-  }
-  lds_barrier();
-  const uint32_t base = partial[blockIdx.x], IA = counters[CNT_SLAB_IA];
-  const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t i0 = blockIdx.x * FC_SLOTS + threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < FC_ITEMS; k++) {
-    if (!keep[k]) continue;
-    const uint32_t o = base + s_cnt[k * 4 + w] + (uint32_t)__popcll(m[k] & below);
-    keys[o] = t[k];
-    slots[o] = IA + i0 + (uint32_t)k * 256u;
-  }
-}
-
-// per tile: the near and far entry counts -> the combined list's range (exclusive scan over the
-// tiles, one workgroup) and the near count (the far render's resume position)
-__global__ __launch_bounds__(1024) void k_slab_ranges(uint32_t* __restrict__ counters,
-                                                      const uint2* __restrict__ ranges_a,
-                                                      const uint2* __restrict__ ranges_b, uint32_t* __restrict__ n_a,
-                                                      uint2* __restrict__ ranges, uint32_t tiles) {
-  __shared__ uint32_t s_w[16];
-  __shared__ uint32_t s_carry;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (tid == 0) s_carry = 0;
-  __syncthreads();
-  for (uint32_t t0 = 0; t0 < tiles; t0 += 1024) {
-    const uint32_t t = t0 + tid;
-    uint32_t na = 0, nb = 0;
-    if (t < tiles) {
-      const uint2 a = ranges_a[t], b = ranges_b[t];
-      na = a.y - a.x, nb = b.y - b.x;
-    }
-    const uint32_t v = na + nb;
-    uint32_t incl = wave_incl_scan(v);
-    if (lane == 63) s_w[wid] = incl;
-    __syncthreads();
-    uint32_t before = s_carry;
-    for (uint32_t w = 0; w < wid; w++) before += s_w[w];
-    const uint32_t start = before + incl - v;
-    if (t < tiles) {
-      ranges[t] = make_uint2(start, start + v);
-      n_a[t] = na;
-    }
-    __syncthreads();
-    if (tid == 1023) s_carry = start + v;
-    __syncthreads();
-  }
-}
-
-// the combined list: tile t's near entries, then its far entries, each in depth (slot) order
-__global__ __launch_bounds__(256) void k_slab_merge(const uint32_t* __restrict__ counters,
-                                                    const uint32_t* __restrict__ near_list,
-                                                    const uint32_t* __restrict__ near_tile,
-                                                    const uint32_t* __restrict__ far_list,
-                                                    const uint32_t* __restrict__ far_tile,
-                                                    const uint2* __restrict__ ranges_a,
-                                                    const uint2* __restrict__ ranges_b,
-                                                    const uint32_t* __restrict__ n_a, const uint2* __restrict__ ranges,
-                                                    uint32_t* __restrict__ combined, uint32_t tiles) {
-  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
-  const uint32_t IA = counters[CNT_SLAB_IA], IB = counters[CNT_SLAB_IB];
-  if (p < IA) {
-    const uint32_t t = near_tile[p];
-    if (t < tiles) combined[ranges[t].x + (p - ranges_a[t].x)] = near_list[p];
-  } else if (p < IA + IB) {
-    const uint32_t q = p - IA, t = far_tile[q];
-    if (t < tiles) combined[ranges[t].x + n_a[t] + (q - ranges_b[t].x)] = far_list[q];
-  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1123,13 +934,7 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
 #endif
 constexpr int FWDQ_NB = GS_FWDQ_NB;  // entries staged per round (<= 64: one per lane)
 static_assert(FWDQ_NB <= 64, "one staged entry per lane");
-// PHASE (depth slabs, fwd_bin_render_slabs): 0 the whole list; 1 the near slab -- a quadrant whose
-// pixels all stopped stores its final outputs and records that (qsat word, qbits bit), any other saves
-// its pixel state (final_T = T, out = the colour sum without the background, n_contrib = last |
-// stopped << 31); 2 the combined list from the near slab's end (n_a[tile]) on, starting from the
-// saved state, then the usual epilogue (a finished quadrant only reports to the tile's completion).
-constexpr uint32_t FWD_STOPPED = 0x80000000u;
-template <bool EXACT, int PHASE = 0>
+template <bool EXACT>
 __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ point_list,
                                                      const uint32_t* __restrict__ point_gid,
@@ -1137,10 +942,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
                                                      float4* __restrict__ inst_splat, float* __restrict__ out,
                                                      float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                      uint32_t* __restrict__ tile_max, ImgPtrs img,
-                                                     const uint32_t* __restrict__ err, uint32_t* __restrict__ err_host,
-                                                     const uint32_t* __restrict__ n_a = nullptr,
-                                                     uint32_t* __restrict__ qsat = nullptr,
-                                                     uint32_t* __restrict__ qbits = nullptr) {
+                                                     const uint32_t* __restrict__ err, uint32_t* __restrict__ err_host) {
   __shared__ float4 s_ent[3 * FWDQ_NB];
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
   const uint32_t b = blockIdx.x;
@@ -1160,26 +962,6 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   const float qx = (float)(tx * GS_TILE + 8 * (wid & 1)), qy = (float)(ty * GS_TILE + 8 * (wid >> 1));
   FwdPix px;
   px.done = __builtin_amdgcn_ballot_w64(!inside);
-  uint32_t base0 = 0;
-  if constexpr (PHASE == 2) {  // resume the near slab's pixel state
-    if (qsat[4 * tile + wid]) {  // finished within the near slab (outputs stored)
-      if (lane == 0)
-        tile_finish(tile, xcd_group(tile, c.gx, c.gy), tile_max[4 * tile + wid], img.tile_done, img.len_hist,
-                    img.tile_brank);
-      return;
-    }
-    base0 = n_a[tile];
-    bool stopped = true;
-    if (inside) {
-      const size_t pix = (size_t)q.py * c.W + q.px, HW = (size_t)c.W * c.H;
-      const uint32_t l = n_contrib[pix];
-      px.T = final_T[pix];
-      px.C0 = out[pix], px.C1 = out[HW + pix], px.C2 = out[2 * HW + pix];
-      px.last = l & ~FWD_STOPPED;
-      stopped = (l & FWD_STOPPED) != 0;
-    }
-    px.done = __builtin_amdgcn_ballot_w64(stopped);
-  }
 #if GS_FWD_PREFETCH
   // two-deep staging pipeline: while batch k is walked, the splat records of batch k + 1 and the
   // ids of batch k + 2 are in flight (the walk issues no global loads, so they overlap it)
@@ -1190,7 +972,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   if (stager && lane < n) pa = splat[3 * gid_n], pb = splat[3 * gid_n + 1], pd = splat[3 * gid_n + 2];
   gid_n = stager && FWDQ_NB + lane < n ? ids[FWDQ_NB] : 0u;
 #endif
-  for (uint32_t base = base0; base < n; base += FWDQ_NB) {
+  for (uint32_t base = 0; base < n; base += FWDQ_NB) {
     if (px.done == ~0ull) break;
     bool meets = false;
 #if GS_FWD_PREFETCH
@@ -1227,24 +1009,6 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
     fwd_walk<EXACT, FWDQ_NB>(ent, s_qlist, qcnt, (float)q.px, (float)q.py, px);
     __builtin_amdgcn_wave_barrier();  // the next round overwrites the staged entries
   }
-  if constexpr (PHASE == 1) {  // the near slab
-    const bool sat = px.done == ~0ull;
-    if (sat) {  // final: no later entry reaches these pixels
-      fwd_store(c, q, inside, px, out, final_T, n_contrib);
-      const uint32_t wmax = wave_max_u32(px.last);
-      if (lane == 0) {
-        tile_max[4 * tile + wid] = wmax;
-        atomicOr(&qbits[tile >> 3], 1u << (4u * (tile & 7u) + (uint32_t)wid));
-      }
-    } else if (inside) {  // the state to resume from
-      const size_t pix = (size_t)q.py * c.W + q.px, HW = (size_t)c.W * c.H;
-      final_T[pix] = px.T;
-      n_contrib[pix] = px.last | ((px.done >> lane) & 1ull ? FWD_STOPPED : 0u);
-      out[pix] = px.C0, out[HW + pix] = px.C1, out[2 * HW + pix] = px.C2;
-    }
-    if (lane == 0) qsat[4 * tile + wid] = sat ? 1u : 0u;
-    return;
-  }
   fwd_store(c, q, inside, px, out, final_T, n_contrib);
   const uint32_t wmax = wave_max_u32(px.last);
   if (lane == 0) {
@@ -1256,72 +1020,6 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
 #ifndef GS_FWD_WAVE
 #define GS_FWD_WAVE 1
 #endif
-void fwd_bin_render_slabs(int P, uint32_t I, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
-                          const SlabPtrs& sl, const ImgPtrs& img, float* out_color, hipStream_t st,
-                          uint32_t* err_host) {
-  const uint32_t tiles = (uint32_t)(c.gx * c.gy);
-  const int tbits = tile_bits((int)tiles);
-  const uint32_t sched_words = 2u * tiles + ORDER_GROUPS * ORDER_BUCKETS + 1u;
-  const int rblocks = (int)xcd_span(tiles) * 32;
-  const bool ex = exact_exp();
-  // near slab: slots [0, I_A) (whole depth ranks); the duplicate writes every slot's tile and
-  // Gaussian, the near tile sort takes the first I_A
-  GS_LAUNCH("slab_split", k_slab_split, dim3(1), dim3(256), 0, st, geo.counters, geo.offsets, slab_target(I), I,
-            sl.ranges_b, sl.qbits, tiles);
-  bool hist0 = false;
-  if (dup_balanced(I, (uint32_t)P)) {
-    hist0 = sort_plan(I, GS_TILE_SORT_BLOCKS).chunk == DUP_SLOTS;
-    GS_LAUNCH("duplicate", k_duplicate_lb, dim3((I + DUP_SLOTS - 1) / DUP_SLOTS, 1), dim3(DUP_THREADS), 0, st, I,
-              geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy, bin.slot_tile,
-              bin.presort_gid, sl.ranges_a, hist0 ? bin.sort_scratch : nullptr, (1u << radix_first_bits(tbits)) - 1u,
-              bin.count, 0ull, 0ull, 0ull, CNT_SLAB_IA);
-  } else {
-    (void)hipMemsetAsync(sl.ranges_a, 0, sizeof(uint2) * (size_t)tiles, st);
-    (void)hipMemcpyAsync(bin.count, &geo.counters[CNT_SLAB_IA], sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
-    GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, geo.counters,
-              geo.sorted_gid, geo.offsets, geo.binrec, c.gx, bin.slot_tile, bin.presort_gid);
-  }
-  radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, bin.count, I, tbits, bin.sort_scratch, st,
-                   false, hist0, nullptr, nullptr, nullptr, bin.slot_tile, GS_TILE_SORT_BLOCKS);
-  GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, bin.count, sl.near_tile, sl.ranges_a,
-            (uint32_t*)img.tile_done, sched_words, tiles, 0ull, 0ull);
-  if (ex)
-    GS_LAUNCH("render_fwd", (k_render_fwd_q<true, 1>), dim3(rblocks), dim3(64), 0, st, c, sl.ranges_a, sl.near_list,
-              bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-              &geo.counters[CNT_ERR], nullptr, nullptr, sl.qsat, sl.qbits);
-  else
-    GS_LAUNCH("render_fwd", (k_render_fwd_q<false, 1>), dim3(rblocks), dim3(64), 0, st, c, sl.ranges_a, sl.near_list,
-              bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-              &geo.counters[CNT_ERR], nullptr, nullptr, sl.qsat, sl.qbits);
-  // far slab: the slots [I_A, I) in tiles with a pixel still running -> I_B sort entries
-  const uint32_t fc_blocks = far_blocks(I);
-  GS_LAUNCH("far_count", k_far_count, dim3(fc_blocks), dim3(256), 0, st, geo.counters, bin.slot_tile, sl.qbits, tiles,
-            sl.partial);
-  GS_LAUNCH("far_scan", k_scan_partials, dim3(1), dim3(1024), 0, st, sl.partial, fc_blocks, &geo.counters[CNT_SLAB_IB]);
-  GS_LAUNCH("far_compact", k_far_compact, dim3(fc_blocks), dim3(256), 0, st, geo.counters, bin.slot_tile, sl.qbits,
-            tiles, sl.partial, sl.keys_a, sl.vals_a);
-  const bool far_in_b = radix_sort_pairs(sl.keys_a, sl.vals_a, sl.keys_b, sl.vals_b, false, &geo.counters[CNT_SLAB_IB],
-                                         I, tbits, bin.sort_scratch, st, false, false, nullptr, nullptr, nullptr, nullptr,
-                                         GS_TILE_SORT_BLOCKS);
-  const uint32_t* far_tile = far_in_b ? sl.keys_b : sl.keys_a;
-  const uint32_t* far_list = far_in_b ? sl.vals_b : sl.vals_a;
-  GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, &geo.counters[CNT_SLAB_IB], far_tile,
-            sl.ranges_b, (uint32_t*)nullptr, 0u, tiles, 0ull, 0ull);
-  // one list per tile (near entries, then far entries), then the render from the saved state
-  GS_LAUNCH("slab_ranges", k_slab_ranges, dim3(1), dim3(1024), 0, st, geo.counters, sl.ranges_a, sl.ranges_b, sl.n_a,
-            img.ranges, tiles);
-  GS_LAUNCH("slab_merge", k_slab_merge, dim3((I + 255) / 256), dim3(256), 0, st, geo.counters, sl.near_list,
-            sl.near_tile, far_list, far_tile, sl.ranges_a, sl.ranges_b, sl.n_a, img.ranges, bin.point_list, tiles);
-  if (ex)
-    GS_LAUNCH("render_fwd", (k_render_fwd_q<true, 2>), dim3(rblocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-              &geo.counters[CNT_ERR], err_host, sl.n_a, sl.qsat);
-  else
-    GS_LAUNCH("render_fwd", (k_render_fwd_q<false, 2>), dim3(rblocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-              &geo.counters[CNT_ERR], err_host, sl.n_a, sl.qsat);
-}
-
 void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
                 hipStream_t st, uint32_t* err_host) {
   const int tiles = c.gx * c.gy;

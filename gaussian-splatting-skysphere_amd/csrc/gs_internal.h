@@ -157,9 +157,6 @@ struct CameraArgs {
 };
 
 constexpr int CNT_I = 1, CNT_ERR = 2, CNT_NREND = 4, CNT_V = 5, CNT_LB_TILE = 9;
-// depth slabs (gs_forward.hip fwd_bin_render_slabs): the far slab's slot count, the near slab's
-// instance count, the far slab's sort entries
-constexpr int CNT_SLAB_NF = 10, CNT_SLAB_IA = 11, CNT_SLAB_IB = 12;
 // advanced by every forward's counter finalize: the look-back scans' epochs (k_scan_lb) differ
 // between HIP-graph replays
 constexpr int CNT_SEQ = 13;
@@ -301,35 +298,7 @@ inline int tile_bits(int tiles) {
   return b;
 }
 
-// Depth slabs: a view with many instances per tile bins and renders its
-// nearest Gaussians (the near slab, about a quarter of the instances) first, then bins the rest only
-// into the tiles that slab left unsaturated, and renders those on from the saved pixel state.
-// Decided from I and the tile count alone (host and device agree on every buffer layout).
-// gs_set_slabs: 0 off, 1 by size (default), 2 always (tests).
-int slab_setting();
-constexpr size_t SLAB_MIN_PER_TILE = 1024;  // instances per tile from which the slabs pay
-inline bool slab_mode(size_t I, int tiles) {
-  const int s = slab_setting();
-  if (GS_SORT_GID || GS_INST_REC) return false;  // the slabs read ids by slot and stage no records
-  return s == 2 ? I >= 2 : (s == 1 && I >= SLAB_MIN_PER_TILE * (size_t)tiles && I >= ((size_t)1 << 21));
-}
-// the near slab: the ranks whose instances start below slab_target(I) (a quarter of I; gs_api.hip)
-uint32_t slab_target(size_t I);
-// workgroups of the far slab's compaction (gs_forward.hip k_far_count / k_far_compact: 4096 slots each)
-inline uint32_t far_blocks(size_t I) { return (uint32_t)((I + 4095) / 4096) + 1u; }
-struct SlabPtrs {
-  uint32_t *keys_a, *vals_a, *keys_b, *vals_b;  // the far slab's tile sort (keys / slots), ping-pong
-  uint2* ranges_a;       // per tile: the near slab's list range (in the near slab's sorted list)
-  uint2* ranges_b;       // per tile: the far slab's list range
-  uint32_t* n_a;         // per tile: the near slab's entries (the far slab's resume position)
-  uint32_t* qsat;        // per tile and quadrant: every pixel stopped within the near slab
-  uint32_t* qbits;       // the same as 4 bits per tile (the far compaction's LDS copy)
-  uint32_t* partial;     // the far slab compaction's per-workgroup counts, then bases (far_blocks(I))
-  uint32_t* near_list;   // the near slab's sorted slots (its tile sort's result)
-  uint32_t* near_tile;   // ... and their tiles
-};
-
-inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base, SlabPtrs* slab = nullptr) {
+inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base) {
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -342,17 +311,6 @@ inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base, SlabPtrs
   size_t o_ss = take(sort_scratch_words(In) * 4);
   size_t o_is = take(GS_INST_REC ? In * 48 : 0);
   size_t o_cn = take(64);
-  // depth slabs: the far slab's sort buffers, per-tile ranges / counts / saturation, the far
-  // compaction's per-workgroup counts, and the combined list (which then is the view's point_list); the far
-  // sort reuses the near sort's scratch
-  const bool sl = slab_mode(I, tiles);
-  const size_t T = (size_t)(tiles > 0 ? tiles : 1);
-  size_t o_sk[4] = {0, 0, 0, 0}, o_ra = 0, o_rb = 0, o_na = 0, o_qs = 0, o_qb = 0, o_sp = 0, o_cl = 0;
-  if (sl) {
-    for (int k = 0; k < 4; k++) o_sk[k] = take(In * 4);
-    o_ra = take(T * 8), o_rb = take(T * 8), o_na = take(T * 4), o_qs = take(T * 16), o_qb = take((T + 7) / 8 * 4);
-    o_sp = take(((size_t)far_blocks(In) + 1) * 4), o_cl = take(In * 4);
-  }
   if (out && base) {
     out->count = (uint32_t*)(base + o_cn);
     out->inst_splat = GS_INST_REC ? (float4*)(base + o_is) : nullptr;
@@ -369,23 +327,6 @@ inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base, SlabPtrs
     out->sorted_tile = in_b ? out->keys_b : out->keys_a;
     // pass p writes aux_a (p even) or presort_gid (p odd): an odd pass count ends in aux_a
     out->point_gid = in_b ? out->aux_a : out->presort_gid;
-    if (sl) {
-      if (slab) {
-        slab->keys_a = (uint32_t*)(base + o_sk[0]);
-        slab->vals_a = (uint32_t*)(base + o_sk[1]);
-        slab->keys_b = (uint32_t*)(base + o_sk[2]);
-        slab->vals_b = (uint32_t*)(base + o_sk[3]);
-        slab->ranges_a = (uint2*)(base + o_ra);
-        slab->ranges_b = (uint2*)(base + o_rb);
-        slab->n_a = (uint32_t*)(base + o_na);
-        slab->qsat = (uint32_t*)(base + o_qs);
-        slab->qbits = (uint32_t*)(base + o_qb);
-        slab->partial = (uint32_t*)(base + o_sp);
-        slab->near_list = out->point_list;
-        slab->near_tile = out->sorted_tile;
-      }
-      out->point_list = (uint32_t*)(base + o_cl);  // the combined list, for every later kernel
-    }
   }
   return off;
 }
@@ -500,10 +441,6 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
 // when nonzero (the host clears the word before it hands it out)
 void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
                 hipStream_t st, uint32_t* err_host = nullptr);
-// binning + compositing of one view in depth slabs (slab_mode(I, tiles); the read-back forward)
-void fwd_bin_render_slabs(int P, uint32_t I, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
-                          const SlabPtrs& slab, const ImgPtrs& img, float* out_color, hipStream_t st,
-                          uint32_t* err_host);
 void mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
                   hipStream_t st);
 void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,

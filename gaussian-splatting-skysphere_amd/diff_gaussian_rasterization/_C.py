@@ -152,8 +152,7 @@ def preprocess_views(backgrounds, means3D, colors, opacity, scales, rotations, s
     out = [(int(nr[k]), radii[k], geoms[k], bounded) for k in range(K)]
     W0, H0 = int(image_widths[0]), int(image_heights[0])
     if os.environ.get("GSRAST_BATCH_VIEWS", "1") != "0" and all(
-            int(w) == W0 and int(h) == H0 for w, h in zip(image_widths, image_heights)) and not _lib.gs_binning_slabs(
-                max(int(nr[k]) for k in range(K)), W0, H0):
+            int(w) == W0 and int(h) == H0 for w, h in zip(image_widths, image_heights)):
         # the K views' binning (duplicate, tile sort, ranges) as one set of launches: every binning
         # buffer is a slice of one allocation, sized for the largest count, which then stands for
         # every view's num_rendered (buffer layout, backward scratch)

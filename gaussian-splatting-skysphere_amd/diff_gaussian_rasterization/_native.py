@@ -121,8 +121,6 @@ SIGNATURES = {
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),
     "gs_knn_mean_dist2": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p]),
     "gs_set_exact_exp": (_c_i, [_c_i]),
-    "gs_set_slabs": (_c_i, [_c_i]),
-    "gs_binning_slabs": (_c_i, [_c_ll, _c_i, _c_i]),
     "gs_ssim_partial_count": (_c_sz, [_c_i, _c_i, _c_i]),
     "gs_ssim_forward": (_c_i, [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_ssim_backward": (_c_i, [_c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 12
+#define GSRAST_ABI_VERSION 13  /* v13: the depth-slab binning (v12's gs_set_slabs / gs_binning_slabs) removed */
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -311,20 +311,6 @@ int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, voi
  * test_gpu_parity.py, fast-mode cases).  The initial mode comes from GSRAST_EXACT_EXP=1.
  * Returns the previous mode.  Set it between steps, not while a step is in flight. */
 int gs_set_exact_exp(int exact);
-
-/* ---- depth slabs (ABI v12, process-wide) ----
- * A view with many instances per tile (num_rendered >= 1024 x tiles and >= 2M) bins and renders
- * in two depth slabs: the nearest ranks holding about a quarter of the instances first, then the
- * rest only into tiles that still have a running pixel, resumed from the saved pixel state.  Every
- * output equals the one-list forward's; the binning buffer then holds only the instances that can
- * be walked, in one list per tile (num_rendered stays the buffer's size).  mode: 0 off (default;
- * initial value from GSRAST_SLABS), 1 by size, 2 always.  (Off by default: on the synthetic C5 scene
- * half of the far instances still land in tiles with a running pixel, and the extra passes cost
- * about what the shorter tile sort saves.)  Returns the previous mode; set it between
- * steps.  gs_binning_slabs: whether a view of num_rendered instances at W x H bins in slabs (such
- * views go through gs_forward_render / gs_forward_bounded, not gs_forward_bin_views). */
-int gs_set_slabs(int mode);
-int gs_binning_slabs(long long num_rendered, int image_width, int image_height);
 
 /* ---- fused SSIM of the photometric loss  <-  utils/loss_utils.py:ssim (train.py:91-92) ----
  * img1, img2: [planes, H, W] fp32 (planes = images x channels), window11_host: the 11 float32

@@ -58,24 +58,3 @@ def test_simple_knn_cpu_fails_loudly():
 
     with pytest.raises(RuntimeError, match="no CPU path"):
         distCUDA2(torch.zeros((5, 3)))
-
-
-def test_depth_slab_decision_and_buffer_sizes():
-    """The depth slabs (ABI v12) are chosen from num_rendered and the tile count alone, so the host's
-    buffer sizes and the kernels' layout agree: C5 (21.6M instances at 1080p, ~2650 per tile) bins in
-    slabs, C3 (4.33M, ~530 per tile) and small views do not; a slab view's binning buffer holds the
-    far slab's sort buffers and the combined list as well; mode 0 turns them off, 2 forces them."""
-    lib = _C._lib
-    prev = lib.gs_set_slabs(1)
-    try:
-        assert lib.gs_binning_slabs(21_600_000, 1920, 1080) == 1
-        assert lib.gs_binning_slabs(4_330_000, 1920, 1080) == 0
-        assert lib.gs_binning_slabs(100_000, 256, 256) == 0
-        with_slabs = lib.gs_binning_buffer_bytes(21_600_000, 1920, 1080)
-        lib.gs_set_slabs(0)
-        assert lib.gs_binning_slabs(21_600_000, 1920, 1080) == 0
-        assert lib.gs_binning_buffer_bytes(21_600_000, 1920, 1080) < with_slabs
-        lib.gs_set_slabs(2)
-        assert lib.gs_binning_slabs(1000, 256, 256) == 1
-    finally:
-        lib.gs_set_slabs(prev)

@@ -13,8 +13,9 @@ Two numerics modes (gs_set_exact_exp):
     within 1e-5 * |ref| + 1e-5 * max|ref| away from those pixels, and the gradients at the
     backward tolerance below for every Gaussian not listed in a tile holding a flagged pixel.
     The flagged count is reported and bounded (<= 0.1 % of the pixels).
-  - Backward: the GPU sums per-pixel terms in fp32 (wave DPP tree -> 4 wave slabs -> per-instance
-    records -> per-Gaussian sequential sum); the oracle sums the identical fp32 terms in fp64.
+  - Backward: the GPU sums per-pixel terms in fp32 (in-lane over the lane's pixels, then the wave's
+    DPP tree -> per-instance records -> per-Gaussian fp64 sum); the oracle sums the identical fp32
+    terms in fp64.
     Per tensor: |gpu - oracle| <= 1e-5 * |oracle| + 1e-5 * max|oracle|  (north-star 1e-5 rel fp32).
 """
 import math
@@ -221,17 +222,10 @@ def _check_forward_fast(ofw, cam, sc, device, bg):
     s = gs_scenes.raster_settings_for(cam, sc.sh_degree, bg=torch.tensor(bg, device=device), device=device)
     d = sc.to(device)
     e = torch.Tensor([])
-    # the one-list forward, whose instance list is the oracle's (with depth slabs -- C5 -- the list
-    # holds only the instances that can be walked; the autograd run of the caller uses the slabs and
-    # must reproduce this colour bit for bit)
-    prev = _C._lib.gs_set_slabs(0)
-    try:
-        num, color, radii, geom, binb, imgb = _C.rasterize_gaussians(
-            s.bg, d.means3D, e, d.opacities, d.scales, d.rotations, s.scale_modifier, e, s.viewmatrix, s.projmatrix,
-            s.tanfovx, s.tanfovy, s.image_height, s.image_width, d.shs, sc.sh_degree, s.campos, False, False)
-        ex = _C.debug_export(sc.P, cam.image_width, cam.image_height, num, geom, binb, imgb, device)
-    finally:
-        _C._lib.gs_set_slabs(prev)
+    num, color, radii, geom, binb, imgb = _C.rasterize_gaussians(
+        s.bg, d.means3D, e, d.opacities, d.scales, d.rotations, s.scale_modifier, e, s.viewmatrix, s.projmatrix,
+        s.tanfovx, s.tanfovy, s.image_height, s.image_width, d.shs, sc.sh_degree, s.campos, False, False)
+    ex = _C.debug_export(sc.P, cam.image_width, cam.image_height, num, geom, binb, imgb, device)
     torch.cuda.synchronize()
     assert num == ofw["num_rendered"]
     np.testing.assert_array_equal(radii.cpu().numpy(), ofw["radii"])
@@ -338,18 +332,10 @@ def test_fast_mode_full_c3_vs_oracle(oracle, device, fast_mode):
 def test_fast_mode_full_c5_vs_oracle(oracle, device, fast_mode):
     """C5 (bench --workload c5) at full size: 5M Gaussians SH3 at 1920x1080, 21.6M instances, most
     of them behind saturated pixels (the record cuts and the longest-first order at their extreme),
-    in the default numerics mode against the oracle; same checks as full C3.  The autograd run bins
-    in depth slabs (gs_set_slabs(1): on by size, as this view qualifies; off by default)."""
-    from diff_gaussian_rasterization import _C
-
+    in the default numerics mode against the oracle; same checks as full C3."""
     cam = gs_scenes.identity_camera(1920, 1080)
     sc = gs_scenes.random_gaussians(5_000_000, 3, cam=cam, seed=0)
-    prev = _C._lib.gs_set_slabs(1)
-    try:
-        assert _C._lib.gs_binning_slabs(21_000_000, 1920, 1080) == 1
-        _fast_mode_parity(oracle, device, cam, sc, np.zeros(3, np.float32))
-    finally:
-        _C._lib.gs_set_slabs(prev)
+    _fast_mode_parity(oracle, device, cam, sc, np.zeros(3, np.float32))
 
 
 def test_fast_mode_is_deterministic(device, fast_mode):

@@ -8,7 +8,8 @@ from collections import defaultdict
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 agg = defaultdict(lambda: defaultdict(list))
 dur = defaultdict(list)
-for f in sorted(glob.glob(os.path.join(root, "pmc_*", "run_counter_collection.csv"))):
+pat = sys.argv[2] if len(sys.argv) > 2 else "pmc_"
+for f in sorted(glob.glob(os.path.join(root, pat + "*", "run_counter_collection.csv"))):
     for row in csv.DictReader(open(f)):
         k = row["Kernel_Name"]
         short = k.split("(")[0].replace("void ", "").split("<")[0].replace("gs::", "")
