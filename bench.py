@@ -706,7 +706,19 @@ def train_step_bench(sc, cam, deg, dev, steps, densify):
     settings = gs_scenes.raster_settings_for(cam, deg, device=dev)
     gt = torch.rand((3, H, W), generator=torch.Generator().manual_seed(2)).to(dev)
     out = {"what": "train.py:86-128 per iteration (one view): render, L1+SSIM (lambda 0.2), backward, "
-                   "densification stats, Adam step, zero_grad; no loss.item() readback"}
+                   "densification stats, Adam step, zero_grad; `fused` / `torch_glue` without the per-iteration "
+                   "loss.item() readback of train.py:99, `fused_item` with it (as unmodified train.py runs)"}
+    # train.py's own loop shape: the loss read back every iteration (host waits for the iteration)
+    model = ts.TrainModel(sc, dev, fused=True)
+    for _ in range(3):
+        ts.train_step(model, settings, gt, fused=True, loss_item=True)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        ts.train_step(model, settings, gt, fused=True, loss_item=True)
+    dt = (time.perf_counter() - t) / steps
+    out["fused_item"] = {"iters_s": round(1.0 / dt, 2), "ms_per_iter": round(1e3 * dt, 4)}
+    del model
     for fused in (True, False):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()

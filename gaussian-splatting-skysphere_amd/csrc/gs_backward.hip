@@ -462,9 +462,6 @@ __global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) GS_WPE_ATTR(GS_BWD_WPE) v
 #ifndef GS_BWDT_MINW
 #define GS_BWDT_MINW 1
 #endif
-#ifndef GS_BWDT_CENTRED
-#define GS_BWDT_CENTRED 1  // 0: moments about the splat mean summed in fp32 (k_render_bwd's form)
-#endif
 
 struct BwdSlot {
   float T, U, d0, d1, d2;
@@ -473,8 +470,9 @@ struct BwdSlot {
 
 // one slot's evaluation + commit for one entry; s[] accumulates the lane's slot terms
 template <bool EXACT>
-__device__ __forceinline__ bool bwd_slot(BwdSlot& q, float pfx, float pfy, float ux, float uy, const float4 xr,
-                                         const float4 co, float bl, uint32_t e, float* s) {
+__device__ __forceinline__ bool bwd_slot(BwdSlot& q, float pfx, float pfy, const float4 xr, const float4 co,
+                                         const float4 br, uint32_t e, float* s) {
+  const float bl = br.x;
   const float dx = xr.x - pfx, dy = xr.y - pfy;
   const float pw = falloff_log2(co, dx, dy);  // log2(e) * power
   const float oG = co.w * exp2_m<EXACT>(pw);
@@ -494,9 +492,12 @@ __device__ __forceinline__ bool bwd_slot(BwdSlot& q, float pfx, float pfy, float
   s[0] = __builtin_fmaf(dch, q.d0, s[0]);
   s[1] = __builtin_fmaf(dch, q.d1, s[1]);
   s[2] = __builtin_fmaf(dch, q.d2, s[2]);
-  // moments of q about the tile centre (ux, uy = pixel - centre, |.| <= 7.5, exact): small terms,
-  // turned into the moments about the splat mean in fp64 at the flush (see k_render_bwd_tw)
-  const float mx = GS_BWDT_CENTRED ? ux : dx, my = GS_BWDT_CENTRED ? uy : dy;
+  // moments of q about the entry's reference point r = the splat mean clamped to the tile's pixel
+  // box (u = dx - (mean - r) = r - pixel): for a splat centred in the tile u is dx itself, for one
+  // centred outside it |u| <= 15 instead of the distance to the mean -- the terms stay small, so
+  // the fp32 sums keep the precision the covariance chain needs.  The flush shifts them to the
+  // mean in fp64 (k_render_bwd_tw).
+  const float mx = dx - br.y, my = dy - br.z;
   const float qx = qq * mx, qy = qq * my;
   s[3] = s[3] + qx;
   s[4] = s[4] + qy;
@@ -522,7 +523,7 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
                                                                     float* __restrict__ gradrec) {
   __shared__ float4 s_xy[64];  // (x, y, r, g)
   __shared__ float4 s_co[64];  // falloff coefficients + opacity (fall_coefs)
-  __shared__ float s_bl[64];   // b
+  __shared__ float4 s_br[64];  // (b, mean - r: x, y, -), r the moments' reference point (bwd_slot)
   __shared__ __attribute__((aligned(16))) float s_acc[64][16];
   const uint32_t tile = __builtin_amdgcn_readfirstlane(tile_order ? tile_order[blockIdx.x] : blockIdx.x);
   if (tile == ~0u) return;  // a hole of the XCD-group launch order
@@ -555,7 +556,6 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
   }
   const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
   const float pfx0 = (float)qx0, pfy0 = (float)qy0;
-  const float ux0 = (float)(lane & 7) - 7.5f, uy0 = (float)(lane >> 3) - 7.5f;  // slot 0 pixel - tile centre
   using lds_float = __attribute__((address_space(3))) float;
   // writer lanes 16 r + 8 h: s[r + 4 h] at slot r + 4 h, their s8 partial at slot 8 + r + 4 h
   lds_float* const acc_lane = (lds_float*)(&s_acc[0][(lane >> 4) + 4 * ((lane >> 3) & 1)]);
@@ -564,21 +564,31 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
   // staging pipeline (one entry per lane): while batch k is walked, the splat records of batch
   // k + 1, the ids of batch k + 2 and (ids by slot) the slots of batch k + 3 are in flight.
   // Batch k's entry of lane t sits at list position range.x + e0 - 64 k, e0 = n_eff - 1 - t.
+  // The loads are unconditional, with list positions below 0 clamped to 0 (a valid entry: the
+  // lane stages nothing then): a load under a condition has to keep the register's old value on
+  // the other path, and the copy that merges the two makes the compiler wait for the load right
+  // where it is issued instead of at the next batch.
   const int32_t e0 = (int32_t)n_eff - 1 - lane;
   const uint32_t* const plist = point_list + range.x;
-  uint32_t slot_c = 0, S1 = 0, G1 = 0, S2 = 0;
-  float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pd = pa;
-  if (e0 >= 0) {
-    slot_c = plist[e0];
-    const uint32_t g0 = GS_SORT_GID ? point_gid[range.x + e0] : point_gid[slot_c];
-    pa = splat[3 * g0], pb = splat[3 * g0 + 1], pd = splat[3 * g0 + 2];
-  }
-  if (e0 - 64 >= 0) {
-    S1 = plist[e0 - 64];
-    G1 = GS_SORT_GID ? point_gid[range.x + e0 - 64] : point_gid[S1];
-  }
-  if (!GS_SORT_GID && e0 - 128 >= 0) S2 = plist[e0 - 128];
+  auto pos = [&](int32_t e) { return (uint32_t)max(e, 0); };
+  uint32_t slot_c = plist[pos(e0)];
+  uint32_t G1 = GS_SORT_GID ? point_gid[range.x + pos(e0)] : point_gid[slot_c];
+  float4 pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
+  uint32_t S1 = plist[pos(e0 - 64)];
+  G1 = GS_SORT_GID ? point_gid[range.x + pos(e0 - 64)] : point_gid[S1];
+  uint32_t S2 = GS_SORT_GID ? 0u : plist[pos(e0 - 128)];
 
+  uint32_t rec_lanes = 0;  // lanes holding a mapped record in their LDS row (the last flushed batch)
+  auto store_records = [&]() {
+    if ((uint32_t)lane < rec_lanes) {
+      const float4* row = reinterpret_cast<const float4*>(&s_acc[lane][0]);
+      const float4 a = row[0], b = row[1], d = row[2];
+      Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)__float_as_uint(d.y) * GRAD_REC);
+      r[0] = Rec3{a.x, a.y, a.z};
+      r[1] = Rec3{a.w, b.x, b.y};
+      r[2] = Rec3{b.z, b.w, d.x};
+    }
+  };
   for (uint32_t base = 0; base < n_eff; base += 64) {
     const uint32_t cnt = min(64u, n_eff - base);
     // stage: lane t holds entry t of the batch (walk order: back to front)
@@ -589,25 +599,27 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
     if (mine) {
       s_xy[lane] = make_float4(pa.x, pa.y, pb.z, pb.w);
       s_co[lane] = fall_coefs(pa.z, pa.w, pb.x, pb.y);
-      s_bl[lane] = pd.x;
+      const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
+      s_br[lane] = make_float4(pd.x, pa.x - fminf(fmaxf(pa.x, x0), x0 + 15.0f),
+                               pa.y - fminf(fmaxf(pa.y, y0), y0 + 15.0f), 0.0f);
       qmask = quadrant_mask(pa.x, pa.y, pa.z, pa.w, pb.x, pd.z, tx, ty);
     }
     // issue the next batch's splat loads, the ids after it and (ids by slot) the slots after those
     const int32_t e1 = e0 - (int32_t)(base + 64);
-    if (e1 >= 0) {
-      slot_c = S1;
-      pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
+    slot_c = S1;
+    pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
+    if (GS_SORT_GID) {
+      S1 = plist[pos(e1 - 64)];
+      G1 = point_gid[range.x + pos(e1 - 64)];
+    } else {
+      S1 = S2;
+      G1 = point_gid[S2];
+      S2 = plist[pos(e1 - 128)];
     }
-    if (e1 - 64 >= 0) {
-      if (GS_SORT_GID) {
-        S1 = plist[e1 - 64];
-        G1 = point_gid[range.x + e1 - 64];
-      } else {
-        S1 = S2;
-        G1 = point_gid[S2];
-      }
-    }
-    if (!GS_SORT_GID && e1 - 128 >= 0) S2 = plist[e1 - 128];
+    // the previous batch's records (mapped by its flush into the lanes' LDS rows, slot in word 9):
+    // stored now, behind this batch's loads, so that the wait for those loads at the next staging
+    // does not also wait for just-issued stores (loads and stores share one counter)
+    if (base > 0) store_records();
     // per-slot entry sets; entries no pixel of quadrant k reaches (e >= qlast[k]) sit at the low bits
     uint64_t M[4];
 #pragma unroll
@@ -624,8 +636,7 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
     while (m) {
       const uint32_t j = (uint32_t)__builtin_ctzll(m);
       m &= m - 1;
-      const float4 xr = s_xy[j], co = s_co[j];
-      const float bl = s_bl[j];
+      const float4 xr = s_xy[j], co = s_co[j], br = s_br[j];
       const uint32_t e = n_eff - 1 - (base + j);
       float s[GRAD_REC];
 #pragma unroll
@@ -634,8 +645,7 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if ((M[k] >> j) & 1ull)
-          con |= bwd_slot<EXACT>(p[k], pfx0 + (float)(8 * (k & 1)), pfy0 + (float)(8 * (k >> 1)),
-                                 ux0 + (float)(8 * (k & 1)), uy0 + (float)(8 * (k >> 1)), xr, co, bl, e, s);
+          con |= bwd_slot<EXACT>(p[k], pfx0 + (float)(8 * (k & 1)), pfy0 + (float)(8 * (k >> 1)), xr, co, br, e, s);
       if (__ballot(con) != 0) {
         wrote |= 1ull << j;
         float d, d8;
@@ -651,7 +661,8 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
       }
     }
     __builtin_amdgcn_wave_barrier();
-    // flush: lane t stores the record of its entry (zeros for an entry no pixel took)
+    // flush: lane t maps the sums of its entry into the record (zeros for an entry no pixel took),
+    // written back into its LDS row with the slot; stored by the next batch (or after the loop)
     if (mine) {
       float S[GRAD_REC];
       if ((wrote >> lane) & 1ull) {
@@ -665,53 +676,30 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
 #pragma unroll
         for (int t = 0; t < GRAD_REC; t++) S[t] = 0.0f;
       }
-      // S3..S7 are the moments of q = o G dL/dalpha about the tile centre; with D = mean - centre
-      // (dx = D.x - ux): sum q dx = D.x S8 - S3, sum q dx^2 = D.x^2 S8 - 2 D.x S3 + S5, ... in fp64,
-      // one rounding to the record (the conic gradient of a long splat is a small difference of
-      // large moments: rounding them term by term in fp32 is what the covariance chain amplifies)
-#if !GS_BWDT_CENTRED
-      Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)slot * GRAD_REC);
-      r[0] = Rec3{S[0], S[1], S[2]};
-      r[1] = Rec3{-ddelx_dx * (ccx * S[3] + ccy * S[4]), -ddely_dy * (ccz * S[4] + ccy * S[3]), -0.5f * S[5]};
-      r[2] = Rec3{-0.5f * S[6], -0.5f * S[7], S[8] != 0.0f ? S[8] / cop : 0.0f};
-#elif GS_BWDT_CENTRED == 2
-      // the same in fp32 with FMAs: its roundings are of the size of the record's own final rounding
-      const float2 mxy = *reinterpret_cast<const float2*>(&s_xy[lane]);
-      const float Dx = mxy.x - ((float)(tx * GS_TILE) + 7.5f), Dy = mxy.y - ((float)(ty * GS_TILE) + 7.5f);
-      const float q0 = S[8], qx = S[3], qy = S[4];
-      const float m1x = __builtin_fmaf(Dx, q0, -qx), m1y = __builtin_fmaf(Dy, q0, -qy);
-      const float m2xx = __builtin_fmaf(Dx, __builtin_fmaf(Dx, q0, -2.0f * qx), S[5]);
-      const float m2xy = __builtin_fmaf(Dx, __builtin_fmaf(Dy, q0, -qy), __builtin_fmaf(-Dy, qx, S[6]));
-      const float m2yy = __builtin_fmaf(Dy, __builtin_fmaf(Dy, q0, -2.0f * qy), S[7]);
-      Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)slot * GRAD_REC);
-      r[0] = Rec3{S[0], S[1], S[2]};
-      r[1] = Rec3{-ddelx_dx * (ccx * m1x + ccy * m1y), -ddely_dy * (ccz * m1y + ccy * m1x), -0.5f * m2xx};
-      r[2] = Rec3{-0.5f * m2xy, -0.5f * m2yy, S[8] != 0.0f ? S[8] / cop : 0.0f};
-#else
-      const float2 mxy = *reinterpret_cast<const float2*>(&s_xy[lane]);
-      // the tile centre is formed here (from scalars), not kept in four VGPRs across the walk
-      int ox = tx * GS_TILE, oy = ty * GS_TILE;
-      asm volatile("" : "+s"(ox), "+s"(oy));
-      const double Dx = (double)mxy.x - ((double)ox + 7.5), Dy = (double)mxy.y - ((double)oy + 7.5), q0 = S[8];
-      // (scheduling barriers keep the fp64 temporaries of one output from living beside the next's)
-      const float m1x = (float)__builtin_fma(Dx, q0, -(double)S[3]), m1y = (float)__builtin_fma(Dy, q0, -(double)S[4]);
+      // S3..S7 are the moments of q about the reference point r; with R = mean - r (dx = u + R):
+      // sum q dx = S3 + R.x S8, sum q dx^2 = S5 + 2 R.x S3 + R.x^2 S8, ... in fp64, one rounding to
+      // the record (R = 0, nothing to shift, for a splat centred in the tile)
+      const float2 R = *reinterpret_cast<const float2*>(&s_br[lane].y);
+      const double Rx = R.x, Ry = R.y, q0 = S[8];
+      const float m1x = (float)__builtin_fma(Rx, q0, (double)S[3]), m1y = (float)__builtin_fma(Ry, q0, (double)S[4]);
       __builtin_amdgcn_sched_barrier(0);
-      const float m2xx = (float)__builtin_fma(Dx, __builtin_fma(Dx, q0, -2.0 * (double)S[3]), (double)S[5]);
+      const float m2xx = (float)__builtin_fma(Rx, __builtin_fma(Rx, q0, 2.0 * (double)S[3]), (double)S[5]);
       __builtin_amdgcn_sched_barrier(0);
-      const float m2xy = (float)__builtin_fma(Dx, __builtin_fma(Dy, q0, -(double)S[4]),
-                                              __builtin_fma(-Dy, (double)S[3], (double)S[6]));
+      const float m2xy = (float)__builtin_fma(Rx, __builtin_fma(Ry, q0, (double)S[4]),
+                                              __builtin_fma(Ry, (double)S[3], (double)S[6]));
       __builtin_amdgcn_sched_barrier(0);
-      const float m2yy = (float)__builtin_fma(Dy, __builtin_fma(Dy, q0, -2.0 * (double)S[4]), (double)S[7]);
+      const float m2yy = (float)__builtin_fma(Ry, __builtin_fma(Ry, q0, 2.0 * (double)S[4]), (double)S[7]);
       __builtin_amdgcn_sched_barrier(0);
-      Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)slot * GRAD_REC);
-      r[0] = Rec3{S[0], S[1], S[2]};
-      r[1] = Rec3{-ddelx_dx * (ccx * m1x + ccy * m1y), -ddely_dy * (ccz * m1y + ccy * m1x), -0.5f * m2xx};
+      float4* row = reinterpret_cast<float4*>(&s_acc[lane][0]);
+      row[0] = make_float4(S[0], S[1], S[2], -ddelx_dx * (ccx * m1x + ccy * m1y));
+      row[1] = make_float4(-ddely_dy * (ccz * m1y + ccy * m1x), -0.5f * m2xx, -0.5f * m2xy, -0.5f * m2yy);
       // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
-      r[2] = Rec3{-0.5f * m2xy, -0.5f * m2yy, S[8] != 0.0f ? S[8] / cop : 0.0f};
-#endif
+      row[2] = make_float4(S[8] != 0.0f ? S[8] / cop : 0.0f, __uint_as_float(slot), 0.0f, 0.0f);
     }
+    rec_lanes = cnt;
     __builtin_amdgcn_wave_barrier();  // the next batch overwrites the staged entries
   }
+  store_records();
 }
 
 // Longest-first launch order for the backward.  A tile's walk is as long as its largest

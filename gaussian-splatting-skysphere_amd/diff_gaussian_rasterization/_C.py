@@ -25,6 +25,22 @@ from . import _native
 _lib = _native.load()
 
 
+def _load_ext():
+    """The torch C++ host fast path (_gs_ext, csrc/gs_torch_ext.cpp) of the plain forward / backward
+    calls, if built (setup_ext.py); GSRAST_NO_EXT=1 keeps every call on the ctypes path."""
+    if os.environ.get("GSRAST_NO_EXT", "0") not in ("", "0"):
+        return None
+    try:
+        from . import _gs_ext
+    except ImportError:
+        return None
+    _gs_ext.init()
+    return _gs_ext
+
+
+_EXT = _load_ext()
+
+
 def _dev_check(t: torch.Tensor, name: str):
     if not t.is_cuda:
         raise RuntimeError(
@@ -196,6 +212,12 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     features_dc [P,1,3], sh_rest features_rest [P,M-1,3]; gs_forward_preprocess_split).
     capacity: the binning buffer is sized for that many instances and the whole forward is
     enqueued without a host wait (gs_forward_bounded); the returned num_rendered is the capacity."""
+    if _EXT is not None and prepared is None and capacity is None and means3D.is_cuda:
+        out = _EXT.forward(background, means3D, colors, opacity, scales, rotations, float(scale_modifier),
+                           cov3D_precomp, viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy), int(image_height),
+                           int(image_width), sh, int(degree), campos, bool(prefiltered), bool(debug), sh_rest)
+        _LAST_NUM_RENDERED[0] = out[0]
+        return out
     x = _Inputs(background, means3D, colors, opacity, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
                 campos, sh_rest=sh_rest)
     if prepared is not None and x.sh_rest is not None:
@@ -290,6 +312,11 @@ def backward_impl(background, means3D, radii, colors, scales, rotations, scale_m
     wait_event: torch.cuda.Event the stream waits for before the kernel that writes the gradients
     (a sink shared with views on other streams).  sh_rest: split SH rows as rasterize_gaussians;
     the `sh` gradient is then that of the concatenation, [P, M, 3]."""
+    if _EXT is not None and not want_all and not sinks and wait_event is None and means3D.is_cuda:
+        return _EXT.backward(background, means3D, radii, colors, scales, rotations, float(scale_modifier),
+                             cov3D_precomp, viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy), dL_dout_color,
+                             sh, int(degree), campos, geomBuffer, int(R), binningBuffer, imageBuffer, bool(debug),
+                             sh_rest)
     x = _Inputs(background, means3D, colors, None, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
                 campos, need_opacity=False, sh_rest=sh_rest)
     P, dev = x.P, x.device

@@ -165,11 +165,12 @@ def prepare_views(rasterizers, means3D, opacities, shs=None, colors_precomp=None
     if binning_capacity is not None:
         caps = ([int(binning_capacity)] * len(ss) if isinstance(binning_capacity, int)
                 else [int(c) for c in binning_capacity])
+    views = [_contiguous_matrix(s.viewmatrix, streams) for s in ss]
+    projs = [_contiguous_matrix(s.projmatrix, streams) for s in ss]
     with torch.no_grad():
         tri = _C.preprocess_views([s.bg for s in ss], means3D.detach(), e(colors_precomp).detach(), opacities.detach(),
                                   e(scales).detach(), e(rotations).detach(), s0.scale_modifier,
-                                  e(cov3D_precomp).detach(), [_contiguous_matrix(s.viewmatrix) for s in ss],
-                                  [_contiguous_matrix(s.projmatrix) for s in ss], [s.tanfovx for s in ss],
+                                  e(cov3D_precomp).detach(), views, projs, [s.tanfovx for s in ss],
                                   [s.tanfovy for s in ss], [s.image_height for s in ss], [s.image_width for s in ss],
                                   e(shs).detach(), s0.sh_degree, [s.campos for s in ss], s0.prefiltered, s0.debug,
                                   streams, caps)
@@ -180,19 +181,28 @@ def prepare_views(rasterizers, means3D, opacities, shs=None, colors_precomp=None
 _CONTIG: dict = {}  # id(camera tensor) -> (weakref, _version, contiguous copy)
 
 
-def _contiguous_matrix(t: torch.Tensor) -> torch.Tensor:
+def _contiguous_matrix(t: torch.Tensor, streams=None) -> torch.Tensor:
     """t.contiguous() for the camera matrices, memoised per source tensor and version.  The
     reference's Camera keeps world_view_transform / full_proj_transform as transposed views
-    (scene/cameras.py:54-56), so every render() would otherwise copy both (one copy launch each)."""
+    (scene/cameras.py:54-56), so every render() would otherwise copy both (one copy launch each).
+    The copy is made on the current stream; `streams` (views rendered on other streams) are
+    recorded on it, so that the allocator does not reuse it while their kernels may still read
+    it after the memo drops it."""
     if t.is_contiguous():
-        return t
-    e = _CONTIG.get(id(t))
-    if e is not None and e[0]() is t and e[1] == t._version:
-        return e[2]
-    c = t.contiguous()
-    if len(_CONTIG) > 256:
-        _CONTIG.clear()
-    _CONTIG[id(t)] = (weakref.ref(t), t._version, c)
+        c = t
+    else:
+        e = _CONTIG.get(id(t))
+        if e is not None and e[0]() is t and e[1] == t._version:
+            c = e[2]
+        else:
+            c = t.contiguous()
+            if len(_CONTIG) > 256:
+                _CONTIG.clear()
+            _CONTIG[id(t)] = (weakref.ref(t), t._version, c)
+    if streams and c.is_cuda:
+        for st in streams:
+            if st is not None:
+                c.record_stream(st)
     return c
 
 

@@ -27,7 +27,7 @@ import torch
 
 import gs_loss
 import gs_train
-from diff_gaussian_rasterization import GaussianRasterizer
+from diff_gaussian_rasterization import GaussianRasterizer, bounded_status
 
 # OptimizationParams defaults (/root/reference/arguments/__init__.py:74-83)
 POSITION_LR_INIT = 0.00016
@@ -86,10 +86,12 @@ class TrainModel:
                 torch.exp(self._scaling), torch.nn.functional.normalize(self._rotation))
 
 
-def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | None = None, split_sh: bool = True):
+def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | None = None, split_sh: bool = True,
+           binning_capacity: int | None = None):
     """gaussian_renderer.render() for the default pipe (SH and covariance in the rasterizer).
     act_leaves (a list): the activated inputs are made autograd leaves (their adjoint then runs in
-    FusedAdam.step_activated) and appended to it as (shs, opacity, scales, rotations)."""
+    FusedAdam.step_activated) and appended to it as (shs, opacity, scales, rotations).
+    binning_capacity: a bounded forward (no host wait; HIP-graph capturable), see train_step."""
     sh_split = None
     if act_leaves is not None and not split_sh:
         acts = gs_train.activate_values(model._features_dc, model._features_rest, model._opacity, model._scaling,
@@ -121,7 +123,7 @@ def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | N
     screenspace_points = torch.empty_like(means3D, requires_grad=True)
     image, radii = GaussianRasterizer(raster_settings=settings)(
         means3D=means3D, means2D=screenspace_points, shs=shs, colors_precomp=None, opacities=opacity, scales=scales,
-        rotations=rotations, cov3D_precomp=None, sh_split=sh_split)
+        rotations=rotations, cov3D_precomp=None, sh_split=sh_split, binning_capacity=binning_capacity)
     return image, screenspace_points, radii
 
 
@@ -133,14 +135,21 @@ def _torch_densification_stats(model: TrainModel, viewspace, radii):
 
 
 def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool = True, densify_stats: bool = True,
-               lambda_dssim: float = LAMBDA_DSSIM, fused_adjoint: bool = True, split_sh: bool = True) -> torch.Tensor:
-    """One iteration (module docstring).  Returns the loss tensor (not read back: the reference's
-    `loss.item()` for its progress bar, train.py:99, is left to the caller).
+               lambda_dssim: float = LAMBDA_DSSIM, fused_adjoint: bool = True, split_sh: bool = True,
+               loss_item: bool = False, binning_capacity: int | None = None):
+    """One iteration (module docstring).  Returns the loss tensor, or with loss_item=True the
+    reference's per-iteration `loss.item()` (train.py:99, its progress-bar EMA): a host read-back
+    that waits for the whole iteration.
     fused_adjoint (with fused): the activation's backward runs inside the Adam update
     (FusedAdam.step_activated), so the raw parameters' gradients are never stored; same floats as
-    activate's backward followed by FusedAdam.step, .grad of the activated parameters stays None."""
+    activate's backward followed by FusedAdam.step, .grad of the activated parameters stays None.
+    binning_capacity: the forward runs bounded (its binning buffer sized ahead, no host wait, so the
+    iteration can be captured in a HIP graph).  A view with more instances than the capacity is
+    invalid: the flags land in the device's bounded status, which train_step reads at the
+    loss.item() sync point (loss_item=True) and raises there -- the iteration that overflowed, not
+    a later one.  Without loss_item the caller polls bounded_status() after its own sync."""
     acts = [] if (fused and fused_adjoint) else None
-    image, viewspace, radii = render(model, settings, fused, acts, split_sh)
+    image, viewspace, radii = render(model, settings, fused, acts, split_sh, binning_capacity)
     if fused:  # the whole loss expression in one fused forward / backward (gs_loss.photometric_loss)
         loss, Ll1 = gs_loss.photometric_loss(image, gt_image, lambda_dssim)
     else:
@@ -162,6 +171,11 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
         else:
             model.optimizer.step()
         model.optimizer.zero_grad(set_to_none=True)
+    if loss_item:
+        value = loss.item()  # train.py:99 (waits for the iteration)
+        if binning_capacity is not None:
+            bounded_status()  # raises if this iteration's bounded forward overflowed its capacity
+        return value
     return loss
 
 

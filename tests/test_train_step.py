@@ -149,3 +149,68 @@ def test_split_sh_with_gradient_bucket_equals_autograd(device):
     for a, r in zip(got, ref):
         assert torch.equal(a.grad, r.grad)
     b.close()
+
+
+def test_bounded_train_step_raises_at_its_own_loss_item(device):
+    """A train step with a bounded forward (binning_capacity) that fits equals the plain step bit
+    for bit; one whose view overflows its capacity raises at that iteration's loss.item() sync
+    (train.py:99), not one call later, and the status is cleared after it."""
+    import gs_train_step as ts
+    from diff_gaussian_rasterization import bounded_status, last_num_rendered
+
+    sc, settings, gt = _setup(device)
+    a, b = ts.TrainModel(sc, device), ts.TrainModel(sc, device)
+    la = ts.train_step(a, settings, gt, loss_item=True)
+    n = last_num_rendered()
+    lb = ts.train_step(b, settings, gt, loss_item=True, binning_capacity=n + 64)
+    assert la == lb
+    for name in ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    with pytest.raises(RuntimeError, match="binning capacity"):
+        ts.train_step(b, settings, gt, loss_item=True, binning_capacity=n // 4)
+    assert bounded_status() == (0, 0)
+
+
+def test_bounded_overflow_in_a_captured_step_raises_in_the_loop(device):
+    """render -> L1 + SSIM -> backward with a bounded forward, captured once into a HIP graph
+    (torch.cuda.CUDAGraph) and replayed in a training loop that polls bounded_status() at its
+    per-iteration sync: replays that fit report nothing; after the capacity is exceeded (the scene
+    grown in place past it) the loop's poll raises at that iteration."""
+    import gs_loss
+    import gs_train_step as ts
+    from diff_gaussian_rasterization import bounded_status, last_num_rendered
+
+    sc, settings, gt = _setup(device)
+    m = ts.TrainModel(sc, device)
+    ts.train_step(m, settings, gt, loss_item=True)
+    n = last_num_rendered()
+    static = {}
+
+    def step():
+        img, _, _ = ts.render(m, settings, fused=True, binning_capacity=n + 256)
+        loss, _ = gs_loss.photometric_loss(img, gt)
+        loss.backward()
+        static["loss"] = loss
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):  # warm-up on the capture stream
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    bounded_status()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for _ in range(3):
+        g.replay()
+        static["loss"].item()
+        assert bounded_status() == (0, 0)
+    # every Gaussian four times as large (in place: the graph reads the same parameter storage)
+    with torch.no_grad():
+        m._scaling.add_(float(np.log(4.0)))
+    g.replay()
+    static["loss"].item()
+    with pytest.raises(RuntimeError, match="binning capacity"):
+        bounded_status()
