@@ -161,6 +161,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="skip the HIP-graph measurement (the same step with bounded binning buffers, captured "
                          "once into a torch.cuda.CUDAGraph and replayed; N = 1)")
+    ap.add_argument("--profile-pass-only", action="store_true",
+                    help="run only the per-kernel event pass (W warm-up + K steps, one stream, as the default run's "
+                         "second pass), print its per-kernel averages as one JSON line and exit: the command "
+                         "`rocprofv3 --kernel-trace --stats` profiles to reproduce roofline.frac")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, check the process group against --gpus, print one JSON line and exit "
                          "before any GPU work (tests of the launcher; GS_BENCH_BACKEND=gloo runs it on CPU)")
@@ -285,6 +289,27 @@ def main():
     rg = ex["ranges"].to(torch.int64)
     walked = int(torch.minimum(tmax, rg[:, 1] - rg[:, 0]).sum())
     del ex, geom_b, bin_b, img_b
+
+    if args.profile_pass_only:
+        # only the kernel-duration pass below (its one-stream step), nothing else on the device
+        for _ in range(args.warmup):
+            step(streams[:1])
+        torch.cuda.synchronize()
+        lib = _native.load()
+        lib.gs_profile_reset()
+        lib.gs_profile_enable(1)
+        for _ in range(args.steps):
+            step(streams[:1])
+        torch.cuda.synchronize()
+        lib.gs_profile_enable(0)
+        prof = _native.profile_stats()
+        if rank == 0:
+            print(json.dumps({"profile_pass": {"workload": args.workload, "steps": args.steps, "warmup": args.warmup,
+                                               "views_per_step": len(my_views),
+                                               "kernels_avg_us": {k: round(1e3 * ms / max(n, 1), 2)
+                                                                  for k, (ms, n) in sorted(prof.items())},
+                                               "launches": {k: n for k, (ms, n) in sorted(prof.items())}}}))
+        return
 
     for _ in range(args.warmup):
         step()

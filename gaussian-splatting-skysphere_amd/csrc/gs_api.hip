@@ -208,6 +208,20 @@ size_t gs_binning_buffer_bytes(long long num_rendered, int W, int H) {
   return bin_layout((size_t)(num_rendered > 0 ? num_rendered : 1), tiles, nullptr, nullptr);
 }
 size_t gs_image_buffer_bytes(int W, int H) { return img_layout(W, H, nullptr, nullptr); }
+long long gs_binning_layout_count(size_t bytes, int W, int H) {
+  // gs_binning_buffer_bytes is non-decreasing in the count, and two counts with the same byte size
+  // have the same aligned array sizes, hence the same layout
+  if (gs_binning_buffer_bytes(1, W, H) > bytes) return 0;
+  long long lo = 1, hi = GS_MAX_INSTANCES;
+  while (lo < hi) {
+    const long long mid = lo + (hi - lo + 1) / 2;
+    if (gs_binning_buffer_bytes(mid, W, H) <= bytes)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
 size_t gs_grad_buffer_bytes(long long num_rendered) {
   const size_t R = (size_t)(num_rendered > 0 ? num_rendered : 1);
   return align_up(R * GRAD_REC * sizeof(float) + sumrec_extra_bytes(R));
@@ -286,9 +300,15 @@ static OrderFlags* order_flags() {
   return &g_order[dev];
 }
 
-// check ring slot k's queued forward (waits for its render kernel); true: failed (error set)
-static bool check_order_slot_locked(OrderFlags& o, int k) {
+// check ring slot k's queued forward (waits for its render kernel; with wait=false a forward whose
+// render has not finished yet stays queued for a later check); true: failed (error set)
+static bool check_order_slot_locked(OrderFlags& o, int k, bool wait = true) {
   if (o.state[k] != 2) return false;
+  if (!wait) {
+    const hipError_t q = hipEventQuery(o.ev[k]);
+    if (q == hipErrorNotReady) return false;
+    if (!check_hip(q, "hipEventQuery")) return true;
+  }
   o.state[k] = 0;
   if (!check_hip(hipEventSynchronize(o.ev[k]), "hipEventSynchronize")) return true;
   if (o.host[16 * k] & ERR_LOOKBACK) {
@@ -298,13 +318,17 @@ static bool check_order_slot_locked(OrderFlags& o, int k) {
   }
   return false;
 }
-// every queued forward's flags
-static bool check_order_flags() {
+// every queued forward's flags.  wait=false (the backward entry points): only the forwards whose
+// render kernel has finished -- a backward is queued right behind its forward's render, and waiting
+// for that render here would stall the host while the device has work; a forward whose render
+// has not finished is checked by the next call (at the latest the next forward, whose instance-count
+// readback comes after it on the stream)
+static bool check_order_flags(bool wait = true) {
   OrderFlags* o = order_flags();
   if (!o) return true;
   std::lock_guard<std::mutex> lk(o->mu);
   bool failed = false;
-  for (int k = 0; k < ORDER_RING; k++) failed |= check_order_slot_locked(*o, k);
+  for (int k = 0; k < ORDER_RING; k++) failed |= check_order_slot_locked(*o, k, wait);
   return failed;
 }
 
@@ -434,11 +458,14 @@ static int forward_preprocess_impl(int P, int D, int M, const float* background,
   // the instance offsets, so the host round trip overlaps device work.
   ReadbackSlot* rb = readback_slot();
   if (!rb) return 1;
-  if (check_order_flags()) return 1;  // an earlier forward's look-back waits
+  // earlier forwards' look-back waits: the finished ones now (no wait before the launches), then,
+  // after this forward's own readback (behind them on the stream), the rest
+  if (check_order_flags(false)) return 1;
   fwd_preprocess(g, c, radii_out, geo, st);
   fwd_order(P, geo, st, rb->dev, rb->ev[0]);
   check_hip(hipEventSynchronize(rb->ev[0]), "hipEventSynchronize");
   if (t_failed) return 1;
+  if (check_order_flags()) return 1;
   return read_view_totals(rb->host, 0, 1, num_rendered_host) ? 0 : 1;
 }
 
@@ -534,7 +561,7 @@ static int preprocess_views_impl(int K, int P, int D, int M, const float* const*
   static thread_local unsigned ev_next = 0;
   hipEvent_t& fork = ev_pre[ev_next++ & 3];
   if (!fork && !check_hip(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "hipEventCreate")) return 1;
-  if (!capacity && check_order_flags()) return 1;  // an earlier forward's look-back waits
+  if (!capacity && check_order_flags(false)) return 1;  // earlier forwards' look-back waits (finished ones)
   uint32_t cap32[FUSED_MAX_VIEWS];
   for (int v = 0; v < K; v++) cap32[v] = capacity ? (uint32_t)capacity[v] : 0xFFFFFFFFu;
   // geometry buffers at one stride (slices of one allocation, as prepare_views makes them): the K
@@ -791,6 +818,58 @@ int gs_forward_bounded(int P, int D, int M, const float* background, int W, int 
                              geom_buffer, capacity, binning_buffer, image_buffer, out_color, true, debug, stream);
 }
 
+// The eager forward with its count read back at the end (gsrast.h): the ordering stores the totals
+// into the readback slot and flags ERR_CAPACITY against `capacity`; the binning and the render are
+// queued behind it on the stream at once, so the device never waits for the host's round trip.
+int gs_forward_counted(int P, int D, int M, const float* background, int W, int H, const float* means3D,
+                       const float* shs, const float* shs_rest, const float* colors_precomp, const float* opacities,
+                       const float* scales, float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                       const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                       float tan_fovy, int prefiltered, int* radii_out, void* geom_buffer, long long capacity,
+                       void* binning_buffer, void* image_buffer, float* out_color, long long* num_rendered_host,
+                       int debug, void* stream) {
+  clear_error(debug);
+  if (num_rendered_host) *num_rendered_host = 0;
+  if (!validate(P, D, M, W, H, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, viewmatrix,
+                projmatrix, campos, background))
+    return 1;
+  if (!validate_split(M, shs, shs_rest, colors_precomp)) return 1;
+  if (P == 0) return 0;
+  if (capacity < 0 || capacity > GS_MAX_INSTANCES) return set_error("capacity out of range"), 1;
+  if (!radii_out || !geom_buffer || !binning_buffer || !image_buffer || !out_color || !num_rendered_host)
+    return set_error("missing buffer pointer"), 1;
+  ReadbackSlot* rb = readback_slot();
+  if (!rb) return 1;
+  if (check_order_flags(false)) return 1;  // earlier forwards' look-back waits (the finished ones)
+  hipStream_t st = (hipStream_t)stream;
+  GeomPtrs geo;
+  geom_layout((size_t)P, &geo, (char*)geom_buffer);
+  GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier,
+                 shs_rest};
+  CameraArgs c = make_camera(background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, prefiltered);
+  fwd_preprocess(g, c, radii_out, geo, st);
+  const uint32_t cap32 = (uint32_t)capacity;
+  fwd_order(P, geo, st, rb->dev, rb->ev[0], &cap32, nullptr);
+  if (t_failed) return 1;
+  if (forward_render_impl(P, background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii_out,
+                          geom_buffer, capacity, binning_buffer, image_buffer, out_color, false, debug, stream))
+    return 1;
+  check_hip(hipEventSynchronize(rb->ev[0]), "hipEventSynchronize");
+  if (t_failed) return 1;
+  // (this forward's render is queued: check the others without waiting for it)
+  if (check_order_flags(false)) return 1;
+  long long I = 0;
+  if (!read_view_totals(rb->host, 0, 1, &I)) return 1;
+  *num_rendered_host = I;
+  if (I > capacity) {
+    // the queued binning and render skipped their work (ERR_CAPACITY): clear the flag so that
+    // gs_forward_render can bin the same geometry into a buffer of the exact size
+    fwd_clear_flags(geo, ERR_CAPACITY, st);
+    return t_failed ? 1 : GS_COUNT_SHORT;
+  }
+  return 0;
+}
+
 int gs_bounded_status(unsigned* flags, long long* instances) {
   clear_error(0);
   BoundedStatus* bs = bounded_status();
@@ -872,8 +951,8 @@ static int backward_impl(int P, int D, int M, const float* background, int W, in
   // the gradient outputs may be shared with views on other streams: order only this last kernel
   if (wait_event && !check_hip(hipStreamWaitEvent(st, (hipEvent_t)wait_event, 0), "hipStreamWaitEvent")) return 1;
   bwd_preprocess(g, c, geo, bin, img, gradrec, (uint32_t)num_rendered, num_rendered > 0, out, st);
-  // the forward's ordering flags, now that this backward's kernels are queued
-  if (!t_failed && check_order_flags()) return 1;
+  // the ordering flags of the forwards that have finished, now that this backward's kernels are queued
+  if (!t_failed && check_order_flags(false)) return 1;
   return t_failed ? 1 : 0;
 }
 
@@ -959,7 +1038,7 @@ int gs_backward_render(int P, int D, int M, const float* background, int W, int 
   float* gradrec = (float*)grad_buffer;
   if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, st);
   bwd_records(g, geo, bin, img, gradrec, (uint32_t)num_rendered, num_rendered > 0, dL_dmeans2D, accumulate, st);
-  if (!t_failed && check_order_flags()) return 1;
+  if (!t_failed && check_order_flags(false)) return 1;
   return t_failed ? 1 : 0;
 }
 

@@ -489,9 +489,6 @@ __device__ __forceinline__ bool bwd_slot(BwdSlot& q, float pfx, float pfy, const
   const float Cd = __builtin_fmaf(bl, q.d2, __builtin_fmaf(xr.w, q.d1, xr.z * q.d0));
   const float dLa = __builtin_fmaf(Tn, Cd, -(q.U * inv));
   const float qq = oGm * dLa;  // dL/dG G = o G dL/dalpha (not gated by the 0.99 clamp)
-  s[0] = __builtin_fmaf(dch, q.d0, s[0]);
-  s[1] = __builtin_fmaf(dch, q.d1, s[1]);
-  s[2] = __builtin_fmaf(dch, q.d2, s[2]);
   // moments of q about the entry's reference point r = the splat mean clamped to the tile's pixel
   // box (u = dx - (mean - r) = r - pixel): for a splat centred in the tile u is dx itself, for one
   // centred outside it |u| <= 15 instead of the distance to the mean -- the terms stay small, so
@@ -499,6 +496,9 @@ __device__ __forceinline__ bool bwd_slot(BwdSlot& q, float pfx, float pfy, const
   // mean in fp64 (k_render_bwd_tw).
   const float mx = dx - br.y, my = dy - br.z;
   const float qx = qq * mx, qy = qq * my;
+  s[0] = __builtin_fmaf(dch, q.d0, s[0]);
+  s[1] = __builtin_fmaf(dch, q.d1, s[1]);
+  s[2] = __builtin_fmaf(dch, q.d2, s[2]);
   s[3] = s[3] + qx;
   s[4] = s[4] + qy;
   s[5] = __builtin_fmaf(qx, mx, s[5]);
@@ -510,6 +510,9 @@ __device__ __forceinline__ bool bwd_slot(BwdSlot& q, float pfx, float pfy, const
   return con;
 }
 
+#ifndef GS_BWDT_ROW
+#define GS_BWDT_ROW 20
+#endif
 template <bool EXACT>
 __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c, const uint2* __restrict__ ranges,
                                                                     const uint32_t* __restrict__ point_list,
@@ -524,7 +527,10 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
   __shared__ float4 s_xy[64];  // (x, y, r, g)
   __shared__ float4 s_co[64];  // falloff coefficients + opacity (fall_coefs)
   __shared__ float4 s_br[64];  // (b, mean - r: x, y, -), r the moments' reference point (bwd_slot)
-  __shared__ __attribute__((aligned(16))) float s_acc[64][16];
+  // entry rows of 20 floats: 16 used; the 80-B stride keeps the lanes' 16-B row accesses of the
+  // flush on distinct banks (64 B would put every 4th lane of a 16-lane group on one bank)
+  constexpr int ROW = GS_BWDT_ROW;
+  __shared__ __attribute__((aligned(16))) float s_acc[64][ROW];
   const uint32_t tile = __builtin_amdgcn_readfirstlane(tile_order ? tile_order[blockIdx.x] : blockIdx.x);
   if (tile == ~0u) return;  // a hole of the XCD-group launch order
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
@@ -652,7 +658,7 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
         wave_sum9_halfrows(s, hi8, d, d8);
         asm volatile("" ::"v"(d), "v"(d8));
         if ((lane & 7) == 0) {
-          uint32_t eo = j * 16;
+          uint32_t eo = j * ROW;
           asm volatile("" : "+s"(eo));
           lds_float* acc = acc_lane + eo;
           acc[0] = d;

@@ -453,6 +453,13 @@ void fwd_order(int P, const GeomPtrs& geo, hipStream_t st, uint32_t* host_counts
   }
 }
 
+__global__ __launch_bounds__(64) void k_clear_flags(uint32_t* __restrict__ err, uint32_t bits) {
+  if (threadIdx.x == 0) err[0] = err[0] & ~bits;
+}
+void fwd_clear_flags(const GeomPtrs& geo, uint32_t bits, hipStream_t st) {
+  GS_LAUNCH("clear_flags", k_clear_flags, dim3(1), dim3(64), 0, st, &geo.counters[CNT_ERR], bits);
+}
+
 // instance offsets in depth order (+ the duplicate's block owner table), after the depth sort
 void fwd_scan(int P, const GeomPtrs& geo, hipStream_t st) {
   const uint32_t n = (uint32_t)P;

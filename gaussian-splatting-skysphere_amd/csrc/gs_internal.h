@@ -431,6 +431,8 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
 void fwd_order(int P, const GeomPtrs& geo, hipStream_t st, uint32_t* host_counts = nullptr,
                hipEvent_t counts_ready = nullptr, const uint32_t* cap = nullptr, uint32_t* sticky = nullptr,
                int views = 1, uint64_t vstride = 0);
+// clear error flag bits in the geometry buffer's counters[CNT_ERR] (stream-ordered)
+void fwd_clear_flags(const GeomPtrs& geo, uint32_t bits, hipStream_t st);
 void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const GeomPtrs& geo, const BinPtrs& bin,
              const ImgPtrs& img, hipStream_t st);
 // the binning of `views` views of one image size at once: view v's geometry / binning / image

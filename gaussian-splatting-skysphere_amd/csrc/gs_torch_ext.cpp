@@ -11,12 +11,16 @@
 // resolves the entry points from that one copy (its per-device state -- bounded status, ordering
 // flags, numerics mode -- stays shared with the ctypes path).  Same exception texts as _C.py.
 // Plain calls only: prepared views, bounded forwards, gradient sinks and the split backward halves
-// stay on the ctypes path.
+// stay on the ctypes path.  The forward reads its instance count back after queueing every launch
+// (gs_forward_counted, binning buffer sized from the last count), so neither the device nor the host
+// idles across the host round trip that upstream's resize callbacks need between the two halves.
 #include <ATen/hip/HIPContext.h>
 #include <c10/core/DeviceGuard.h>
 #include <dlfcn.h>
 #include <torch/extension.h>
 
+#include <algorithm>
+#include <atomic>
 #include <string>
 
 namespace {
@@ -26,6 +30,9 @@ using fwd_pre_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, f_cp,
                           f_cp, float, float, int, int*, void*, long long*, int, void*);
 using fwd_render_t = int (*)(int, f_cp, int, int, f_cp, f_cp, f_cp, float, float, const int*, void*, long long, void*,
                              void*, float*, int, void*);
+using fwd_counted_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, f_cp, f_cp, f_cp, float, f_cp, f_cp, f_cp,
+                              f_cp, f_cp, float, float, int, int*, void*, long long, void*, void*, float*, long long*,
+                              int, void*);
 using bwd_acc_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, f_cp, f_cp, float, f_cp, f_cp, f_cp, f_cp,
                           f_cp, float, float, const int*, const void*, long long, const void*, const void*, f_cp,
                           void*, float*, float*, float*, float*, float*, float*, float*, float*, unsigned, void*,
@@ -38,12 +45,14 @@ using bwd_acc_split_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp,
 struct Fns {
   fwd_pre_t preprocess = nullptr, preprocess_split = nullptr;
   fwd_render_t render = nullptr;
+  fwd_counted_t counted = nullptr;
   bwd_acc_t backward = nullptr;
   bwd_acc_split_t backward_split = nullptr;
   size_t (*geom_bytes)(int) = nullptr;
   size_t (*binning_bytes)(long long, int, int) = nullptr;
   size_t (*image_bytes)(int, int) = nullptr;
   size_t (*grad_bytes)(long long) = nullptr;
+  long long (*layout_count)(size_t, int, int) = nullptr;
   const char* (*last_error)() = nullptr;
 } F;
 
@@ -57,12 +66,14 @@ void init() {
   resolve(F.preprocess, "gs_forward_preprocess");
   resolve(F.preprocess_split, "gs_forward_preprocess_split");
   resolve(F.render, "gs_forward_render");
+  resolve(F.counted, "gs_forward_counted");
   resolve(F.backward, "gs_backward_accumulate");
   resolve(F.backward_split, "gs_backward_accumulate_split");
   resolve(F.geom_bytes, "gs_geom_buffer_bytes");
   resolve(F.binning_bytes, "gs_binning_buffer_bytes");
   resolve(F.image_bytes, "gs_image_buffer_bytes");
   resolve(F.grad_bytes, "gs_grad_buffer_bytes");
+  resolve(F.layout_count, "gs_binning_layout_count");
   resolve(F.last_error, "gs_last_error");
 }
 
@@ -143,6 +154,21 @@ struct Inputs {
 
 inline void* stream_of(const c10::Device& dev) { return at::hip::getCurrentHIPStream(dev.index()).stream(); }
 
+// Instance count of the last forward per device: the next forward sizes its binning buffer ahead
+// of its count from it (gs_forward_counted), so the count is read back once every launch is queued
+// instead of between the two halves.  A forward whose count outgrew the estimate bins again into a
+// buffer of the exact size (the geometry is kept); the first forward on a device, a debug forward
+// and that fallback run the two-call path.
+constexpr int GS_COUNT_DEVICES = 64;
+std::atomic<long long> g_count_est[GS_COUNT_DEVICES];
+constexpr long long GS_CAP_ROUND = 1 << 16;
+
+long long capacity_for(long long est) {
+  const long long want = est + est / 8 + GS_CAP_ROUND;  // +12.5 % and one rounding step of headroom
+  const long long cap = (want + GS_CAP_ROUND - 1) / GS_CAP_ROUND * GS_CAP_ROUND;
+  return std::min<long long>(cap, (1ll << 31) - 1);
+}
+
 // _C.rasterize_gaussians (no prepared view, no capacity): both halves of the forward
 py::tuple forward(const at::Tensor& background, const at::Tensor& means3D, const c10::optional<at::Tensor>& colors,
                   const c10::optional<at::Tensor>& opacity, const c10::optional<at::Tensor>& scales,
@@ -165,21 +191,49 @@ py::tuple forward(const at::Tensor& background, const at::Tensor& means3D, const
   at::Tensor out_color = at::empty({3, H, W}, f32o);
   at::Tensor radii = at::empty({x.P}, f32o.dtype(at::kInt));
   at::Tensor geom = at::empty({(int64_t)F.geom_bytes((int)x.P)}, u8);
+  at::Tensor img = at::empty({(int64_t)F.image_bytes((int)W, (int)H)}, u8);
   long long nr = 0;
   const bool split = x.sh_rest.defined();
-  check((split ? F.preprocess_split : F.preprocess)(
-            (int)x.P, (int)degree, (int)x.M, fp(x.bg), (int)W, (int)H, fp(x.means3D), fp(x.sh),
-            split ? fp(x.sh_rest) : fp(x.colors), fp(x.opacity), fp(x.scales), (float)scale_modifier,
-            fp(x.rotations), fp(x.cov3D), fp(x.view), fp(x.proj), fp(x.campos), (float)tan_fovx, (float)tan_fovy,
-            (int)prefiltered, radii.data_ptr<int>(), geom.data_ptr(), &nr, (int)debug, st),
-        "rasterize_gaussians (preprocess)");
+  const int di = x.dev.index();
+  std::atomic<long long>* est = di >= 0 && di < GS_COUNT_DEVICES ? &g_count_est[di] : nullptr;
+  const long long e = est ? est->load(std::memory_order_relaxed) : 0;
+  if (e > 0 && !debug) {
+    const long long cap = capacity_for(e);
+    at::Tensor binning = at::empty({(int64_t)F.binning_bytes(cap, (int)W, (int)H)}, u8);
+    const int rc = F.counted((int)x.P, (int)degree, (int)x.M, fp(x.bg), (int)W, (int)H, fp(x.means3D), fp(x.sh),
+                             fp(x.sh_rest), fp(x.colors), fp(x.opacity), fp(x.scales), (float)scale_modifier,
+                             fp(x.rotations), fp(x.cov3D), fp(x.view), fp(x.proj), fp(x.campos), (float)tan_fovx,
+                             (float)tan_fovy, (int)prefiltered, radii.data_ptr<int>(), geom.data_ptr(), cap,
+                             binning.data_ptr(), img.data_ptr(), out_color.data_ptr<float>(), &nr, (int)debug, st);
+    if (rc != 2) check(rc, "rasterize_gaussians");
+    est->store(nr, std::memory_order_relaxed);
+    if (rc == 0) return py::make_tuple((int64_t)nr, out_color, radii, geom, binning, img);
+    // (2: more instances than the estimate; radii and geometry are complete, nr exact)
+  } else {
+    check((split ? F.preprocess_split : F.preprocess)(
+              (int)x.P, (int)degree, (int)x.M, fp(x.bg), (int)W, (int)H, fp(x.means3D), fp(x.sh),
+              split ? fp(x.sh_rest) : fp(x.colors), fp(x.opacity), fp(x.scales), (float)scale_modifier,
+              fp(x.rotations), fp(x.cov3D), fp(x.view), fp(x.proj), fp(x.campos), (float)tan_fovx, (float)tan_fovy,
+              (int)prefiltered, radii.data_ptr<int>(), geom.data_ptr(), &nr, (int)debug, st),
+          "rasterize_gaussians (preprocess)");
+    if (est) est->store(nr, std::memory_order_relaxed);
+  }
   at::Tensor binning = at::empty({(int64_t)F.binning_bytes(nr, (int)W, (int)H)}, u8);
-  at::Tensor img = at::empty({(int64_t)F.image_bytes((int)W, (int)H)}, u8);
   check(F.render((int)x.P, fp(x.bg), (int)W, (int)H, fp(x.view), fp(x.proj), fp(x.campos), (float)tan_fovx,
                  (float)tan_fovy, radii.data_ptr<int>(), geom.data_ptr(), nr, binning.data_ptr(), img.data_ptr(),
                  out_color.data_ptr<float>(), (int)debug, st),
         "rasterize_gaussians (render)");
   return py::make_tuple((int64_t)nr, out_color, radii, geom, binning, img);
+}
+
+// _C.binning_layout_count: the instance count the binning buffer is laid out for (R, or the capacity
+// of a gs_forward_counted buffer)
+long long layout_count(long long R, const at::Tensor& binning, int64_t W, int64_t H) {
+  const size_t n = (size_t)binning.numel();
+  if (n == F.binning_bytes(R, (int)W, (int)H)) return R;
+  const long long L = F.layout_count(n, (int)W, (int)H);
+  TORCH_CHECK(L >= R, "binningBuffer (", n, " bytes) is too small for num_rendered = ", R);
+  return L;
 }
 
 // _C.backward_impl with want_all=False, no gradient sinks and no wait event
@@ -216,6 +270,7 @@ py::tuple backward(const at::Tensor& background, const at::Tensor& means3D, cons
   at::Tensor dpix = f32(dL_dout_color, "dL_dout_color", x.dev);
   c10::DeviceGuard guard(x.dev);
   void* st = stream_of(x.dev);
+  R = layout_count((long long)R, binning, W, H);
   at::Tensor scratch = at::empty({(int64_t)F.grad_bytes((long long)R)}, f32o.dtype(at::kByte));
   const at::Tensor sc_out = has_sr ? g_sc : at::Tensor(), rot_out = has_sr ? g_rot : at::Tensor();
   if (x.sh_rest.defined()) {  // split SH rows: SH colours, so no dL/dcolors output
@@ -240,6 +295,16 @@ py::tuple backward(const at::Tensor& background, const at::Tensor& means3D, cons
   return result();
 }
 
+// the per-device estimate the next forward sizes its binning buffer from (tests; 0: none yet)
+long long count_estimate(int64_t device) {
+  TORCH_CHECK(device >= 0 && device < GS_COUNT_DEVICES, "device index out of range");
+  return g_count_est[device].load();
+}
+void set_count_estimate(int64_t device, long long n) {
+  TORCH_CHECK(device >= 0 && device < GS_COUNT_DEVICES, "device index out of range");
+  g_count_est[device].store(std::max<long long>(n, 0));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -247,4 +312,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("init", &init);
   m.def("forward", &forward);
   m.def("backward", &backward);
+  m.def("count_estimate", &count_estimate);
+  m.def("set_count_estimate", &set_count_estimate);
 }

@@ -296,6 +296,21 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     return num_rendered, out_color, radii, geom, binning, img
 
 
+def binning_layout_count(R, binningBuffer, W, H):
+    """The instance count binningBuffer is laid out for, which the C-ABI calls take as num_rendered:
+    R for a buffer of gs_binning_buffer_bytes(R) bytes (the two-call, bounded and prepared
+    forwards); for a buffer the eager forward sized ahead of its count (gs_forward_counted: the
+    returned num_rendered is the exact count, the buffer holds the capacity) that capacity."""
+    R = int(R)
+    n = binningBuffer.numel()
+    if n == _lib.gs_binning_buffer_bytes(R, W, H):
+        return R
+    L = int(_lib.gs_binning_layout_count(n, W, H))
+    if L < R:
+        raise RuntimeError(f"binningBuffer ({n} bytes) is too small for num_rendered = {R}")
+    return L
+
+
 # gradient outputs of the backward, in the upstream return order, with their GS_ACC_* bit
 GRAD_NAMES = ("means2D", "colors", "opacity", "means3D", "cov3D", "sh", "scales", "rotations")
 GS_ACC = {n: 1 << k for k, n in enumerate(GRAD_NAMES)}
@@ -357,9 +372,10 @@ def backward_impl(background, means3D, radii, colors, scales, rotations, scale_m
         return ret
     dpix = _f32(dL_dout_color, "dL_dout_color", dev)
     o = {n: (outs[n] if computed[n] else None) for n in GRAD_NAMES}
+    R = binning_layout_count(R, binningBuffer, W, H)
     with torch.cuda.device(dev):
         st = _stream(dev)
-        grad_scratch = torch.empty((_lib.gs_grad_buffer_bytes(int(R)),), dtype=torch.uint8, device=dev)
+        grad_scratch = torch.empty((_lib.gs_grad_buffer_bytes(R),), dtype=torch.uint8, device=dev)
         wait = ctypes.c_void_p(wait_event.cuda_event) if wait_event is not None else None
         if x.sh_rest is not None:  # split SH rows: SH colours, so no dL/dcolors output
             _native.check(
@@ -398,9 +414,10 @@ def backward_render(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fo
     proj = _f32(projmatrix, "projmatrix", dev, host_ok=True)
     cam = _f32(campos, "campos", dev, host_ok=True)
     dpix = _f32(dL_dout_color, "dL_dout_color", dev)
+    R = binning_layout_count(R, binningBuffer, W, H)
     with torch.cuda.device(dev):
         st = _stream(dev)
-        grad_scratch = torch.empty((_lib.gs_grad_buffer_bytes(int(R)),), dtype=torch.uint8, device=dev)
+        grad_scratch = torch.empty((_lib.gs_grad_buffer_bytes(R),), dtype=torch.uint8, device=dev)
         _native.check(
             _lib.gs_backward_render(P, int(degree), int(M), _ptr(bg), W, H, _ptr(view), _ptr(proj), _ptr(cam),
                                     float(tan_fovx), float(tan_fovy), _ptr(geomBuffer), int(R), _ptr(binningBuffer),
@@ -477,8 +494,9 @@ def debug_export(P, W, H, num_rendered, geomBuffer, binningBuffer, imageBuffer, 
     u32 = dict(dtype=torch.int32, device=device)
     f32 = dict(dtype=torch.float32, device=device)
     gx, gy = (W + 15) // 16, (H + 15) // 16
+    L = binning_layout_count(num_rendered, binningBuffer, W, H) if P > 0 else int(num_rendered)
     out = dict(
-        point_list=torch.zeros((max(num_rendered, 1),), **u32),
+        point_list=torch.zeros((max(L, 1),), **u32),
         ranges=torch.zeros((gx * gy, 2), **u32),
         xy=torch.zeros((P, 2), **f32),
         conic_opacity=torch.zeros((P, 4), **f32),
@@ -491,7 +509,7 @@ def debug_export(P, W, H, num_rendered, geomBuffer, binningBuffer, imageBuffer, 
     if P > 0:
         with torch.cuda.device(device):
             _native.check(
-                _lib.gs_debug_export(P, W, H, int(num_rendered), _ptr(geomBuffer), _ptr(binningBuffer),
+                _lib.gs_debug_export(P, W, H, L, _ptr(geomBuffer), _ptr(binningBuffer),
                                      _ptr(imageBuffer), *[_ptr(out[k]) for k in (
                                          "point_list", "ranges", "xy", "conic_opacity", "rgb", "depth",
                                          "tiles_touched", "final_T", "n_contrib")], _stream(device)),
@@ -504,9 +522,10 @@ def debug_export_slots(W, H, num_rendered, binningBuffer, imageBuffer, device):
     """(slots[num_rendered], tile_cut[tiles]) as int32 device tensors: the depth-ordered instance slot of
     each entry of the tile-sorted list and each tile's backward record cut (valid after a backward)."""
     gx, gy = (W + 15) // 16, (H + 15) // 16
-    slots = torch.zeros((max(int(num_rendered), 1),), dtype=torch.int32, device=device)
+    L = binning_layout_count(num_rendered, binningBuffer, W, H)
+    slots = torch.zeros((max(L, 1),), dtype=torch.int32, device=device)
     cuts = torch.zeros((gx * gy,), dtype=torch.int32, device=device)
     with torch.cuda.device(device):
-        _native.check(_lib.gs_debug_export_slots(W, H, int(num_rendered), _ptr(binningBuffer), _ptr(imageBuffer),
+        _native.check(_lib.gs_debug_export_slots(W, H, L, _ptr(binningBuffer), _ptr(imageBuffer),
                                                  _ptr(slots), _ptr(cuts), _stream(device)), "debug_export_slots")
     return slots[:int(num_rendered)], cuts

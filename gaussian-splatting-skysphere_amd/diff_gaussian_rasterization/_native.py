@@ -117,6 +117,13 @@ SIGNATURES = {
         _c_i,
         [_c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_f, _c_p, _c_ll, _c_p, _c_p, _c_p, _c_i, _c_i, _c_p],
     ),
+    # ABI v14: the eager forward with its instance count read back at the end
+    "gs_forward_counted": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_f, _c_f, _c_i, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, ctypes.POINTER(_c_ll), _c_i, _c_p],
+    ),
+    "gs_binning_layout_count": (_c_ll, [_c_sz, _c_i, _c_i]),
     "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),
     "gs_knn_mean_dist2": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p]),

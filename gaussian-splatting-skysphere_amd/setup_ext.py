@@ -13,7 +13,8 @@ setup(
     name="gs_torch_ext",
     ext_modules=[CppExtension("diff_gaussian_rasterization._gs_ext", ["csrc/gs_torch_ext.cpp"],
                               include_dirs=["/opt/rocm/include"],
-                              extra_compile_args=["-O2", "-D__HIP_PLATFORM_AMD__=1"])],
+                              extra_compile_args=["-O2", "-g0", "-D__HIP_PLATFORM_AMD__=1"],
+                              extra_link_args=["-s"])],
     cmdclass={"build_ext": BuildExtension},
     # objects in a temporary directory; the module lands in diff_gaussian_rasterization/
     script_args=["build_ext", "--inplace", "-t", os.path.join(tempfile.gettempdir(), "gs_ext_build"),

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 13  /* v13: the depth-slab binning (v12's gs_set_slabs / gs_binning_slabs) removed */
+#define GSRAST_ABI_VERSION 14  /* v14: gs_forward_counted + gs_binning_layout_count (v13: depth slabs removed) */
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -69,6 +69,11 @@ size_t gs_geom_buffer_bytes(int P);
 size_t gs_binning_buffer_bytes(long long num_rendered, int image_width, int image_height);
 size_t gs_image_buffer_bytes(int image_width, int image_height);
 size_t gs_grad_buffer_bytes(long long num_rendered);
+/* The instance count a binning buffer of `bytes` bytes is laid out for: the largest n with
+ * gs_binning_buffer_bytes(n, W, H) <= bytes (every such n gives the same layout).  A buffer that
+ * gs_forward_counted filled for `capacity` instances goes to the backward with this count in place
+ * of num_rendered. */
+long long gs_binning_layout_count(size_t bytes, int image_width, int image_height);
 
 /* ---- forward, part 1: preprocess, cull, depth order, instance offsets ----
  * P Gaussians; D = active SH degree; M = SH coefficients per colour (stride of shs, 0 if none).
@@ -125,6 +130,27 @@ int gs_forward_bounded(int P, int D, int M, const float* background, int image_w
                        const float* campos, float tan_fovx, float tan_fovy, int prefiltered, int* radii_out,
                        void* geom_buffer, long long capacity, void* binning_buffer, void* image_buffer,
                        float* out_color, int debug, void* stream);
+/* ---- forward in one call, count read back at the end (ABI 14) ----
+ * _C.rasterize_gaussians' eager path without the mid-call host wait of gs_forward_preprocess: the
+ * caller sizes binning_buffer for an estimate `capacity` (gs_binning_buffer_bytes(capacity, W, H)),
+ * every launch is queued, then the call waits for the instance count -- stored into pinned memory by
+ * the first depth-sort launch, so by then normally long written -- and returns it in
+ * *num_rendered_host (exact, as upstream's num_rendered).
+ *   0: the count fitted.  The binning buffer is laid out for `capacity` instances: the backward takes
+ *      gs_binning_layout_count(its bytes, W, H) (= capacity) where it takes num_rendered.
+ *   2 (GS_COUNT_SHORT): the count exceeds `capacity`; nothing was composited.  radii_out and
+ *      geom_buffer are complete: gs_forward_render with a binning buffer for *num_rendered_host
+ *      finishes the forward exactly as the two-call path does.
+ *   1: error (gs_last_error()), as gs_forward_preprocess.
+ * shs_rest: split SH rows as gs_forward_preprocess_split (shs = features_dc), or NULL. */
+#define GS_COUNT_SHORT 2
+int gs_forward_counted(int P, int D, int M, const float* background, int image_width, int image_height,
+                       const float* means3D, const float* shs, const float* shs_rest, const float* colors_precomp,
+                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                       const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                       const float* campos, float tan_fovx, float tan_fovy, int prefiltered, int* radii_out,
+                       void* geom_buffer, long long capacity, void* binning_buffer, void* image_buffer,
+                       float* out_color, long long* num_rendered_host, int debug, void* stream);
 /* The bounded forms of the two-call forward: gs_forward_preprocess_views without the readback
  * (capacity: K binning capacities; nothing waits), then gs_forward_render_bounded per view with
  * that view's capacity in place of num_rendered.  Same sticky status as gs_forward_bounded. */

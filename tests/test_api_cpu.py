@@ -58,3 +58,32 @@ def test_simple_knn_cpu_fails_loudly():
 
     with pytest.raises(RuntimeError, match="no CPU path"):
         distCUDA2(torch.zeros((5, 3)))
+
+
+def test_binning_layout_count_inverts_buffer_bytes():
+    """gs_binning_layout_count (ABI 14): the count a binning buffer of n bytes is laid out for -- the
+    backward of a gs_forward_counted forward takes it in place of num_rendered."""
+    lib = _C._lib
+    for W, H in ((16, 16), (800, 800), (1920, 1080)):
+        assert lib.gs_binning_layout_count(0, W, H) == 0
+        for n in (1, 2, 63, 64, 65, 1000, 65_536, 1_234_567, 4_310_000, 40_000_000):
+            b = lib.gs_binning_buffer_bytes(n, W, H)
+            L = lib.gs_binning_layout_count(b, W, H)
+            assert L >= n and lib.gs_binning_buffer_bytes(L, W, H) == b
+            assert lib.gs_binning_buffer_bytes(L + 1, W, H) > b
+            assert lib.gs_binning_layout_count(b - 1, W, H) < n
+
+
+def test_torch_host_extension_loads():
+    """The torch C++ host path is built in-tree and binds libgsrast.so's symbols (no GPU call)."""
+    import os
+
+    if os.environ.get("GSRAST_NO_EXT", "0") not in ("", "0"):
+        pytest.skip("GSRAST_NO_EXT set")
+    assert _C._EXT is not None, "diff_gaussian_rasterization/_gs_ext*.so missing: run setup_ext.py"
+    for name in ("forward", "backward", "count_estimate", "set_count_estimate"):
+        assert callable(getattr(_C._EXT, name))
+    e = _C._EXT.count_estimate(7)
+    _C._EXT.set_count_estimate(7, 12345)
+    assert _C._EXT.count_estimate(7) == 12345
+    _C._EXT.set_count_estimate(7, e)

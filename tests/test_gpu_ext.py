@@ -1,0 +1,123 @@
+"""GPU tests of the torch C++ host path (diff_gaussian_rasterization._gs_ext, csrc/gs_torch_ext.cpp)
+and of the forward it runs, gs_forward_counted (ABI 14: every launch queued, the instance count read
+back at the end, the binning buffer sized ahead from the last count).
+
+  - the extension is the path a plain GaussianRasterizer call takes on a GPU box;
+  - its outputs and gradients are bit-identical to the ctypes two-call path (gs_forward_preprocess
+    + gs_forward_render), for the concatenated and the split SH rows, and num_rendered is the exact
+    instance count (upstream semantics), not the capacity;
+  - a forward whose count outgrows the estimate (the fallback: the same geometry binned again into
+    an exact buffer) and one far below it (a larger layout than its count) give the same bits;
+  - debug_export reads a counted forward's buffers (layout count vs num_rendered).
+"""
+import pytest
+import torch
+
+import gs_scenes
+
+pytestmark = pytest.mark.gpu
+
+W, H = 320, 240
+
+
+def _leaves(d):
+    return [d.means3D.clone().requires_grad_(True), d.shs.clone().requires_grad_(True),
+            d.opacities.clone().requires_grad_(True), d.scales.clone().requires_grad_(True),
+            d.rotations.clone().requires_grad_(True)]
+
+
+def _fwd_bwd(rast, d, dpix, split=False):
+    p = _leaves(d)
+    m2 = torch.zeros_like(p[0], requires_grad=True)
+    kw = {}
+    if split:
+        kw["sh_split"] = (p[1].detach()[:, :1].contiguous(), p[1].detach()[:, 1:].contiguous())
+    img, radii = rast(means3D=p[0], means2D=m2, opacities=p[2], shs=p[1], scales=p[3], rotations=p[4], **kw)
+    img.backward(dpix)
+    torch.cuda.synchronize()
+    return [img.detach(), radii, m2.grad] + [t.grad for t in p]
+
+
+def _assert_same(ref, got, what):
+    for k, (a, b) in enumerate(zip(ref, got)):
+        assert torch.equal(a, b), (what, k, float((a.float() - b.float()).abs().max()))
+
+
+def _ext():
+    from diff_gaussian_rasterization import _C
+
+    assert _C._EXT is not None, "the torch C++ host path (_gs_ext) is not loaded on this GPU box"
+    return _C
+
+
+def test_ext_is_the_eager_path(device):
+    _C = _ext()
+    import diff_gaussian_rasterization as dgr
+
+    d = gs_scenes.random_gaussians(5_000, 3, seed=1, ball_radius=2.0).to(device)
+    cam = gs_scenes.circle_cameras(1, 6.0, W, H)[0]
+    rast = dgr.GaussianRasterizer(gs_scenes.raster_settings_for(cam, 3, device=device))
+    calls = []
+    real = _C._EXT
+
+    class Spy:
+        def __getattr__(self, name):
+            calls.append(name)
+            return getattr(real, name)
+
+    _C._EXT = Spy()
+    try:
+        _fwd_bwd(rast, d, gs_scenes.dl_dimage(H, W, seed=2).to(device))
+    finally:
+        _C._EXT = real
+    assert calls == ["forward", "backward"]
+
+
+@pytest.mark.parametrize("split", [False, True], ids=["concat_sh", "split_sh"])
+def test_counted_forward_equals_two_call_forward(device, split, monkeypatch):
+    _C = _ext()
+    import diff_gaussian_rasterization as dgr
+
+    d = gs_scenes.random_gaussians(20_000, 3, seed=5, ball_radius=2.0).to(device)
+    dpix = gs_scenes.dl_dimage(H, W, seed=3).to(device)
+    dev = torch.device(device).index or 0
+    for cam in gs_scenes.circle_cameras(3, 6.0, W, H):
+        rast = dgr.GaussianRasterizer(gs_scenes.raster_settings_for(cam, 3, device=device))
+        with monkeypatch.context() as m:
+            m.setattr(_C, "_EXT", None)
+            ref = _fwd_bwd(rast, d, dpix, split)
+            n = dgr.last_num_rendered()
+        # estimates: none (two-call path), about right, far above, below the count (fallback)
+        for est in (0, n, 4 * n + 100_000, n // 3):
+            _C._EXT.set_count_estimate(dev, est)
+            got = _fwd_bwd(rast, d, dpix, split)
+            _assert_same(ref, got, ("estimate", est))
+            assert dgr.last_num_rendered() == n  # exact, not the capacity
+            assert _C._EXT.count_estimate(dev) == n
+
+
+def test_counted_forward_buffers_and_debug_export(device):
+    _C = _ext()
+    d = gs_scenes.random_gaussians(8_000, 3, seed=7, ball_radius=2.0).to(device)
+    cam = gs_scenes.circle_cameras(1, 6.0, W, H)[0]
+    s = gs_scenes.raster_settings_for(cam, 3, device=device)
+    args = (s.bg, d.means3D, torch.empty(0, device=device), d.opacities, d.scales, d.rotations, s.scale_modifier,
+            torch.empty(0, device=device), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, H, W, d.shs,
+            s.sh_degree, s.campos, s.prefiltered, False)
+    dev = torch.device(device).index or 0
+    _C._EXT.set_count_estimate(dev, 0)
+    n0, img0, radii0, geom0, bin0, imgbuf0 = _C.rasterize_gaussians(*args)
+    _C._EXT.set_count_estimate(dev, 5 * n0)
+    n1, img1, radii1, geom1, bin1, imgbuf1 = _C.rasterize_gaussians(*args)
+    assert n1 == n0 and torch.equal(img0, img1) and torch.equal(radii0, radii1)
+    assert bin1.numel() > bin0.numel()  # laid out for the capacity
+    L = _C.binning_layout_count(n1, bin1, W, H)
+    assert L > n1 and _C._lib.gs_binning_buffer_bytes(L, W, H) == bin1.numel()
+    assert _C.binning_layout_count(n0, bin0, W, H) == n0
+    e0 = _C.debug_export(d.means3D.shape[0], W, H, n0, geom0, bin0, imgbuf0, d.means3D.device)
+    e1 = _C.debug_export(d.means3D.shape[0], W, H, n1, geom1, bin1, imgbuf1, d.means3D.device)
+    torch.cuda.synchronize()
+    for k in e0:
+        assert torch.equal(e0[k], e1[k]), k
+    with pytest.raises(RuntimeError, match="too small"):
+        _C.binning_layout_count(n0 + 1_000_000, bin0, W, H)
