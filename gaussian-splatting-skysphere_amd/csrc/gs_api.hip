@@ -332,6 +332,15 @@ static bool check_order_flags(bool wait = true) {
   return failed;
 }
 
+// forward q's flags now (waits for its render kernel), if its word still holds them; true: failed
+static bool check_order_seq(unsigned long long q) {
+  OrderFlags* o = order_flags();
+  if (!o) return true;
+  std::lock_guard<std::mutex> lk(o->mu);
+  const int k = (int)(q % ORDER_RING);
+  return o->seq - q <= (unsigned long long)ORDER_RING && check_order_slot_locked(*o, k);
+}
+
 // The device word this forward's render kernel stores its ordering flags into, and (*seq_out) the
 // forward's sequence number; null on error.
 static uint32_t* order_flags_word(unsigned long long* seq_out) {
@@ -643,7 +652,8 @@ int gs_forward_preprocess_views_bounded(int K, int P, int D, int M, const float*
 static int forward_render_impl(int P, const float* background, int W, int H, const float* viewmatrix,
                                const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
                                const int* radii, void* geom_buffer, long long num_rendered, void* binning_buffer,
-                               void* image_buffer, float* out_color, bool bounded, int debug, void* stream) {
+                               void* image_buffer, float* out_color, bool bounded, int debug, void* stream,
+                               unsigned long long* oseq_out = nullptr) {
   clear_error(debug);
   if (P <= 0) return 0;
   if (W <= 0 || H <= 0) return set_error("image size must be positive"), 1;
@@ -670,6 +680,7 @@ static int forward_render_impl(int P, const float* background, int W, int H, con
   fwd_bin(P, (uint32_t)num_rendered, c, radii, geo, bin, img, st);
   fwd_render(c, geo, bin, img, out_color, st, flags_word);
   if (!bounded) {
+    if (oseq_out) *oseq_out = oseq;
     if (t_failed) release_order_word(oseq);
     else if (queue_order_flags(st, oseq)) return 1;
   }
@@ -851,8 +862,10 @@ int gs_forward_counted(int P, int D, int M, const float* background, int W, int 
   const uint32_t cap32 = (uint32_t)capacity;
   fwd_order(P, geo, st, rb->dev, rb->ev[0], &cap32, nullptr);
   if (t_failed) return 1;
+  unsigned long long oseq = 0;
   if (forward_render_impl(P, background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii_out,
-                          geom_buffer, capacity, binning_buffer, image_buffer, out_color, false, debug, stream))
+                          geom_buffer, capacity, binning_buffer, image_buffer, out_color, false, debug, stream,
+                          &oseq))
     return 1;
   check_hip(hipEventSynchronize(rb->ev[0]), "hipEventSynchronize");
   if (t_failed) return 1;
@@ -865,7 +878,11 @@ int gs_forward_counted(int P, int D, int M, const float* background, int W, int 
     // the queued binning and render skipped their work (ERR_CAPACITY): clear the flag so that
     // gs_forward_render can bin the same geometry into a buffer of the exact size
     fwd_clear_flags(geo, ERR_CAPACITY, st);
-    return t_failed ? 1 : GS_COUNT_SHORT;
+    // the skipped render carries this ordering's look-back flags: read them now (it finishes
+    // quickly, having skipped its work), so a timed-out ordering fails here, once, instead of
+    // again at the next call through the re-binned forward's flags
+    if (t_failed || check_order_seq(oseq)) return 1;
+    return GS_COUNT_SHORT;
   }
   return 0;
 }

@@ -8,7 +8,9 @@ back at the end, the binning buffer sized ahead from the last count).
     instance count (upstream semantics), not the capacity;
   - a forward whose count outgrows the estimate (the fallback: the same geometry binned again into
     an exact buffer) and one far below it (a larger layout than its count) give the same bits;
-  - debug_export reads a counted forward's buffers (layout count vs num_rendered).
+  - debug_export reads a counted forward's buffers (layout count vs num_rendered);
+  - a timed-out look-back in a forward that outgrew its estimate fails in that forward, once (the
+    skipped render's flags are read before re-binning), and the next call is clean.
 """
 import pytest
 import torch
@@ -121,3 +123,32 @@ def test_counted_forward_buffers_and_debug_export(device):
         assert torch.equal(e0[k], e1[k]), k
     with pytest.raises(RuntimeError, match="too small"):
         _C.binning_layout_count(n0 + 1_000_000, bin0, W, H)
+
+
+def test_short_forward_with_timed_out_lookback_fails_once(device):
+    _C = _ext()
+    import diff_gaussian_rasterization as dgr
+
+    lib = _C._lib
+    cam = gs_scenes.identity_camera(320, 240)
+    d = gs_scenes.random_gaussians(200_000, 0, cam=cam, seed=60).to(device)
+    rast = dgr.GaussianRasterizer(gs_scenes.raster_settings_for(cam, 0, device=device))
+
+    def fwd():
+        return rast(means3D=d.means3D, means2D=torch.zeros_like(d.means3D), opacities=d.opacities, shs=d.shs,
+                    scales=d.scales, rotations=d.rotations)
+
+    ref, _ = fwd()
+    torch.cuda.synchronize()
+    dev = torch.device(device).index or 0
+    _C._EXT.set_count_estimate(dev, 1)  # the next forward outgrows its buffer
+    prev = lib.gs_debug_set_scan_spin_limit(0)
+    try:
+        with pytest.raises(RuntimeError, match="look-back wait"):
+            fwd()
+        torch.cuda.synchronize()
+    finally:
+        lib.gs_debug_set_scan_spin_limit(prev)
+    img, _ = fwd()  # clean: nothing left over from the failed forward
+    torch.cuda.synchronize()
+    assert torch.equal(img, ref)

@@ -316,6 +316,11 @@ def test_lookback_timeout_is_reported(device):
         return rast(means3D=means3D, means2D=torch.zeros_like(d.means3D), opacities=d.opacities, shs=d.shs,
                     scales=d.scales, rotations=d.rotations)
 
+    # one clean forward first: the torch host path then sizes the next binning buffer from this
+    # scene's count, so the timed-out forward below fits it (the case where the count outgrows the
+    # estimate fails in the forward itself: test_gpu_ext.py)
+    fwd(d.means3D)
+    torch.cuda.synchronize()
     # forward only: the next forward reports it
     prev = lib.gs_debug_set_scan_spin_limit(0)
     try:
