@@ -31,7 +31,8 @@ def per_kernel(counter, d):
             continue
         short = k.split("(")[0].replace("void ", "").split("<")[0].replace("gs::", "")
         short = short[2:] if short.startswith("k_") else short
-        short = {"duplicate_lb": "duplicate", "preprocess_bwd_reg": "preprocess_bwd", "render_fwd_q": "render_fwd"}.get(short, short)  # bench.py names
+        short = {"duplicate_lb": "duplicate", "preprocess_bwd_reg": "preprocess_bwd", "render_fwd_q": "render_fwd",
+                 "render_bwd_tw": "render_bwd"}.get(short, short)  # bench.py names
         per_dispatch[row["Dispatch_Id"]] += float(row["Counter_Value"])
         names[row["Dispatch_Id"]] = short
     for disp, v in per_dispatch.items():
