@@ -15,6 +15,7 @@
 // (gs_forward_counted, binning buffer sized from the last count), so neither the device nor the host
 // idles across the host round trip that upstream's resize callbacks need between the two halves.
 #include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 #include <dlfcn.h>
 #include <torch/extension.h>
@@ -33,6 +34,19 @@ using fwd_render_t = int (*)(int, f_cp, int, int, f_cp, f_cp, f_cp, float, float
 using fwd_counted_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, f_cp, f_cp, f_cp, float, f_cp, f_cp, f_cp,
                               f_cp, f_cp, float, float, int, int*, void*, long long, void*, void*, float*, long long*,
                               int, void*);
+using pre_views_t = int (*)(int, int, int, int, const float* const*, const int*, const int*, f_cp, f_cp, f_cp, f_cp, f_cp,
+                            float, f_cp, f_cp, const float* const*, const float* const*, const float* const*, f_cp, f_cp,
+                            int, int* const*, void* const*, long long*, int, void*, void* const*);
+using pre_views_bounded_t = int (*)(int, int, int, int, const float* const*, const int*, const int*, f_cp, f_cp, f_cp,
+                                    f_cp, f_cp, float, f_cp, f_cp, const float* const*, const float* const*,
+                                    const float* const*, f_cp, f_cp, int, int* const*, void* const*, const long long*,
+                                    int, void*, void* const*);
+using bin_views_t = int (*)(int, int, int, int, void* const*, const long long*, void* const*, void* const*, int, void*,
+                            void* const*);
+using render_binned_t = int (*)(int, f_cp, int, int, f_cp, f_cp, f_cp, float, float, void*, long long, void*, void*,
+                                float*, int, int, void*);
+using bwd_render_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, float, float, const void*, long long,
+                             const void*, const void*, f_cp, void*, float*, unsigned, int, void*);
 using bwd_acc_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, f_cp, f_cp, float, f_cp, f_cp, f_cp, f_cp,
                           f_cp, float, float, const int*, const void*, long long, const void*, const void*, f_cp,
                           void*, float*, float*, float*, float*, float*, float*, float*, float*, unsigned, void*,
@@ -46,6 +60,12 @@ struct Fns {
   fwd_pre_t preprocess = nullptr, preprocess_split = nullptr;
   fwd_render_t render = nullptr;
   fwd_counted_t counted = nullptr;
+  fwd_render_t render_bounded = nullptr;
+  pre_views_t pre_views = nullptr;
+  pre_views_bounded_t pre_views_bounded = nullptr;
+  bin_views_t bin_views = nullptr;
+  render_binned_t render_binned = nullptr;
+  bwd_render_t bwd_render = nullptr;
   bwd_acc_t backward = nullptr;
   bwd_acc_split_t backward_split = nullptr;
   size_t (*geom_bytes)(int) = nullptr;
@@ -67,6 +87,12 @@ void init() {
   resolve(F.preprocess_split, "gs_forward_preprocess_split");
   resolve(F.render, "gs_forward_render");
   resolve(F.counted, "gs_forward_counted");
+  resolve(F.render_bounded, "gs_forward_render_bounded");
+  resolve(F.pre_views, "gs_forward_preprocess_views");
+  resolve(F.pre_views_bounded, "gs_forward_preprocess_views_bounded");
+  resolve(F.bin_views, "gs_forward_bin_views");
+  resolve(F.render_binned, "gs_forward_render_binned");
+  resolve(F.bwd_render, "gs_backward_render");
   resolve(F.backward, "gs_backward_accumulate");
   resolve(F.backward_split, "gs_backward_accumulate_split");
   resolve(F.geom_bytes, "gs_geom_buffer_bytes");
@@ -295,6 +321,192 @@ py::tuple backward(const at::Tensor& background, const at::Tensor& means3D, cons
   return result();
 }
 
+// ---- the multi-view path (prepare_views, prepared renders, deferred backwards) ----
+
+// _C.preprocess_views: the first half of K views' forwards in one set of launches, then (same
+// image size, GSRAST_BATCH_VIEWS unset or not 0) their binning in one set; per view the tuple
+// (num_rendered, radii, geom, bounded[, binning, img]) that _C.rasterize_gaussians(prepared=) takes.
+// streams: the views' HIP stream handles (or empty: the current stream); the view's buffers are
+// recorded on its stream, as _C.py does.
+py::list preprocess_views(const std::vector<at::Tensor>& backgrounds, const at::Tensor& means3D,
+                          const c10::optional<at::Tensor>& colors, const c10::optional<at::Tensor>& opacity,
+                          const c10::optional<at::Tensor>& scales, const c10::optional<at::Tensor>& rotations,
+                          double scale_modifier, const c10::optional<at::Tensor>& cov3D,
+                          const std::vector<at::Tensor>& viewmatrices, const std::vector<at::Tensor>& projmatrices,
+                          const std::vector<double>& tan_fovx, const std::vector<double>& tan_fovy,
+                          const std::vector<int64_t>& heights, const std::vector<int64_t>& widths,
+                          const c10::optional<at::Tensor>& sh, int64_t degree, const std::vector<at::Tensor>& campos,
+                          bool prefiltered, bool debug, const std::vector<int64_t>& streams,
+                          const c10::optional<std::vector<int64_t>>& capacities) {
+  const int K = (int)viewmatrices.size();
+  TORCH_CHECK(K >= 1 && K <= 8, "preprocess_views: 1 to 8 views per call");
+  TORCH_CHECK(backgrounds.size() == (size_t)K && projmatrices.size() == (size_t)K && tan_fovx.size() == (size_t)K &&
+                  tan_fovy.size() == (size_t)K && heights.size() == (size_t)K && widths.size() == (size_t)K &&
+                  campos.size() == (size_t)K && (streams.empty() || streams.size() == (size_t)K),
+              "preprocess_views: one entry per view in every per-view argument");
+  Inputs x(backgrounds[0], means3D, colors, opacity, scales, rotations, cov3D, viewmatrices[0], projmatrices[0], sh,
+           campos[0], true, c10::nullopt);
+  const auto u8 = at::TensorOptions().dtype(at::kByte).device(x.dev);
+  const auto i32 = at::TensorOptions().dtype(at::kInt).device(x.dev);
+  std::vector<at::Tensor> radii(K), geoms(K), bgs(K), views(K), projs(K), cams(K);
+  for (int k = 0; k < K; k++) radii[k] = at::empty({x.P}, i32);
+  const int64_t gb = x.P ? (int64_t)F.geom_bytes((int)x.P) : 0;
+  at::Tensor geom_all = at::empty({K * gb}, u8);
+  for (int k = 0; k < K; k++) geoms[k] = geom_all.narrow(0, k * gb, gb);
+  py::list out;
+  if (x.P == 0) {
+    for (int k = 0; k < K; k++) out.append(py::make_tuple(0, radii[k], geoms[k], false));
+    return out;
+  }
+  TORCH_CHECK(!capacities.has_value() || capacities->size() == (size_t)K, "preprocess_views: one capacity per view");
+  for (int k = 0; k < K; k++) {
+    bgs[k] = k ? f32(backgrounds[k], "background", x.dev, true) : x.bg;
+    views[k] = k ? f32(viewmatrices[k], "viewmatrix", x.dev, true) : x.view;
+    projs[k] = k ? f32(projmatrices[k], "projmatrix", x.dev, true) : x.proj;
+    cams[k] = k ? f32(campos[k], "campos", x.dev, true) : x.campos;
+  }
+  c10::DeviceGuard guard(x.dev);
+  void* st = stream_of(x.dev);
+  const float *bgp[8], *vp_[8], *pp[8], *cp[8];
+  int wv[8], hv[8];
+  float tx[8], ty[8];
+  int* rp[8];
+  void *gp[8], *vst[8];
+  long long nr[8] = {};
+  for (int k = 0; k < K; k++) {
+    bgp[k] = fp(bgs[k]), vp_[k] = fp(views[k]), pp[k] = fp(projs[k]), cp[k] = fp(cams[k]);
+    wv[k] = (int)widths[k], hv[k] = (int)heights[k], tx[k] = (float)tan_fovx[k], ty[k] = (float)tan_fovy[k];
+    rp[k] = radii[k].data_ptr<int>(), gp[k] = geoms[k].data_ptr();
+    vst[k] = streams.empty() ? nullptr : reinterpret_cast<void*>(streams[k]);
+  }
+  const bool bounded = capacities.has_value();
+  if (bounded) {
+    for (int k = 0; k < K; k++) nr[k] = (*capacities)[k];
+    check(F.pre_views_bounded(K, (int)x.P, (int)degree, (int)x.M, bgp, wv, hv, fp(x.means3D), fp(x.sh), fp(x.colors),
+                              fp(x.opacity), fp(x.scales), (float)scale_modifier, fp(x.rotations), fp(x.cov3D), vp_, pp,
+                              cp, tx, ty, (int)prefiltered, rp, gp, nr, (int)debug, st,
+                              streams.empty() ? nullptr : vst),
+          "preprocess_views");
+  } else {
+    check(F.pre_views(K, (int)x.P, (int)degree, (int)x.M, bgp, wv, hv, fp(x.means3D), fp(x.sh), fp(x.colors),
+                      fp(x.opacity), fp(x.scales), (float)scale_modifier, fp(x.rotations), fp(x.cov3D), vp_, pp, cp, tx,
+                      ty, (int)prefiltered, rp, gp, nr, (int)debug, st, streams.empty() ? nullptr : vst),
+          "preprocess_views");
+  }
+  bool same_size = true;
+  for (int k = 1; k < K; k++) same_size = same_size && wv[k] == wv[0] && hv[k] == hv[0];
+  static const bool batch = [] {
+    const char* e = getenv("GSRAST_BATCH_VIEWS");
+    return !(e && e[0] == '0' && e[1] == 0);
+  }();
+  std::vector<py::tuple> tuples;
+  if (batch && same_size) {
+    // the K views' binning as one set of launches: every binning buffer a slice of one allocation,
+    // sized for the largest count, which then stands for every view's num_rendered
+    long long I = 0;
+    for (int k = 0; k < K; k++) I = std::max(I, nr[k]);
+    const int64_t bb = (int64_t)F.binning_bytes(I, wv[0], hv[0]), ib = (int64_t)F.image_bytes(wv[0], hv[0]);
+    at::Tensor bin_all = at::empty({K * bb}, u8), img_all = at::empty({K * ib}, u8);
+    void *bp[8], *ip[8];
+    std::vector<at::Tensor> bins(K), imgs(K);
+    for (int k = 0; k < K; k++) {
+      bins[k] = bin_all.narrow(0, k * bb, bb), imgs[k] = img_all.narrow(0, k * ib, ib);
+      bp[k] = bins[k].data_ptr(), ip[k] = imgs[k].data_ptr();
+    }
+    check(F.bin_views(K, (int)x.P, wv[0], hv[0], gp, nr, bp, ip, (int)debug, st, streams.empty() ? nullptr : vst),
+          "preprocess_views (binning)");
+    for (int k = 0; k < K; k++) tuples.push_back(py::make_tuple((int64_t)I, radii[k], geoms[k], bounded, bins[k], imgs[k]));
+    if (!streams.empty())
+      for (int k = 0; k < K; k++) {
+        // (torch on ROCm keys its HIP streams as CUDA streams)
+        const c10::Stream sk =
+            at::hip::getStreamFromExternalMasqueradingAsCUDA((hipStream_t)vst[k], x.dev.index()).unwrap();
+        radii[k].record_stream(sk), geoms[k].record_stream(sk), bins[k].record_stream(sk), imgs[k].record_stream(sk);
+      }
+  } else {
+    for (int k = 0; k < K; k++) tuples.push_back(py::make_tuple((int64_t)nr[k], radii[k], geoms[k], bounded));
+    if (!streams.empty())
+      for (int k = 0; k < K; k++) {
+        // (torch on ROCm keys its HIP streams as CUDA streams)
+        const c10::Stream sk =
+            at::hip::getStreamFromExternalMasqueradingAsCUDA((hipStream_t)vst[k], x.dev.index()).unwrap();
+        radii[k].record_stream(sk), geoms[k].record_stream(sk);
+      }
+  }
+  for (auto& t : tuples) out.append(t);
+  return out;
+}
+
+// _C.rasterize_gaussians(prepared=): the rest of a view's forward after preprocess_views
+py::tuple forward_prepared(const at::Tensor& background, const at::Tensor& means3D, const at::Tensor& viewmatrix,
+                           const at::Tensor& projmatrix, double tan_fovx, double tan_fovy, int64_t H, int64_t W,
+                           const at::Tensor& campos, bool debug, const py::tuple& prepared) {
+  TORCH_CHECK(means3D.dim() == 2 && means3D.size(1) == 3, "means3D must have dimensions (num_points, 3)");
+  dev_check(means3D, "means3D");
+  const c10::Device dev = means3D.device();
+  const int64_t P = means3D.size(0);
+  const auto f32o = at::TensorOptions().dtype(at::kFloat).device(dev);
+  const auto u8 = at::TensorOptions().dtype(at::kByte).device(dev);
+  const long long nr = prepared[0].cast<long long>();
+  at::Tensor radii = prepared[1].cast<at::Tensor>(), geom = prepared[2].cast<at::Tensor>();
+  const bool bounded = prepared.size() > 3 && prepared[3].cast<bool>();
+  if (P == 0)
+    return py::make_tuple(0, at::zeros({3, H, W}, f32o), at::zeros({0}, f32o.dtype(at::kInt)), at::empty({0}, u8),
+                          at::empty({0}, u8), at::empty({0}, u8));
+  TORCH_CHECK(radii.numel() == P && geom.numel() == (int64_t)F.geom_bytes((int)P),
+              "rasterize_gaussians: the prepared view does not match these inputs");
+  at::Tensor bg = f32(background, "background", dev, true), view = f32(viewmatrix, "viewmatrix", dev, true);
+  at::Tensor proj = f32(projmatrix, "projmatrix", dev, true), cam = f32(campos, "campos", dev, true);
+  c10::DeviceGuard guard(dev);
+  void* st = stream_of(dev);
+  at::Tensor out_color = at::empty({3, H, W}, f32o);
+  if (prepared.size() > 4) {  // binned with the other prepared views: the compositing only
+    at::Tensor binning = prepared[4].cast<at::Tensor>(), img = prepared[5].cast<at::Tensor>();
+    TORCH_CHECK(img.numel() == (int64_t)F.image_bytes((int)W, (int)H),
+                "rasterize_gaussians: the prepared view was binned for another image size");
+    check(F.render_binned((int)P, fp(bg), (int)W, (int)H, fp(view), fp(proj), fp(cam), (float)tan_fovx,
+                          (float)tan_fovy, geom.data_ptr(), nr, binning.data_ptr(), img.data_ptr(),
+                          out_color.data_ptr<float>(), (int)bounded, (int)debug, st),
+          "rasterize_gaussians (render)");
+    return py::make_tuple((int64_t)nr, out_color, radii, geom, binning, img);
+  }
+  at::Tensor binning = at::empty({(int64_t)F.binning_bytes(nr, (int)W, (int)H)}, u8);
+  at::Tensor img = at::empty({(int64_t)F.image_bytes((int)W, (int)H)}, u8);
+  check((bounded ? F.render_bounded : F.render)((int)P, fp(bg), (int)W, (int)H, fp(view), fp(proj), fp(cam),
+                                                (float)tan_fovx, (float)tan_fovy, radii.data_ptr<int>(),
+                                                geom.data_ptr(), nr, binning.data_ptr(), img.data_ptr(),
+                                                out_color.data_ptr<float>(), (int)debug, st),
+        "rasterize_gaussians (render)");
+  return py::make_tuple((int64_t)nr, out_color, radii, geom, binning, img);
+}
+
+// _C.backward_render: the per-tile half of one view's backward (its record sums stay in the
+// geometry buffer) and its dL_dmeans2D [P, 3] (or None)
+py::object backward_render(const at::Tensor& background, const at::Tensor& viewmatrix, const at::Tensor& projmatrix,
+                           const at::Tensor& campos, double tan_fovx, double tan_fovy, const at::Tensor& dL_dout_color,
+                           int64_t P, int64_t degree, int64_t M, const at::Tensor& geom, int64_t R,
+                           const at::Tensor& binning, const at::Tensor& img, bool want_means2D, bool debug) {
+  const c10::Device dev = geom.device();
+  const int64_t H = dL_dout_color.size(1), W = dL_dout_color.size(2);
+  const auto f32o = at::TensorOptions().dtype(at::kFloat).device(dev);
+  at::Tensor dm2 = want_means2D ? at::empty({P, 3}, f32o) : at::Tensor();
+  auto ret = [&]() -> py::object { return dm2.defined() ? py::cast(dm2) : py::none(); };
+  if (P == 0) return ret();
+  at::Tensor bg = f32(background, "background", dev, true), view = f32(viewmatrix, "viewmatrix", dev, true);
+  at::Tensor proj = f32(projmatrix, "projmatrix", dev, true), cam = f32(campos, "campos", dev, true);
+  at::Tensor dpix = f32(dL_dout_color, "dL_dout_color", dev);
+  R = layout_count((long long)R, binning, W, H);
+  c10::DeviceGuard guard(dev);
+  void* st = stream_of(dev);
+  at::Tensor scratch = at::empty({(int64_t)F.grad_bytes((long long)R)}, f32o.dtype(at::kByte));
+  check(F.bwd_render((int)P, (int)degree, (int)M, fp(bg), (int)W, (int)H, fp(view), fp(proj), fp(cam),
+                     (float)tan_fovx, (float)tan_fovy, geom.data_ptr(), (long long)R, binning.data_ptr(),
+                     img.data_ptr(), fp(dpix), scratch.data_ptr(), dm2.defined() ? dm2.data_ptr<float>() : nullptr, 0u,
+                     (int)debug, st),
+        "rasterize_gaussians_backward (render half)");
+  return ret();
+}
+
 // the per-device estimate the next forward sizes its binning buffer from (tests; 0: none yet)
 long long count_estimate(int64_t device) {
   TORCH_CHECK(device >= 0 && device < GS_COUNT_DEVICES, "device index out of range");
@@ -312,6 +524,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("init", &init);
   m.def("forward", &forward);
   m.def("backward", &backward);
+  m.def("preprocess_views", &preprocess_views);
+  m.def("forward_prepared", &forward_prepared);
+  m.def("backward_render", &backward_render);
   m.def("count_estimate", &count_estimate);
   m.def("set_count_estimate", &set_count_estimate);
 }

@@ -132,6 +132,13 @@ def preprocess_views(backgrounds, means3D, colors, opacity, scales, rotations, s
     K = len(viewmatrices)
     if not 1 <= K <= 8:
         raise RuntimeError("preprocess_views: 1 to 8 views per call")
+    if _EXT is not None and means3D.is_cuda:
+        return list(_EXT.preprocess_views(
+            list(backgrounds), means3D, colors, opacity, scales, rotations, float(scale_modifier), cov3D_precomp,
+            list(viewmatrices), list(projmatrices), [float(t) for t in tan_fovx], [float(t) for t in tan_fovy],
+            [int(h) for h in image_heights], [int(w) for w in image_widths], sh, int(degree), list(campos),
+            bool(prefiltered), bool(debug), [s.cuda_stream for s in streams] if streams is not None else [],
+            None if capacities is None else [int(c) for c in capacities]))
     xs = [_Inputs(backgrounds[k], means3D, colors, opacity, scales, rotations, cov3D_precomp, viewmatrices[k],
                   projmatrices[k], sh, campos[k]) for k in range(K)]
     x, dev = xs[0], xs[0].device
@@ -212,6 +219,9 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     features_dc [P,1,3], sh_rest features_rest [P,M-1,3]; gs_forward_preprocess_split).
     capacity: the binning buffer is sized for that many instances and the whole forward is
     enqueued without a host wait (gs_forward_bounded); the returned num_rendered is the capacity."""
+    if _EXT is not None and prepared is not None and capacity is None and sh_rest is None and means3D.is_cuda:
+        return _EXT.forward_prepared(background, means3D, viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy),
+                                     int(image_height), int(image_width), campos, bool(debug), tuple(prepared))
     if _EXT is not None and prepared is None and capacity is None and means3D.is_cuda:
         out = _EXT.forward(background, means3D, colors, opacity, scales, rotations, float(scale_modifier),
                            cov3D_precomp, viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy), int(image_height),
@@ -404,6 +414,10 @@ def backward_render(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fo
                     geomBuffer, R, binningBuffer, imageBuffer, want_means2D, debug):
     """Per-tile half of the backward (gs_backward_render): the view's per-Gaussian record sums,
     kept in geomBuffer for backward_gaussians, and its dL_dmeans2D [P, 3] (or None)."""
+    if _EXT is not None and geomBuffer.is_cuda:
+        return _EXT.backward_render(background, viewmatrix, projmatrix, campos, float(tan_fovx), float(tan_fovy),
+                                    dL_dout_color, int(P), int(degree), int(M), geomBuffer, int(R), binningBuffer,
+                                    imageBuffer, bool(want_means2D), bool(debug))
     dev = geomBuffer.device
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     dm2 = torch.empty((P, 3), dtype=torch.float32, device=dev) if want_means2D else None
