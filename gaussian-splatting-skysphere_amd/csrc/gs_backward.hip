@@ -470,14 +470,15 @@ struct BwdSlot {
 
 // one slot's evaluation + commit for one entry; s[] accumulates the lane's slot terms
 template <bool EXACT>
-__device__ __forceinline__ bool bwd_slot(BwdSlot& q, float pfx, float pfy, const float4 xr, const float4 co,
+__device__ __forceinline__ uint64_t bwd_slot(BwdSlot& q, float pfx, float pfy, const float4 xr, const float4 co,
                                          const float4 br, uint32_t e, float* s) {
   const float bl = br.x;
   const float dx = xr.x - pfx, dy = xr.y - pfy;
   const float pw = falloff_log2(co, dx, dy);  // log2(e) * power
   const float oG = co.w * exp2_m<EXACT>(pw);
   // same decision as the forward (k_render_fwd_q): alpha = min(0.99, o G) >= 1/255 <=> o G >= 1/255
-  const bool con = e < q.last && (!EXACT || pw <= 0.0f) && oG >= 1.0f / 255.0f;
+  const bool c_walk = e < q.last, c_alpha = oG >= 1.0f / 255.0f, c_pw = !EXACT || pw <= 0.0f;
+  const bool con = c_walk && c_pw && c_alpha;
   // a non-contributing pixel runs as an o G = 0 entry: T and U pass through unchanged bit for bit
   const float oGm = con ? oG : 0.0f;
   const float ae = __builtin_amdgcn_fmed3f(oGm, 0.0f, 0.99f);
@@ -507,7 +508,11 @@ __device__ __forceinline__ bool bwd_slot(BwdSlot& q, float pfx, float pfy, const
   s[8] = s[8] + qq;
   q.T = Tn;
   q.U = __builtin_fmaf(Cd, dch, q.U);
-  return con;
+  // the lanes where this slot contributes, from the compares' own lane masks (a ballot of their
+  // conjunction would be re-materialised through a VGPR: two VALU per slot)
+  uint64_t m = __builtin_amdgcn_ballot_w64(c_walk) & __builtin_amdgcn_ballot_w64(c_alpha);
+  if constexpr (EXACT) m &= __builtin_amdgcn_ballot_w64(c_pw);
+  return m;
 }
 
 #ifndef GS_BWDT_ROW
@@ -647,12 +652,12 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
       float s[GRAD_REC];
 #pragma unroll
       for (int t = 0; t < GRAD_REC; t++) s[t] = 0.0f;
-      bool con = false;
+      uint64_t con = 0;  // lanes with a contributing slot
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if ((M[k] >> j) & 1ull)
           con |= bwd_slot<EXACT>(p[k], pfx0 + (float)(8 * (k & 1)), pfy0 + (float)(8 * (k >> 1)), xr, co, br, e, s);
-      if (__ballot(con) != 0) {
+      if (con != 0) {
         wrote |= 1ull << j;
         float d, d8;
         wave_sum9_halfrows(s, hi8, d, d8);
