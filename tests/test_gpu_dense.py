@@ -14,9 +14,10 @@ opacity and colour (SH or precomputed) gradients 1e-5 * |ref| + 1e-5 * max|ref|.
 screen-position gradient and the covariance chain behind it (means2D, means3D, scales, rotations,
 cov3D) sum terms with cancellation over hundreds of pixels, each term carrying the T recovered by
 repeated division, so fp32 itself moves them by about 1e-5 of their max: they get 1e-5 * |ref| +
-1e-4 * max|ref| (the bound tests/test_gpu_parity.py uses for the chain against the oracle) and,
-as the conditioning check, a max deviation within 4x that of the same
-dense reference evaluated in fp32 (one other valid fp32 order), plus 1e-5 of the max."""
+5e-5 * max|ref| (round 4, tile-wave backward: the largest measured is 2.5e-5, dmeans3D of the
+scale_modifier case, where the dense fp32 run deviates as much) and, as the conditioning check, a
+max deviation within 4x that of the same dense reference evaluated in fp32 (one other valid fp32
+order), plus 1e-5 of the max."""
 import math
 
 import numpy as np
@@ -54,7 +55,7 @@ def _dense(cam, leaves, W, H, bg, deg, mod, dtype, device, flag_rel=1e-5, flag_T
     return t, res
 
 
-def _run_and_compare(cam, leaves, W, H, bg, deg=0, mod=1.0, seed=0, device=None, chain_frac=1e-4, flag_rel=1e-5,
+def _run_and_compare(cam, leaves, W, H, bg, deg=0, mod=1.0, seed=0, device=None, chain_frac=5e-5, flag_rel=1e-5,
                      flag_T_rel=None, noise_check=True):
     from diff_gaussian_rasterization import GaussianRasterizer
 
@@ -166,8 +167,8 @@ def test_hip_vs_dense_large_and_needle_splats(device):
     large splats are opaque (alpha up to the 0.99 clamp, where one ulp of alpha is 1e-5 of 1 - alpha,
     so T drifts ~1e-4 relative along a walk): alpha decisions within 2e-4 and T-stop decisions
     within 1e-3 (relative) of their thresholds are flagged.  Every Gaussian, needles included, is
-    held to the fixed bounds -- for the covariance chain the 2e-3 of max that the oracle test gives
-    needles (measured: means3D / scales 5e-5 / 8e-5, rotations 5e-4 of max); the 4x-of-dense-fp32
+    held to the fixed bounds -- for the covariance chain 1e-3 of max (measured, round 4: means3D /
+    scales 4.9e-5 / 8.1e-5, rotations 5.4e-4 of max); the 4x-of-dense-fp32
     check is left out here: the kernels follow
     upstream's covariance-backward formulas, whose fp32 conditioning on needles differs from that of
     the autograd graph the dense fp32 run differentiates (against the oracle's own fp32 order they
@@ -181,4 +182,4 @@ def test_hip_vs_dense_large_and_needle_splats(device):
     leaves = {k: getattr(d, k) for k in ("means3D", "opacities", "shs", "scales", "rotations")}
     leaves["means2D"] = torch.zeros_like(d.means3D)
     _run_and_compare(cam, leaves, W, H, torch.tensor([0.1, 0.2, 0.3], device=device), deg=2, seed=23, device=device,
-                     flag_rel=2e-4, flag_T_rel=1e-3, chain_frac=2e-3, noise_check=False)
+                     flag_rel=2e-4, flag_T_rel=1e-3, chain_frac=1e-3, noise_check=False)
