@@ -21,7 +21,7 @@
 #include <torch/extension.h>
 
 #include <algorithm>
-#include <atomic>
+#include <mutex>
 #include <string>
 
 namespace {
@@ -180,14 +180,40 @@ struct Inputs {
 
 inline void* stream_of(const c10::Device& dev) { return at::hip::getCurrentHIPStream(dev.index()).stream(); }
 
-// Instance count of the last forward per device: the next forward sizes its binning buffer ahead
-// of its count from it (gs_forward_counted), so the count is read back once every launch is queued
-// instead of between the two halves.  A forward whose count outgrew the estimate bins again into a
-// buffer of the exact size (the geometry is kept); the first forward on a device, a debug forward
-// and that fallback run the two-call path.
-constexpr int GS_COUNT_DEVICES = 64;
-std::atomic<long long> g_count_est[GS_COUNT_DEVICES];
+// Instance-count estimates per (device, P, W, H): the next forward of that shape sizes its binning
+// buffer ahead of its count (gs_forward_counted), so the count is read back once every launch is
+// queued instead of between the two halves.  The estimate follows the recent maximum (the counts of
+// a training loop's cameras differ view to view): max(count, 0.98 x the previous estimate).  A
+// forward whose count outgrew its buffer bins again into one of the exact size (the geometry is
+// kept); a shape's first forward, a debug forward and that fallback run the two-call path.  Keyed
+// by shape, so a small scene rendered after a large one is not given the large one's buffer.
+constexpr int GS_EST_SLOTS = 128;
+struct CountEst {
+  int64_t P = -1;
+  int W = 0, H = 0, dev = -1;
+  long long est = 0;
+};
+std::mutex g_est_mu;
+CountEst g_est[GS_EST_SLOTS];
 constexpr long long GS_CAP_ROUND = 1 << 16;
+
+int est_slot(int dev, int64_t P, int W, int H) {
+  const uint64_t h = (uint64_t)P * 0x9E3779B97F4A7C15ull ^ ((uint64_t)W << 20 | (uint64_t)H << 4 | (uint64_t)dev);
+  return (int)((h ^ (h >> 29)) % GS_EST_SLOTS);
+}
+long long est_get(int dev, int64_t P, int W, int H) {
+  std::lock_guard<std::mutex> lk(g_est_mu);
+  const CountEst& e = g_est[est_slot(dev, P, W, H)];
+  return (e.P == P && e.W == W && e.H == H && e.dev == dev) ? e.est : 0;
+}
+void est_put(int dev, int64_t P, int W, int H, long long n, bool reset = false) {
+  std::lock_guard<std::mutex> lk(g_est_mu);
+  CountEst& e = g_est[est_slot(dev, P, W, H)];
+  const bool same = e.P == P && e.W == W && e.H == H && e.dev == dev;
+  const long long decayed = same && !reset ? e.est - e.est / 50 : 0;
+  e.P = P, e.W = W, e.H = H, e.dev = dev;
+  e.est = std::max<long long>(n, decayed);
+}
 
 long long capacity_for(long long est) {
   const long long want = est + est / 8 + GS_CAP_ROUND;  // +12.5 % and one rounding step of headroom
@@ -221,8 +247,7 @@ py::tuple forward(const at::Tensor& background, const at::Tensor& means3D, const
   long long nr = 0;
   const bool split = x.sh_rest.defined();
   const int di = x.dev.index();
-  std::atomic<long long>* est = di >= 0 && di < GS_COUNT_DEVICES ? &g_count_est[di] : nullptr;
-  const long long e = est ? est->load(std::memory_order_relaxed) : 0;
+  const long long e = est_get(di, x.P, (int)W, (int)H);
   if (e > 0 && !debug) {
     const long long cap = capacity_for(e);
     at::Tensor binning = at::empty({(int64_t)F.binning_bytes(cap, (int)W, (int)H)}, u8);
@@ -232,7 +257,7 @@ py::tuple forward(const at::Tensor& background, const at::Tensor& means3D, const
                              (float)tan_fovy, (int)prefiltered, radii.data_ptr<int>(), geom.data_ptr(), cap,
                              binning.data_ptr(), img.data_ptr(), out_color.data_ptr<float>(), &nr, (int)debug, st);
     if (rc != 2) check(rc, "rasterize_gaussians");
-    est->store(nr, std::memory_order_relaxed);
+    est_put(di, x.P, (int)W, (int)H, nr);
     if (rc == 0) return py::make_tuple((int64_t)nr, out_color, radii, geom, binning, img);
     // (2: more instances than the estimate; radii and geometry are complete, nr exact)
   } else {
@@ -242,7 +267,7 @@ py::tuple forward(const at::Tensor& background, const at::Tensor& means3D, const
               fp(x.rotations), fp(x.cov3D), fp(x.view), fp(x.proj), fp(x.campos), (float)tan_fovx, (float)tan_fovy,
               (int)prefiltered, radii.data_ptr<int>(), geom.data_ptr(), &nr, (int)debug, st),
           "rasterize_gaussians (preprocess)");
-    if (est) est->store(nr, std::memory_order_relaxed);
+    est_put(di, x.P, (int)W, (int)H, nr);
   }
   at::Tensor binning = at::empty({(int64_t)F.binning_bytes(nr, (int)W, (int)H)}, u8);
   check(F.render((int)x.P, fp(x.bg), (int)W, (int)H, fp(x.view), fp(x.proj), fp(x.campos), (float)tan_fovx,
@@ -507,14 +532,13 @@ py::object backward_render(const at::Tensor& background, const at::Tensor& viewm
   return ret();
 }
 
-// the per-device estimate the next forward sizes its binning buffer from (tests; 0: none yet)
-long long count_estimate(int64_t device) {
-  TORCH_CHECK(device >= 0 && device < GS_COUNT_DEVICES, "device index out of range");
-  return g_count_est[device].load();
+// the estimate the next forward of this shape sizes its binning buffer from (tests; 0: none yet,
+// the two-call path); set_count_estimate replaces it (0: forget it)
+long long count_estimate(int64_t device, int64_t P, int64_t W, int64_t H) {
+  return est_get((int)device, P, (int)W, (int)H);
 }
-void set_count_estimate(int64_t device, long long n) {
-  TORCH_CHECK(device >= 0 && device < GS_COUNT_DEVICES, "device index out of range");
-  g_count_est[device].store(std::max<long long>(n, 0));
+void set_count_estimate(int64_t device, int64_t P, int64_t W, int64_t H, long long n) {
+  est_put((int)device, P, (int)W, (int)H, std::max<long long>(n, 0), true);
 }
 
 }  // namespace

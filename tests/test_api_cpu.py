@@ -84,7 +84,8 @@ def test_torch_host_extension_loads():
     for name in ("forward", "backward", "preprocess_views", "forward_prepared", "backward_render", "count_estimate",
                  "set_count_estimate"):
         assert callable(getattr(_C._EXT, name))
-    e = _C._EXT.count_estimate(7)
-    _C._EXT.set_count_estimate(7, 12345)
-    assert _C._EXT.count_estimate(7) == 12345
-    _C._EXT.set_count_estimate(7, e)
+    assert _C._EXT.count_estimate(7, 1000, 64, 48) == 0
+    _C._EXT.set_count_estimate(7, 1000, 64, 48, 12345)
+    assert _C._EXT.count_estimate(7, 1000, 64, 48) == 12345
+    assert _C._EXT.count_estimate(7, 1001, 64, 48) == 0  # per shape
+    _C._EXT.set_count_estimate(7, 1000, 64, 48, 0)

@@ -90,12 +90,14 @@ def test_counted_forward_equals_two_call_forward(device, split, monkeypatch):
             ref = _fwd_bwd(rast, d, dpix, split)
             n = dgr.last_num_rendered()
         # estimates: none (two-call path), about right, far above, below the count (fallback)
+        P = d.means3D.shape[0]
         for est in (0, n, 4 * n + 100_000, n // 3):
-            _C._EXT.set_count_estimate(dev, est)
+            _C._EXT.set_count_estimate(dev, P, W, H, est)
             got = _fwd_bwd(rast, d, dpix, split)
             _assert_same(ref, got, ("estimate", est))
             assert dgr.last_num_rendered() == n  # exact, not the capacity
-            assert _C._EXT.count_estimate(dev) == n
+            e = _C._EXT.count_estimate(dev, P, W, H)
+            assert e >= n and (est > n or e == n), (est, e, n)  # the recent maximum
 
 
 def test_counted_forward_buffers_and_debug_export(device):
@@ -107,9 +109,10 @@ def test_counted_forward_buffers_and_debug_export(device):
             torch.empty(0, device=device), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, H, W, d.shs,
             s.sh_degree, s.campos, s.prefiltered, False)
     dev = torch.device(device).index or 0
-    _C._EXT.set_count_estimate(dev, 0)
+    P = d.means3D.shape[0]
+    _C._EXT.set_count_estimate(dev, P, W, H, 0)
     n0, img0, radii0, geom0, bin0, imgbuf0 = _C.rasterize_gaussians(*args)
-    _C._EXT.set_count_estimate(dev, 5 * n0)
+    _C._EXT.set_count_estimate(dev, P, W, H, 5 * n0)
     n1, img1, radii1, geom1, bin1, imgbuf1 = _C.rasterize_gaussians(*args)
     assert n1 == n0 and torch.equal(img0, img1) and torch.equal(radii0, radii1)
     assert bin1.numel() > bin0.numel()  # laid out for the capacity
@@ -141,7 +144,7 @@ def test_short_forward_with_timed_out_lookback_fails_once(device):
     ref, _ = fwd()
     torch.cuda.synchronize()
     dev = torch.device(device).index or 0
-    _C._EXT.set_count_estimate(dev, 1)  # the next forward outgrows its buffer
+    _C._EXT.set_count_estimate(dev, 200_000, 320, 240, 1)  # the next forward outgrows its buffer
     prev = lib.gs_debug_set_scan_spin_limit(0)
     try:
         with pytest.raises(RuntimeError, match="look-back wait"):
@@ -152,3 +155,25 @@ def test_short_forward_with_timed_out_lookback_fails_once(device):
     img, _ = fwd()  # clean: nothing left over from the failed forward
     torch.cuda.synchronize()
     assert torch.equal(img, ref)
+
+
+def test_count_estimates_are_kept_per_shape(device):
+    """A small scene rendered after a large one is not sized from the large one's count: the
+    estimates are keyed by (device, P, W, H) and follow each shape's recent maximum."""
+    _C = _ext()
+    import diff_gaussian_rasterization as dgr
+
+    dev = torch.device(device).index or 0
+    cam = gs_scenes.circle_cameras(1, 6.0, W, H)[0]
+    rast = dgr.GaussianRasterizer(gs_scenes.raster_settings_for(cam, 3, device=device))
+    big = gs_scenes.random_gaussians(40_000, 3, seed=8, ball_radius=2.0).to(device)
+    small = gs_scenes.random_gaussians(3_000, 3, seed=9, ball_radius=2.0).to(device)
+    dpix = gs_scenes.dl_dimage(H, W, seed=3).to(device)
+    for sc in (big, small):
+        _C._EXT.set_count_estimate(dev, sc.means3D.shape[0], W, H, 0)
+    _fwd_bwd(rast, big, dpix)
+    nb = dgr.last_num_rendered()
+    _fwd_bwd(rast, small, dpix)
+    ns = dgr.last_num_rendered()
+    assert _C._EXT.count_estimate(dev, 40_000, W, H) == nb
+    assert _C._EXT.count_estimate(dev, 3_000, W, H) == ns < nb

@@ -34,7 +34,7 @@ assert X is not None
 
 def fwd(counted):
     if not counted:
-        X.set_count_estimate(0, 0)
+        X.set_count_estimate(0, P, W, H, 0)
     return X.forward(*args[:-1], args[-1], None)
 
 
@@ -72,4 +72,4 @@ for counted in (False, True):
           f"back-to-back: {timed(lambda: bwd(out), False, a.steps):8.1f} us")
     print(f"{tag} fwd+bwd  from idle: {timed(lambda: bwd(fwd(counted)), True, a.steps):8.1f} us   "
           f"back-to-back: {timed(lambda: bwd(fwd(counted)), False, a.steps):8.1f} us")
-print("estimate", X.count_estimate(0), "num_rendered", out[0])
+print("estimate", X.count_estimate(0, P, W, H), "num_rendered", out[0])
