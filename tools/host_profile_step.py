@@ -23,6 +23,8 @@ ap.add_argument("--workload", default="c2", choices=sorted(WL))
 ap.add_argument("--steps", type=int, default=300)
 ap.add_argument("--views", type=int, default=4)
 ap.add_argument("--sort", default="tottime")
+ap.add_argument("--capacity", type=int, default=None, help="bounded views (binning_capacity): no count readback")
+ap.add_argument("--streams", type=int, default=2)
 a = ap.parse_args()
 P, deg, W, H = WL[a.workload]
 dev = torch.device("cuda:0")
@@ -34,7 +36,7 @@ params = [t.clone().requires_grad_(True) for t in (sc.means3D, sc.shs, sc.opacit
 dpix = gs_scenes.dl_dimage(H, W, seed=1).to(dev)
 rasts = [GaussianRasterizer(gs_scenes.raster_settings_for(c, deg, device=dev)) for c in cams]
 bucket = vp.GradBucket(params, lazy_zero=True, defer=True, chunks=1)
-streams = [torch.cuda.Stream(dev) for _ in range(2)]
+streams = [torch.cuda.Stream(dev) for _ in range(a.streams)]
 
 
 def view_fn(r, pre):
@@ -49,7 +51,7 @@ def view_fn(r, pre):
 def step():
     bucket.zero_grad()
     pre = prepare_views(rasts, params[0], params[2], shs=params[1], scales=params[3], rotations=params[4],
-                        streams=[streams[k % 2] for k in range(len(rasts))])
+                        streams=[streams[k % len(streams)] for k in range(len(rasts))], binning_capacity=a.capacity)
     vp.run_views([view_fn(r, p) for r, p in zip(rasts, pre)], streams)
     bucket.finalize()
 
