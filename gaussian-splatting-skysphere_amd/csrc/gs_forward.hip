@@ -753,7 +753,9 @@ struct FwdPix {
 
 // Walk one quadrant wave's list of qcnt staged entries (the list is padded with 2 FWD_ILP zero
 // offsets) for the lane's pixel.
-template <bool EXACT, int NB>
+// PAD: the list's padding points at a staged dummy entry of opacity 0 (alpha 0 at every pixel), so
+// the walk needs no per-entry end-of-list test
+template <bool EXACT, int NB, bool PAD = false>
 __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist, uint32_t qcnt, float pfx, float pfy,
                                          FwdPix& px) {
   // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
@@ -790,7 +792,7 @@ __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist,
       // within ~1e-3 px of a splat centre, so the fast mode leaves the test out (the backward
       // matches it entry for entry)
       const uint64_t m_a = __builtin_amdgcn_ballot_w64((!EXACT || pw[u] <= 0.0f) && al[u] >= 1.0f / 255.0f);
-      uint64_t m_cu = k + u < qcnt ? m_a & ~px.done : 0ull;
+      uint64_t m_cu = (PAD || k + u < qcnt) ? m_a & ~px.done : 0ull;
       if constexpr (EXACT) {  // upstream's order, T (1 - alpha) and (rgb alpha) T, mirrored by the oracle
         const float tT = px.T * (1.0f - al[u]);
         // T would drop below 1e-4: stop before this entry
@@ -941,6 +943,11 @@ __global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uin
 #endif
 constexpr int FWDQ_NB = GS_FWDQ_NB;  // entries staged per round (<= 64: one per lane)
 static_assert(FWDQ_NB <= 64, "one staged entry per lane");
+#ifndef GS_FWD_PAD
+#define GS_FWD_PAD 1
+#endif
+// record stride of the staged batch: one more than the batch for the padding's dummy entry
+constexpr int FWDQ_NBS = FWDQ_NB + (GS_FWD_PAD ? 1 : 0);
 template <bool EXACT>
 __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ point_list,
@@ -950,8 +957,10 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
                                                      float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                      uint32_t* __restrict__ tile_max, ImgPtrs img,
                                                      const uint32_t* __restrict__ err, uint32_t* __restrict__ err_host) {
-  __shared__ float4 s_ent[3 * FWDQ_NB];
+  __shared__ float4 s_ent[3 * FWDQ_NBS];
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
+  if (GS_FWD_PAD && threadIdx.x < 3)  // the dummy entry: position 0, opacity 0 (never contributes)
+    s_ent[threadIdx.x * FWDQ_NBS + FWDQ_NB] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   const uint32_t b = blockIdx.x;
   const uint32_t tile = xcd_tile(b & 7, b >> 5, c.gx, c.gy);
   if (tile == ~0u) return;  // (grid padded to whole groups of 8 tiles)
@@ -998,8 +1007,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
         r[0] = a, r[1] = bb, r[2] = d;
       }
       s_ent[lane] = make_float4(a.x, a.y, bb.z, bb.w);
-      s_ent[FWDQ_NB + lane] = fall_coefs(a.z, a.w, bb.x, bb.y);
-      s_ent[2 * FWDQ_NB + lane] = make_float4(d.x, __uint_as_float(base + lane + 1), 0.0f, 0.0f);
+      s_ent[FWDQ_NBS + lane] = fall_coefs(a.z, a.w, bb.x, bb.y);
+      s_ent[2 * FWDQ_NBS + lane] = make_float4(d.x, __uint_as_float(base + lane + 1), 0.0f, 0.0f);
       meets = d.z >= 0.0f && ellipse_meets_rect(a.x, a.y, a.z, a.w, bb.x, d.z, qx, qx + 7.0f, qy, qy + 7.0f);
     }
 #if GS_FWD_PREFETCH
@@ -1011,9 +1020,9 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
       s_qlist[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
           16u * lane;
     const uint32_t qcnt = (uint32_t)__popcll(m);
-    if (lane < 2 * FWD_ILP) s_qlist[qcnt + lane] = 0;
+    if (lane < 2 * FWD_ILP) s_qlist[qcnt + lane] = GS_FWD_PAD ? 16u * FWDQ_NB : 0u;
     __builtin_amdgcn_wave_barrier();
-    fwd_walk<EXACT, FWDQ_NB>(ent, s_qlist, qcnt, (float)q.px, (float)q.py, px);
+    fwd_walk<EXACT, FWDQ_NBS, GS_FWD_PAD != 0>(ent, s_qlist, qcnt, (float)q.px, (float)q.py, px);
     __builtin_amdgcn_wave_barrier();  // the next round overwrites the staged entries
   }
   fwd_store(c, q, inside, px, out, final_T, n_contrib);
