@@ -323,12 +323,14 @@ static bool check_order_slot_locked(OrderFlags& o, int k, bool wait = true) {
 // for that render here would stall the host while the device has work; a forward whose render
 // has not finished is checked by the next call (at the latest the next forward, whose instance-count
 // readback comes after it on the stream)
-static bool check_order_flags(bool wait = true) {
+// skip: a forward (sequence number) left out, e.g. the caller's own, whose render was just queued
+static bool check_order_flags(bool wait = true, long long skip = -1) {
   OrderFlags* o = order_flags();
   if (!o) return true;
   std::lock_guard<std::mutex> lk(o->mu);
   bool failed = false;
-  for (int k = 0; k < ORDER_RING; k++) failed |= check_order_slot_locked(*o, k, wait);
+  for (int k = 0; k < ORDER_RING; k++)
+    if (skip < 0 || k != (int)(skip % ORDER_RING)) failed |= check_order_slot_locked(*o, k, wait);
   return failed;
 }
 
@@ -364,7 +366,9 @@ static uint32_t* order_flags_word(unsigned long long* seq_out) {
   return o->dev + 16 * k;
 }
 // the render kernel that stores forward `q`'s flags is queued on `st`: record its event, then
-// check the forwards queued before it
+// check the forwards queued before it whose renders have finished (no wait: the views of a step
+// render on two streams, and waiting here for the previous view's render stalled the host for that
+// render's length in every step; the unfinished ones are checked after the next count readback)
 static bool queue_order_flags(hipStream_t st, unsigned long long q) {
   OrderFlags* o = order_flags();
   if (!o) return true;
@@ -377,7 +381,7 @@ static bool queue_order_flags(hipStream_t st, unsigned long long q) {
   o->state[k] = 2;
   bool failed = false;
   for (int j = 0; j < ORDER_RING; j++)
-    if (j != k) failed |= check_order_slot_locked(*o, j);
+    if (j != k) failed |= check_order_slot_locked(*o, j, false);
   return failed;
 }
 // a forward that reserved a word and failed before queueing its render gives the word back
@@ -607,6 +611,7 @@ static int preprocess_views_impl(int K, int P, int D, int M, const float* const*
   if (capacity) return t_failed ? 1 : 0;
   for (int v = 0; v < (batched ? 1 : K); v++) check_hip(hipEventSynchronize(rb->ev[v]), "hipEventSynchronize");
   if (t_failed) return 1;
+  if (check_order_flags()) return 1;  // the rest of the earlier forwards (behind their renders, as a rule)
   for (int v = 0; v < K; v++)
     if (!read_view_totals(rb->host + 8 * v, v, K, &num_rendered_host[v])) return 1;
   return 0;
@@ -869,8 +874,8 @@ int gs_forward_counted(int P, int D, int M, const float* background, int W, int 
     return 1;
   check_hip(hipEventSynchronize(rb->ev[0]), "hipEventSynchronize");
   if (t_failed) return 1;
-  // (this forward's render is queued: check the others without waiting for it)
-  if (check_order_flags(false)) return 1;
+  // (this forward's render is queued: check the others, without waiting for it)
+  if (check_order_flags(true, (long long)oseq)) return 1;
   long long I = 0;
   if (!read_view_totals(rb->host, 0, 1, &I)) return 1;
   *num_rendered_host = I;

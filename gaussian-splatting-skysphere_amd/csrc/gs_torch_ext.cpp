@@ -23,6 +23,9 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <vector>
+
+#include "gsrast.h"
 
 namespace {
 
@@ -68,6 +71,7 @@ struct Fns {
   bwd_render_t bwd_render = nullptr;
   bwd_acc_t backward = nullptr;
   bwd_acc_split_t backward_split = nullptr;
+  decltype(&gs_backward_gaussians_range) bwd_gaussians = nullptr;
   size_t (*geom_bytes)(int) = nullptr;
   size_t (*binning_bytes)(long long, int, int) = nullptr;
   size_t (*image_bytes)(int, int) = nullptr;
@@ -95,6 +99,7 @@ void init() {
   resolve(F.bwd_render, "gs_backward_render");
   resolve(F.backward, "gs_backward_accumulate");
   resolve(F.backward_split, "gs_backward_accumulate_split");
+  resolve(F.bwd_gaussians, "gs_backward_gaussians_range");
   resolve(F.geom_bytes, "gs_geom_buffer_bytes");
   resolve(F.binning_bytes, "gs_binning_buffer_bytes");
   resolve(F.image_bytes, "gs_image_buffer_bytes");
@@ -537,6 +542,52 @@ py::object backward_render(const at::Tensor& background, const at::Tensor& viewm
 long long count_estimate(int64_t device, int64_t P, int64_t W, int64_t H) {
   return est_get((int)device, P, (int)W, (int)H);
 }
+// _C.backward_gaussians: the per-Gaussian half of the backward for several views at once.
+// views: [(viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, W, H, geomBuffer)]; outs: {name:
+// buffer}; wait_event: a hipEvent_t handle (0: none); count < 0: the Gaussians [first, P)
+void backward_gaussians(const at::Tensor& means3D, const c10::optional<at::Tensor>& sh,
+                        const c10::optional<at::Tensor>& colors, const c10::optional<at::Tensor>& scales,
+                        const c10::optional<at::Tensor>& rotations, const c10::optional<at::Tensor>& cov3D,
+                        double scale_modifier, int64_t degree, const py::list& views, const py::dict& outs,
+                        int64_t accumulate, int64_t wait_event, bool debug, int64_t first, int64_t count) {
+  Inputs x(at::Tensor(), means3D, colors, c10::nullopt, scales, rotations, cov3D, at::Tensor(), at::Tensor(), sh,
+           at::Tensor(), false, c10::nullopt);
+  const int K = (int)views.size();
+  if (x.P == 0 || K == 0) return;
+  std::vector<at::Tensor> keep;
+  keep.reserve(3 * K);
+  std::vector<gs_view_grad> arr(K);
+  for (int k = 0; k < K; k++) {
+    const py::tuple v = views[k].cast<py::tuple>();
+    TORCH_CHECK(v.size() == 8, "backward_gaussians: a view is (viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, "
+                               "W, H, geomBuffer)");
+    at::Tensor vm = f32(v[0].cast<at::Tensor>(), "viewmatrix", x.dev, true);
+    at::Tensor pm = f32(v[1].cast<at::Tensor>(), "projmatrix", x.dev, true);
+    at::Tensor cp = v[2].is_none() ? at::Tensor() : f32(v[2].cast<at::Tensor>(), "campos", x.dev, true);
+    keep.push_back(vm), keep.push_back(pm), keep.push_back(cp);
+    arr[k] = gs_view_grad{fp(vm), fp(pm), fp(cp), (float)v[3].cast<double>(), (float)v[4].cast<double>(),
+                          v[5].cast<int>(), v[6].cast<int>(), v[7].cast<at::Tensor>().data_ptr()};
+  }
+  auto out = [&](const char* n) -> float* {
+    if (!outs.contains(n)) return nullptr;
+    const py::object o = outs[n];
+    if (o.is_none()) return nullptr;
+    const at::Tensor t = o.cast<at::Tensor>();
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous() && t.device() == x.dev, "backward_gaussians: ", n,
+                " output must be a contiguous float32 tensor on ", x.dev.str());
+    return t.data_ptr<float>();
+  };
+  float *o_col = out("colors"), *o_op = out("opacity"), *o_m3 = out("means3D"), *o_cov = out("cov3D");
+  float *o_sh = out("sh"), *o_sc = out("scales"), *o_rot = out("rotations");
+  const int64_t n = count < 0 ? x.P - first : count;
+  c10::DeviceGuard guard(x.dev);
+  check(F.bwd_gaussians((int)x.P, (int)first, (int)n, (int)degree, (int)x.M, fp(x.means3D), fp(x.sh), fp(x.colors),
+                        fp(x.scales), (float)scale_modifier, fp(x.rotations), fp(x.cov3D), K, arr.data(), o_col, o_op,
+                        o_m3, o_cov, o_sh, o_sc, o_rot, (unsigned)accumulate, reinterpret_cast<void*>(wait_event),
+                        (int)debug, stream_of(x.dev)),
+        "rasterize_gaussians_backward (per-Gaussian half)");
+}
+
 void set_count_estimate(int64_t device, int64_t P, int64_t W, int64_t H, long long n) {
   est_put((int)device, P, (int)W, (int)H, std::max<long long>(n, 0), true);
 }
@@ -551,6 +602,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("preprocess_views", &preprocess_views);
   m.def("forward_prepared", &forward_prepared);
   m.def("backward_render", &backward_render);
+  m.def("backward_gaussians", &backward_gaussians);
   m.def("count_estimate", &count_estimate);
   m.def("set_count_estimate", &set_count_estimate);
 }

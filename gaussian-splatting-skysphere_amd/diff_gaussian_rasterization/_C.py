@@ -448,6 +448,11 @@ def backward_gaussians(means3D, sh, colors, scales, rotations, cov3D_precomp, sc
     after its backward_render); outs: {name: buffer} for colors / opacity / means3D / cov3D / sh /
     scales / rotations (absent: not produced); accumulate: GS_ACC bits of the first view.
     first / count: only the Gaussians [first, first + count) (gs_backward_gaussians_range)."""
+    if _EXT is not None and means3D.is_cuda:
+        return _EXT.backward_gaussians(means3D, sh, colors, scales, rotations, cov3D_precomp, float(scale_modifier),
+                                       int(degree), views, outs, int(accumulate),
+                                       wait_event.cuda_event if wait_event is not None else 0, bool(debug),
+                                       int(first), -1 if count is None else int(count))
     x = _Inputs(None, means3D, colors, None, scales, rotations, cov3D_precomp, views[0][0],
                 views[0][1], sh, views[0][2], need_opacity=False)
     P, dev = x.P, x.device

@@ -165,8 +165,10 @@ def prepare_views(rasterizers, means3D, opacities, shs=None, colors_precomp=None
     if binning_capacity is not None:
         caps = ([int(binning_capacity)] * len(ss) if isinstance(binning_capacity, int)
                 else [int(c) for c in binning_capacity])
-    views = [_contiguous_matrix(s.viewmatrix, streams) for s in ss]
-    projs = [_contiguous_matrix(s.projmatrix, streams) for s in ss]
+    # view k's matrices are read on the current stream (the preprocess) and on streams[k]
+    own = [None] * len(ss) if not streams else [[streams[k]] for k in range(len(ss))]
+    views = [_contiguous_matrix(s.viewmatrix, o) for s, o in zip(ss, own)]
+    projs = [_contiguous_matrix(s.projmatrix, o) for s, o in zip(ss, own)]
     with torch.no_grad():
         tri = _C.preprocess_views([s.bg for s in ss], means3D.detach(), e(colors_precomp).detach(), opacities.detach(),
                                   e(scales).detach(), e(rotations).detach(), s0.scale_modifier,
@@ -268,9 +270,14 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii)
-        inputs = (means3D, means2D, sh_input, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
-        ctx.sinks = [(k, name, inputs[k], _sink_owner(inputs[k])) for k, name in _SINK_INPUTS
-                     if _sink_owner(inputs[k]) is not None] if _SINKS else []
+        sinks = []
+        if _SINKS:
+            inputs = (means3D, means2D, sh_input, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
+            for k, name in _SINK_INPUTS:
+                owner = _sink_owner(inputs[k])
+                if owner is not None:
+                    sinks.append((k, name, inputs[k], owner))
+        ctx.sinks = sinks
         return color, radii
 
     @staticmethod

@@ -57,6 +57,7 @@ class GradBucket:
         # row written once per step instead of once per view.  Same fp32 sums as without.
         self.defers = defer
         self._deferred = []
+        self._ev_pool = []  # recorded-and-waited events of retired deferred views, reused by defer_view
         # stream ordering of the writes into the bucket: the last writer's event and stream (views
         # rendered on several streams add into one bucket one after another; their forward passes,
         # sorts and tile backward passes overlap)
@@ -173,7 +174,7 @@ class GradBucket:
         if self._deferred and not _same_inputs(self._deferred[0][0], inputs):
             self.flush()  # another set of Gaussians: finish the pending views first
         st = torch.cuda.current_stream(view[7].device)
-        ev = torch.cuda.Event()
+        ev = self._ev_pool.pop() if self._ev_pool else torch.cuda.Event()
         ev.record(st)
         sunk = [(name, t) for k, name, t, o in ctx.sinks if o is self and ctx.needs_input_grad[k] and k != 1]
         self._deferred.append((inputs, view, ev, sunk))
@@ -217,6 +218,8 @@ class GradBucket:
             if isinstance(t, torch.Tensor) and t.is_cuda and t.numel():
                 t.record_stream(cur)
         self.written(cur)
+        # the views' events are waited on (enqueued) already: free to record again
+        self._ev_pool += [d[2] for d in self._deferred]
         self._deferred = []
 
     def flush(self):
@@ -337,10 +340,34 @@ def run_views(view_fns: Sequence, streams: Sequence) -> None:
     for s in streams:
         s.wait_stream(main)
     for k, fn in enumerate(view_fns):
-        with torch.cuda.stream(streams[k % len(streams)]):
+        with _on_stream(streams[k % len(streams)], main):
             fn()
     for s in streams:
         main.wait_stream(s)
+
+
+class _on_stream:
+    """torch.cuda.stream(s) for a stream of the current device whose current stream is `main`:
+    the same two stream switches without the context manager's device lookups (≈ 20 µs of host
+    time per view, measured in tools/host_phases.py).  Another device's stream takes torch's path."""
+
+    __slots__ = ("s", "main", "ctx")
+
+    def __init__(self, s, main):
+        self.s, self.main, self.ctx = s, main, None
+
+    def __enter__(self):
+        s = self.s
+        if s.device_index != self.main.device_index:
+            self.ctx = torch.cuda.stream(s)
+            return self.ctx.__enter__()
+        torch._C._cuda_setStream(stream_id=s.stream_id, device_index=s.device_index, device_type=s.device_type)
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            return self.ctx.__exit__(*exc)
+        m = self.main
+        torch._C._cuda_setStream(stream_id=m.stream_id, device_index=m.device_index, device_type=m.device_type)
 
 
 def allreduce_grads(params: Iterable[torch.Tensor], group=None, average: bool = False):

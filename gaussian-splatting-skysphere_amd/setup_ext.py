@@ -12,7 +12,7 @@ os.chdir(HERE)
 setup(
     name="gs_torch_ext",
     ext_modules=[CppExtension("diff_gaussian_rasterization._gs_ext", ["csrc/gs_torch_ext.cpp"],
-                              include_dirs=["/opt/rocm/include"],
+                              include_dirs=["/opt/rocm/include", os.path.join(HERE, "..", "include")],
                               extra_compile_args=["-O2", "-g0", "-D__HIP_PLATFORM_AMD__=1"],
                               extra_link_args=["-s"])],
     cmdclass={"build_ext": BuildExtension},

@@ -25,6 +25,7 @@ ap.add_argument("--views", type=int, default=4)
 ap.add_argument("--sort", default="tottime")
 ap.add_argument("--capacity", type=int, default=None, help="bounded views (binning_capacity): no count readback")
 ap.add_argument("--streams", type=int, default=2)
+ap.add_argument("--lines", type=int, default=40)
 a = ap.parse_args()
 P, deg, W, H = WL[a.workload]
 dev = torch.device("cuda:0")
@@ -80,4 +81,4 @@ for _ in range(a.steps):
     step()
 torch.cuda.synchronize()
 pr.disable()
-pstats.Stats(pr).sort_stats(a.sort).print_stats(40)
+pstats.Stats(pr).sort_stats(a.sort).print_stats(a.lines)
