@@ -81,8 +81,8 @@ def test_torch_host_extension_loads():
     if os.environ.get("GSRAST_NO_EXT", "0") not in ("", "0"):
         pytest.skip("GSRAST_NO_EXT set")
     assert _C._EXT is not None, "diff_gaussian_rasterization/_gs_ext*.so missing: run setup_ext.py"
-    for name in ("forward", "backward", "preprocess_views", "forward_prepared", "backward_render", "count_estimate",
-                 "set_count_estimate"):
+    for name in ("forward", "backward", "preprocess_views", "forward_prepared", "backward_render",
+                 "backward_gaussians", "count_estimate", "set_count_estimate"):
         assert callable(getattr(_C._EXT, name))
     assert _C._EXT.count_estimate(7, 1000, 64, 48) == 0
     _C._EXT.set_count_estimate(7, 1000, 64, 48, 12345)

@@ -10,7 +10,8 @@ back at the end, the binning buffer sized ahead from the last count).
     an exact buffer) and one far below it (a larger layout than its count) give the same bits;
   - debug_export reads a counted forward's buffers (layout count vs num_rendered);
   - a timed-out look-back in a forward that outgrew its estimate fails in that forward, once (the
-    skipped render's flags are read before re-binning), and the next call is clean.
+    skipped render's flags are read before re-binning), and the next call is clean;
+  - a deferred GradBucket's per-Gaussian pass runs through the ext, bit-identical to ctypes.
 """
 import pytest
 import torch
@@ -177,3 +178,59 @@ def test_count_estimates_are_kept_per_shape(device):
     ns = dgr.last_num_rendered()
     assert _C._EXT.count_estimate(dev, 40_000, W, H) == nb
     assert _C._EXT.count_estimate(dev, 3_000, W, H) == ns < nb
+
+
+class _Spy:
+    """Forwards every attribute of the ext module; counts backward_gaussians calls."""
+
+    def __init__(self, ext):
+        self.ext, self.calls = ext, 0
+
+    def __getattr__(self, name):
+        if name == "backward_gaussians":
+            self.calls += 1
+        return getattr(self.ext, name)
+
+
+def test_deferred_pass_goes_through_ext_and_equals_ctypes(device, monkeypatch):
+    """A deferred GradBucket's per-Gaussian pass (finalize -> _C.backward_gaussians) runs through
+    the ext (round 4), and its gradients are bit-identical to the ctypes bridge's."""
+    _C = _ext()
+    import gs_view_parallel as vp
+    from diff_gaussian_rasterization import GaussianRasterizer
+
+    cams = gs_scenes.circle_cameras(2, 6.0, W, H)
+    d = gs_scenes.random_gaussians(8_000, 3, seed=9, ball_radius=2.0).to(device)
+    rasts = [GaussianRasterizer(gs_scenes.raster_settings_for(c, 3, device=device)) for c in cams]
+    dpix = [gs_scenes.dl_dimage(H, W, seed=70 + v).to(device) for v in range(2)]
+
+    def step():
+        p = _leaves(d)
+        b = vp.GradBucket(p, lazy_zero=True, defer=True)
+        b.zero_grad()
+        for r, dp in zip(rasts, dpix):
+            m2 = torch.zeros_like(p[0], requires_grad=True)
+            img, _ = r(means3D=p[0], means2D=m2, opacities=p[2], shs=p[1], scales=p[3], rotations=p[4])
+            img.backward(dp)
+        b.finalize()
+        torch.cuda.synchronize()
+        out = [t.grad.clone() for t in p]
+        b.close()
+        return out
+
+    spy = _Spy(_C._EXT)
+    monkeypatch.setattr(_C, "_EXT", spy)
+    got = step()
+    assert spy.calls >= 1, "the deferred per-Gaussian pass did not go through the ext"
+    ref_fn = _C.backward_gaussians
+
+    def ctypes_pass(*a, **kw):
+        e, _C._EXT = _C._EXT, None
+        try:
+            return ref_fn(*a, **kw)
+        finally:
+            _C._EXT = e
+
+    monkeypatch.setattr(_C, "backward_gaussians", ctypes_pass)
+    ref = step()
+    _assert_same(ref, got, "deferred pass ext vs ctypes")
