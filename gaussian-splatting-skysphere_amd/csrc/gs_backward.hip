@@ -34,6 +34,51 @@ extern "C" int gs_debug_bwd_stats(unsigned long long* host_out, int reset) {
 }
 #endif
 
+#ifdef GS_BWD_TIMING
+// diagnostic build only (-DGS_BWD_TIMING, tools/bwd_timing.py): per backward wave (launch position
+// b = blockIdx.x) [b][0] start / [1] end s_memrealtime stamps (100 MHz), [2] tile << 32 | n_eff,
+// [3] xcc_id << 32 | hw_id, [4] entries walked << 32 | slots evaluated.  No output reads them.
+constexpr int BWD_TIMING_MAX = 1 << 16;
+__device__ unsigned long long g_bwd_timing[BWD_TIMING_MAX][5];
+extern "C" int gs_debug_bwd_timing(unsigned long long* host_out, int n, int reset) {
+  if (n > BWD_TIMING_MAX) n = BWD_TIMING_MAX;
+  if (host_out && hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_bwd_timing), (size_t)n * 5 * 8) != hipSuccess) return 1;
+  if (reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_bwd_timing)) != hipSuccess) return 1;
+    if (hipMemset(p, 0, sizeof(g_bwd_timing)) != hipSuccess) return 1;
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+  }
+  return 0;
+}
+__device__ __forceinline__ unsigned long long bwd_stamp() {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+__device__ __forceinline__ void bwd_timing_record(unsigned long long t0, uint32_t tile, uint32_t n_eff,
+                                                  uint32_t walked, uint32_t slots) {
+  const unsigned long long t1 = bwd_stamp();
+  if (threadIdx.x == 0 && blockIdx.x < BWD_TIMING_MAX) {
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    unsigned long long* o = g_bwd_timing[blockIdx.x];
+    o[0] = t0;
+    o[1] = t1;
+    o[2] = ((unsigned long long)tile << 32) | n_eff;
+    o[3] = ((unsigned long long)xcc << 32) | hw;
+    o[4] = ((unsigned long long)walked << 32) | slots;
+  }
+}
+#define GS_BWD_T0() const unsigned long long t_start = bwd_stamp()
+#define GS_BWD_TREC(tile, n_eff, walked, slots) bwd_timing_record(t_start, tile, n_eff, walked, slots)
+#else
+#define GS_BWD_T0() (void)0
+#define GS_BWD_TREC(tile, n_eff, walked, slots) (void)0
+#endif
+
 // culling-side evaluation of one entry for a lane's two pixels (independent of the pixel state)
 struct Eval {
   float4 co;
@@ -536,6 +581,7 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
   // banks, measured 343 -> 361 us at C3)
   constexpr int ROW = GS_BWDT_ROW;
   __shared__ __attribute__((aligned(16))) float s_acc[64][ROW];
+  GS_BWD_T0();
   const uint32_t tile = __builtin_amdgcn_readfirstlane(tile_order ? tile_order[blockIdx.x] : blockIdx.x);
   if (tile == ~0u) return;  // a hole of the XCD-group launch order
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
@@ -546,7 +592,13 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
   const uint4 qm = reinterpret_cast<const uint4*>(tile_max)[tile];
   const uint32_t qlast[4] = {min(qm.x, n), min(qm.y, n), min(qm.z, n), min(qm.w, n)};
   const uint32_t n_eff = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
-  if (n_eff == 0) return;  // no instance walked: no records (k_sum_records reads none below a cut of 0)
+  if (n_eff == 0) {
+    GS_BWD_TREC(tile, 0u, 0u, 0u);
+    return;  // no instance walked: no records (k_sum_records reads none below a cut of 0)
+  }
+#ifdef GS_BWD_TIMING
+  uint32_t t_walked = 0, t_slots = 0;
+#endif
 
   const size_t HW = (size_t)c.W * c.H;
   const int qx0 = tx * GS_TILE + (lane & 7), qy0 = ty * GS_TILE + (lane >> 3);
@@ -652,6 +704,10 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
       float s[GRAD_REC];
 #pragma unroll
       for (int t = 0; t < GRAD_REC; t++) s[t] = 0.0f;
+#ifdef GS_BWD_TIMING
+      t_walked++;
+      t_slots += ((M[0] >> j) & 1ull) + ((M[1] >> j) & 1ull) + ((M[2] >> j) & 1ull) + ((M[3] >> j) & 1ull);
+#endif
       uint64_t con = 0;  // lanes with a contributing slot
 #pragma unroll
       for (int k = 0; k < 4; k++)
@@ -711,6 +767,7 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
     __builtin_amdgcn_wave_barrier();  // the next batch overwrites the staged entries
   }
   store_records();
+  GS_BWD_TREC(tile, n_eff, t_walked, t_slots);
 }
 
 // Longest-first launch order for the backward.  A tile's walk is as long as its largest

@@ -29,55 +29,29 @@
 
 namespace {
 
-using f_cp = const float*;
-using fwd_pre_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, f_cp, f_cp, float, f_cp, f_cp, f_cp, f_cp,
-                          f_cp, float, float, int, int*, void*, long long*, int, void*);
-using fwd_render_t = int (*)(int, f_cp, int, int, f_cp, f_cp, f_cp, float, float, const int*, void*, long long, void*,
-                             void*, float*, int, void*);
-using fwd_counted_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, f_cp, f_cp, f_cp, float, f_cp, f_cp, f_cp,
-                              f_cp, f_cp, float, float, int, int*, void*, long long, void*, void*, float*, long long*,
-                              int, void*);
-using pre_views_t = int (*)(int, int, int, int, const float* const*, const int*, const int*, f_cp, f_cp, f_cp, f_cp, f_cp,
-                            float, f_cp, f_cp, const float* const*, const float* const*, const float* const*, f_cp, f_cp,
-                            int, int* const*, void* const*, long long*, int, void*, void* const*);
-using pre_views_bounded_t = int (*)(int, int, int, int, const float* const*, const int*, const int*, f_cp, f_cp, f_cp,
-                                    f_cp, f_cp, float, f_cp, f_cp, const float* const*, const float* const*,
-                                    const float* const*, f_cp, f_cp, int, int* const*, void* const*, const long long*,
-                                    int, void*, void* const*);
-using bin_views_t = int (*)(int, int, int, int, void* const*, const long long*, void* const*, void* const*, int, void*,
-                            void* const*);
-using render_binned_t = int (*)(int, f_cp, int, int, f_cp, f_cp, f_cp, float, float, void*, long long, void*, void*,
-                                float*, int, int, void*);
-using bwd_render_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, float, float, const void*, long long,
-                             const void*, const void*, f_cp, void*, float*, unsigned, int, void*);
-using bwd_acc_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, f_cp, f_cp, float, f_cp, f_cp, f_cp, f_cp,
-                          f_cp, float, float, const int*, const void*, long long, const void*, const void*, f_cp,
-                          void*, float*, float*, float*, float*, float*, float*, float*, float*, unsigned, void*,
-                          int, void*);
-using bwd_acc_split_t = int (*)(int, int, int, f_cp, int, int, f_cp, f_cp, f_cp, f_cp, f_cp, float, f_cp, f_cp, f_cp,
-                                f_cp, f_cp, float, float, const int*, const void*, long long, const void*,
-                                const void*, f_cp, void*, float*, float*, float*, float*, float*, float*, float*,
-                                unsigned, void*, int, void*);
-
+// the entry points' types come from include/gsrast.h itself, so a signature change there fails this
+// build instead of calling the library with the wrong arguments (and init() checks the loaded
+// library's ABI version against the header's)
 struct Fns {
-  fwd_pre_t preprocess = nullptr, preprocess_split = nullptr;
-  fwd_render_t render = nullptr;
-  fwd_counted_t counted = nullptr;
-  fwd_render_t render_bounded = nullptr;
-  pre_views_t pre_views = nullptr;
-  pre_views_bounded_t pre_views_bounded = nullptr;
-  bin_views_t bin_views = nullptr;
-  render_binned_t render_binned = nullptr;
-  bwd_render_t bwd_render = nullptr;
-  bwd_acc_t backward = nullptr;
-  bwd_acc_split_t backward_split = nullptr;
+  decltype(&gs_forward_preprocess) preprocess = nullptr;
+  decltype(&gs_forward_preprocess_split) preprocess_split = nullptr;
+  decltype(&gs_forward_render) render = nullptr;
+  decltype(&gs_forward_counted) counted = nullptr;
+  decltype(&gs_forward_render_bounded) render_bounded = nullptr;
+  decltype(&gs_forward_preprocess_views) pre_views = nullptr;
+  decltype(&gs_forward_preprocess_views_bounded) pre_views_bounded = nullptr;
+  decltype(&gs_forward_bin_views) bin_views = nullptr;
+  decltype(&gs_forward_render_binned) render_binned = nullptr;
+  decltype(&gs_backward_render) bwd_render = nullptr;
+  decltype(&gs_backward_accumulate) backward = nullptr;
+  decltype(&gs_backward_accumulate_split) backward_split = nullptr;
   decltype(&gs_backward_gaussians_range) bwd_gaussians = nullptr;
-  size_t (*geom_bytes)(int) = nullptr;
-  size_t (*binning_bytes)(long long, int, int) = nullptr;
-  size_t (*image_bytes)(int, int) = nullptr;
-  size_t (*grad_bytes)(long long) = nullptr;
-  long long (*layout_count)(size_t, int, int) = nullptr;
-  const char* (*last_error)() = nullptr;
+  decltype(&gs_geom_buffer_bytes) geom_bytes = nullptr;
+  decltype(&gs_binning_buffer_bytes) binning_bytes = nullptr;
+  decltype(&gs_image_buffer_bytes) image_bytes = nullptr;
+  decltype(&gs_grad_buffer_bytes) grad_bytes = nullptr;
+  decltype(&gs_binning_layout_count) layout_count = nullptr;
+  decltype(&gs_last_error) last_error = nullptr;
 } F;
 
 template <typename T>
@@ -87,6 +61,11 @@ void resolve(T& fn, const char* name) {
 }
 
 void init() {
+  decltype(&gs_abi_version) abi = nullptr;
+  resolve(abi, "gs_abi_version");
+  TORCH_CHECK(abi() == GSRAST_ABI_VERSION, "gs_torch_ext: the loaded libgsrast.so has ABI ", abi(),
+              ", this extension was built against include/gsrast.h ABI ", GSRAST_ABI_VERSION,
+              ": rebuild the extension (setup_ext.py) or the library");
   resolve(F.preprocess, "gs_forward_preprocess");
   resolve(F.preprocess_split, "gs_forward_preprocess_split");
   resolve(F.render, "gs_forward_render");

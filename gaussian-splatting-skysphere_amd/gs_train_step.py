@@ -139,7 +139,8 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
                loss_item: bool = False, binning_capacity: int | None = None):
     """One iteration (module docstring).  Returns the loss tensor, or with loss_item=True the
     reference's per-iteration `loss.item()` (train.py:99, its progress-bar EMA): a host read-back
-    that waits for the whole iteration.
+    that waits for the forward and backward, taken where train.py takes it (before the statistics
+    and the optimizer step).
     fused_adjoint (with fused): the activation's backward runs inside the Adam update
     (FusedAdam.step_activated), so the raw parameters' gradients are never stored; same floats as
     activate's backward followed by FusedAdam.step, .grad of the activated parameters stays None.
@@ -147,7 +148,8 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
     iteration can be captured in a HIP graph).  A view with more instances than the capacity is
     invalid: the flags land in the device's bounded status, which train_step reads at the
     loss.item() sync point (loss_item=True) and raises there -- the iteration that overflowed, not
-    a later one.  Without loss_item the caller polls bounded_status() after its own sync."""
+    a later one, and before its optimizer step.  Without loss_item the caller polls
+    bounded_status() after its own sync."""
     acts = [] if (fused and fused_adjoint) else None
     image, viewspace, radii = render(model, settings, fused, acts, split_sh, binning_capacity)
     if fused:  # the whole loss expression in one fused forward / backward (gs_loss.photometric_loss)
@@ -156,6 +158,14 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
         Ll1 = gs_loss.l1_loss(image, gt_image)
         loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - gs_loss.ssim(image, gt_image))
     loss.backward()
+    value = None
+    if loss_item:
+        # train.py:99 reads loss.item() here, after the backward and before the statistics and the
+        # optimizer step (train.py:115-128): an iteration whose bounded forward overflowed raises
+        # now, before any parameter, moment or statistic is updated from its invalid gradients
+        value = loss.item()
+        if binning_capacity is not None:
+            bounded_status()
     with torch.no_grad():
         if densify_stats:
             if fused:
@@ -171,12 +181,7 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
         else:
             model.optimizer.step()
         model.optimizer.zero_grad(set_to_none=True)
-    if loss_item:
-        value = loss.item()  # train.py:99 (waits for the iteration)
-        if binning_capacity is not None:
-            bounded_status()  # raises if this iteration's bounded forward overflowed its capacity
-        return value
-    return loss
+    return value if loss_item else loss
 
 
 def train_step_views(model: TrainModel, bucket, views, lambda_dssim: float = LAMBDA_DSSIM, densify_stats: bool = True,

@@ -166,9 +166,29 @@ def test_bounded_train_step_raises_at_its_own_loss_item(device):
     assert la == lb
     for name in ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
+    names = ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
+
+    def snapshot(m):
+        st = m.optimizer.state_dict()["state"]
+        moments = {(i, k): v.clone() for i, s in st.items() for k, v in s.items() if torch.is_tensor(v)}
+        steps = {(i, k): v for i, s in st.items() for k, v in s.items() if not torch.is_tensor(v)}
+        return ({n: getattr(m, n).detach().clone() for n in names}, moments, steps,
+                [t.clone() for t in (m.max_radii2D, m.xyz_gradient_accum, m.denom)])
+
+    before = snapshot(b)
     with pytest.raises(RuntimeError, match="binning capacity"):
         ts.train_step(b, settings, gt, loss_item=True, binning_capacity=n // 4)
     assert bounded_status() == (0, 0)
+    # the overflowing iteration raised at its loss.item() (train.py:99), before the statistics and
+    # the optimizer step: no parameter, moment, step count or statistic took its gradients
+    after = snapshot(b)
+    for n_ in names:
+        assert torch.equal(before[0][n_], after[0][n_]), n_
+    assert before[1].keys() == after[1].keys() and before[2] == after[2]
+    for k in before[1]:
+        assert torch.equal(before[1][k], after[1][k]), k
+    for x, y in zip(before[3], after[3]):
+        assert torch.equal(x, y)
 
 
 def test_bounded_overflow_in_a_captured_step_raises_in_the_loop(device):
