@@ -146,7 +146,7 @@ __global__ void k_export_list(uint32_t I, const uint32_t* counters, const uint32
     out[k] = 0xFFFFFFFFu;
     return;
   }
-  const uint32_t s = GS_SORT_GID ? k : point_list[k];
+  const uint32_t s = point_list[k];
   out[k] = s < I ? ids[s] : 0xFFFFFFFFu;
 }
 __global__ void k_export_splat(int P, const float4* splat, float* xy, float* co, float* rgb, float* depth) {
@@ -209,8 +209,11 @@ size_t gs_binning_buffer_bytes(long long num_rendered, int W, int H) {
 }
 size_t gs_image_buffer_bytes(int W, int H) { return img_layout(W, H, nullptr, nullptr); }
 long long gs_binning_layout_count(size_t bytes, int W, int H) {
-  // gs_binning_buffer_bytes is non-decreasing in the count, and two counts with the same byte size
-  // have the same aligned array sizes, hence the same layout
+  // every array of bin_layout has a size that never decreases with the count (sort_scratch_words
+  // is a monotone bound, not sort_plan's nb), so gs_binning_buffer_bytes is non-decreasing, and two
+  // counts with the same byte size have the same aligned array sizes, hence the same layout: the
+  // largest count that fits `bytes` lays the buffer out exactly as the count it was sized for
+  // (tests/test_abi.py checks this around the sort's block-count steps at k * 2^23 instances)
   if (gs_binning_buffer_bytes(1, W, H) > bytes) return 0;
   long long lo = 1, hi = GS_MAX_INSTANCES;
   while (lo < hi) {
@@ -224,7 +227,7 @@ long long gs_binning_layout_count(size_t bytes, int W, int H) {
 }
 size_t gs_grad_buffer_bytes(long long num_rendered) {
   const size_t R = (size_t)(num_rendered > 0 ? num_rendered : 1);
-  return align_up(R * GRAD_REC * sizeof(float) + sumrec_extra_bytes(R));
+  return align_up(R * GRAD_REC * sizeof(float));
 }
 
 // Pinned, device-mapped host words: kernels store into them directly (vector stores through the
@@ -512,12 +515,8 @@ int gs_forward_preprocess_split(int P, int D, int M, const float* background, in
 // The K views' depth sorts as one set of launches (contiguous geometry buffers); GSRAST_BATCH_VIEWS=0
 // in the environment runs them view by view on the views' streams (A/B runs; the Python layer then
 // also bins the views one by one)
-#ifndef GS_BATCH_ORDER_MAX
-#define GS_BATCH_ORDER_MAX (2 << 20)
-#endif
-#ifndef GS_BATCH_BIN_MAX
-#define GS_BATCH_BIN_MAX (8u << 20)  // instances per view up to which gs_forward_bin_views batches
-#endif
+constexpr int GS_BATCH_ORDER_MAX = 2 << 20;      // Gaussians up to which the views' depth sorts batch
+constexpr uint32_t GS_BATCH_BIN_MAX = 8u << 20;  // instances per view up to which gs_forward_bin_views batches
 static bool batch_views() {
   static const bool on = [] {
     const char* e = getenv("GSRAST_BATCH_VIEWS");
@@ -866,12 +865,15 @@ int gs_forward_counted(int P, int D, int M, const float* background, int W, int 
   fwd_preprocess(g, c, radii_out, geo, st);
   const uint32_t cap32 = (uint32_t)capacity;
   fwd_order(P, geo, st, rb->dev, rb->ev[0], &cap32, nullptr);
-  if (t_failed) return 1;
+  // the count readback is queued into this thread's slot: every return from here on waits for it,
+  // so no kernel of this call can still write the slot's words when the thread's next call reads them
+  auto drain = [&]() { (void)hipEventSynchronize(rb->ev[0]); };
+  if (t_failed) return drain(), 1;
   unsigned long long oseq = 0;
   if (forward_render_impl(P, background, W, H, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii_out,
                           geom_buffer, capacity, binning_buffer, image_buffer, out_color, false, debug, stream,
                           &oseq))
-    return 1;
+    return drain(), 1;
   check_hip(hipEventSynchronize(rb->ev[0]), "hipEventSynchronize");
   if (t_failed) return 1;
   // (this forward's render is queued: check the others, without waiting for it)
@@ -1407,7 +1409,7 @@ int gs_debug_export(int P, int W, int H, long long num_rendered, const void* geo
   img_layout(W, H, &img, (char*)image_buffer);
   if (point_list && num_rendered > 0)
     GS_LAUNCH("export_list", k_export_list, dim3((unsigned)((num_rendered + 255) / 256)), dim3(256), 0, st,
-              (uint32_t)num_rendered, geo.counters, bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid,
+              (uint32_t)num_rendered, geo.counters, bin.point_list, bin.presort_gid,
               point_list);
   if (ranges) check_hip(hipMemcpyAsync(ranges, img.ranges, sizeof(uint2) * gx * gy, hipMemcpyDeviceToDevice, st), "copy");
   if (xy || conic_opacity || rgb || depth)
@@ -1416,7 +1418,9 @@ int gs_debug_export(int P, int W, int H, long long num_rendered, const void* geo
   if (tiles_touched)
     check_hip(hipMemcpyAsync(tiles_touched, geo.tiles, sizeof(uint32_t) * P, hipMemcpyDeviceToDevice, st), "copy");
   if (final_T)
-    check_hip(hipMemcpyAsync(final_T, img.final_T, sizeof(float) * W * H, hipMemcpyDeviceToDevice, st), "copy");
+    // T_final is the fourth word of each pixel's fin record
+    check_hip(hipMemcpy2DAsync(final_T, sizeof(float), reinterpret_cast<const char*>(img.fin) + 12, sizeof(float4),
+                               sizeof(float), (size_t)W * H, hipMemcpyDeviceToDevice, st), "copy");
   if (n_contrib)
     check_hip(hipMemcpyAsync(n_contrib, img.n_contrib, sizeof(uint32_t) * W * H, hipMemcpyDeviceToDevice, st), "copy");
   return t_failed ? 1 : 0;

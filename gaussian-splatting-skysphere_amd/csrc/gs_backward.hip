@@ -20,91 +20,16 @@
 
 namespace gs {
 
-#ifdef GS_BWD_STATS
-// instrumentation build only (-DGS_BWD_STATS): [0..64] applied entries by contributing-lane count,
-// [65] evaluated entries, [67] contributing pixels summed over them
-__device__ unsigned long long g_bwd_stats[80];
-extern "C" int gs_debug_bwd_stats(unsigned long long* host_out, int reset) {
-  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_bwd_stats), sizeof(g_bwd_stats)) != hipSuccess) return 1;
-  if (reset) {
-    static const unsigned long long z[80] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_stats), z, sizeof(z)) != hipSuccess) return 1;
-  }
-  return 0;
-}
-#endif
-
-#ifdef GS_BWD_TIMING
-// diagnostic build only (-DGS_BWD_TIMING, tools/bwd_timing.py): per backward wave (launch position
-// b = blockIdx.x) [b][0] start / [1] end s_memrealtime stamps (100 MHz), [2] tile << 32 | n_eff,
-// [3] xcc_id << 32 | hw_id, [4] entries walked << 32 | slots evaluated.  No output reads them.
-constexpr int BWD_TIMING_MAX = 1 << 16;
-__device__ unsigned long long g_bwd_timing[BWD_TIMING_MAX][5];
-extern "C" int gs_debug_bwd_timing(unsigned long long* host_out, int n, int reset) {
-  if (n > BWD_TIMING_MAX) n = BWD_TIMING_MAX;
-  if (host_out && hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_bwd_timing), (size_t)n * 5 * 8) != hipSuccess) return 1;
-  if (reset) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_bwd_timing)) != hipSuccess) return 1;
-    if (hipMemset(p, 0, sizeof(g_bwd_timing)) != hipSuccess) return 1;
-    if (hipDeviceSynchronize() != hipSuccess) return 1;
-  }
-  return 0;
-}
-__device__ __forceinline__ unsigned long long bwd_stamp() {
-  __builtin_amdgcn_sched_barrier(0);
-  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-__device__ __forceinline__ void bwd_timing_record(unsigned long long t0, uint32_t tile, uint32_t n_eff,
-                                                  uint32_t walked, uint32_t slots) {
-  const unsigned long long t1 = bwd_stamp();
-  if (threadIdx.x == 0 && blockIdx.x < BWD_TIMING_MAX) {
-    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-    unsigned long long* o = g_bwd_timing[blockIdx.x];
-    o[0] = t0;
-    o[1] = t1;
-    o[2] = ((unsigned long long)tile << 32) | n_eff;
-    o[3] = ((unsigned long long)xcc << 32) | hw;
-    o[4] = ((unsigned long long)walked << 32) | slots;
-  }
-}
-#define GS_BWD_T0() const unsigned long long t_start = bwd_stamp()
-#define GS_BWD_TREC(tile, n_eff, walked, slots) bwd_timing_record(t_start, tile, n_eff, walked, slots)
+#ifdef GS_TIMING
+// diagnostic build only (-DGS_TIMING, tools/bwd_timing.py): per persistent backward wave b
+// (blockIdx.x): start / end stamps, units walked, hw ids, entries walked / slots evaluated
+GS_TIMING_BUFFER(g_bwd_timing, gs_debug_bwd_timing)
+#define GS_BWD_T0() const unsigned long long t_start = timing_stamp()
+#define GS_BWD_TREC(units, walked, slots) timing_record(g_bwd_timing, t_start, units, 0u, walked, slots)
 #else
 #define GS_BWD_T0() (void)0
-#define GS_BWD_TREC(tile, n_eff, walked, slots) (void)0
+#define GS_BWD_TREC(units, walked, slots) (void)0
 #endif
-
-// culling-side evaluation of one entry for a lane's two pixels (independent of the pixel state)
-struct Eval {
-  float4 co;
-  float dx;
-  f2 dy, oG;
-  bool cA, cB;
-};
-template <bool EXACT>
-__device__ __forceinline__ Eval eval_pair(float4 xy, float4 co, float pfx, f2 pfy, uint32_t e, uint32_t lastA,
-                                          uint32_t lastB) {
-  Eval v;
-  v.co = co;
-  v.dx = xy.x - pfx;
-  v.dy = xy.y - pfy;
-  const f2 power = falloff_log2_pk(co, v.dx, v.dy);  // log2(e) * power (co: fall_coefs)
-  const f2 G = exp2_pk_m<EXACT>(power);
-  // two scalar multiplies: a packed one would first copy the opacity into a register pair
-  v.oG.x = co.w * G.x;
-  v.oG.y = co.w * G.y;
-  // fast mode drops upstream's `power > 0` skip exactly as the forward does (k_render_fwd).
-  // alpha = min(0.99, o G) >= 1/255 is tested as o G >= 1/255 (the same decision: 0.99 > 1/255);
-  // the clamp itself is applied by the commit, to the contributors only
-  v.cA = e < lastA && (!EXACT || power.x <= 0.0f) && v.oG.x >= 1.0f / 255.0f;
-  v.cB = e < lastB && (!EXACT || power.y <= 0.0f) && v.oG.y >= 1.0f / 255.0f;
-  return v;
-}
 
 // a 36-B gradient record as three 12-B stores (global_store_dwordx3; 4-B alignment is enough)
 struct __attribute__((aligned(4))) Rec3 {
@@ -118,396 +43,38 @@ __device__ __forceinline__ void load_rec(const float* p, float* v) {
   v[0] = a.a, v[1] = a.b, v[2] = a.c, v[3] = b.a, v[4] = b.b, v[5] = b.c, v[6] = c.a, v[7] = c.b, v[8] = c.c;
 }
 
-constexpr int BWD_THREADS = 128;  // 2 wave64 per tile; each lane owns pixels (x, y) and (x, y + 8)
-#ifndef GS_BWD_BATCH
-#define GS_BWD_BATCH 64
-#endif
-#ifndef GS_BWD_ILP
-#define GS_BWD_ILP 1
-#endif
-#ifndef GS_PBWD_REG
-#define GS_PBWD_REG 1  // 0: the LDS-staged SH rows variant (113 vs 109.5 us at C3)
-#endif
-#ifndef GS_BWD_PREFETCH
-#define GS_BWD_PREFETCH 1
-#endif
-#ifndef GS_BWD_ABLATE
-#define GS_BWD_ABLATE 0  // timing-only builds (wrong gradients): 1 no wave reduction, 2 no commit, 3 no walk
-#endif
-#ifndef GS_BWD_HALFROW
-#define GS_BWD_HALFROW 1  // 0: row sums (4 DPP steps) with one writer lane per row
-#endif
-// LDS row of one per-wave partial record: s0..7 + the partials of s8 (8 half-row or 4 row ones)
-constexpr int ACC_STRIDE = GS_BWD_HALFROW ? 16 : 12;
-#ifndef GS_BWD_MINW
-#define GS_BWD_MINW 1
-#endif
-constexpr int BWD_BATCH = GS_BWD_BATCH;  // entries staged per round (64: 9 KB LDS/block -> 8 waves/SIMD)
-constexpr int BWD_GROUPS = BWD_BATCH / 64;
-constexpr int BWD_STAGE_ROUNDS = (BWD_BATCH + BWD_THREADS - 1) / BWD_THREADS;
-static_assert(BWD_BATCH % 64 == 0, "batch must be whole waves");
-
-// Tile backward.  Wave w covers the 8x16 half [x0 + 8w, +8) x [y0, +16) of the tile; a lane holds
-// two vertically adjacent pixels so every per-pixel quantity is a 2-vector (v_pk_*_f32).  The
-// per-entry gradient terms of the two pixels are pre-summed in the lane, summed over the wave
-// (wave_sum9_rows) and stored into the wave's LDS record by one lane per row.
-template <bool EXACT>
-__global__ __launch_bounds__(BWD_THREADS, GS_BWD_MINW) GS_WPE_ATTR(GS_BWD_WPE) void k_render_bwd(CameraArgs c, const uint2* __restrict__ ranges,
-                                                            const uint32_t* __restrict__ point_list,
-                                                            // GS_SORT_GID: ids by list position, else by slot
-                                                            const uint32_t* __restrict__ point_gid,
-                                                            const float4* __restrict__ splat,
-                                                            const float4* __restrict__ inst_splat,
-                                                            const float* __restrict__ final_T,
-                                                            const uint32_t* __restrict__ n_contrib,
-                                                            const uint32_t* __restrict__ tile_max,
-                                                            const uint32_t* __restrict__ tile_order,
-                                                            const float* __restrict__ dL_dpix,
-                                                            float* __restrict__ gradrec) {
-  // entry j: three 16-B records at one LDS byte offset 16 j (one address register per entry):
-  //   (x, y, r, g) | falloff coefficients + opacity (fall_coefs) | (b, -, -, -)
-  __shared__ float4 s_ent[3 * BWD_BATCH];
-  __shared__ float4 s_cr[BWD_BATCH];  // raw conic (xx, xy, yy) for the record mapping
-  __shared__ uint32_t s_slot[BWD_BATCH];
-  __shared__ uint64_t s_mask[BWD_GROUPS][2];  // [64-entry group][half]
-  __shared__ float s_acc[2][BWD_BATCH][ACC_STRIDE];
-  const uint32_t tile = tile_order ? tile_order[blockIdx.x] : blockIdx.x;
-  if (tile == ~0u) return;  // a hole of the XCD-group launch order (uniform, before any barrier)
-  const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int px = tx * GS_TILE + 8 * wid + (lane & 7);
-  const int pyA = ty * GS_TILE + (lane >> 3), pyB = pyA + 8;
-  const bool inA = px < c.W && pyA < c.H, inB = px < c.W && pyB < c.H;
-  const float pfx = (float)px;
-  const f2 pfy = {(float)pyA, (float)pyB};
-  const uint2 range = ranges[tile];
-  const uint32_t n = range.y - range.x;
-  const uint4 qm = reinterpret_cast<const uint4*>(tile_max)[tile];  // per-quadrant largest n_contrib
-  const uint32_t n_eff = min(max(max(qm.x, qm.y), max(qm.z, qm.w)), n);
-
-  const size_t HW = (size_t)c.W * c.H;
-  const size_t pixA = inA ? (size_t)pyA * c.W + px : 0, pixB = inB ? (size_t)pyB * c.W + px : 0;
-  const f2 T_final = {inA ? final_T[pixA] : 0.0f, inB ? final_T[pixB] : 0.0f};
-  f2 T = T_final;
-  const uint32_t lastA = inA ? n_contrib[pixA] : 0u, lastB = inB ? n_contrib[pixB] : 0u;
-  const f2 dp0 = {inA ? dL_dpix[pixA] : 0.0f, inB ? dL_dpix[pixB] : 0.0f};
-  const f2 dp1 = {inA ? dL_dpix[HW + pixA] : 0.0f, inB ? dL_dpix[HW + pixB] : 0.0f};
-  const f2 dp2 = {inA ? dL_dpix[2 * HW + pixA] : 0.0f, inB ? dL_dpix[2 * HW + pixB] : 0.0f};
-  const f2 bg_dot = c.bg[0] * dp0 + c.bg[1] * dp1 + c.bg[2] * dp2;
-  // U = S + T_final bg . dL/dpix, S = sum over the entries behind the current one of
-  // (colour . dL/dpix) alpha T: the suffix the upstream carries as accum_rec / last_alpha
-  f2 U = T_final * bg_dot;
-  const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
-  const uint32_t wave_last = __builtin_amdgcn_readfirstlane(wave_max_u32(max(lastA, lastB)));
-
-  // this lane's row slot of entry 0's record, as an LDS (32-bit) pointer: the per-entry address
-  // is then one 32-bit add instead of a 64-bit multiply-add on a generic pointer
-  using lds_float = __attribute__((address_space(3))) float;
-#if GS_BWD_HALFROW
-  // writer lanes 16 r + 8 h: s[r + 4 h] at slot r + 4 h, their s8 partial at slot 8 + r + 4 h
-  lds_float* const acc_lane = (lds_float*)(&s_acc[wid][0][(lane >> 4) + 4 * ((lane >> 3) & 1)]);
-  const bool hi8 = (lane & 8) != 0;
-#else
-  lds_float* const acc_lane = (lds_float*)(&s_acc[wid][0][lane >> 4]);
-#endif
-  // gradient commit of entry j (walk order) for the lane's contributing pixels
-  auto apply = [&](uint32_t j, const Eval& v, const float4 xr) {
-    const float4 rgb = make_float4(xr.z, xr.w, s_ent[2 * BWD_BATCH + j].x, 0.0f);
-    const f2 dy = v.dy;
-    const float dx = v.dx;
-    const bool cA = v.cA, cB = v.cB;
-    // Reduced form of the upstream per-pair terms (same quantities, fewer ops per pixel):
-    //   s0..2 = sum alpha T dL/dpix_c;  q = dL/dG * G;  s3 = sum q dx, s4 = sum q dy;
-    //   s5 = sum q dx^2, s6 = sum q dx dy, s7 = sum q dy^2;  s8 = sum G dL/dalpha,
-    // summed over the lane's two pixels (same column: dx is shared).  A pixel that does not
-    // contribute gets dL/dalpha = alpha T = 0, which zeroes all of its terms.
-    // The flush maps the wave sums to the upstream record: dmean2D.x = -W/2 (cxx S3 + cxy S4),
-    // dmean2D.y = -H/2 (cyy S4 + cxy S3), dconic = -S5/2, -S6/2, -S7/2.
-    // dL/dalpha: upstream's accum_rec recurrence gives T_i accum_rec_i . dL/dpix = S_i / (1 - a_i)
-    // with S_i = sum_{j behind i} Cd_j a_j T_j, so dL/dalpha = T_i Cd_i - U / (1 - a_i) with
-    // U = S_i + T_final bg . dL/dpix, and U grows by Cd_i a_i T_i once entry i is done.
-    // A pixel that does not contribute is run as an o G = 0 (alpha = 0) entry: T and U then pass
-    // through unchanged bit for bit (1 / (1 - 0) = 1, fma(x, 0, U) = U), and its colour and
-    // q = o G dL/dalpha terms vanish (dL/dalpha is finite).
-    const f2 oGm = {cA ? v.oG.x : 0.0f, cB ? v.oG.y : 0.0f};
-    // min(0.99, o G) as a median with 0 (o G >= 0): v_med3 needs no NaN-canonicalising v_max
-    const f2 ae = {__builtin_amdgcn_fmed3f(oGm.x, 0.0f, 0.99f), __builtin_amdgcn_fmed3f(oGm.y, 0.0f, 0.99f)};
-    const f2 omA = 1.f - ae;
-    f2 inv = {__builtin_amdgcn_rcpf(omA.x), __builtin_amdgcn_rcpf(omA.y)};
-    // exact mode: one Newton step (~0.5 ulp, like the IEEE divide).  Fast mode: the hardware
-    // reciprocal alone (<= 1 ulp; the T recovered over ~200 entries drifts ~1e-6 relative at
-    // most, and 1 / (1 - 0) = 1 exactly, so non-contributing pixels still pass T through)
-    if constexpr (EXACT) inv = pk_fma(inv, pk_fma(-omA, inv, (f2)(1.0f)), inv);
-    const f2 Tn = T * inv;
-    const f2 dch = ae * Tn;
-    const f2 Cd = pk_fma((f2)(rgb.z), dp2, pk_fma((f2)(rgb.y), dp1, rgb.x * dp0));
-    const f2 dLa = pk_fma(Tn, Cd, -(U * inv));
-    const f2 q = oGm * dLa;  // dL/dG G = o G dL/dalpha (not gated by the 0.99 clamp)
-    const f2 w4 = q * dy;
-    float s[GRAD_REC];
-    s[0] = __builtin_fmaf(dch.x, dp0.x, dch.y * dp0.y);
-    s[1] = __builtin_fmaf(dch.x, dp1.x, dch.y * dp1.y);
-    s[2] = __builtin_fmaf(dch.x, dp2.x, dch.y * dp2.y);
-    s[8] = q.x + q.y;  // sum_px o G dL/dalpha: dL/dopacity = S8 / o at the flush
-    s[3] = dx * s[8];
-    s[4] = w4.x + w4.y;
-    s[5] = dx * s[3];
-    s[6] = dx * s[4];
-    s[7] = __builtin_fmaf(w4.x, dy.x, w4.y * dy.y);
-    T = Tn;
-    U = pk_fma(Cd, dch, U);
-#if GS_BWD_ABLATE == 1  // timing only: no wave reduction
-    float d = s[(lane >> 3) & 7], d8 = s[8];
-    asm volatile("" ::"v"(d), "v"(d8));
-    if ((lane & 7) == 0) {
-      uint32_t eo = j * ACC_STRIDE;
-      asm volatile("" : "+s"(eo));
-      lds_float* acc = acc_lane + eo;
-      acc[0] = d;
-      acc[8] = d8;
-    }
-#elif GS_BWD_HALFROW
-    float d, d8;
-    wave_sum9_halfrows(s, hi8, d, d8);
-    asm volatile("" ::"v"(d), "v"(d8));
-    if ((lane & 7) == 0) {
-      uint32_t eo = j * ACC_STRIDE;
-      asm volatile("" : "+s"(eo));
-      lds_float* acc = acc_lane + eo;
-      acc[0] = d;
-      acc[8] = d8;
-    }
-#else
-    // wave sums: row r of d0 / d1 holds s[r] / s[4 + r]; every row of d8 a quarter of s[8]
-    float d0, d1, d8;
-    wave_sum9_rows(s, d0, d1, d8);
-    // materialise the sums with EXEC full: keeps the last DPP add out of the store branch, where
-    // it could not fold into v_add_f32_dpp
-    asm volatile("" ::"v"(d0), "v"(d1), "v"(d8));
-    if ((lane & 15) == 0) {
-      // scalar entry offset, kept out of a 64-bit multiply-add (the asm pins it in an SGPR)
-      uint32_t eo = j * ACC_STRIDE;
-      asm volatile("" : "+s"(eo));
-      lds_float* acc = acc_lane + eo;
-      acc[0] = d0;
-      acc[4] = d1;
-      acc[8] = d8;
-    }
-#endif
-  };
-
-#if GS_BWD_PREFETCH
-  // staging pipeline (wave 0 stages, one entry per lane): while batch k is walked, the splat
-  // records of batch k + 1, the ids of batch k + 2 and (ids by slot) the slots of batch k + 3
-  // are in flight; the walk issues no global loads, so they overlap it.  Batch k's entry of
-  // lane t sits at list position range.x + e0 - 64 k, e0 = n_eff - 1 - t.
-  static_assert(BWD_BATCH == 64, "prefetch: one staged entry per lane of wave 0");
-  const int32_t e0 = (int32_t)n_eff - 1 - tid;  // (a tile list holds < 2^31 entries)
-  const uint32_t* const plist = point_list + range.x;
-  uint32_t slot_c = 0, S1 = 0, G1 = 0, S2 = 0;
-  float4 pa, pb, pd;
-#if GS_INST_REC
-  // the forward's per-instance records, read by list position (contiguous; no id gathers)
-  const float4* const rec = inst_splat + 3 * (size_t)range.x;
-  if (tid < 64 && e0 >= 0) {
-    slot_c = plist[e0];
-    pa = rec[3 * e0], pb = rec[3 * e0 + 1], pd = rec[3 * e0 + 2];
-  }
-  (void)S1, (void)G1, (void)S2, (void)point_gid, (void)splat;
-#else
-  if (tid < 64) {
-    if (e0 >= 0) {
-      slot_c = plist[e0];
-      const uint32_t g0 = GS_SORT_GID ? point_gid[range.x + e0] : point_gid[slot_c];
-      pa = splat[3 * g0], pb = splat[3 * g0 + 1], pd = splat[3 * g0 + 2];
-    }
-    if (e0 - 64 >= 0) {
-      S1 = plist[e0 - 64];
-      G1 = GS_SORT_GID ? point_gid[range.x + e0 - 64] : point_gid[S1];
-    }
-    if (!GS_SORT_GID && e0 - 128 >= 0) S2 = plist[e0 - 128];
-  }
-#endif
-#endif
-  for (uint32_t base = 0; base < n_eff; base += BWD_BATCH) {
-    const uint32_t cnt = min((uint32_t)BWD_BATCH, n_eff - base);
-    lds_barrier();
-#if GS_BWD_PREFETCH
-    if (tid < 64) {
-      uint32_t hm = 0;
-      const int t = tid;
-      if ((uint32_t)t < cnt) {
-        const uint32_t slot = slot_c;
-        const float4 a = pa, b = pb, d = pd;
-        s_ent[t] = make_float4(a.x, a.y, b.z, b.w);
-        s_ent[BWD_BATCH + t] = fall_coefs(a.z, a.w, b.x, b.y);
-        s_ent[2 * BWD_BATCH + t] = make_float4(d.x, 0.0f, 0.0f, 0.0f);
-        s_cr[t] = make_float4(a.z, a.w, b.x, b.y);  // raw conic + opacity
-        s_slot[t] = slot;
-        hm = half_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
-      }
-      const int32_t e1 = e0 - (int32_t)(base + 64);
-#if GS_INST_REC
-      // issue the next batch's slot and record loads
-      if (e1 >= 0) {
-        slot_c = plist[e1];
-        pa = rec[3 * e1], pb = rec[3 * e1 + 1], pd = rec[3 * e1 + 2];
-      }
-#else
-      // issue the next batch's splat loads, the ids after it and (ids by slot) the slots after those
-      if (e1 >= 0) {
-        slot_c = S1;
-        pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
-      }
-      if (e1 - 64 >= 0) {
-        if (GS_SORT_GID) {
-          S1 = plist[e1 - 64];
-          G1 = point_gid[range.x + e1 - 64];
-        } else {
-          S1 = S2;
-          G1 = point_gid[S2];
-        }
-      }
-      if (!GS_SORT_GID && e1 - 128 >= 0) S2 = plist[e1 - 128];
-#endif
-      const uint64_t b0 = __ballot(hm & 1u), b1 = __ballot(hm & 2u);
-      if (lane == 0) {
-        s_mask[0][0] = b0;
-        s_mask[0][1] = b1;
-      }
-    }
-#else
-#pragma unroll
-    for (int h = 0; h < BWD_STAGE_ROUNDS; h++) {
-      const int t = tid + BWD_THREADS * h;
-      if (t >= BWD_BATCH) break;  // (wave-uniform)
-      uint32_t hm = 0;
-      if ((uint32_t)t < cnt) {
-        const uint32_t e = n_eff - 1 - (base + t);
-        const uint32_t slot = point_list[range.x + e];
-        const uint32_t gid = GS_SORT_GID ? point_gid[range.x + e] : point_gid[slot];
-        const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
-        s_ent[t] = make_float4(a.x, a.y, b.z, b.w);
-        s_ent[BWD_BATCH + t] = fall_coefs(a.z, a.w, b.x, b.y);
-        s_ent[2 * BWD_BATCH + t] = make_float4(d.x, 0.0f, 0.0f, 0.0f);
-        s_cr[t] = make_float4(a.z, a.w, b.x, b.y);  // raw conic + opacity
-        s_slot[t] = slot;
-        hm = half_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
-      }
-      const uint64_t b0 = __ballot(hm & 1u), b1 = __ballot(hm & 2u);
-      if (lane == 0) {
-        s_mask[t >> 6][0] = b0;
-        s_mask[t >> 6][1] = b1;
-      }
-    }
-#endif
-    {
-      float4* z4 = reinterpret_cast<float4*>(&s_acc[wid][0][0]);
-#pragma unroll
-      for (int k = 0; k < (ACC_STRIDE * BWD_BATCH / 4 + 63) / 64; k++)
-        if (k * 64 + lane < ACC_STRIDE * BWD_BATCH / 4) z4[k * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    lds_barrier();
-#pragma unroll 1
-    for (int g = 0; g < BWD_GROUPS; g++) {
-      uint64_t m = uniform_u64(s_mask[g][wid]);
-#if GS_BWD_ABLATE == 3  // timing only: staging and flush, no walk
-      m = 0;
-#endif
-      // entries no pixel of this wave reaches (e >= wave_last) sit at the low bits: drop them
-      const int jmin = (int)n_eff - (int)wave_last - (int)base - g * 64;  // j - 64 g >= jmin
-      if (jmin > 0) m &= jmin >= 64 ? 0ull : ~((1ull << jmin) - 1ull);
-#if GS_BWD_ILP == 2
-      // two entries per trip: the two evaluations are independent (ILP); the commits stay in order
-      while (m) {
-        const uint32_t j0 = (uint32_t)(g * 64 + __builtin_ctzll(m));
-        m &= m - 1;
-        const bool has1 = m != 0;
-        const uint32_t j1 = has1 ? (uint32_t)(g * 64 + __builtin_ctzll(m)) : j0;
-        if (has1) m &= m - 1;
-        const float4 x0 = s_ent[j0], x1 = s_ent[j1];
-        const Eval v0 = eval_pair<EXACT>(x0, s_ent[BWD_BATCH + j0], pfx, pfy, n_eff - 1 - (base + j0), lastA, lastB);
-        Eval v1 = eval_pair<EXACT>(x1, s_ent[BWD_BATCH + j1], pfx, pfy, n_eff - 1 - (base + j1), lastA, lastB);
-        v1.cA = v1.cA && has1;
-        v1.cB = v1.cB && has1;
-        if (__ballot(v0.cA || v0.cB) != 0) apply(j0, v0, x0);
-        if (__ballot(v1.cA || v1.cB) != 0) apply(j1, v1, x1);
-      }
-#else
-      while (m) {
-        const uint32_t j = (uint32_t)(g * 64 + __builtin_ctzll(m));
-        m &= m - 1;
-        const float4 xr = s_ent[j];
-        const Eval v = eval_pair<EXACT>(xr, s_ent[BWD_BATCH + j], pfx, pfy, n_eff - 1 - (base + j), lastA, lastB);
-#ifdef GS_BWD_STATS
-        {
-          const uint64_t bm = __ballot(v.cA || v.cB);
-          const unsigned long long npix = __popcll(__ballot(v.cA)) + __popcll(__ballot(v.cB));
-          if (lane == 0) {
-            atomicAdd(&g_bwd_stats[__popcll(bm)], 1ull);
-            atomicAdd(&g_bwd_stats[65], 1ull);
-            atomicAdd(&g_bwd_stats[67], npix);
-          }
-        }
-#endif
-#if GS_BWD_ABLATE == 2  // timing only: evaluation and test, no commit
-        if (__ballot(v.cA || v.cB) != 0) asm volatile("" ::"v"(v.oG.x), "v"(v.oG.y));
-#else
-        if (__ballot(v.cA || v.cB) != 0) apply(j, v, xr);
-#endif
-      }
-#endif
-    }
-    lds_barrier();
-#pragma unroll
-    for (int h = 0; h < BWD_STAGE_ROUNDS; h++) {
-      const int t = tid + BWD_THREADS * h;
-      if (t < BWD_BATCH && (uint32_t)t < cnt) {
-        float S[GRAD_REC];
-#pragma unroll
-        for (int k = 0; k < 8; k++) S[k] = s_acc[0][t][k] + s_acc[1][t][k];
-        S[8] = 0.0f;
-#pragma unroll
-        for (int k = 8; k < ACC_STRIDE; k++) S[8] += s_acc[0][t][k] + s_acc[1][t][k];
-        const float4 co = s_cr[t];
-        Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)s_slot[t] * GRAD_REC);
-        r[0] = Rec3{S[0], S[1], S[2]};
-        r[1] = Rec3{-ddelx_dx * (co.x * S[3] + co.y * S[4]), -ddely_dy * (co.z * S[4] + co.y * S[3]), -0.5f * S[5]};
-        // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
-        r[2] = Rec3{-0.5f * S[6], -0.5f * S[7], S[8] != 0.0f ? S[8] / co.w : 0.0f};
-      }
-    }
-  }
-
-  // instances past the last contributor of every pixel have no record: k_sum_records skips them
-  // (tile_cut)
-
-}
-
 // ------------------------------------------------------------------------------------------
-// Tile-wave backward (round 4, the default): ONE wave64 per tile, four pixel slots per lane.
+// Segmented tile-wave backward (round 5): ONE wave64 per (tile, depth segment), four pixel slots
+// per lane, persistent waves taking segments from a device queue.
+//
+// Round 4's kernel ran one wave per tile.  Its per-wave stamps (tools/bwd_timing.py,
+// profiles/r05_bwd_timing_c3_v0.json) show what set its time: every SIMD held its 5 waves for the
+// first 60 % of the launch, then drained -- 8,160 tile waves of ~220 walked entries each are only
+// 1.6 generations of the 5,120 resident slots, so the last generation's waves (started at 58 % of
+// the span, each ~45 % of the span long) left the SIMDs 4,123 / 2,998 / 1,703 / 217 resident waves
+// in the last four tenths: ~25 % of the launch was drain.  Splitting each tile's list into depth
+// segments of SEG entries makes the units short and uniform, and a queue keeps every SIMD fed
+// until the last ~one segment.
+//
+// A segment [lo, hi) of a tile is walked back to front like the whole list was: it needs each
+// pixel's state at hi -- the transmittance T_hi and U_hi = sum over the entries behind hi of
+// (colour . dL/dpix) alpha T + T_final bg . dL/dpix.  The forward's quadrant waves store (T, C) at
+// every segment boundary they reach (ckpt, C = the colour composited so far); with C_fin the
+// pixel's final colour (fin), U_hi = dL/dpix . (C_fin - C_hi) + T_final bg . dL/dpix.  A quadrant
+// whose pixels all stopped before hi (hi >= its largest n_contrib) starts from the final state, as
+// the whole-list walk did.  The per-entry arithmetic is unchanged; the start states are the
+// forward's own T (not recovered by division across the segments behind), so the gradients differ
+// from round 4's in rounding only.
 //
 // Lane l owns pixel (l & 7, l >> 3) of each 8x8 quadrant k of the tile (slot k).  A staged entry
 // carries the set of quadrants its alpha >= 1/255 ellipse meets (the forward's per-quadrant cull)
-// and the walk evaluates and commits only those slots: the C3 oracle study
-// (tools/bwd_layout_stats.py, profiles/r04_bwd_layout_stats_c3.txt) puts the pixel slots
-// evaluated per walked entry at 143 (quadrant slots) against 193 for the two 8x16 half waves of
-// k_render_bwd, and the nine per-entry sums are reduced over the wave ONCE per tile entry (0.86
-// reductions per walked entry instead of 1.36).  The lane's slots are pre-summed in registers
-// (one FMA per term and slot).  One wave per workgroup: staging, walk and flush need no workgroup
-// barrier, and every lane stages (and later flushes) one entry of a 64-entry batch, keeping that
-// entry's raw conic, opacity and slot in its registers.
-// Same per-pixel recurrence and decisions as k_render_bwd (and as the forward); only the order in
-// which a tile entry's per-pixel terms are summed differs.
+// and the walk evaluates and commits only those slots (143 pixel slots per walked entry at C3
+// against 193 for two 8x16 half waves, tools/bwd_layout_stats.py), and the nine per-entry sums are
+// reduced over the wave ONCE per tile entry.  The lane's slots are pre-summed in registers (one FMA
+// per term and slot).  One wave per workgroup: staging, walk and flush need no workgroup barrier,
+// and every lane stages (and later flushes) one entry of a 64-entry batch, keeping that entry's raw
+// conic, opacity and slot in its registers.
 // ------------------------------------------------------------------------------------------
-#ifndef GS_BWD_TW
-#define GS_BWD_TW 1
-#endif
-#ifndef GS_BWDT_MINW
-#define GS_BWDT_MINW 1
-#endif
-
 struct BwdSlot {
   float T, U, d0, d1, d2;
   uint32_t last;
@@ -539,7 +106,7 @@ __device__ __forceinline__ uint64_t bwd_slot(BwdSlot& q, float pfx, float pfy, c
   // box (u = dx - (mean - r) = r - pixel): for a splat centred in the tile u is dx itself, for one
   // centred outside it |u| <= 15 instead of the distance to the mean -- the terms stay small, so
   // the fp32 sums keep the precision the covariance chain needs.  The flush shifts them to the
-  // mean in fp64 (k_render_bwd_tw).
+  // mean in fp64 (k_render_bwd_seg).
   const float mx = dx - br.y, my = dy - br.z;
   const float qx = qq * mx, qy = qq * my;
   s[0] = __builtin_fmaf(dch, q.d0, s[0]);
@@ -560,89 +127,259 @@ __device__ __forceinline__ uint64_t bwd_slot(BwdSlot& q, float pfx, float pfy, c
   return m;
 }
 
-#ifndef GS_BWDT_ROW
-#define GS_BWDT_ROW 16
-#endif
+struct SegArgs {
+  const float4* fin;        // per pixel (C0, C1, C2, T_final)
+  const float4* ckpt;       // segment-boundary states (bin_layout: ckpt)
+  const uint2* table;       // per XCD group, cap (tile, segment) units: full segments from the front,
+  uint32_t cap;             //   partial ones from the back
+  uint32_t* sched;          // SCHED_* words (image buffer); the take counters are zeroed by k_tile_cut
+};
+
 template <bool EXACT>
-__global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c, const uint2* __restrict__ ranges,
-                                                                    const uint32_t* __restrict__ point_list,
-                                                                    const uint32_t* __restrict__ point_gid,
-                                                                    const float4* __restrict__ splat,
-                                                                    const float* __restrict__ final_T,
-                                                                    const uint32_t* __restrict__ n_contrib,
-                                                                    const uint32_t* __restrict__ tile_max,
-                                                                    const uint32_t* __restrict__ tile_order,
-                                                                    const float* __restrict__ dL_dpix,
-                                                                    float* __restrict__ gradrec) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_render_bwd_seg(CameraArgs c, const uint2* __restrict__ ranges,
+                                                       const uint32_t* __restrict__ point_list,
+                                                       const uint32_t* __restrict__ point_gid,
+                                                       const float4* __restrict__ splat,
+                                                       const uint32_t* __restrict__ n_contrib,
+                                                       const uint32_t* __restrict__ tile_max, SegArgs sa,
+                                                       const float* __restrict__ dL_dpix,
+                                                       float* __restrict__ gradrec) {
   __shared__ float4 s_xy[64];  // (x, y, r, g)
   __shared__ float4 s_co[64];  // falloff coefficients + opacity (fall_coefs)
   __shared__ float4 s_br[64];  // (b, mean - r: x, y, -), r the moments' reference point (bwd_slot)
   // entry rows of 16 floats (a stride of 20, which puts the flush's 16-B row reads on distinct
-  // banks, measured 343 -> 361 us at C3)
-  constexpr int ROW = GS_BWDT_ROW;
+  // banks, measured 343 -> 361 us at C3 in round 4)
+  constexpr int ROW = 16;
   __shared__ __attribute__((aligned(16))) float s_acc[64][ROW];
   GS_BWD_T0();
-  const uint32_t tile = __builtin_amdgcn_readfirstlane(tile_order ? tile_order[blockIdx.x] : blockIdx.x);
-  if (tile == ~0u) return;  // a hole of the XCD-group launch order
-  const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int lane = threadIdx.x;
-  const uint2 range = ranges[tile];
-  const uint32_t n = range.y - range.x;
-  // per-quadrant largest n_contrib (the forward's quadrant waves): slot k's walk ends there
-  const uint4 qm = reinterpret_cast<const uint4*>(tile_max)[tile];
-  const uint32_t qlast[4] = {min(qm.x, n), min(qm.y, n), min(qm.z, n), min(qm.w, n)};
-  const uint32_t n_eff = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
-  if (n_eff == 0) {
-    GS_BWD_TREC(tile, 0u, 0u, 0u);
-    return;  // no instance walked: no records (k_sum_records reads none below a cut of 0)
-  }
-#ifdef GS_BWD_TIMING
-  uint32_t t_walked = 0, t_slots = 0;
+  // Units are queued per XCD group (the tiles whose forward ran on XCD g): a wave takes its own
+  // XCD's units first (their splat records were fetched into this XCD's L2 by neighbouring tiles),
+  // then helps the other groups in turn.  Which XCD runs a wave only affects where a unit is
+  // walked, never its result.
+  uint32_t grp = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
+  uint32_t tried = 1;
+  auto group_total = [&](uint32_t g, uint32_t& nfront) {
+    nfront = __builtin_amdgcn_readfirstlane(sa.sched[SCHED_FRONT + SCHED_STRIDE * g]);
+    return nfront + __builtin_amdgcn_readfirstlane(sa.sched[SCHED_BACK + SCHED_STRIDE * g]);
+  };
+  auto take_unit = [&](uint32_t g) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(&sa.sched[SCHED_NEXT + SCHED_STRIDE * g], 1u);
+    return t;
+  };
+  uint32_t nfront, total = group_total(grp, nfront);
+  uint32_t s_cur = __builtin_amdgcn_readfirstlane(take_unit(grp));
+#ifdef GS_TIMING
+  uint32_t t_walked = 0, t_slots = 0, t_segs = 0;
 #endif
-
   const size_t HW = (size_t)c.W * c.H;
-  const int qx0 = tx * GS_TILE + (lane & 7), qy0 = ty * GS_TILE + (lane >> 3);
-  BwdSlot p[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int px = qx0 + 8 * (k & 1), py = qy0 + 8 * (k >> 1);
-    const bool in = px < c.W && py < c.H;
-    const size_t pix = in ? (size_t)py * c.W + px : 0;
-    const float Tf = in ? final_T[pix] : 0.0f;
-    p[k].T = Tf;
-    p[k].last = in ? n_contrib[pix] : 0u;
-    p[k].d0 = in ? dL_dpix[pix] : 0.0f;
-    p[k].d1 = in ? dL_dpix[HW + pix] : 0.0f;
-    p[k].d2 = in ? dL_dpix[2 * HW + pix] : 0.0f;
-    // U = S + T_final bg . dL/dpix (see k_render_bwd)
-    p[k].U = Tf * (c.bg[0] * p[k].d0 + c.bg[1] * p[k].d1 + c.bg[2] * p[k].d2);
-  }
   const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
-  const float pfx0 = (float)qx0, pfy0 = (float)qy0;
+  // the background in scalar registers (loop-invariant vector registers would cost the walk's budget)
+  const float bgd[3] = {__uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(c.bg[0]))),
+                        __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(c.bg[1]))),
+                        __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(c.bg[2])))};
   using lds_float = __attribute__((address_space(3))) float;
   // writer lanes 16 r + 8 h: s[r + 4 h] at slot r + 4 h, their s8 partial at slot 8 + r + 4 h
   lds_float* const acc_lane = (lds_float*)(&s_acc[0][(lane >> 4) + 4 * ((lane >> 3) & 1)]);
   const bool hi8 = (lane & 8) != 0;
+  // lanes holding a mapped record in their LDS row (the last flushed batch, possibly of the previous
+  // unit: its stores go out behind the next batch's loads, as within a unit)
+  uint32_t rec_lanes = 0;
+  // every wave leaves once every group's queue is empty (the counters only grow)
+  for (;;) {
+    if (s_cur >= total) {
+      if (tried == ORDER_GROUPS) break;
+      tried++;
+      grp = (grp + 1u) & 7u;
+      total = group_total(grp, nfront);
+      s_cur = __builtin_amdgcn_readfirstlane(take_unit(grp));
+      continue;
+    }
+    const uint2 unit = sa.table[(size_t)grp * sa.cap + (s_cur < nfront ? s_cur : sa.cap - 1u - (s_cur - nfront))];
+    const uint32_t tile = __builtin_amdgcn_readfirstlane(unit.x), seg = __builtin_amdgcn_readfirstlane(unit.y);
+    const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
+    const uint2 range = ranges[tile];
+    const uint32_t n = range.y - range.x;
+    // per-quadrant largest n_contrib (the forward's quadrant waves): slot k's walk ends there
+    const uint4 qm = reinterpret_cast<const uint4*>(tile_max)[tile];
+    const uint32_t qlast[4] = {min(qm.x, n), min(qm.y, n), min(qm.z, n), min(qm.w, n)};
+    const uint32_t n_eff = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
+    const uint32_t lo = SEG * seg, hi = min(lo + SEG, n_eff);  // this unit's list positions [lo, hi)
+    // the states at hi (read for every slot, used where the quadrant's walk goes on behind hi; the
+    // unit that ends at n_eff reads the array's first states instead, unused)
+    const float4* const ck = sa.ckpt + (hi < n_eff ? ((size_t)(range.x / SEG + hi / SEG) << 8) : 0);
+    const int qx0 = tx * GS_TILE + (lane & 7), qy0 = ty * GS_TILE + (lane >> 3);
+    BwdSlot p[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int px = qx0 + 8 * (k & 1), py = qy0 + 8 * (k >> 1);
+      const bool in = px < c.W && py < c.H;
+      const size_t pix = in ? (size_t)py * c.W + px : 0;
+      const float4 f = in ? sa.fin[pix] : make_float4(0.f, 0.f, 0.f, 0.f);
+      p[k].last = in ? n_contrib[pix] : 0u;
+      p[k].d0 = in ? dL_dpix[pix] : 0.0f;
+      p[k].d1 = in ? dL_dpix[HW + pix] : 0.0f;
+      p[k].d2 = in ? dL_dpix[2 * HW + pix] : 0.0f;
+      // U = S + T_final bg . dL/dpix (S: the (colour . dL/dpix) alpha T of the entries behind)
+      const float ub = f.w * (bgd[0] * p[k].d0 + bgd[1] * p[k].d1 + bgd[2] * p[k].d2);
+      // the quadrant's walk goes on behind hi: the forward's state there (uniform select; the load is
+      // unconditional so the unit's loads are all in flight at once)
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      const v4f tv = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(ck + 64 * k + lane));
+      const float4 t = make_float4(tv.x, tv.y, tv.z, tv.w);
+      const bool behind = hi < qlast[k];
+      p[k].T = behind ? t.x : f.w;
+      p[k].U = behind ? __builtin_fmaf(p[k].d2, f.z - t.w, __builtin_fmaf(p[k].d1, f.y - t.z, p[k].d0 * (f.x - t.y))) + ub
+                      : ub;
+    }
+    const float pfx0 = (float)qx0, pfy0 = (float)qy0;
 
-  // staging pipeline (one entry per lane): while batch k is walked, the splat records of batch
-  // k + 1, the ids of batch k + 2 and (ids by slot) the slots of batch k + 3 are in flight.
-  // Batch k's entry of lane t sits at list position range.x + e0 - 64 k, e0 = n_eff - 1 - t.
-  // The loads are unconditional, with list positions below 0 clamped to 0 (a valid entry: the
-  // lane stages nothing then): a load under a condition has to keep the register's old value on
-  // the other path, and the copy that merges the two makes the compiler wait for the load right
-  // where it is issued instead of at the next batch.
-  const int32_t e0 = (int32_t)n_eff - 1 - lane;
-  const uint32_t* const plist = point_list + range.x;
-  auto pos = [&](int32_t e) { return (uint32_t)max(e, 0); };
-  uint32_t slot_c = plist[pos(e0)];
-  uint32_t G1 = GS_SORT_GID ? point_gid[range.x + pos(e0)] : point_gid[slot_c];
-  float4 pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
-  uint32_t S1 = plist[pos(e0 - 64)];
-  G1 = GS_SORT_GID ? point_gid[range.x + pos(e0 - 64)] : point_gid[S1];
-  uint32_t S2 = GS_SORT_GID ? 0u : plist[pos(e0 - 128)];
+    // staging pipeline (one entry per lane): while batch b is walked, the splat records of batch
+    // b + 1, the ids of batch b + 2 and the slots of batch b + 3 are in flight.  Batch b's entry of
+    // lane t sits at list position e0 - 64 b, e0 = hi - 1 - t.  The loads are unconditional, with
+    // positions below lo clamped to lo (a valid entry of this unit: a cache hit, no traffic): a
+    // load under a condition has to keep the register's old value on the other path, and the copy
+    // that merges the two makes the compiler wait for the load right where it is issued.
+    const int32_t e0 = (int32_t)hi - 1 - lane;
+    const uint32_t* const plist = point_list + range.x;
+    auto pos = [&](int32_t e) { return (uint32_t)max(e, (int32_t)lo); };
+    uint32_t slot_c = plist[pos(e0)];
+    uint32_t G1 = point_gid[slot_c];
+    float4 pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
+    uint32_t S1 = plist[pos(e0 - 64)];
+    G1 = point_gid[S1];
+    uint32_t S2 = plist[pos(e0 - 128)];
 
-  uint32_t rec_lanes = 0;  // lanes holding a mapped record in their LDS row (the last flushed batch)
-  auto store_records = [&]() {
+    auto store_records = [&]() {
+      if ((uint32_t)lane < rec_lanes) {
+        const float4* row = reinterpret_cast<const float4*>(&s_acc[lane][0]);
+        const float4 a = row[0], b = row[1], d = row[2];
+        Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)__float_as_uint(d.y) * GRAD_REC);
+        r[0] = Rec3{a.x, a.y, a.z};
+        r[1] = Rec3{a.w, b.x, b.y};
+        r[2] = Rec3{b.z, b.w, d.x};
+      }
+    };
+    const uint32_t len = hi - lo;
+    for (uint32_t base = 0; base < len; base += 64) {
+      const uint32_t cnt = min(64u, len - base);
+      // stage: lane t holds entry t of the batch (walk order: back to front)
+      const bool mine = (uint32_t)lane < cnt;
+      const uint32_t slot = slot_c;
+      const float ccx = pa.z, ccy = pa.w, ccz = pb.x, cop = pb.y;  // raw conic + opacity (flush)
+      uint32_t qmask = 0;
+      if (mine) {
+        s_xy[lane] = make_float4(pa.x, pa.y, pb.z, pb.w);
+        s_co[lane] = fall_coefs(pa.z, pa.w, pb.x, pb.y);
+        const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
+        s_br[lane] = make_float4(pd.x, pa.x - fminf(fmaxf(pa.x, x0), x0 + 15.0f),
+                                 pa.y - fminf(fmaxf(pa.y, y0), y0 + 15.0f), 0.0f);
+        qmask = quadrant_mask(pa.x, pa.y, pa.z, pa.w, pb.x, pd.z, tx, ty);
+      }
+      // issue the next batch's splat loads, the ids after it and the slots after those
+      const int32_t e1 = e0 - (int32_t)(base + 64);
+      slot_c = S1;
+      pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
+      S1 = S2;
+      G1 = point_gid[S2];
+      S2 = plist[pos(e1 - 128)];
+      // the previous batch's records (mapped by its flush into the lanes' LDS rows, slot in word 9):
+      // stored now, behind this batch's loads, so that the wait for those loads at the next staging
+      // does not also wait for just-issued stores (loads and stores share one counter)
+      store_records();
+      // per-slot entry sets; entries no pixel of quadrant k reaches (e >= qlast[k]) sit at the low bits
+      uint64_t M[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint64_t mk = __ballot((qmask >> k) & 1u);
+        const int jmin = (int)hi - (int)qlast[k] - (int)base;  // entry j reaches quadrant k iff j >= jmin
+        if (jmin > 0) mk &= jmin >= 64 ? 0ull : ~((1ull << jmin) - 1ull);
+        M[k] = mk;
+      }
+      __builtin_amdgcn_wave_barrier();
+      uint64_t m = (M[0] | M[1]) | (M[2] | M[3]);
+      uint64_t wrote = 0;
+#pragma unroll 1
+      while (m) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const float4 xr = s_xy[j], co = s_co[j], br = s_br[j];
+        const uint32_t e = hi - 1 - (base + j);
+        float s[GRAD_REC];
+#pragma unroll
+        for (int t = 0; t < GRAD_REC; t++) s[t] = 0.0f;
+#ifdef GS_TIMING
+        t_walked++;
+        t_slots += ((M[0] >> j) & 1ull) + ((M[1] >> j) & 1ull) + ((M[2] >> j) & 1ull) + ((M[3] >> j) & 1ull);
+#endif
+        uint64_t con = 0;  // lanes with a contributing slot
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if ((M[k] >> j) & 1ull)
+            con |= bwd_slot<EXACT>(p[k], pfx0 + (float)(8 * (k & 1)), pfy0 + (float)(8 * (k >> 1)), xr, co, br, e, s);
+        if (con != 0) {
+          wrote |= 1ull << j;
+          float d, d8;
+          wave_sum9_halfrows(s, hi8, d, d8);
+          asm volatile("" ::"v"(d), "v"(d8));
+          if ((lane & 7) == 0) {
+            uint32_t eo = j * ROW;
+            asm volatile("" : "+s"(eo));
+            lds_float* acc = acc_lane + eo;
+            acc[0] = d;
+            acc[8] = d8;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // flush: lane t maps the sums of its entry into the record (zeros for an entry no pixel took),
+      // written back into its LDS row with the slot; stored by the next batch (or after the loop)
+      if (mine) {
+        float S[GRAD_REC];
+        if ((wrote >> lane) & 1ull) {
+          const float4 a0 = *reinterpret_cast<const float4*>(&s_acc[lane][0]);
+          const float4 a1 = *reinterpret_cast<const float4*>(&s_acc[lane][4]);
+          const float4 a2 = *reinterpret_cast<const float4*>(&s_acc[lane][8]);
+          const float4 a3 = *reinterpret_cast<const float4*>(&s_acc[lane][12]);
+          S[0] = a0.x, S[1] = a0.y, S[2] = a0.z, S[3] = a0.w, S[4] = a1.x, S[5] = a1.y, S[6] = a1.z, S[7] = a1.w;
+          S[8] = ((a2.x + a2.y) + (a2.z + a2.w)) + ((a3.x + a3.y) + (a3.z + a3.w));
+        } else {
+#pragma unroll
+          for (int t = 0; t < GRAD_REC; t++) S[t] = 0.0f;
+        }
+        // S3..S7 are the moments of q about the reference point r; with R = mean - r (dx = u + R):
+        // sum q dx = S3 + R.x S8, sum q dx^2 = S5 + 2 R.x S3 + R.x^2 S8, ... in fp64, one rounding to
+        // the record (R = 0, nothing to shift, for a splat centred in the tile)
+        const float2 R = *reinterpret_cast<const float2*>(&s_br[lane].y);
+        const double Rx = R.x, Ry = R.y, q0 = S[8];
+        const float m1x = (float)__builtin_fma(Rx, q0, (double)S[3]), m1y = (float)__builtin_fma(Ry, q0, (double)S[4]);
+        __builtin_amdgcn_sched_barrier(0);
+        const float m2xx = (float)__builtin_fma(Rx, __builtin_fma(Rx, q0, 2.0 * (double)S[3]), (double)S[5]);
+        __builtin_amdgcn_sched_barrier(0);
+        const float m2xy = (float)__builtin_fma(Rx, __builtin_fma(Ry, q0, (double)S[4]),
+                                                __builtin_fma(Ry, (double)S[3], (double)S[6]));
+        __builtin_amdgcn_sched_barrier(0);
+        const float m2yy = (float)__builtin_fma(Ry, __builtin_fma(Ry, q0, 2.0 * (double)S[4]), (double)S[7]);
+        __builtin_amdgcn_sched_barrier(0);
+        float4* row = reinterpret_cast<float4*>(&s_acc[lane][0]);
+        row[0] = make_float4(S[0], S[1], S[2], -ddelx_dx * (ccx * m1x + ccy * m1y));
+        row[1] = make_float4(-ddely_dy * (ccz * m1y + ccy * m1x), -0.5f * m2xx, -0.5f * m2xy, -0.5f * m2yy);
+        // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
+        row[2] = make_float4(S[8] != 0.0f ? S[8] / cop : 0.0f, __uint_as_float(slot), 0.0f, 0.0f);
+      }
+      rec_lanes = cnt;
+      __builtin_amdgcn_wave_barrier();  // the next batch overwrites the staged entries
+    }
+    // the next unit (a value held across the walk would cost a register: 96 VGPRs for 5 waves / SIMD)
+    const uint32_t take = take_unit(grp);
+#ifdef GS_TIMING
+    t_segs++;
+#endif
+    s_cur = __builtin_amdgcn_readfirstlane(take);
+  }
+  // the last unit's records
+  auto store_last = [&]() {
     if ((uint32_t)lane < rec_lanes) {
       const float4* row = reinterpret_cast<const float4*>(&s_acc[lane][0]);
       const float4 a = row[0], b = row[1], d = row[2];
@@ -652,148 +389,22 @@ __global__ __launch_bounds__(64, GS_BWDT_MINW) void k_render_bwd_tw(CameraArgs c
       r[2] = Rec3{b.z, b.w, d.x};
     }
   };
-  for (uint32_t base = 0; base < n_eff; base += 64) {
-    const uint32_t cnt = min(64u, n_eff - base);
-    // stage: lane t holds entry t of the batch (walk order: back to front)
-    const bool mine = (uint32_t)lane < cnt;
-    const uint32_t slot = slot_c;
-    const float ccx = pa.z, ccy = pa.w, ccz = pb.x, cop = pb.y;  // raw conic + opacity (flush)
-    uint32_t qmask = 0;
-    if (mine) {
-      s_xy[lane] = make_float4(pa.x, pa.y, pb.z, pb.w);
-      s_co[lane] = fall_coefs(pa.z, pa.w, pb.x, pb.y);
-      const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
-      s_br[lane] = make_float4(pd.x, pa.x - fminf(fmaxf(pa.x, x0), x0 + 15.0f),
-                               pa.y - fminf(fmaxf(pa.y, y0), y0 + 15.0f), 0.0f);
-      qmask = quadrant_mask(pa.x, pa.y, pa.z, pa.w, pb.x, pd.z, tx, ty);
-    }
-    // issue the next batch's splat loads, the ids after it and (ids by slot) the slots after those
-    const int32_t e1 = e0 - (int32_t)(base + 64);
-    slot_c = S1;
-    pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
-    if (GS_SORT_GID) {
-      S1 = plist[pos(e1 - 64)];
-      G1 = point_gid[range.x + pos(e1 - 64)];
-    } else {
-      S1 = S2;
-      G1 = point_gid[S2];
-      S2 = plist[pos(e1 - 128)];
-    }
-    // the previous batch's records (mapped by its flush into the lanes' LDS rows, slot in word 9):
-    // stored now, behind this batch's loads, so that the wait for those loads at the next staging
-    // does not also wait for just-issued stores (loads and stores share one counter)
-    if (base > 0) store_records();
-    // per-slot entry sets; entries no pixel of quadrant k reaches (e >= qlast[k]) sit at the low bits
-    uint64_t M[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      uint64_t mk = __ballot((qmask >> k) & 1u);
-      const int jmin = (int)n_eff - (int)qlast[k] - (int)base;  // entry j reaches quadrant k iff j >= jmin
-      if (jmin > 0) mk &= jmin >= 64 ? 0ull : ~((1ull << jmin) - 1ull);
-      M[k] = mk;
-    }
-    __builtin_amdgcn_wave_barrier();
-    uint64_t m = (M[0] | M[1]) | (M[2] | M[3]);
-    uint64_t wrote = 0;
-#pragma unroll 1
-    while (m) {
-      const uint32_t j = (uint32_t)__builtin_ctzll(m);
-      m &= m - 1;
-      const float4 xr = s_xy[j], co = s_co[j], br = s_br[j];
-      const uint32_t e = n_eff - 1 - (base + j);
-      float s[GRAD_REC];
-#pragma unroll
-      for (int t = 0; t < GRAD_REC; t++) s[t] = 0.0f;
-#ifdef GS_BWD_TIMING
-      t_walked++;
-      t_slots += ((M[0] >> j) & 1ull) + ((M[1] >> j) & 1ull) + ((M[2] >> j) & 1ull) + ((M[3] >> j) & 1ull);
-#endif
-      uint64_t con = 0;  // lanes with a contributing slot
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        if ((M[k] >> j) & 1ull)
-          con |= bwd_slot<EXACT>(p[k], pfx0 + (float)(8 * (k & 1)), pfy0 + (float)(8 * (k >> 1)), xr, co, br, e, s);
-      if (con != 0) {
-        wrote |= 1ull << j;
-        float d, d8;
-        wave_sum9_halfrows(s, hi8, d, d8);
-        asm volatile("" ::"v"(d), "v"(d8));
-        if ((lane & 7) == 0) {
-          uint32_t eo = j * ROW;
-          asm volatile("" : "+s"(eo));
-          lds_float* acc = acc_lane + eo;
-          acc[0] = d;
-          acc[8] = d8;
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    // flush: lane t maps the sums of its entry into the record (zeros for an entry no pixel took),
-    // written back into its LDS row with the slot; stored by the next batch (or after the loop)
-    if (mine) {
-      float S[GRAD_REC];
-      if ((wrote >> lane) & 1ull) {
-        const float4 a0 = *reinterpret_cast<const float4*>(&s_acc[lane][0]);
-        const float4 a1 = *reinterpret_cast<const float4*>(&s_acc[lane][4]);
-        const float4 a2 = *reinterpret_cast<const float4*>(&s_acc[lane][8]);
-        const float4 a3 = *reinterpret_cast<const float4*>(&s_acc[lane][12]);
-        S[0] = a0.x, S[1] = a0.y, S[2] = a0.z, S[3] = a0.w, S[4] = a1.x, S[5] = a1.y, S[6] = a1.z, S[7] = a1.w;
-        S[8] = ((a2.x + a2.y) + (a2.z + a2.w)) + ((a3.x + a3.y) + (a3.z + a3.w));
-      } else {
-#pragma unroll
-        for (int t = 0; t < GRAD_REC; t++) S[t] = 0.0f;
-      }
-      // S3..S7 are the moments of q about the reference point r; with R = mean - r (dx = u + R):
-      // sum q dx = S3 + R.x S8, sum q dx^2 = S5 + 2 R.x S3 + R.x^2 S8, ... in fp64, one rounding to
-      // the record (R = 0, nothing to shift, for a splat centred in the tile)
-      const float2 R = *reinterpret_cast<const float2*>(&s_br[lane].y);
-      const double Rx = R.x, Ry = R.y, q0 = S[8];
-      const float m1x = (float)__builtin_fma(Rx, q0, (double)S[3]), m1y = (float)__builtin_fma(Ry, q0, (double)S[4]);
-      __builtin_amdgcn_sched_barrier(0);
-      const float m2xx = (float)__builtin_fma(Rx, __builtin_fma(Rx, q0, 2.0 * (double)S[3]), (double)S[5]);
-      __builtin_amdgcn_sched_barrier(0);
-      const float m2xy = (float)__builtin_fma(Rx, __builtin_fma(Ry, q0, (double)S[4]),
-                                              __builtin_fma(Ry, (double)S[3], (double)S[6]));
-      __builtin_amdgcn_sched_barrier(0);
-      const float m2yy = (float)__builtin_fma(Ry, __builtin_fma(Ry, q0, 2.0 * (double)S[4]), (double)S[7]);
-      __builtin_amdgcn_sched_barrier(0);
-      float4* row = reinterpret_cast<float4*>(&s_acc[lane][0]);
-      row[0] = make_float4(S[0], S[1], S[2], -ddelx_dx * (ccx * m1x + ccy * m1y));
-      row[1] = make_float4(-ddely_dy * (ccz * m1y + ccy * m1x), -0.5f * m2xx, -0.5f * m2xy, -0.5f * m2yy);
-      // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
-      row[2] = make_float4(S[8] != 0.0f ? S[8] / cop : 0.0f, __uint_as_float(slot), 0.0f, 0.0f);
-    }
-    rec_lanes = cnt;
-    __builtin_amdgcn_wave_barrier();  // the next batch overwrites the staged entries
-  }
-  store_records();
-  GS_BWD_TREC(tile, n_eff, t_walked, t_slots);
+  store_last();
+  GS_BWD_TREC(t_segs, t_walked, t_slots);
 }
 
-// Longest-first launch order for the backward.  A tile's walk is as long as its largest
-// n_contrib (the forward's per-quadrant maxima), which varies ~10x across an image, and dense
-// tiles sit together: in index order the last workgroups to start include heavy ones and the
-// grid ends on a long tail.  The forward buckets every tile by that length and ranks it in its
-// bucket of its XCD group (tile_finish); here each thread places one tile at (bucket base + rank)
-// within the group's launch positions, so the heavy tiles start first and the tail is made of
-// light ones (list scheduling, LPT).  The order inside a bucket is arbitrary: a tile's outputs do
-// not depend on when it runs.
-constexpr int ORDER_THREADS = 256;
-// Also (always) each tile's record cut: records exist only for a tile's first n_eff instances
-// (those its walk reaches, n_eff = its largest n_contrib); tile_cut = 1 + the slot of the last
-// of them.  A tile's list is in slot order, so k_sum_records keeps a record of slot s in tile T
-// iff s < tile_cut[T] and the backward writes no zero records for the rest.
-__global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __restrict__ len_hist,
-                                                              const uint32_t* __restrict__ tile_brank, uint32_t gx,
-                                                              uint32_t gy, uint32_t* __restrict__ order,
-                                                              const uint32_t* __restrict__ tile_max,
-                                                              const uint2* __restrict__ ranges,
-                                                              const uint32_t* __restrict__ point_list,
-                                                              uint32_t* __restrict__ tile_cut,
-                                                              uint32_t* __restrict__ cut_max) {
-  __shared__ uint32_t s_base[ORDER_GROUPS][ORDER_BUCKETS];
-  const uint32_t tid = threadIdx.x, t = blockIdx.x * ORDER_THREADS + tid, lane = tid & 63, wid = tid >> 6;
-  const uint32_t tiles = gx * gy;
+// Per tile (before the backward): the record cut -- 1 + the slot of the tile's last walked
+// instance; records exist only for a tile's first n_eff instances (those its walk reaches, n_eff =
+// its largest n_contrib), and a tile's list is in slot order, so k_sum_records keeps a record of
+// slot s in tile T iff s < tile_cut[T] and the backward writes no zero records for the rest -- and
+// the largest cut.  Also resets the backward's unit queue (the forward built the units).
+constexpr int CUT_THREADS = 256;
+__global__ __launch_bounds__(CUT_THREADS) void k_tile_cut(uint32_t tiles, const uint32_t* __restrict__ tile_max,
+                                                          const uint2* __restrict__ ranges,
+                                                          const uint32_t* __restrict__ point_list,
+                                                          uint32_t* __restrict__ tile_cut, uint32_t* __restrict__ sched) {
+  const uint32_t t = blockIdx.x * CUT_THREADS + threadIdx.x;
+  if (t < ORDER_GROUPS) sched[SCHED_NEXT + SCHED_STRIDE * t] = 0u;
   uint32_t cut = 0;
   if (t < tiles) {
     const uint4 q = reinterpret_cast<const uint4*>(tile_max)[t];
@@ -802,58 +413,43 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __
     cut = n_eff ? point_list[r.x + n_eff - 1] + 1u : 0u;
     tile_cut[t] = cut;
   }
-  {
-    // the largest cut (all lanes take part in the wave max): k_sum_records stops there -- slots
-    // are in depth order, so past it no tile walked an instance
-    const uint32_t wm = wave_max_u32(cut);
-    if (lane == 0 && wm) atomicMax(cut_max, wm);
+  // the largest cut (all lanes take part in the wave max): k_sum_records stops there -- slots are in
+  // depth order, so past it no tile walked an instance
+  const uint32_t wm = wave_max_u32(cut);
+  if ((threadIdx.x & 63) == 0 && wm) atomicMax(&sched[SCHED_CUT_MAX], wm);
+}
+
+// resident 64-lane workgroups of the backward on this device (its persistent grid)
+template <bool EXACT>
+static uint32_t bwd_seg_waves() {
+  static uint32_t n[2][64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  uint32_t& w = n[EXACT ? 1 : 0][dev & 63];
+  if (w == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_render_bwd_seg<EXACT>, 64, 0) != hipSuccess ||
+        per_cu <= 0)
+      per_cu = 20;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    w = (uint32_t)per_cu * (uint32_t)cus;
   }
-  if (!order) return;  // (uniform)
-  const uint32_t br = t < tiles ? tile_brank[t] : 0u;
-  static_assert(ORDER_BUCKETS == 64 && ORDER_GROUPS == 2 * (ORDER_THREADS / 64), "two groups per wave");
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const uint32_t g = wid + h * (ORDER_THREADS / 64);
-    const uint32_t v = len_hist[g * ORDER_BUCKETS + lane];
-    s_base[g][lane] = wave_incl_scan(v) - v;
-  }
-  lds_barrier();
-  // the j-th tile of group g (longest first) takes launch position 8 j + g
-  if (t < tiles) {
-    const uint32_t g = xcd_group(t, gx, gy);
-    order[ORDER_GROUPS * (s_base[g][br >> 22] + (br & 0x3FFFFFu)) + g] = t;
-  }
-  // launch positions past the end of their group: holes (the backward skips them)
-  if (t < xcd_slots(tiles) && t / ORDER_GROUPS >= xcd_group_size(t % ORDER_GROUPS, tiles)) order[t] = ~0u;
+  return w;
 }
 
 void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                 const float* dL_dpix, float* gradrec, hipStream_t st) {
-  const int tiles = c.gx * c.gy;
-  uint32_t* order = img.tile_order;
-  const uint32_t slots = xcd_slots((uint32_t)tiles);
-  GS_LAUNCH("tile_order", k_tile_order, dim3((slots + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
-            img.len_hist, img.tile_brank, (uint32_t)c.gx, (uint32_t)c.gy, order, img.tile_max, img.ranges,
-            bin.point_list, img.tile_cut, img.cut_max);
-  if (GS_BWD_TW) {
-    if (exact_exp())
-      GS_LAUNCH("render_bwd", k_render_bwd_tw<true>, dim3(slots), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max,
-                order, dL_dpix, gradrec);
-    else
-      GS_LAUNCH("render_bwd", k_render_bwd_tw<false>, dim3(slots), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max,
-                order, dL_dpix, gradrec);
-    return;
-  }
+  (void)P;
+  const uint32_t tiles = (uint32_t)(c.gx * c.gy);
+  GS_LAUNCH("tile_cut", k_tile_cut, dim3((tiles + CUT_THREADS - 1) / CUT_THREADS), dim3(CUT_THREADS), 0, st, tiles,
+            img.tile_max, img.ranges, bin.point_list, img.tile_cut, img.sched);
+  const SegArgs sa{img.fin, bin.ckpt, bin.seg_table, bin.seg_cap, img.sched};
   if (exact_exp())
-    GS_LAUNCH("render_bwd", k_render_bwd<true>, dim3(slots), dim3(BWD_THREADS), 0, st, c, img.ranges,
-              bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, img.final_T, img.n_contrib, img.tile_max, order,
-              dL_dpix, gradrec);
+    GS_LAUNCH("render_bwd", k_render_bwd_seg<true>, dim3(bwd_seg_waves<true>()), dim3(64), 0, st, c, img.ranges,
+              bin.point_list, bin.presort_gid, geo.splat, img.n_contrib, img.tile_max, sa, dL_dpix, gradrec);
   else
-    GS_LAUNCH("render_bwd", k_render_bwd<false>, dim3(slots), dim3(BWD_THREADS), 0, st, c, img.ranges,
-              bin.point_list, GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, img.final_T, img.n_contrib, img.tile_max, order,
-              dL_dpix, gradrec);
+    GS_LAUNCH("render_bwd", k_render_bwd_seg<false>, dim3(bwd_seg_waves<false>()), dim3(64), 0, st, c, img.ranges,
+              bin.point_list, bin.presort_gid, geo.splat, img.n_contrib, img.tile_max, sa, dL_dpix, gradrec);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -867,13 +463,7 @@ void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& 
 // large splat's tile partials cancel, so the cross-tile sum is kept in fp64).  The total goes
 // back into the owner's first record.  Fixed order throughout: deterministic.
 // ------------------------------------------------------------------------------------------
-#ifndef GS_SUMREC_WAVES
-#define GS_SUMREC_WAVES 4
-#endif
-#ifndef GS_SUMREC_ABLATE
-#define GS_SUMREC_ABLATE 0  // timing-only builds (wrong sums): 1 no record loads, 2 no scan, 3 no cut test
-#endif
-constexpr int SUMREC_WAVES = GS_SUMREC_WAVES;
+constexpr int SUMREC_WAVES = 4;  // (2 or 8 measured within 2 us at C3)
 // one step of the segmented wave scan: v += (shifted v) when the shifted lane has the same owner
 // (owners are carried +1 so a lane without a source (0) never matches)
 template <int CTRL, int ROW_MASK>
@@ -934,25 +524,10 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
       const uint32_t kn = base + 64 + lane;
 #pragma unroll
       for (int c = 0; c < GRAD_REC; c++) vn[c] = 0.0f;
-#if GS_SUMREC_ABLATE == 1  // timing only: no record loads
-      const bool h = kn < S1 && kn < tile_cut[slot_tile[kn]];
-      if (h) vn[0] = 1.0f;
-#elif GS_SUMREC_ABLATE == 3  // timing only: no cut test (every slot's record loaded)
-      const bool h = kn < S1;
-      if (h) load_rec(gradrec + (size_t)kn * GRAD_REC, vn);
-#else
       const bool h = kn < S1 && kn < tile_cut[slot_tile[kn]];
       if (h) load_rec(gradrec + (size_t)kn * GRAD_REC, vn);
-#endif
       hn = __ballot(h);
     }
-#if GS_SUMREC_ABLATE == 2  // timing only: no segmented scan / accumulation
-    if (hc) {
-      asm volatile("" ::"v"(v[0]), "v"(v[4]), "v"(v[8]));
-      jbase += (uint32_t)__popcll(__ballot(my_off >= base && my_off < base + 64));
-      continue;
-    }
-#endif
     if (hc == 0) {
       // no record in the chunk (every slot behind its tile's walk, as for most of a dense
       // scene's instances): only count the owners that start in it
@@ -992,141 +567,11 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
   }
 }
 
-// Slot-parallel record sums (GS_SUMREC_SLOTS=1; off by default: at C3 it measured 65 us against the
-// rank-parallel kernel's 56-62 us per view, the per-chunk partials and the join costing more than the
-// parallelism gained).  k_sum_records gives a wave 64
-// depth ranks and sweeps their records chunk after chunk: a chain of dependent loads per chunk
-// (slot -> tile -> cut -> record) with only V / 64 waves to hide it.  Here wave c takes the
-// instance slots [64 c, 64 c + 64) -- I / 64 independent waves: each slot's owner comes from the
-// duplicate's presort_gid (a Gaussian's slots are contiguous), the chunk's records are summed per
-// owner with the same segmented DPP scan, and an owner that lies inside the chunk is written
-// directly.  An owner that spans chunks leaves its per-chunk fp32 partials (head, whole chunks,
-// tail); k_sum_records_join adds them in chunk order in fp64.  Deterministic; the same sums as
-// k_sum_records up to where the chunk boundaries fall (fp32 partials, fp64 accumulation).
-#ifndef GS_SUMREC_SLOTS
-#define GS_SUMREC_SLOTS 0
-#endif
-constexpr uint32_t SR_IN = 1u, SR_OUT = 2u, SR_WHOLE = 4u;  // chunk flags
-// scratch after the records: per chunk two partials (9 f32: [0] its first owner's part when that
-// owner began in an earlier chunk, [1] its last owner's part when that owner continues) + flags
-inline size_t sumrec_chunks(size_t R) { return (R + 63) / 64; }
-size_t sumrec_extra_bytes(size_t R) {
-  if (!GS_SUMREC_SLOTS) return 0;
-  const size_t n = sumrec_chunks(R);
-  return n * 2 * GRAD_REC * sizeof(float) + n * sizeof(uint32_t);
-}
-
-__global__ __launch_bounds__(256) void k_sum_records_slots(const uint32_t* __restrict__ counters,
-                                                           const uint32_t* __restrict__ presort_gid,
-                                                           const uint32_t* __restrict__ slot_tile,
-                                                           const uint32_t* __restrict__ tile_cut,
-                                                           const uint32_t* __restrict__ cut_max,
-                                                           const float* __restrict__ gradrec, float* __restrict__ gsum,
-                                                           float* __restrict__ part, uint32_t* __restrict__ flags,
-                                                           uint32_t R, uint32_t P) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);  // chunk of this wave
-  if (counters[CNT_ERR] & ERR_INVALID) {
-    // the forward's instance list is invalid (reported by the host): no valid records, zero sums
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < P; i += gridDim.x * 256)
-      for (int k = 0; k < GRAD_REC; k++) gsum[(size_t)i * GRAD_REC + k] = 0.0f;
-    return;
-  }
-  const uint32_t I = min(counters[CNT_I], R);
-  const uint32_t k0 = c * 64;
-  if (k0 >= I) return;  // wave-uniform; no workgroup barrier in this kernel
-  const uint32_t k = k0 + lane;
-  const bool valid = k < I;
-  const uint32_t gid = valid ? presort_gid[k] : 0xFFFFFFFFu;
-  // records exist below the slot's tile cut (and below the largest cut)
-  const bool has = valid && k < *cut_max && k < tile_cut[slot_tile[k]];
-  float v[GRAD_REC];
-#pragma unroll
-  for (int q = 0; q < GRAD_REC; q++) v[q] = 0.0f;
-  if (has) load_rec(gradrec + (size_t)k * GRAD_REC, v);
-  // neighbours across the chunk edges (same owner: the owner spans chunks)
-  const uint32_t before = k0 > 0 ? presort_gid[k0 - 1] : 0xFFFFFFFEu;
-  const uint32_t after = k0 + 64 < I ? presort_gid[k0 + 64] : 0xFFFFFFFEu;
-  const uint32_t own1 = valid ? gid + 1 : 0;
-  if (__ballot(has)) {  // (uniform) a chunk without records (behind every walk) only writes zeros
-    seg_scan_step<0x111, 0xF>(v, own1);  // row_shr:1
-    seg_scan_step<0x112, 0xF>(v, own1);  // row_shr:2
-    seg_scan_step<0x114, 0xF>(v, own1);  // row_shr:4
-    seg_scan_step<0x118, 0xF>(v, own1);  // row_shr:8
-    seg_scan_step<0x142, 0xA>(v, own1);  // row_bcast:15 -> rows 1, 3
-    seg_scan_step<0x143, 0xC>(v, own1);  // row_bcast:31 -> rows 2, 3
-  }
-  const uint32_t gid_first = (uint32_t)__shfl((int)gid, 0, 64);
-  const uint32_t nv = min(64u, I - k0);
-  const uint32_t gid_last = (uint32_t)__shfl((int)gid, (int)nv - 1, 64);
-  const bool in = before == gid_first, out = after == gid_last;
-  const uint32_t next = lane + 1 < nv ? (uint32_t)__shfl_down((int)gid, 1, 64) : 0xFFFFFFFDu;
-  const bool end = valid && next != gid;  // last slot of its owner within the chunk
-  if (end) {
-    const bool first_seg = gid == gid_first, last_seg = lane + 1 == nv;
-    if ((first_seg && in) || (last_seg && out)) {
-      // a part of an owner that spans chunks: [0] the continued first owner (also when it fills the
-      // whole chunk and continues), [1] the last owner that begins here and continues
-      float* pp = part + ((size_t)c * 2 + ((first_seg && in) ? 0 : 1)) * GRAD_REC;
-#pragma unroll
-      for (int q = 0; q < GRAD_REC; q++) pp[q] = v[q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < GRAD_REC; q++) gsum[(size_t)gid * GRAD_REC + q] = v[q];
-    }
-  }
-  if (lane == 0) flags[c] = (in ? SR_IN : 0u) | (out ? SR_OUT : 0u) | (gid_first == gid_last ? SR_WHOLE : 0u);
-}
-
-// One lane per chunk whose first owner began in an earlier chunk and ends here: that owner's parts,
-// head chunk first, summed in fp64.
-__global__ __launch_bounds__(256) void k_sum_records_join(const uint32_t* __restrict__ counters,
-                                                          const uint32_t* __restrict__ presort_gid,
-                                                          const float* __restrict__ part,
-                                                          const uint32_t* __restrict__ flags,
-                                                          float* __restrict__ gsum, uint32_t R) {
-  if (counters[CNT_ERR] & ERR_INVALID) return;
-  const uint32_t I = min(counters[CNT_I], R);
-  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
-  if ((size_t)c * 64 >= I) return;
-  const uint32_t f = flags[c];
-  // the owner's tail is here unless it fills this chunk and continues
-  if (!(f & SR_IN) || ((f & SR_WHOLE) && (f & SR_OUT))) return;
-  uint32_t h = c;  // the head chunk: back over the whole chunks the owner fills
-  do {
-    h--;
-  } while ((flags[h] & SR_WHOLE) && (flags[h] & SR_IN));
-  // head: the owner begins there as its last owner ([1]); the later chunks hold it first ([0])
-  double acc[GRAD_REC];
-  const float* ph = part + ((size_t)h * 2 + 1) * GRAD_REC;
-#pragma unroll
-  for (int q = 0; q < GRAD_REC; q++) acc[q] = (double)ph[q];
-  for (uint32_t j = h + 1; j <= c; j++) {
-    const float* pj = part + (size_t)j * 2 * GRAD_REC;
-#pragma unroll
-    for (int q = 0; q < GRAD_REC; q++) acc[q] += (double)pj[q];
-  }
-  const size_t gid = presort_gid[(size_t)c * 64];
-#pragma unroll
-  for (int q = 0; q < GRAD_REC; q++) gsum[gid * GRAD_REC + q] = (float)acc[q];
-}
-
 static void launch_sum_records(const GaussianArgs& g, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                                float* gradrec, uint32_t R, hipStream_t st) {
-  if (GS_SUMREC_SLOTS) {
-    const uint32_t nch = (uint32_t)sumrec_chunks(R);
-    float* part = gradrec + (size_t)R * GRAD_REC;
-    uint32_t* fl = reinterpret_cast<uint32_t*>(part + (size_t)nch * 2 * GRAD_REC);
-    GS_LAUNCH("sum_records", k_sum_records_slots, dim3((nch + 3) / 4), dim3(256), 0, st, geo.counters,
-              bin.presort_gid, bin.slot_tile, img.tile_cut, img.cut_max, gradrec, geo.gsum, part, fl, R,
-              (uint32_t)g.P);
-    GS_LAUNCH("sum_records_join", k_sum_records_join, dim3((nch + 255) / 256), dim3(256), 0, st, geo.counters,
-              bin.presort_gid, part, fl, geo.gsum, R);
-    return;
-  }
   GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
             dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
-            img.cut_max, gradrec, geo.gsum, (uint32_t)g.P);
+            img.sched + SCHED_CUT_MAX, gradrec, geo.gsum, (uint32_t)g.P);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1428,36 +873,19 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
   }
 }
 
-template <int DEG>  // -1: colours precomputed (no SH gradient)
-__global__ __launch_bounds__(256) void k_preprocess_bwd(GaussianArgs g, CameraArgs c,
-                                                        const uint32_t* __restrict__ tiles,
-                                                             const uint8_t* __restrict__ clamped,
-                                                        const float* __restrict__ gsum, GradOut out) {
-  extern __shared__ float s_sh[];  // DEG >= 0: [256][3M + 1] SH rows, then dL/dsh rows
-  const int i0 = blockIdx.x * 256, i = i0 + (int)threadIdx.x;
-  const int nG = min(256, g.P - i0);
-  const int rowf = 3 * g.M, stride = rowf + 1;
-  float* row = s_sh + threadIdx.x * stride;
-  if (DEG >= 0) {
-    rows_to_lds(g.shs + (size_t)i0 * rowf, s_sh, nG, rowf, stride);
-    lds_barrier();
-  }
-  if (i < g.P) preprocess_bwd_one<DEG>(i, g, c, tiles, clamped, gsum, out, row);
-  if (DEG >= 0) {
-    if (out.acc & GS_ACC_SH) {  // (uniform) accumulation: the lane adds its own row
-      if (i < g.P)
-        for (int k = 0; k < rowf; k++) out.dsh[(size_t)i * rowf + k] += row[k];
-      return;
-    }
-    lds_barrier();
-    lds_to_rows(s_sh, out.dsh + (size_t)i0 * rowf, nG, rowf, stride);
-  }
+// colours precomputed (no SH gradient)
+__global__ __launch_bounds__(256) void k_preprocess_bwd_colors(GaussianArgs g, CameraArgs c,
+                                                               const uint32_t* __restrict__ tiles,
+                                                               const uint8_t* __restrict__ clamped,
+                                                               const float* __restrict__ gsum, GradOut out) {
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  if (i < g.P) preprocess_bwd_one<-1>(i, g, c, tiles, clamped, gsum, out, nullptr);
 }
 
-// Register variant (GS_PBWD_REG, the default): the lane loads its own SH row (first 3K floats, 16-B loads when
+// Register variant: the lane loads its own SH row (first 3K floats, 16-B loads when
 // the rows allow) and stores dL/dsh the same way; no LDS, so occupancy is set by registers alone.
 template <int DEG, bool SPLIT = false>  // SPLIT: SH rows from g.shs (features_dc) + g.shs_rest
-__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PBWD_WPE) void k_preprocess_bwd_reg(GaussianArgs g, CameraArgs c,
+__global__ __launch_bounds__(256) void k_preprocess_bwd_reg(GaussianArgs g, CameraArgs c,
                                                             const uint32_t* __restrict__ tiles,
                                                             const uint8_t* __restrict__ clamped,
                                                             const float* __restrict__ gsum, GradOut out) {
@@ -1522,16 +950,13 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PBWD_WPE) void k_preprocess_bwd
   for (int k = KF; k < rowf; k++) dst[k] = 0.0f;
 }
 
-// Staged variant (GS_PBWD_STAGE, degree 3 with whole 48-float rows, dL/dsh written not added):
+// Staged variant (degree 3 with whole 48-float rows, dL/dsh written not added):
 // the workgroup's 256 SH rows come in (stage_sh_rows48) and its 256 dL/dsh rows go out as
 // contiguous blocks of coalesced 16-B accesses through LDS, instead of 12-16 lane-strided loads /
 // stores per lane each touching 64 cache lines; the lane's row moves between LDS and registers
 // with 16-B reads / writes.  53 KB of LDS per workgroup (3 waves per SIMD, the register variant
 // ran at 4): 124 -> 100 us at C3.  (Keeping the row in LDS for the SH backward instead of
 // registers: 101 us; the same staging in the forward preprocess: 80 -> 85 us, not used.)
-#ifndef GS_PBWD_STAGE
-#define GS_PBWD_STAGE 1
-#endif
 template <bool SPLIT>
 __global__ __launch_bounds__(256) void k_preprocess_bwd_stage(GaussianArgs g, CameraArgs c,
                                                               const uint32_t* __restrict__ tiles,
@@ -1594,20 +1019,17 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd_stage(GaussianArgs g, Ca
 // r = (first ? v : r + v): the bucket arithmetic of one view's write / `grad += g`
 __device__ __forceinline__ void vput(float& r, float v, bool first) { r = first ? v : r + v; }
 
-// GS_BWDG_LDS: the workgroup's 256 SH rows come in (and their gradient rows go out) as one
+// The workgroup's 256 SH rows come in (and their gradient rows go out) as one
 // contiguous block through LDS -- coalesced 16-B accesses -- instead of one lane-strided 192-B
 // row per lane (every load instruction touching 64 cache lines).  The kernel runs at 2 waves per
 // SIMD for its registers anyway, so the 53 KB of LDS per workgroup costs no occupancy.
-#ifndef GS_BWDG_LDS
-#define GS_BWDG_LDS 1
-#endif
 constexpr int BG_ROW = 52;  // staged row stride (floats): 16-B aligned, conflict-free 16-B reads
 
 template <int DEG>  // -1: colours precomputed (no SH gradient)
 __global__ __launch_bounds__(256) void k_backward_gaussians(GaussianArgs g, FusedViews fv, GradOut out) {
   constexpr int D = DEG < 0 ? 0 : DEG;
   constexpr int KF = DEG < 0 ? 1 : 3 * (D + 1) * (D + 1);
-  constexpr bool LDS = GS_BWDG_LDS && DEG >= 0 && KF % 4 == 0;
+  constexpr bool LDS = DEG >= 0 && KF % 4 == 0;
   __shared__ __attribute__((aligned(16))) float s_rows[LDS ? 256 * BG_ROW : 1];
   const int i0 = blockIdx.x * 256;
   const int i = i0 + (int)threadIdx.x;
@@ -1830,13 +1252,12 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
   if (have_records) launch_sum_records(g, geo, bin, img, gradrec, R, st);
   dim3 grid((g.P + 255) / 256), block(256);
   const bool sh = g.colors == nullptr && g.shs != nullptr && out.dsh != nullptr;
-  const size_t lds = sh ? (size_t)256 * (3 * g.M + 1) * sizeof(float) : 0;
   if (!sh) {
-    GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<-1>, grid, block, 0, st, g, c, geo.tiles, geo.clamped,
-              geo.gsum, out);
+    GS_LAUNCH("preprocess_bwd", k_preprocess_bwd_colors, grid, block, 0, st, g, c, geo.tiles, geo.clamped, geo.gsum,
+              out);
     return;
   }
-  if (GS_PBWD_STAGE && sh_stage_ok(g) && (((uintptr_t)out.dsh) & 15) == 0 && !(out.acc & GS_ACC_SH)) {
+  if (sh_stage_ok(g) && (((uintptr_t)out.dsh) & 15) == 0 && !(out.acc & GS_ACC_SH)) {
     if (g.shs_rest)
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd_stage<true>, grid, block, 0, st, g, c, geo.tiles, geo.clamped,
                 geo.gsum, out);
@@ -1859,7 +1280,6 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
 #undef GS_PBWD_SPLIT
     return;
   }
-  if (GS_PBWD_REG) {
   switch (g.D) {
     case 0:
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd_reg<0>, grid, block, 0, st, g, c, geo.tiles, geo.clamped, geo.gsum, out);
@@ -1872,26 +1292,6 @@ void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& 
       break;
     default:
       GS_LAUNCH("preprocess_bwd", k_preprocess_bwd_reg<3>, grid, block, 0, st, g, c, geo.tiles, geo.clamped, geo.gsum, out);
-      break;
-  }
-  return;
-  }
-  switch (g.D) {
-    case 0:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<0>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,
-                geo.gsum, out);
-      break;
-    case 1:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<1>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,
-                geo.gsum, out);
-      break;
-    case 2:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<2>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,
-                geo.gsum, out);
-      break;
-    default:
-      GS_LAUNCH("preprocess_bwd", k_preprocess_bwd<3>, grid, block, lds, st, g, c, geo.tiles, geo.clamped,
-                geo.gsum, out);
       break;
   }
 }

@@ -205,7 +205,7 @@ __device__ __forceinline__ void workgroup_totals(uint32_t area, bool culled, WgT
 // DEPTH_DROP for every other Gaussian: the first depth-sort pass drops them, which is the
 // visibility compaction.
 template <int DEG>
-__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
+__global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c, int* __restrict__ radii,
                                                     float4* __restrict__ splat, float4* __restrict__ binrec,
                                                     uint32_t* __restrict__ depth_key,
                                                     uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess(Gaus
 
 // The split-SH preprocess: k_preprocess's body with the split row loader (preprocess_one SPLIT).
 template <int DEG>
-__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PRE_WPE) void k_preprocess_split(
+__global__ __launch_bounds__(256) void k_preprocess_split(
     GaussianArgs g, CameraArgs c, int* __restrict__ radii, float4* __restrict__ splat, float4* __restrict__ binrec,
     uint32_t* __restrict__ depth_key, uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
     WgTotals* __restrict__ wg) {
@@ -281,7 +281,7 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
 // the Gaussian's inputs come from HBM once, the later views read them from the caches.  The
 // per-view workgroup totals go to each view's WgTotals slots as in k_preprocess.
 template <int DEG>
-__global__ __launch_bounds__(256) GS_WPE_ATTR(GS_PV_WPE) void k_preprocess_views(GaussianArgs g, PreViews pv) {
+__global__ __launch_bounds__(256) void k_preprocess_views(GaussianArgs g, PreViews pv) {
   const int i = blockIdx.x * 256 + (int)threadIdx.x;
   for (int v = 0; v < pv.K; v++) {
     const GeomPtrs& geo = pv.geo[v];
@@ -340,12 +340,9 @@ struct DstOffsets {
   }
 };
 
-#ifndef GS_TILE_SORT_BLOCKS
-#define GS_TILE_SORT_BLOCKS 4096  // workgroups per tile-sort pass (sort_plan)
-#endif
-#ifndef GS_DEPTH_SORT_BLOCKS
-#define GS_DEPTH_SORT_BLOCKS 4096  // workgroups per depth-sort pass (sort_plan)
-#endif
+// workgroups per tile-sort / depth-sort pass (sort_plan): one per 2048-key tile up to 8M keys
+// (128 or 256 depth-sort workgroups, smaller histograms but longer scatters: 961 -> 953 / 924 it/s)
+constexpr uint32_t GS_TILE_SORT_BLOCKS = 4096, GS_DEPTH_SORT_BLOCKS = 4096;
 // The extra workgroup of the first depth-sort histogram launch: the view's totals from the preprocess
 // workgroups' WgTotals (64-bit instance sum: an overflow of the 32-bit instance positions is seen
 // exactly), written to the view's counters (which need no zeroing beforehand: every counter the
@@ -647,11 +644,11 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
 // tile ranges over the sorted instance list, 4 instances per lane
 __global__ __launch_bounds__(256) void k_ranges(uint32_t I, const uint32_t* __restrict__ n_dev,
                                                 const uint32_t* __restrict__ tile, uint2* __restrict__ ranges,
-                                                uint32_t* __restrict__ sched, uint32_t sched_words, uint32_t tiles,
+                                                uint32_t* __restrict__ sched, uint32_t n_sched, uint32_t tiles,
                                                 uint64_t bs, uint64_t is) {
   n_dev = vptr(n_dev, bs), tile = vptr(tile, bs), ranges = vptr(ranges, is), sched = vptr(sched, is);
-  // clear the render's per-tile completion counters and length buckets (k_render_fwd* epilogue)
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sched_words; i += gridDim.x * 256) sched[i] = 0u;
+  // clear the render's per-tile completion words and the backward queue (k_render_fwd_q epilogue)
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_sched; i += gridDim.x * 256) sched[i] = 0u;
   I = min(I, *n_dev);  // the capacity I, or the count when below it
   const uint32_t k0 = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (k0 >= I) return;
@@ -687,7 +684,7 @@ void fwd_bin(int P, uint32_t I, const CameraArgs& c, const int* radii, const Geo
 void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
                    const ImgPtrs& img, uint64_t gs, uint64_t bs, uint64_t is, hipStream_t st) {
   const int tiles = c.gx * c.gy;
-  const uint32_t sched_words = 2u * (uint32_t)tiles + ORDER_GROUPS * ORDER_BUCKETS + 1u;
+  const uint32_t sched_n = sched_words((uint32_t)tiles);
   if (I == 0 || !dup_balanced(I, (uint32_t)P)) {
     // no instances (capacity 0), or more than DUP_SLOTS per Gaussian on average: view by view
     for (int v = 0; v < views; v++) {
@@ -699,17 +696,17 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
       img_layout(c.W, c.H, &im, (char*)img.ranges + (uint64_t)v * is);
       if (I == 0) {
         (void)hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
-        (void)hipMemsetAsync(im.tile_done, 0, sizeof(uint32_t) * sched_words, st);
+        (void)hipMemsetAsync(im.tile_fin, 0, sizeof(uint32_t) * sched_n, st);
         continue;
       }
       (void)hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
       GS_LAUNCH("duplicate", k_duplicate, dim3((P + 255) / 256), dim3(256), 0, st, (uint32_t)P, g.counters,
                 g.sorted_gid, g.offsets, g.binrec, c.gx, bb.slot_tile, bb.presort_gid);
       radix_sort_pairs(bb.keys_a, bb.vals_a, bb.keys_b, bb.vals_b, true, &g.counters[CNT_NREND], I, tile_bits(tiles),
-                       bb.sort_scratch, st, false, false, GS_SORT_GID ? bb.presort_gid : nullptr, bb.aux_a,
-                       bb.presort_gid, bb.slot_tile, GS_TILE_SORT_BLOCKS);
+                       bb.sort_scratch, st, false, false, nullptr, nullptr, nullptr, bb.slot_tile,
+                       GS_TILE_SORT_BLOCKS);
       GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, &g.counters[CNT_NREND],
-                bb.sorted_tile, im.ranges, (uint32_t*)im.tile_done, sched_words, (uint32_t)tiles, 0ull, 0ull);
+                bb.sorted_tile, im.ranges, im.tile_fin, sched_n, (uint32_t)tiles, 0ull, 0ull);
     }
     return;
   }
@@ -721,14 +718,12 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
             geo.counters, geo.dup_first, geo.sorted_gid, geo.offsets, geo.binrec, c.gx, c.gy, bin.slot_tile,
             bin.presort_gid, img.ranges, hist0 ? bin.sort_scratch : nullptr, (1u << radix_first_bits(tbits)) - 1u,
             bin.count, gs, bs, is);
-  // GS_SORT_GID: the Gaussian ids travel with the slots (aux stream): the renders then read
-  // point_gid contiguously instead of gathering presort_gid[slot].  The device count bounds the
-  // sort (I is the buffers' capacity, which may exceed it).
+  // the device count bounds the sort (I is the buffers' capacity, which may exceed it)
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, bin.count, I, tbits, bin.sort_scratch, st,
-                   false, hist0, GS_SORT_GID ? bin.presort_gid : nullptr, bin.aux_a, bin.presort_gid, bin.slot_tile,
+                   false, hist0, nullptr, nullptr, nullptr, bin.slot_tile,
                    GS_TILE_SORT_BLOCKS, views, bs);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024, views), dim3(256), 0, st, I, bin.count, bin.sorted_tile,
-            img.ranges, (uint32_t*)img.tile_done, sched_words, (uint32_t)tiles, bs, is);
+            img.ranges, img.tile_fin, sched_n, (uint32_t)tiles, bs, is);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -739,10 +734,8 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
 //   (x, y, r, g) | falloff coefficients + opacity | (b, bits(entry index + 1), -, -)
 // and each quadrant wave's dense list holds the offsets (u32), read FWD_ILP = 4 at a time with one
 // 16-B LDS read: a list entry costs no address arithmetic, no unpacking and no dependent list read.
-#ifndef GS_FWD_ILP
-#define GS_FWD_ILP 4
-#endif
-constexpr int FWD_ILP = GS_FWD_ILP;  // a multiple of 4 (whole 16-B list reads)
+// (8 entries per trip: 60 -> 74 VGPRs, 8 -> 6 waves per SIMD, render_fwd 174 -> 189 us)
+constexpr int FWD_ILP = 4;  // a multiple of 4 (whole 16-B list reads)
 static_assert(FWD_ILP % 4 == 0, "list groups are read 16 B at a time");
 
 struct FwdPix {
@@ -751,11 +744,10 @@ struct FwdPix {
   uint64_t done;  // lane mask (wave-uniform): pixels that stopped or lie outside the image
 };
 
-// Walk one quadrant wave's list of qcnt staged entries (the list is padded with 2 FWD_ILP zero
-// offsets) for the lane's pixel.
-// PAD: the list's padding points at a staged dummy entry of opacity 0 (alpha 0 at every pixel), so
-// the walk needs no per-entry end-of-list test
-template <bool EXACT, int NB, bool PAD = false>
+// Walk one quadrant wave's list of qcnt staged entries for the lane's pixel.  The list is padded
+// with 2 FWD_ILP offsets of a staged dummy entry of opacity 0 (alpha 0 at every pixel), so the walk
+// needs no per-entry end-of-list test (175.8 -> 172.6 us at C3).
+template <bool EXACT, int NB>
 __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist, uint32_t qcnt, float pfx, float pfy,
                                          FwdPix& px) {
   // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
@@ -792,7 +784,7 @@ __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist,
       // within ~1e-3 px of a splat centre, so the fast mode leaves the test out (the backward
       // matches it entry for entry)
       const uint64_t m_a = __builtin_amdgcn_ballot_w64((!EXACT || pw[u] <= 0.0f) && al[u] >= 1.0f / 255.0f);
-      uint64_t m_cu = (PAD || k + u < qcnt) ? m_a & ~px.done : 0ull;
+      uint64_t m_cu = m_a & ~px.done;
       if constexpr (EXACT) {  // upstream's order, T (1 - alpha) and (rgb alpha) T, mirrored by the oracle
         const float tT = px.T * (1.0f - al[u]);
         // T would drop below 1e-4: stop before this entry
@@ -825,31 +817,53 @@ __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist,
   }
 }
 
-// Epilogue of one quadrant wave (one lane): one 64-bit atomic per wave adds 1 (finished waves, low
-// 3 bits) plus a one-hot bit of the quadrant's walk-length class (bit 8 + class).  The tile's
-// fourth finisher gets the other three from the returned value, with no fence: the highest set
-// bit of the sum is the tile's longest class (or one above it, when classes coincide and carry),
-// which is all the longest-first order needs.  It takes a rank in that bucket; k_tile_order turns
-// (bucket, rank) into the backward's launch order.
-__device__ __forceinline__ void tile_finish(uint32_t tile, uint32_t grp, uint32_t wave_last,
-                                            uint64_t* __restrict__ tile_done, uint32_t* __restrict__ len_hist,
-                                            uint32_t* __restrict__ tile_brank) {
-  // length classes on a log scale, four per octave
-  const uint32_t cls = min((uint32_t)(4.0f * __log2f((float)wave_last + 1.0f)), 47u);
-  const uint64_t mine = (1ull << (8 + cls)) + 1ull;
-  const uint64_t old = atomicAdd((unsigned long long*)&tile_done[tile], (unsigned long long)mine);
-  if ((old & 7ull) != 3ull) return;
-  const uint32_t top = 63u - (uint32_t)__builtin_clzll((old + mine) >> 8);  // 0 .. 49
-  const uint32_t b = (uint32_t)ORDER_BUCKETS - 1u - top;                    // descending length
-  tile_brank[tile] = b << 22 | atomicAdd(&len_hist[grp * ORDER_BUCKETS + b], 1u);
+#ifdef GS_TIMING
+// diagnostic build only: per quadrant wave b (blockIdx.x): tile << 32 | quadrant, batches staged <<
+// 32 | entries walked (tools/fwd_timing.py)
+GS_TIMING_BUFFER(g_fwd_timing, gs_debug_fwd_timing)
+#endif
+
+// Epilogue of one quadrant wave (whole wave): the tile's largest n_contrib and the backward's units.
+// Lane 0 raises the tile's maximum (one atomicMax, whose return it waits for) and only then counts
+// itself finished (atomicAdd), so when the fourth finisher sees a count of 3 every other wave's
+// maximum is already in; it reads the tile's maximum n_eff back (atomicMax with 0) and queues the
+// tile's backward units in its XCD group's table (the group whose XCD ran this tile's waves): the
+// full SEG-entry segments of [0, n_eff) from the table's front, the partial last one (if any) from
+// its back, so the queue hands out the short units last.
+__device__ __forceinline__ void tile_finish(uint32_t tile, uint32_t wave_last, uint32_t* __restrict__ tile_fin,
+                                            uint32_t* __restrict__ sched, uint2* __restrict__ table, uint32_t cap) {
+  const uint32_t lane = threadIdx.x;
+  uint32_t n1 = 0;  // n_eff + 1 on the tile's fourth finisher, else 0
+  if (lane == 0) {
+    uint32_t* const tf = tile_fin + TILE_FIN_STRIDE * tile;
+    const uint32_t om = atomicMax(&tf[0], wave_last);
+    uint32_t one = 1u;
+    asm volatile("" : "+v"(one) : "v"(om));  // the count is issued after the maximum has landed
+    if (atomicAdd(&tf[1], one) == 3u) n1 = atomicMax(&tf[0], 0u) + 1u;
+  }
+  n1 = __builtin_amdgcn_readfirstlane(n1);
+  if (n1 <= 1u) return;  // (uniform) not the last quadrant, or nothing walked
+  const uint32_t n_eff = n1 - 1u, full = n_eff / SEG, part = n_eff % SEG != 0u ? 1u : 0u;
+  const uint32_t grp = tile % ORDER_GROUPS;
+  uint2* const tab = table + (size_t)grp * cap;
+  uint32_t bf = 0, bp = 0;
+  if (lane == 0) {
+    if (full) bf = atomicAdd(&sched[SCHED_FRONT + SCHED_STRIDE * grp], full);
+    if (part) bp = atomicAdd(&sched[SCHED_BACK + SCHED_STRIDE * grp], 1u);
+  }
+  bf = __builtin_amdgcn_readfirstlane(bf);
+  bp = __builtin_amdgcn_readfirstlane(bp);
+  for (uint32_t j = lane; j < full; j += 64) tab[bf + j] = make_uint2(tile, j);
+  if (part && lane == 0) tab[cap - 1u - bp] = make_uint2(tile, full);
 }
 
+// fin = (C0, C1, C2, T_final) for the backward's segment starts; out = C + T_final bg
 __device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q, bool inside, const FwdPix& px,
-                                          float* __restrict__ out, float* __restrict__ final_T,
+                                          float* __restrict__ out, float4* __restrict__ fin,
                                           uint32_t* __restrict__ n_contrib) {
   if (inside) {
     const size_t pix = (size_t)q.py * c.W + q.px, HW = (size_t)c.W * c.H;
-    final_T[pix] = px.T;
+    fin[pix] = make_float4(px.C0, px.C1, px.C2, px.T);
     n_contrib[pix] = px.last;
     out[pix] = px.C0 + px.T * c.bg[0];
     out[HW + pix] = px.C1 + px.T * c.bg[1];
@@ -857,113 +871,37 @@ __device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q,
   }
 }
 
-// One 256-lane workgroup per tile; 256-entry batches staged by the whole workgroup.
-template <bool EXACT>
-__global__ __launch_bounds__(GS_BLOCK) void k_render_fwd(CameraArgs c, const uint2* __restrict__ ranges,
-                                                         const uint32_t* __restrict__ point_list,
-                                                         const uint32_t* __restrict__ point_gid,
-                                                         const float4* __restrict__ splat,
-                                                         float4* __restrict__ inst_splat, float* __restrict__ out,
-                                                         float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                                                         uint32_t* __restrict__ tile_max, ImgPtrs img,
-                                                         const uint32_t* __restrict__ err,
-                                                         uint32_t* __restrict__ err_host) {
-  __shared__ float4 s_ent[3 * GS_BLOCK];
-  if (blockIdx.x == 0 && threadIdx.x == 0 && err_host && *err) err_host[0] = *err;
-  __shared__ uint64_t s_mask[4][4];  // [staging wave][quadrant]: batch entries whose alpha box meets the quadrant
-  __shared__ __attribute__((aligned(16))) uint32_t s_qlist[4][GS_BLOCK + 2 * FWD_ILP];  // per quadrant wave: byte offsets
-  const uint32_t tile = blockIdx.x;
-  const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const QuadPix q = quad_pixel(tx, ty, wid, lane);
-  const bool inside = q.px < c.W && q.py < c.H;
-  const uint2 range = ranges[tile];
-  // a sort / scan look-back that timed out (reported by the host) leaves no valid list: render none
-  const uint32_t n = (*err & ERR_INVALID) ? 0u : range.y - range.x;
-  const char* ent = reinterpret_cast<const char*>(s_ent);
-  FwdPix px;
-  px.done = __builtin_amdgcn_ballot_w64(!inside);
-  for (uint32_t base = 0; base < n; base += GS_BLOCK) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (__syncthreads_and(px.done == ~0ull)) break;
-    const uint32_t cnt = min((uint32_t)GS_BLOCK, n - base);
-    uint32_t qmask = 0;
-    if ((uint32_t)tid < cnt) {
-      const uint32_t gid = GS_SORT_GID ? point_gid[range.x + base + tid] : point_gid[point_list[range.x + base + tid]];
-      const float4 a = splat[3 * gid], b = splat[3 * gid + 1], d = splat[3 * gid + 2];
-      if (GS_INST_REC) {
-        float4* r = inst_splat + 3 * (size_t)(range.x + base + tid);
-        r[0] = a, r[1] = b, r[2] = d;
-      }
-      s_ent[tid] = make_float4(a.x, a.y, b.z, b.w);
-      s_ent[GS_BLOCK + tid] = fall_coefs(a.z, a.w, b.x, b.y);
-      s_ent[2 * GS_BLOCK + tid] = make_float4(d.x, __uint_as_float(base + tid + 1), 0.0f, 0.0f);
-      qmask = quadrant_mask(a.x, a.y, a.z, a.w, b.x, d.z, tx, ty);
-    }
-    publish_masks(qmask, s_mask, tid);
-    lds_barrier();
-    if (px.done == ~0ull) continue;
-    // dense, in-order list of this quadrant's entries (as LDS byte offsets), built by the wave
-    uint32_t qcnt = 0;
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-      const uint64_t m = uniform_u64(s_mask[g][wid]);
-      if ((m >> lane) & 1ull)
-        s_qlist[wid][qcnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-            16u * (g * 64 + lane);
-      qcnt += (uint32_t)__popcll(m);
-    }
-    if (lane < 2 * FWD_ILP) s_qlist[wid][qcnt + lane] = 0;  // pad the last group and the prefetch (masked below)
-    __builtin_amdgcn_wave_barrier();
-    fwd_walk<EXACT, GS_BLOCK>(ent, s_qlist[wid], qcnt, (float)q.px, (float)q.py, px);
-  }
-  fwd_store(c, q, inside, px, out, final_T, n_contrib);
-  const uint32_t wmax = wave_max_u32(px.last);
-  if (lane == 0) {
-    tile_max[4 * tile + wid] = wmax;
-    tile_finish(tile, xcd_group(tile, c.gx, c.gy), wmax, img.tile_done, img.len_hist, img.tile_brank);
-  }
-}
-
 // One wave per (tile, quadrant), no workgroup barriers: each wave stages the tile's entries 64 at
 // a time, culls them to its own quadrant and walks them, and finishes as soon as its 64 pixels
-// are done (the workgroup version waits for its slowest quadrant).  Workgroup b takes the
-// (b / 32)-th tile of XCD group b % 8 (xcd_tile), quadrant (b / 8) % 4, so the four quadrant
-// waves of a tile, and (GS_XCD_STRIPS) its neighbour tiles, share the workgroup-to-XCD round
-// robin (b % 8) and their repeated entry loads hit one L2.
-#ifndef GS_FWD_PREFETCH
-#define GS_FWD_PREFETCH 0  // 1 (needs GS_SORT_GID): measured 168 -> 179 us at C3, the loads past the stop are wasted
-#endif
-#if GS_FWD_PREFETCH && !GS_SORT_GID
-#error "GS_FWD_PREFETCH reads the ids by list position (GS_SORT_GID)"
-#endif
-#ifndef GS_FWDQ_NB
-#define GS_FWDQ_NB 64
-#endif
-constexpr int FWDQ_NB = GS_FWDQ_NB;  // entries staged per round (<= 64: one per lane)
-static_assert(FWDQ_NB <= 64, "one staged entry per lane");
-#ifndef GS_FWD_PAD
-#define GS_FWD_PAD 1
-#endif
+// are done (a workgroup per tile would wait for its slowest quadrant: 203 -> 188 us at C3 when this
+// went in).  Workgroup b takes the (b / 32)-th tile of XCD group b % 8 (xcd_tile), quadrant
+// (b / 8) % 4, so the four quadrant waves of a tile share the workgroup-to-XCD round robin (b % 8)
+// and their repeated entry loads hit one L2.  At every multiple of SEG entries it reaches, the wave
+// stores its pixels' (T, C) for the backward's depth segments (BinPtrs::ckpt).
+// (Tried and not kept: the next batch's ids / records prefetched one batch ahead, 168 -> 179 us --
+// the loads past the stop are wasted; 32-entry batches, 174 -> 195 us.)
+constexpr int FWDQ_NB = 64;  // entries staged per round (one per lane)
 // record stride of the staged batch: one more than the batch for the padding's dummy entry
-constexpr int FWDQ_NBS = FWDQ_NB + (GS_FWD_PAD ? 1 : 0);
+constexpr int FWDQ_NBS = FWDQ_NB + 1;
 template <bool EXACT>
 __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ point_list,
                                                      const uint32_t* __restrict__ point_gid,
-                                                     const float4* __restrict__ splat,
-                                                     float4* __restrict__ inst_splat, float* __restrict__ out,
-                                                     float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                                                     uint32_t* __restrict__ tile_max, ImgPtrs img,
+                                                     const float4* __restrict__ splat, float* __restrict__ out,
+                                                     ImgPtrs img, float4* __restrict__ ckpt,
+                                                     uint2* __restrict__ table, uint32_t cap,
                                                      const uint32_t* __restrict__ err, uint32_t* __restrict__ err_host) {
   __shared__ float4 s_ent[3 * FWDQ_NBS];
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
-  if (GS_FWD_PAD && threadIdx.x < 3)  // the dummy entry: position 0, opacity 0 (never contributes)
+  if (threadIdx.x < 3)  // the dummy entry: position 0, opacity 0 (never contributes)
     s_ent[threadIdx.x * FWDQ_NBS + FWDQ_NB] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   const uint32_t b = blockIdx.x;
   const uint32_t tile = xcd_tile(b & 7, b >> 5, c.gx, c.gy);
   if (tile == ~0u) return;  // (grid padded to whole groups of 8 tiles)
+#ifdef GS_TIMING
+  const unsigned long long t_start = timing_stamp();
+  uint32_t t_batches = 0, t_walked = 0;
+#endif
   const int wid = (int)((b >> 3) & 3);
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int lane = threadIdx.x;
@@ -976,89 +914,67 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   const uint32_t n = (*err & ERR_INVALID) ? 0u : range.y - range.x;
   const char* ent = reinterpret_cast<const char*>(s_ent);
   const float qx = (float)(tx * GS_TILE + 8 * (wid & 1)), qy = (float)(ty * GS_TILE + 8 * (wid >> 1));
+  float4* const ck = ckpt + ((size_t)(range.x / SEG) << 8) + 64 * wid + lane;
   FwdPix px;
   px.done = __builtin_amdgcn_ballot_w64(!inside);
-#if GS_FWD_PREFETCH
-  // two-deep staging pipeline: while batch k is walked, the splat records of batch k + 1 and the
-  // ids of batch k + 2 are in flight (the walk issues no global loads, so they overlap it)
-  const bool stager = lane < (uint32_t)FWDQ_NB;
-  const uint32_t* ids = point_gid + range.x + lane;
-  uint32_t gid_n = stager && lane < n ? ids[0] : 0u;
-  float4 pa, pb, pd;
-  if (stager && lane < n) pa = splat[3 * gid_n], pb = splat[3 * gid_n + 1], pd = splat[3 * gid_n + 2];
-  gid_n = stager && FWDQ_NB + lane < n ? ids[FWDQ_NB] : 0u;
-#endif
   for (uint32_t base = 0; base < n; base += FWDQ_NB) {
     if (px.done == ~0ull) break;
     bool meets = false;
-#if GS_FWD_PREFETCH
-    if (stager && base + lane < n) {
-      const float4 a = pa, bb = pb, d = pd;
-#else
     if (lane < (uint32_t)FWDQ_NB && base + lane < n) {
-      const uint32_t gid = GS_SORT_GID ? point_gid[range.x + base + lane] : point_gid[point_list[range.x + base + lane]];
+      const uint32_t gid = point_gid[point_list[range.x + base + lane]];
       const float4 a = splat[3 * gid], bb = splat[3 * gid + 1], d = splat[3 * gid + 2];
-#endif
-      if (GS_INST_REC) {
-        // every quadrant wave that stages the batch stores it (identical bytes; the tile's four
-        // waves run on one XCD, so the copies meet in its L2): the union of the waves' batches
-        // covers every entry the backward walks
-        float4* r = inst_splat + 3 * (size_t)(range.x + base + lane);
-        r[0] = a, r[1] = bb, r[2] = d;
-      }
       s_ent[lane] = make_float4(a.x, a.y, bb.z, bb.w);
       s_ent[FWDQ_NBS + lane] = fall_coefs(a.z, a.w, bb.x, bb.y);
       s_ent[2 * FWDQ_NBS + lane] = make_float4(d.x, __uint_as_float(base + lane + 1), 0.0f, 0.0f);
       meets = d.z >= 0.0f && ellipse_meets_rect(a.x, a.y, a.z, a.w, bb.x, d.z, qx, qx + 7.0f, qy, qy + 7.0f);
     }
-#if GS_FWD_PREFETCH
-    if (stager && base + FWDQ_NB + lane < n) pa = splat[3 * gid_n], pb = splat[3 * gid_n + 1], pd = splat[3 * gid_n + 2];
-    gid_n = stager && base + 2 * FWDQ_NB + lane < n ? ids[base + 2 * FWDQ_NB] : 0u;
-#endif
     const uint64_t m = __ballot(meets);
     if (meets)
       s_qlist[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
           16u * lane;
     const uint32_t qcnt = (uint32_t)__popcll(m);
-    if (lane < 2 * FWD_ILP) s_qlist[qcnt + lane] = GS_FWD_PAD ? 16u * FWDQ_NB : 0u;
+    if (lane < 2 * FWD_ILP) s_qlist[qcnt + lane] = 16u * FWDQ_NB;
+    // a segment boundary the backward may start from (this quadrant still runs: its largest
+    // n_contrib may lie behind it).  Stored once this batch's loads have landed: loads and stores
+    // share one wait counter, so a store issued ahead of them would hold their wait until its
+    // write completes (measured: before the staging loads, render_fwd 172 -> 242 us at SEG 128)
+    if (base != 0 && base % SEG == 0) {
+      // non-temporal: read once, by the backward; kept out of the L2 that caches the splat records
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(v4f{px.T, px.C0, px.C1, px.C2}, reinterpret_cast<v4f*>(ck + ((size_t)(base / SEG) << 8)));
+    }
     __builtin_amdgcn_wave_barrier();
-    fwd_walk<EXACT, FWDQ_NBS, GS_FWD_PAD != 0>(ent, s_qlist, qcnt, (float)q.px, (float)q.py, px);
+#ifdef GS_TIMING
+    t_batches++;
+    t_walked += qcnt;
+#endif
+    fwd_walk<EXACT, FWDQ_NBS>(ent, s_qlist, qcnt, (float)q.px, (float)q.py, px);
     __builtin_amdgcn_wave_barrier();  // the next round overwrites the staged entries
   }
-  fwd_store(c, q, inside, px, out, final_T, n_contrib);
+  // the tile's bookkeeping first: its atomics return values this wave waits for, and loads and
+  // stores share one wait counter -- issued after the pixel stores, the waits would also hold the
+  // wave (and its slot) until those stores completed
   const uint32_t wmax = wave_max_u32(px.last);
-  if (lane == 0) {
-    tile_max[4 * tile + wid] = wmax;
-    tile_finish(tile, xcd_group(tile, c.gx, c.gy), wmax, img.tile_done, img.len_hist, img.tile_brank);
-  }
+  tile_finish(tile, wmax, img.tile_fin, img.sched, table, cap);
+  if (lane == 0) img.tile_max[4 * tile + wid] = wmax;
+  fwd_store(c, q, inside, px, out, img.fin, img.n_contrib);
+#ifdef GS_TIMING
+  timing_record(g_fwd_timing, t_start, tile, (uint32_t)wid, t_batches, t_walked);
+#endif
 }
 
-#ifndef GS_FWD_WAVE
-#define GS_FWD_WAVE 1
-#endif
 void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img, float* out_color,
                 hipStream_t st, uint32_t* err_host) {
   const int tiles = c.gx * c.gy;
-  if (GS_FWD_WAVE) {
-    const int blocks = (int)xcd_span((uint32_t)tiles) * 32;
-    if (exact_exp())
-      GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-                &geo.counters[CNT_ERR], err_host);
-    else
-      GS_LAUNCH("render_fwd", k_render_fwd_q<false>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-                GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-                &geo.counters[CNT_ERR], err_host);
-    return;
-  }
+  const int blocks = (int)xcd_span((uint32_t)tiles) * 32;
   if (exact_exp())
-    GS_LAUNCH("render_fwd", k_render_fwd<true>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-                &geo.counters[CNT_ERR], err_host);
+    GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
+              bin.presort_gid, geo.splat, out_color, img, bin.ckpt, bin.seg_table, bin.seg_cap,
+              &geo.counters[CNT_ERR], err_host);
   else
-    GS_LAUNCH("render_fwd", k_render_fwd<false>, dim3(tiles), dim3(GS_BLOCK), 0, st, c, img.ranges, bin.point_list,
-              GS_SORT_GID ? bin.point_gid : bin.presort_gid, geo.splat, bin.inst_splat, out_color, img.final_T, img.n_contrib, img.tile_max, img,
-                &geo.counters[CNT_ERR], err_host);
+    GS_LAUNCH("render_fwd", k_render_fwd_q<false>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
+              bin.presort_gid, geo.splat, out_color, img, bin.ckpt, bin.seg_table, bin.seg_cap,
+              &geo.counters[CNT_ERR], err_host);
 }
 
 // ------------------------------------------------------------------------------------------

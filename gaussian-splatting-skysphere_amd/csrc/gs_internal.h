@@ -7,10 +7,12 @@
 //                                    clamped u8 | depth-sort keys/vals x2 u32 (keys_a: depth keys
 //                                    written by preprocess) | offsets u32 |
 //                                    scan partials | sort scratch | counters
-//   binning   (per instance, I)      tile keys/vals x2 u32 | presort_gid u32 | sort scratch
-//   image     (per pixel / tile)     ranges uint2 | final_T f32 | n_contrib u32 | tile_max u32 x4
-//                                    (largest n_contrib of each 8x8 quadrant) | tile_order u32 |
-//                                    tile_done u32 + length buckets | bucket rank u32
+//   binning   (per instance, I)      tile keys/vals x2 u32 | presort_gid u32 | sort scratch |
+//                                    segment-boundary states float4 x 256 per SEG instances |
+//                                    backward units uint2 (I / SEG + tiles + 1)
+//   image     (per pixel / tile)     ranges uint2 | fin float4 (final colour, T) | n_contrib u32 |
+//                                    tile_max u32 x4 (largest n_contrib of each 8x8 quadrant) |
+//                                    tile_cut u32 | tile_fin u32 x2 per tile + SCHED words
 //   gradient  (per instance, I)      9 f32 per (Gaussian, tile) instance (backward scratch)
 #pragma once
 #include <stddef.h>
@@ -26,12 +28,9 @@ namespace gs {
 // the CPU oracle), false = hardware v_exp_f32 (default).  Process-wide, read at launch time.
 bool exact_exp();
 
-// GS_SORT_GID: the tile sort carries the Gaussian ids as an aux stream (point_gid, read by list
-// position); 0: the renders look the id up by slot (presort_gid[slot]).  Measured at C3: the aux
-// stream costs +16 us over the two tile-sort scatters and saves 8 us in render_fwd.
-#ifndef GS_SORT_GID
-#define GS_SORT_GID 0
-#endif
+// The renders look a sorted instance's Gaussian id up by its presort slot (presort_gid[slot]).
+// (Carrying the ids through the tile sort as an aux stream instead, read by list position, cost
+// +16 us over the two tile-sort scatters and saved 8 us in render_fwd at C3: not kept.)
 
 constexpr int GRAD_REC = 9;    // dcolor(3), dmean2D(2), dconic(xx, xy, yy), dopacity
 
@@ -255,42 +254,36 @@ struct BinPtrs {
   uint32_t* presort_gid;
   uint32_t* sort_scratch;
   uint32_t* point_list;  // sorted presort slots (= vals_a or vals_b after the tile sort)
-  uint32_t* point_gid;   // Gaussian id of every sorted instance (presort_gid carried through the tile
-                         // sort as its aux stream: the renders read it contiguously, no slot -> id gather)
-  uint32_t* aux_a;       // the tile sort's aux ping buffer (pong: presort_gid, no longer needed)
   uint32_t* sorted_tile;
   uint32_t* slot_tile;   // tile of every instance slot (duplicate output, kept: the tile sort's
                          // first pass reads it and writes keys_b)
-  float4* inst_splat;    // GS_INST_REC: the 48-B splat record of every instance the forward staged, by
-                         // list position (the backward streams it instead of gathering slot -> id -> splat)
   uint32_t* count;       // [0]: the view's instance count bounded by the buffer's capacity (the duplicate
                          // writes it; the tile sort and k_ranges read it from this buffer)
+  // segment-boundary pixel states (T, C0, C1, C2) the forward's quadrant waves store at list
+  // positions SEG j (j >= 1) of a tile: entry [(range.x / SEG + j) * 256 + 64 quadrant + lane]
+  // (distinct for every (tile, j): range.x / SEG + j <= (range.y - 1) / SEG < I / SEG + 1)
+  float4* ckpt;
+  // the backward's units (tile, segment), one table of seg_cap entries per XCD group (tile % 8): full
+  // segments from its front, partial ones from its back
+  uint2* seg_table;
+  uint32_t seg_cap;
 };
 
-// Occupancy requests (amdgpu_waves_per_eu) for register-limited kernels; 0 = the compiler's choice.
-#define GS_WPE_ATTR(n) __attribute__((amdgpu_waves_per_eu((n) > 0 ? (n) : 1)))
-#ifndef GS_BWD_WPE
-#define GS_BWD_WPE 0
+// Depth segments of the backward (k_render_bwd_seg): a tile's list is walked in units of SEG
+// entries, each started from the pixel states the forward stored at the unit's far end.
+#ifndef GS_SEG
+#define GS_SEG 128
 #endif
-#ifndef GS_PV_WPE
-#define GS_PV_WPE 0
-#endif
-#ifndef GS_PBWD_WPE
-#define GS_PBWD_WPE 0
-#endif
-#ifndef GS_PRE_WPE
-#define GS_PRE_WPE 0
-#endif
+constexpr uint32_t SEG = GS_SEG;
+static_assert(SEG % 64 == 0, "segments are whole 64-entry batches");
+inline size_t seg_ckpts(size_t I) { return I / SEG + 1; }
+inline size_t seg_units(size_t I, size_t tiles) { return I / SEG + tiles + 1; }
 
-// GS_INST_REC = 1: the forward's quadrant waves store each staged entry's splat record at its list
-// position; the backward reads those contiguously (no id / splat gathers in the backward).
-// Measured at C3 (one call, both builds): render_bwd PMC traffic 664 -> 324 MB (1.44x its
-// algorithmic bytes) but 401 -> 396 us only -- the kernel is VALU-issue bound, not fetch bound --
-// while the forward's stores (every quadrant wave that stages a batch stores it) cost 175 -> 232
-// us: 1027 -> 983 it/s.  Off by default.
-#ifndef GS_INST_REC
-#define GS_INST_REC 0
-#endif
+
+// (Tried in round 2 and not kept: the forward's quadrant waves storing each staged entry's 48-B splat
+// record at its list position for the backward to stream instead of gathering slot -> id -> splat.
+// render_bwd PMC traffic 664 -> 324 MB but 401 -> 396 us only -- not fetch bound -- while the
+// forward's redundant stores cost 175 -> 232 us.)
 
 inline int tile_bits(int tiles) {
   int b = 1;
@@ -307,89 +300,70 @@ inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base) {
   };
   size_t In = I ? I : 1;
   size_t o_ka = take(In * 4), o_va = take(In * 4), o_kb = take(In * 4), o_vb = take(In * 4);
-  size_t o_pg = take(In * 4), o_st = take(In * 4), o_ax = take(GS_SORT_GID ? In * 4 : 0);
+  size_t o_pg = take(In * 4), o_st = take(In * 4);
   size_t o_ss = take(sort_scratch_words(In) * 4);
-  size_t o_is = take(GS_INST_REC ? In * 48 : 0);
   size_t o_cn = take(64);
+  size_t o_ck = take(seg_ckpts(In) * 256 * 16);
+  size_t o_su = take(seg_units(In, (size_t)tiles) * 8 * 8);
   if (out && base) {
     out->count = (uint32_t*)(base + o_cn);
-    out->inst_splat = GS_INST_REC ? (float4*)(base + o_is) : nullptr;
+    out->ckpt = (float4*)(base + o_ck);
+    out->seg_table = (uint2*)(base + o_su);
+    out->seg_cap = (uint32_t)seg_units(In, (size_t)tiles);
     out->keys_a = (uint32_t*)(base + o_ka);
     out->vals_a = (uint32_t*)(base + o_va);
     out->keys_b = (uint32_t*)(base + o_kb);
     out->vals_b = (uint32_t*)(base + o_vb);
     out->presort_gid = (uint32_t*)(base + o_pg);
     out->slot_tile = (uint32_t*)(base + o_st);
-    out->aux_a = (uint32_t*)(base + o_ax);
     out->sort_scratch = (uint32_t*)(base + o_ss);
     bool in_b = radix_passes(tile_bits(tiles)) % 2 == 1;
     out->point_list = in_b ? out->vals_b : out->vals_a;
     out->sorted_tile = in_b ? out->keys_b : out->keys_a;
-    // pass p writes aux_a (p even) or presort_gid (p odd): an odd pass count ends in aux_a
-    out->point_gid = in_b ? out->aux_a : out->presort_gid;
   }
   return off;
 }
 
 struct ImgPtrs {
   uint2* ranges;
-  float* final_T;
+  float4* fin;           // per pixel: (C0, C1, C2, T_final), the composited colour without background
   uint32_t* n_contrib;
   uint32_t* tile_max;
-  uint32_t* tile_order;  // backward launch order (k_tile_order)
-  uint32_t* tile_cut;    // per tile: 1 + the slot of its last walked instance (0: none), k_tile_order
-  uint64_t* tile_done;   // per tile: finished quadrant waves + their length bits (zeroed by k_ranges),
-  uint32_t* len_hist;    //   then ORDER_GROUPS x ORDER_BUCKETS walk-length bucket counts
-  uint32_t* tile_brank;  // bucket << 22 | rank within the bucket, per tile
-  uint32_t* cut_max;     // the largest tile_cut (after len_hist; zeroed with it): no instance slot at
-                         // or past it has a gradient record
+  uint32_t* tile_cut;    // per tile: 1 + the slot of its last walked instance (0: none), k_tile_cut
+  uint32_t* tile_fin;    // per tile: [2 t] largest n_contrib of the finished quadrant waves, [2 t + 1]
+                         // their count (zeroed by k_ranges, with the SCHED words after them)
+  uint32_t* sched;       // = tile_fin + 2 tiles: SCHED_* words
 };
+// words of ImgPtrs::sched, per XCD group g (tile % ORDER_GROUPS): backward units queued from the front
+// (full segments) / back (partial) of the group's unit table, the backward's take counter; then the
+// largest tile_cut (no instance slot at or past it has a record).  Every counter has a 128-B line of
+// its own (word SCHED_* + SCHED_STRIDE g): atomics on one line from many waves serialise -- with
+// the 25 counters packed into one line, render_bwd took 2,100 us and render_fwd 243 us at C3, one
+// line each: 348 / 179 us.
+constexpr int SCHED_STRIDE = 32;
+constexpr int SCHED_FRONT = 0, SCHED_BACK = 8 * SCHED_STRIDE, SCHED_NEXT = 16 * SCHED_STRIDE,
+              SCHED_CUT_MAX = 24 * SCHED_STRIDE, SCHED_WORDS = 25 * SCHED_STRIDE;
+#ifndef GS_TF_STRIDE
+#define GS_TF_STRIDE 2
+#endif
+constexpr uint32_t TILE_FIN_STRIDE = GS_TF_STRIDE;  // words per tile of tile_fin ([0] max, [1] count)
+// scheduling words zeroed per binning (k_ranges)
+inline uint32_t sched_words(uint32_t tiles) { return TILE_FIN_STRIDE * tiles + SCHED_WORDS; }
 
-// Backward launch order: tiles bucketed by walk length (largest n_contrib), longest first.
-constexpr int ORDER_BUCKETS = 64;
-// Tiles are ordered within ORDER_GROUPS groups: group g fills launch positions g, g + 8, g + 16,
-// ..., the workgroups the dispatcher sends to XCD g (workgroup b runs on XCD b % 8), and the
-// forward places group g's tiles on XCD g the same way.  GS_XCD_STRIPS = 1: group g is the g-th
-// eighth of the tiles in column-major order, a vertical strip of the image, so a splat's
-// neighbouring tiles (both directions) run on one XCD and its record is fetched into one L2;
-// 0: group = tile % 8 (XCD g owns every 8th tile column).
+// The forward's quadrant waves are laid out in ORDER_GROUPS groups: group g = tile % 8 fills
+// workgroups g, g + 8, g + 16, ..., which the dispatcher sends to one XCD (workgroup b runs on XCD
+// b % 8), so the four quadrant waves of a tile share that XCD's L2 (XCD g owns every 8th tile
+// column); the backward's units of group g are taken first by the waves running on XCD g.
+// (Measured in round 2: each XCD rendering a vertical strip of the image instead, so that a splat's
+// neighbouring tiles in both directions share one L2, made both renders slower: render_fwd 174 ->
+// 184 us, render_bwd 404 -> 417 us.)
 constexpr int ORDER_GROUPS = 8;
-#ifndef GS_XCD_STRIPS
-#define GS_XCD_STRIPS 0  // 1 measured at C3: render_fwd 174 -> 184 us, render_bwd 404 -> 417 us
-#endif
-// tiles per group (the last groups may hold fewer; their launch positions past it are holes)
+// tiles per group (the last groups may hold one fewer)
 __host__ __device__ inline uint32_t xcd_span(uint32_t tiles) { return (tiles + ORDER_GROUPS - 1) / ORDER_GROUPS; }
-// launch positions of a per-tile grid ordered by XCD group (8 x the largest group)
-__host__ __device__ inline uint32_t xcd_slots(uint32_t tiles) {
-  return GS_XCD_STRIPS ? ORDER_GROUPS * xcd_span(tiles) : tiles;
-}
-__host__ __device__ inline uint32_t xcd_group(uint32_t tile, uint32_t gx, uint32_t gy) {
-#if GS_XCD_STRIPS
-  return ((tile % gx) * gy + tile / gx) / xcd_span(gx * gy);
-#else
-  (void)gx, (void)gy;
-  return tile % ORDER_GROUPS;
-#endif
-}
-__host__ __device__ inline uint32_t xcd_group_size(uint32_t g, uint32_t tiles) {
-#if GS_XCD_STRIPS
-  const uint32_t s = xcd_span(tiles), lo = g * s;
-  return lo >= tiles ? 0u : (tiles - lo < s ? tiles - lo : s);
-#else
-  return (tiles + ORDER_GROUPS - 1 - g) / ORDER_GROUPS;
-#endif
-}
-// the k-th tile of group g (index order within the group; ~0u past its end)
+// the k-th tile of group g (~0u past its end)
 __host__ __device__ inline uint32_t xcd_tile(uint32_t g, uint32_t k, uint32_t gx, uint32_t gy) {
-  const uint32_t tiles = gx * gy;
-#if GS_XCD_STRIPS
-  const uint32_t p = g * xcd_span(tiles) + k;  // column-major position
-  if (k >= xcd_span(tiles) || p >= tiles) return ~0u;
-  return (p % gy) * gx + p / gy;
-#else
   const uint32_t t = ORDER_GROUPS * k + g;
-  return t < tiles ? t : ~0u;
-#endif
+  return t < gx * gy ? t : ~0u;
 }
 
 inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
@@ -403,22 +377,61 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t npix = (size_t)W * H;
   if (tiles == 0) tiles = 1;
   if (npix == 0) npix = 1;
-  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16), o_o = take((size_t)xcd_slots((uint32_t)tiles) * 4), o_c = take(tiles * 4),
-         o_d = take(tiles * 8 + ORDER_GROUPS * ORDER_BUCKETS * 4 + 4), o_b = take(tiles * 4);
+  size_t o_r = take(tiles * 8), o_f = take(npix * 16), o_n = take(npix * 4), o_m = take(tiles * 16),
+         o_c = take(tiles * 4), o_d = take((size_t)sched_words((uint32_t)tiles) * 4);
   if (out && base) {
     out->ranges = (uint2*)(base + o_r);
-    out->final_T = (float*)(base + o_t);
+    out->fin = (float4*)(base + o_f);
     out->n_contrib = (uint32_t*)(base + o_n);
     out->tile_max = (uint32_t*)(base + o_m);
-    out->tile_order = (uint32_t*)(base + o_o);
     out->tile_cut = (uint32_t*)(base + o_c);
-    out->tile_done = (uint64_t*)(base + o_d);
-    out->len_hist = (uint32_t*)(out->tile_done + tiles);
-    out->cut_max = out->len_hist + ORDER_GROUPS * ORDER_BUCKETS;
-    out->tile_brank = (uint32_t*)(base + o_b);
+    out->tile_fin = (uint32_t*)(base + o_d);
+    out->sched = out->tile_fin + TILE_FIN_STRIDE * tiles;
   }
   return off;
 }
+
+#ifdef GS_TIMING
+// Diagnostic builds only (-DGS_TIMING; tools/bwd_timing.py, tools/fwd_timing.py): per-wave
+// s_memrealtime stamps (100 MHz) of the render kernels, one buffer per kernel (per code object):
+// [b][0] start, [1] end, [2] a << 32 | b, [3] xcc_id << 32 | hw_id, [4] c << 32 | d (the kernel's
+// own counts).  Nothing in the kernels reads them.
+constexpr int TIMING_MAX = 1 << 16;
+#define GS_TIMING_BUFFER(buf, fn)                                                                   \
+  __device__ unsigned long long buf[TIMING_MAX][5];                                                 \
+  extern "C" int fn(unsigned long long* host_out, int n, int reset) {                               \
+    if (n > TIMING_MAX) n = TIMING_MAX;                                                             \
+    if (host_out && hipMemcpyFromSymbol(host_out, HIP_SYMBOL(buf), (size_t)n * 5 * 8) != hipSuccess) \
+      return 1;                                                                                     \
+    if (reset) {                                                                                    \
+      void* p = nullptr;                                                                            \
+      if (hipGetSymbolAddress(&p, HIP_SYMBOL(buf)) != hipSuccess) return 1;                          \
+      if (hipMemset(p, 0, sizeof(buf)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return 1; \
+    }                                                                                               \
+    return 0;                                                                                       \
+  }
+__device__ __forceinline__ unsigned long long timing_stamp() {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+__device__ __forceinline__ void timing_record(unsigned long long (*buf)[5], unsigned long long t0, uint32_t a,
+                                              uint32_t b, uint32_t c, uint32_t d) {
+  const unsigned long long t1 = timing_stamp();
+  if (threadIdx.x == 0 && blockIdx.x < TIMING_MAX) {
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    unsigned long long* o = buf[blockIdx.x];
+    o[0] = t0;
+    o[1] = t1;
+    o[2] = ((unsigned long long)a << 32) | b;
+    o[3] = ((unsigned long long)xcc << 32) | hw;
+    o[4] = ((unsigned long long)c << 32) | d;
+  }
+}
+#endif
 
 // ---- stages (gs_forward.hip / gs_backward.hip) ----
 void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st);
@@ -489,8 +502,6 @@ void bwd_records(const GaussianArgs& g, const GeomPtrs& geo, const BinPtrs& bin,
 void bwd_preprocess(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin,
                     const ImgPtrs& img, float* gradrec, uint32_t R,
                     bool have_records, const GradOut& out, hipStream_t st);
-// bytes of the gradient scratch past the R records (gs_grad_buffer_bytes)
-size_t sumrec_extra_bytes(size_t R);
 void knn_mean_dist2(int P, const float* pts, float* out, char* scratch, hipStream_t st);
 void ssim_forward(int planes, int H, int W, const float* win11, const float* img1, const float* img2, float* dmaps,
                   float* partial, float* plane_sum, hipStream_t st);

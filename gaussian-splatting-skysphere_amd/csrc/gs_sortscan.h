@@ -324,14 +324,12 @@ inline int radix_width(int end_bit) {
   const int np = radix_passes(end_bit);
   return (end_bit + np - 1) / np;
 }
-#ifndef GS_SORT_NARROW_FIRST
-#define GS_SORT_NARROW_FIRST 1
-#endif
-// width of the first pass: the full width, or (GS_SORT_NARROW_FIRST) the remainder (13 -> 6 + 7)
+// width of the first pass: the remainder (13 -> 6 + 7; the narrower digit first saved 3.6 us over
+// the C3 tile sort's six scatters)
 inline int radix_first_bits(int end_bit) {
   const int w = radix_width(end_bit);
   if (end_bit <= w) return end_bit;
-  return GS_SORT_NARROW_FIRST ? end_bit - (radix_passes(end_bit) - 1) * w : w;
+  return end_bit - (radix_passes(end_bit) - 1) * w;
 }
 
 // max_blocks: workgroups per pass (each takes whole 2048-key tiles); fewer, longer workgroups
@@ -347,11 +345,15 @@ inline SortPlan sort_plan(uint64_t n_max, uint32_t max_blocks = SORT_MAX_BLOCKS)
   return p;
 }
 
-// scratch words needed by radix_sort_pairs: [digit][block] histogram + per-digit row totals
+// scratch words needed by radix_sort_pairs: [digit][block] histogram + per-digit row totals.  Sized
+// for min(tiles, SORT_MAX_BLOCKS) blocks, an upper bound of sort_plan's nb (which drops when n passes
+// a multiple of SORT_MAX_BLOCKS tiles) that never decreases with n: every buffer size built from it
+// grows monotonically with its count, which gs_binning_layout_count's search relies on.
 inline size_t sort_scratch_words(uint64_t n_max) {
-  SortPlan p = sort_plan(n_max);
-  size_t hist = (size_t)RADIX * p.nb;
-  return hist + RADIX + 16;
+  uint64_t tiles = (n_max + SORT_TILE - 1) / SORT_TILE;
+  if (tiles == 0) tiles = 1;
+  const size_t nb = (size_t)(tiles < SORT_MAX_BLOCKS ? tiles : SORT_MAX_BLOCKS);
+  return (size_t)RADIX * nb + RADIX + 16;
 }
 
 // View batching: one launch sorts the same-shaped arrays of several views (blockIdx.y = view) whose
@@ -453,19 +455,10 @@ static __global__ __launch_bounds__(SORT_THREADS) void k_radix_rowscan(uint32_t*
 
 // AUX: a second value stream travels with the keys (aux_in[i] -> aux_out[pos]).  BITS: the digit
 // width, a template parameter so the ballot ranking unrolls.
-#ifndef GS_SCATTER_WPE
-// > 0: ask for that many waves per SIMD (register budget 512 / WPE).  With the 32-bit positions the
-// scatter takes 86 VGPRs (5 waves / SIMD; 64-bit: 108, 4 waves): C3 1026 -> 1037 it/s, scatter
-// 19.4 -> 18.1 us, C5 486 -> 496 it/s.  6 (80 VGPRs, one spill): no further change.
-#define GS_SCATTER_WPE 0
-#endif
-#if GS_SCATTER_WPE > 0
-#define GS_SCATTER_ATTR __attribute__((amdgpu_waves_per_eu(GS_SCATTER_WPE)))
-#else
-#define GS_SCATTER_ATTR
-#endif
+// 32-bit positions: the scatter takes 86 VGPRs (5 waves / SIMD; 64-bit: 108, 4 waves): C3 1026 ->
+// 1037 it/s, scatter 19.4 -> 18.1 us.  6 waves requested (80 VGPRs, one spill): no further change.
 template <bool AUX, int BITS>
-__global__ __launch_bounds__(SORT_THREADS) GS_SCATTER_ATTR void k_radix_scatter(
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, const uint32_t* n_dev, uint32_t n_max, int shift, uint32_t chunk,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ row_total, bool drop,

@@ -23,13 +23,10 @@
 
 namespace gs {
 
-#ifndef GS_ADAM_NT
-// 1: non-temporal 16-B loads / stores.  C3 train step: k_adam 310 -> 264 us, and the next
+// k_adam uses non-temporal 16-B loads / stores.  C3 train step: k_adam 310 -> 264 us, and the next
 // iteration's k_activate_fwd 100 -> 72 us (no dirty lines of the update left to write back).
 // Non-temporal accesses in the activation kernels measured slower or neutral (their lane-strided
 // scalar stores lose the cache's line merging: k_activate_bwd 101 -> 354 us).
-#define GS_ADAM_NT 1
-#endif
 // One launch updates up to ADAM_MAX_TENSORS parameter tensors; a thread owns 4 consecutive
 // elements of one tensor (16-B loads/stores of p, g, m, v when aligned, scalar tail otherwise).
 struct AdamLaunch {
@@ -111,23 +108,14 @@ __global__ __launch_bounds__(256) void k_adam(AdamLaunch a, uint64_t total_chunk
   const bool vec = i + 4 <= n && (((uintptr_t)p | (uintptr_t)m | (uintptr_t)v) & 15) == 0 &&
                    (mode == AG_SH_DC || mode == AG_SH_REST || (((uintptr_t)g) & 15) == 0);
   if (vec) {
-#if GS_ADAM_NT
     // streaming: every byte is touched once per step and the step's 1.65 GB (C3) exceeds the caches
     typedef float v4f __attribute__((ext_vector_type(4)));
     v4f P = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
     v4f M = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(m));
     v4f V = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(v));
-#else
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    v4f P = *reinterpret_cast<const v4f*>(p), M = *reinterpret_cast<const v4f*>(m), V = *reinterpret_cast<const v4f*>(v);
-#endif
     float G[4];
     if (mode == AG_PLAIN) {
-#if GS_ADAM_NT
       const v4f Gv = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(g));
-#else
-      const v4f Gv = *reinterpret_cast<const v4f*>(g);
-#endif
       G[0] = Gv.x, G[1] = Gv.y, G[2] = Gv.z, G[3] = Gv.w;
     } else if (mode == AG_NORMALIZE) {
       const float4 gq = *reinterpret_cast<const float4*>(g);
@@ -154,13 +142,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamLaunch a, uint64_t total_chunk
       adam_one(pe, G[e], me, ve, a, ss, ib, wd);
       P[e] = pe, M[e] = me, V[e] = ve;
     }
-#if GS_ADAM_NT
     __builtin_nontemporal_store(P, reinterpret_cast<v4f*>(p));
     __builtin_nontemporal_store(M, reinterpret_cast<v4f*>(m));
     __builtin_nontemporal_store(V, reinterpret_cast<v4f*>(v));
-#else
-    *reinterpret_cast<v4f*>(p) = P, *reinterpret_cast<v4f*>(m) = M, *reinterpret_cast<v4f*>(v) = V;
-#endif
   } else {
     const int cnt = (int)(n - i < 4 ? n - i : 4);
     float G[4];

@@ -41,6 +41,32 @@ def test_sizing_functions_run_without_gpu():
     assert lib.gs_grad_buffer_bytes(10) >= 360
 
 
+def test_binning_layout_count_recovers_the_sized_layout():
+    """The backward recovers the binning buffer's layout count from its byte size
+    (gs_binning_layout_count): the largest count whose gs_binning_buffer_bytes fits.  That is only the
+    layout the buffer was sized for if the size never decreases with the count -- in particular
+    across the radix sort's block-count steps, where sort_plan's block count drops (every
+    4096 x 2048 = 2^23 instances).  Counts around those steps and random ones."""
+    import random
+
+    from diff_gaussian_rasterization import _native
+
+    lib = _native.load()
+    W, H = 1920, 1080
+    step = 1 << 23
+    counts = [1, 63, 64, 65, 2047, 2048, 2049, 4_330_000]
+    for k in (1, 2, 3):
+        counts += [k * step + d for d in (-2049, -2048, -1, 0, 1, 2048, 2049)]
+    rng = random.Random(0)
+    counts += [rng.randrange(1, 40_000_000) for _ in range(40)]
+    for c in sorted(counts):
+        b = lib.gs_binning_buffer_bytes(c, W, H)
+        assert lib.gs_binning_buffer_bytes(c + 1, W, H) >= b, c
+        assert lib.gs_binning_buffer_bytes(c + 2048, W, H) >= b, c
+        L = lib.gs_binning_layout_count(b, W, H)
+        assert L >= c and lib.gs_binning_buffer_bytes(L, W, H) == b, (c, L)
+
+
 def test_code_object_targets_gfx950():
     from diff_gaussian_rasterization import _native
 

@@ -1,13 +1,9 @@
-"""Critical path of the backward render: per-wave start / end stamps of one launch.
+"""Critical path of the forward render (k_render_fwd_q): per quadrant-wave start / end stamps.
 
-Needs a library built with -DGS_BWD_TIMING (make -C gaussian-splatting-skysphere_amd BUILD=build_timing
-EXTRA=-DGS_BWD_TIMING) and GSRAST_LIB pointing at it.  Runs the batch-1 loop (bench.py's single_view
-shape), then one more iteration with the stamp buffer cleared, and reports for the persistent
-segmented kernel (k_render_bwd_seg): the launch's span, when its waves end (the drain), the resident
-waves over time, the units and entries each wave took, per-XCD spans.  The stamps are
-s_memrealtime (100 MHz).  Round 4's one-wave-per-tile kernel (k_render_bwd_tw) was measured with the
-previous version of this script (git history; profiles/r05_bwd_timing_c3_v0.json).
-"""
+Needs a library built with -DGS_TIMING (make -C gaussian-splatting-skysphere_amd BUILD=build_timing
+EXTRA=-DGS_TIMING) and GSRAST_LIB pointing at it.  Runs the batch-1 loop (bench.py's single_view
+shape), then stamped iterations, and reports the launch's span, the resident waves over time, when
+the last waves start and how long waves last (by batches staged and entries walked)."""
 import argparse
 import ctypes
 import json
@@ -27,7 +23,7 @@ from diff_gaussian_rasterization import GaussianRasterizer, _native  # noqa: E40
 WL = {"c3": (1_000_000, 3, 1920, 1080), "c2": (100_000, 3, 800, 800), "c5": (5_000_000, 3, 1920, 1080)}
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c3")
-ap.add_argument("--reps", type=int, default=3, help="stamped launches (each one iteration after warm-up)")
+ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 P, deg, W, H = WL[a.workload]
@@ -39,8 +35,8 @@ bucket = vp.GradBucket(params, lazy_zero=True, defer=False)
 dpix = gs_scenes.dl_dimage(H, W).to(dev)
 r = GaussianRasterizer(gs_scenes.raster_settings_for(cam, deg, device=dev))
 lib = _native.load()
-lib.gs_debug_bwd_timing.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, ctypes.c_int]
-lib.gs_debug_bwd_timing.restype = ctypes.c_int
+lib.gs_debug_fwd_timing.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, ctypes.c_int]
+lib.gs_debug_fwd_timing.restype = ctypes.c_int
 
 
 def step():
@@ -54,52 +50,47 @@ def step():
 for _ in range(20):
     step()
 torch.cuda.synchronize()
-slots = 1 << 16  # the timing buffer's capacity (BWD_TIMING_MAX waves)
+slots = 1 << 16
 reports = []
 for rep in range(a.reps):
-    assert lib.gs_debug_bwd_timing(None, 0, 1) == 0
+    assert lib.gs_debug_fwd_timing(None, 0, 1) == 0
     lib.gs_profile_reset()
     lib.gs_profile_enable(1)
     step()
     torch.cuda.synchronize()
     lib.gs_profile_enable(0)
-    ev_us = 1e3 * _native.profile_stats()["render_bwd"][0]
+    ev_us = 1e3 * _native.profile_stats()["render_fwd"][0]
     buf = (ctypes.c_ulonglong * (slots * 5))()
-    assert lib.gs_debug_bwd_timing(buf, slots, 0) == 0
+    assert lib.gs_debug_fwd_timing(buf, slots, 0) == 0
     d = np.frombuffer(buf, dtype=np.uint64).reshape(slots, 5)
     d = d[d[:, 1] != 0]
     t0 = d[:, 0].astype(np.int64)
     t1 = d[:, 1].astype(np.int64)
     base = t0.min()
-    s_us = (t0 - base) / 100.0  # 100 MHz -> us
+    s_us = (t0 - base) / 100.0
     e_us = (t1 - base) / 100.0
     dur = e_us - s_us
-    units = (d[:, 2] >> 32).astype(np.int64)  # backward units (tile, depth segment) the wave walked
-    walked = (d[:, 4] >> 32).astype(np.int64)
-    nslots = (d[:, 4] & 0xFFFFFFFF).astype(np.int64)
-    xcc = (d[:, 3] >> 32).astype(np.int64) & 0xF
+    batches = (d[:, 4] >> 32).astype(np.int64)
+    walked = (d[:, 4] & 0xFFFFFFFF).astype(np.int64)
     span = e_us.max()
     nb = int(np.ceil(span)) + 1
     occ = np.zeros(nb)
     for s, e in zip(s_us, e_us):
         occ[int(s):int(np.ceil(e))] += 1
-    per_xcd = {}
-    for x in range(8):
-        m = xcc == x
-        if m.any():
-            per_xcd[int(x)] = {"waves": int(m.sum()), "last_end": round(float(e_us[m].max()), 1),
-                               "units": int(units[m].sum()), "entries": int(walked[m].sum())}
-    frac_run = {f"{f:.2f}": int(((s_us <= f * span) & (e_us > f * span)).sum()) for f in (0.5, 0.7, 0.8, 0.9, 0.95)}
+    X = np.stack([np.ones_like(dur), batches, walked], 1)
+    coef, *_ = np.linalg.lstsq(X, dur, rcond=None)
     rep_d = {
         "workload": a.workload, "rep": rep, "event_us": round(ev_us, 1), "span_us": round(float(span), 1),
-        "waves": int(len(dur)), "units": int(units.sum()), "entries_walked": int(walked.sum()),
-        "slots_evaluated": int(nslots.sum()), "last_start_us": round(float(s_us.max()), 1),
-        "end_pct_of_span": {p: round(float(np.percentile(e_us, p) / span), 3) for p in (1, 10, 50, 90, 99)},
-        "units_per_wave": {p: int(np.percentile(units, p)) for p in (1, 50, 99)},
+        "waves": int(len(dur)), "max_resident": int(occ.max()),
+        "last_start_us": round(float(s_us.max()), 1), "longest_wave_us": round(float(dur.max()), 1),
+        "dur_pct": {p: round(float(np.percentile(dur, p)), 1) for p in (10, 50, 90, 99)},
+        "batches_pct": {p: int(np.percentile(batches, p)) for p in (10, 50, 90, 99)},
+        "walked_pct": {p: int(np.percentile(walked, p)) for p in (10, 50, 90, 99)},
+        "model_us": {"const": round(float(coef[0]), 2), "per_batch": round(float(coef[1]), 3),
+                     "per_entry": round(float(coef[2]), 4)},
         "resident_waves_by_10pct": [round(float(occ[int(i * nb / 10):int((i + 1) * nb / 10)].mean()), 0)
                                     for i in range(10)],
-        "running_at_frac_of_span": frac_run,
-        "per_xcd": per_xcd,
+        "starts_by_10pct": [int(((s_us >= i * span / 10) & (s_us < (i + 1) * span / 10)).sum()) for i in range(10)],
     }
     reports.append(rep_d)
     print(json.dumps(rep_d), flush=True)
