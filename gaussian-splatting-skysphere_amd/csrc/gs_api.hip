@@ -1418,9 +1418,7 @@ int gs_debug_export(int P, int W, int H, long long num_rendered, const void* geo
   if (tiles_touched)
     check_hip(hipMemcpyAsync(tiles_touched, geo.tiles, sizeof(uint32_t) * P, hipMemcpyDeviceToDevice, st), "copy");
   if (final_T)
-    // T_final is the fourth word of each pixel's fin record
-    check_hip(hipMemcpy2DAsync(final_T, sizeof(float), reinterpret_cast<const char*>(img.fin) + 12, sizeof(float4),
-                               sizeof(float), (size_t)W * H, hipMemcpyDeviceToDevice, st), "copy");
+    check_hip(hipMemcpyAsync(final_T, img.final_T, sizeof(float) * W * H, hipMemcpyDeviceToDevice, st), "copy");
   if (n_contrib)
     check_hip(hipMemcpyAsync(n_contrib, img.n_contrib, sizeof(uint32_t) * W * H, hipMemcpyDeviceToDevice, st), "copy");
   return t_failed ? 1 : 0;

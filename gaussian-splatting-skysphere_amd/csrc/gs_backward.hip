@@ -21,14 +21,14 @@
 namespace gs {
 
 #ifdef GS_TIMING
-// diagnostic build only (-DGS_TIMING, tools/bwd_timing.py): per persistent backward wave b
-// (blockIdx.x): start / end stamps, units walked, hw ids, entries walked / slots evaluated
+// diagnostic build only (-DGS_TIMING, tools/bwd_timing.py): per backward wave b (blockIdx.x): start /
+// end stamps, tile << 32 | n_eff, hw ids, entries walked << 32 | slots evaluated
 GS_TIMING_BUFFER(g_bwd_timing, gs_debug_bwd_timing)
 #define GS_BWD_T0() const unsigned long long t_start = timing_stamp()
-#define GS_BWD_TREC(units, walked, slots) timing_record(g_bwd_timing, t_start, units, 0u, walked, slots)
+#define GS_BWD_TREC(tile, n_eff, walked, slots) timing_record(g_bwd_timing, t_start, tile, n_eff, walked, slots)
 #else
 #define GS_BWD_T0() (void)0
-#define GS_BWD_TREC(units, walked, slots) (void)0
+#define GS_BWD_TREC(tile, n_eff, walked, slots) (void)0
 #endif
 
 // a 36-B gradient record as three 12-B stores (global_store_dwordx3; 4-B alignment is enough)
@@ -44,37 +44,22 @@ __device__ __forceinline__ void load_rec(const float* p, float* v) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Segmented tile-wave backward (round 5): ONE wave64 per (tile, depth segment), four pixel slots
-// per lane, persistent waves taking segments from a device queue.
-//
-// Round 4's kernel ran one wave per tile.  Its per-wave stamps (tools/bwd_timing.py,
-// profiles/r05_bwd_timing_c3_v0.json) show what set its time: every SIMD held its 5 waves for the
-// first 60 % of the launch, then drained -- 8,160 tile waves of ~220 walked entries each are only
-// 1.6 generations of the 5,120 resident slots, so the last generation's waves (started at 58 % of
-// the span, each ~45 % of the span long) left the SIMDs 4,123 / 2,998 / 1,703 / 217 resident waves
-// in the last four tenths: ~25 % of the launch was drain.  Splitting each tile's list into depth
-// segments of SEG entries makes the units short and uniform, and a queue keeps every SIMD fed
-// until the last ~one segment.
-//
-// A segment [lo, hi) of a tile is walked back to front like the whole list was: it needs each
-// pixel's state at hi -- the transmittance T_hi and U_hi = sum over the entries behind hi of
-// (colour . dL/dpix) alpha T + T_final bg . dL/dpix.  The forward's quadrant waves store (T, C) at
-// every segment boundary they reach (ckpt, C = the colour composited so far); with C_fin the
-// pixel's final colour (fin), U_hi = dL/dpix . (C_fin - C_hi) + T_final bg . dL/dpix.  A quadrant
-// whose pixels all stopped before hi (hi >= its largest n_contrib) starts from the final state, as
-// the whole-list walk did.  The per-entry arithmetic is unchanged; the start states are the
-// forward's own T (not recovered by division across the segments behind), so the gradients differ
-// from round 4's in rounding only.
+// Tile-wave backward: ONE wave64 per tile, four pixel slots per lane.
 //
 // Lane l owns pixel (l & 7, l >> 3) of each 8x8 quadrant k of the tile (slot k).  A staged entry
 // carries the set of quadrants its alpha >= 1/255 ellipse meets (the forward's per-quadrant cull)
-// and the walk evaluates and commits only those slots (143 pixel slots per walked entry at C3
-// against 193 for two 8x16 half waves, tools/bwd_layout_stats.py), and the nine per-entry sums are
-// reduced over the wave ONCE per tile entry.  The lane's slots are pre-summed in registers (one FMA
-// per term and slot).  One wave per workgroup: staging, walk and flush need no workgroup barrier,
-// and every lane stages (and later flushes) one entry of a 64-entry batch, keeping that entry's raw
-// conic, opacity and slot in its registers.
+// and the walk evaluates and commits only those slots: the C3 oracle study
+// (tools/bwd_layout_stats.py, profiles/r04_bwd_layout_stats_c3.txt) puts the pixel slots
+// evaluated per walked entry at 143 (quadrant slots) against 193 for the two 8x16 half waves of
+// k_render_bwd, and the nine per-entry sums are reduced over the wave ONCE per tile entry (0.86
+// reductions per walked entry instead of 1.36).  The lane's slots are pre-summed in registers
+// (one FMA per term and slot).  One wave per workgroup: staging, walk and flush need no workgroup
+// barrier, and every lane stages (and later flushes) one entry of a 64-entry batch, keeping that
+// entry's raw conic, opacity and slot in its registers.
+// Same per-pixel recurrence and decisions as k_render_bwd (and as the forward); only the order in
+// which a tile entry's per-pixel terms are summed differs.
 // ------------------------------------------------------------------------------------------
+
 struct BwdSlot {
   float T, U, d0, d1, d2;
   uint32_t last;
@@ -106,7 +91,7 @@ __device__ __forceinline__ uint64_t bwd_slot(BwdSlot& q, float pfx, float pfy, c
   // box (u = dx - (mean - r) = r - pixel): for a splat centred in the tile u is dx itself, for one
   // centred outside it |u| <= 15 instead of the distance to the mean -- the terms stay small, so
   // the fp32 sums keep the precision the covariance chain needs.  The flush shifts them to the
-  // mean in fp64 (k_render_bwd_seg).
+  // mean in fp64 (k_render_bwd_tw).
   const float mx = dx - br.y, my = dy - br.z;
   const float qx = qq * mx, qy = qq * my;
   s[0] = __builtin_fmaf(dch, q.d0, s[0]);
@@ -127,259 +112,86 @@ __device__ __forceinline__ uint64_t bwd_slot(BwdSlot& q, float pfx, float pfy, c
   return m;
 }
 
-struct SegArgs {
-  const float4* fin;        // per pixel (C0, C1, C2, T_final)
-  const float4* ckpt;       // segment-boundary states (bin_layout: ckpt)
-  const uint2* table;       // per XCD group, cap (tile, segment) units: full segments from the front,
-  uint32_t cap;             //   partial ones from the back
-  uint32_t* sched;          // SCHED_* words (image buffer); the take counters are zeroed by k_tile_cut
-};
-
 template <bool EXACT>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_render_bwd_seg(CameraArgs c, const uint2* __restrict__ ranges,
-                                                       const uint32_t* __restrict__ point_list,
-                                                       const uint32_t* __restrict__ point_gid,
-                                                       const float4* __restrict__ splat,
-                                                       const uint32_t* __restrict__ n_contrib,
-                                                       const uint32_t* __restrict__ tile_max, SegArgs sa,
-                                                       const float* __restrict__ dL_dpix,
-                                                       float* __restrict__ gradrec) {
+__global__ __launch_bounds__(64) void k_render_bwd_tw(CameraArgs c, const uint2* __restrict__ ranges,
+                                                                    const uint32_t* __restrict__ point_list,
+                                                                    const uint32_t* __restrict__ point_gid,
+                                                                    const float4* __restrict__ splat,
+                                                                    const float* __restrict__ final_T,
+                                                                    const uint32_t* __restrict__ n_contrib,
+                                                                    const uint32_t* __restrict__ tile_max,
+                                                                    const uint32_t* __restrict__ tile_order,
+                                                                    const float* __restrict__ dL_dpix,
+                                                                    float* __restrict__ gradrec) {
   __shared__ float4 s_xy[64];  // (x, y, r, g)
   __shared__ float4 s_co[64];  // falloff coefficients + opacity (fall_coefs)
   __shared__ float4 s_br[64];  // (b, mean - r: x, y, -), r the moments' reference point (bwd_slot)
   // entry rows of 16 floats (a stride of 20, which puts the flush's 16-B row reads on distinct
-  // banks, measured 343 -> 361 us at C3 in round 4)
+  // banks, measured 343 -> 361 us at C3)
   constexpr int ROW = 16;
   __shared__ __attribute__((aligned(16))) float s_acc[64][ROW];
   GS_BWD_T0();
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(tile_order ? tile_order[blockIdx.x] : blockIdx.x);
+  if (tile == ~0u) return;  // a hole of the XCD-group launch order
+  const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int lane = threadIdx.x;
-  // Units are queued per XCD group (the tiles whose forward ran on XCD g): a wave takes its own
-  // XCD's units first (their splat records were fetched into this XCD's L2 by neighbouring tiles),
-  // then helps the other groups in turn.  Which XCD runs a wave only affects where a unit is
-  // walked, never its result.
-  uint32_t grp = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
-  uint32_t tried = 1;
-  auto group_total = [&](uint32_t g, uint32_t& nfront) {
-    nfront = __builtin_amdgcn_readfirstlane(sa.sched[SCHED_FRONT + SCHED_STRIDE * g]);
-    return nfront + __builtin_amdgcn_readfirstlane(sa.sched[SCHED_BACK + SCHED_STRIDE * g]);
-  };
-  auto take_unit = [&](uint32_t g) {
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(&sa.sched[SCHED_NEXT + SCHED_STRIDE * g], 1u);
-    return t;
-  };
-  uint32_t nfront, total = group_total(grp, nfront);
-  uint32_t s_cur = __builtin_amdgcn_readfirstlane(take_unit(grp));
+  const uint2 range = ranges[tile];
+  const uint32_t n = range.y - range.x;
+  // per-quadrant largest n_contrib (the forward's quadrant waves): slot k's walk ends there
+  const uint4 qm = reinterpret_cast<const uint4*>(tile_max)[tile];
+  const uint32_t qlast[4] = {min(qm.x, n), min(qm.y, n), min(qm.z, n), min(qm.w, n)};
+  const uint32_t n_eff = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
+  if (n_eff == 0) {
+    GS_BWD_TREC(tile, 0u, 0u, 0u);
+    return;  // no instance walked: no records (k_sum_records reads none below a cut of 0)
+  }
 #ifdef GS_TIMING
-  uint32_t t_walked = 0, t_slots = 0, t_segs = 0;
+  uint32_t t_walked = 0, t_slots = 0;
 #endif
+
   const size_t HW = (size_t)c.W * c.H;
+  const int qx0 = tx * GS_TILE + (lane & 7), qy0 = ty * GS_TILE + (lane >> 3);
+  BwdSlot p[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int px = qx0 + 8 * (k & 1), py = qy0 + 8 * (k >> 1);
+    const bool in = px < c.W && py < c.H;
+    const size_t pix = in ? (size_t)py * c.W + px : 0;
+    const float Tf = in ? final_T[pix] : 0.0f;
+    p[k].T = Tf;
+    p[k].last = in ? n_contrib[pix] : 0u;
+    p[k].d0 = in ? dL_dpix[pix] : 0.0f;
+    p[k].d1 = in ? dL_dpix[HW + pix] : 0.0f;
+    p[k].d2 = in ? dL_dpix[2 * HW + pix] : 0.0f;
+    // U = S + T_final bg . dL/dpix (see k_render_bwd)
+    p[k].U = Tf * (c.bg[0] * p[k].d0 + c.bg[1] * p[k].d1 + c.bg[2] * p[k].d2);
+  }
   const float ddelx_dx = (float)(0.5 * c.W), ddely_dy = (float)(0.5 * c.H);
-  // the background in scalar registers (loop-invariant vector registers would cost the walk's budget)
-  const float bgd[3] = {__uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(c.bg[0]))),
-                        __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(c.bg[1]))),
-                        __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(c.bg[2])))};
+  const float pfx0 = (float)qx0, pfy0 = (float)qy0;
   using lds_float = __attribute__((address_space(3))) float;
   // writer lanes 16 r + 8 h: s[r + 4 h] at slot r + 4 h, their s8 partial at slot 8 + r + 4 h
   lds_float* const acc_lane = (lds_float*)(&s_acc[0][(lane >> 4) + 4 * ((lane >> 3) & 1)]);
   const bool hi8 = (lane & 8) != 0;
-  // lanes holding a mapped record in their LDS row (the last flushed batch, possibly of the previous
-  // unit: its stores go out behind the next batch's loads, as within a unit)
-  uint32_t rec_lanes = 0;
-  // every wave leaves once every group's queue is empty (the counters only grow)
-  for (;;) {
-    if (s_cur >= total) {
-      if (tried == ORDER_GROUPS) break;
-      tried++;
-      grp = (grp + 1u) & 7u;
-      total = group_total(grp, nfront);
-      s_cur = __builtin_amdgcn_readfirstlane(take_unit(grp));
-      continue;
-    }
-    const uint2 unit = sa.table[(size_t)grp * sa.cap + (s_cur < nfront ? s_cur : sa.cap - 1u - (s_cur - nfront))];
-    const uint32_t tile = __builtin_amdgcn_readfirstlane(unit.x), seg = __builtin_amdgcn_readfirstlane(unit.y);
-    const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
-    const uint2 range = ranges[tile];
-    const uint32_t n = range.y - range.x;
-    // per-quadrant largest n_contrib (the forward's quadrant waves): slot k's walk ends there
-    const uint4 qm = reinterpret_cast<const uint4*>(tile_max)[tile];
-    const uint32_t qlast[4] = {min(qm.x, n), min(qm.y, n), min(qm.z, n), min(qm.w, n)};
-    const uint32_t n_eff = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
-    const uint32_t lo = SEG * seg, hi = min(lo + SEG, n_eff);  // this unit's list positions [lo, hi)
-    // the states at hi (read for every slot, used where the quadrant's walk goes on behind hi; the
-    // unit that ends at n_eff reads the array's first states instead, unused)
-    const float4* const ck = sa.ckpt + (hi < n_eff ? ((size_t)(range.x / SEG + hi / SEG) << 8) : 0);
-    const int qx0 = tx * GS_TILE + (lane & 7), qy0 = ty * GS_TILE + (lane >> 3);
-    BwdSlot p[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int px = qx0 + 8 * (k & 1), py = qy0 + 8 * (k >> 1);
-      const bool in = px < c.W && py < c.H;
-      const size_t pix = in ? (size_t)py * c.W + px : 0;
-      const float4 f = in ? sa.fin[pix] : make_float4(0.f, 0.f, 0.f, 0.f);
-      p[k].last = in ? n_contrib[pix] : 0u;
-      p[k].d0 = in ? dL_dpix[pix] : 0.0f;
-      p[k].d1 = in ? dL_dpix[HW + pix] : 0.0f;
-      p[k].d2 = in ? dL_dpix[2 * HW + pix] : 0.0f;
-      // U = S + T_final bg . dL/dpix (S: the (colour . dL/dpix) alpha T of the entries behind)
-      const float ub = f.w * (bgd[0] * p[k].d0 + bgd[1] * p[k].d1 + bgd[2] * p[k].d2);
-      // the quadrant's walk goes on behind hi: the forward's state there (uniform select; the load is
-      // unconditional so the unit's loads are all in flight at once)
-      typedef float v4f __attribute__((ext_vector_type(4)));
-      const v4f tv = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(ck + 64 * k + lane));
-      const float4 t = make_float4(tv.x, tv.y, tv.z, tv.w);
-      const bool behind = hi < qlast[k];
-      p[k].T = behind ? t.x : f.w;
-      p[k].U = behind ? __builtin_fmaf(p[k].d2, f.z - t.w, __builtin_fmaf(p[k].d1, f.y - t.z, p[k].d0 * (f.x - t.y))) + ub
-                      : ub;
-    }
-    const float pfx0 = (float)qx0, pfy0 = (float)qy0;
 
-    // staging pipeline (one entry per lane): while batch b is walked, the splat records of batch
-    // b + 1, the ids of batch b + 2 and the slots of batch b + 3 are in flight.  Batch b's entry of
-    // lane t sits at list position e0 - 64 b, e0 = hi - 1 - t.  The loads are unconditional, with
-    // positions below lo clamped to lo (a valid entry of this unit: a cache hit, no traffic): a
-    // load under a condition has to keep the register's old value on the other path, and the copy
-    // that merges the two makes the compiler wait for the load right where it is issued.
-    const int32_t e0 = (int32_t)hi - 1 - lane;
-    const uint32_t* const plist = point_list + range.x;
-    auto pos = [&](int32_t e) { return (uint32_t)max(e, (int32_t)lo); };
-    uint32_t slot_c = plist[pos(e0)];
-    uint32_t G1 = point_gid[slot_c];
-    float4 pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
-    uint32_t S1 = plist[pos(e0 - 64)];
-    G1 = point_gid[S1];
-    uint32_t S2 = plist[pos(e0 - 128)];
+  // staging pipeline (one entry per lane): while batch k is walked, the splat records of batch
+  // k + 1, the ids of batch k + 2 and (ids by slot) the slots of batch k + 3 are in flight.
+  // Batch k's entry of lane t sits at list position range.x + e0 - 64 k, e0 = n_eff - 1 - t.
+  // The loads are unconditional, with list positions below 0 clamped to 0 (a valid entry: the
+  // lane stages nothing then): a load under a condition has to keep the register's old value on
+  // the other path, and the copy that merges the two makes the compiler wait for the load right
+  // where it is issued instead of at the next batch.
+  const int32_t e0 = (int32_t)n_eff - 1 - lane;
+  const uint32_t* const plist = point_list + range.x;
+  auto pos = [&](int32_t e) { return (uint32_t)max(e, 0); };
+  uint32_t slot_c = plist[pos(e0)];
+  uint32_t G1 = point_gid[slot_c];
+  float4 pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
+  uint32_t S1 = plist[pos(e0 - 64)];
+  G1 = point_gid[S1];
+  uint32_t S2 = plist[pos(e0 - 128)];
 
-    auto store_records = [&]() {
-      if ((uint32_t)lane < rec_lanes) {
-        const float4* row = reinterpret_cast<const float4*>(&s_acc[lane][0]);
-        const float4 a = row[0], b = row[1], d = row[2];
-        Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)__float_as_uint(d.y) * GRAD_REC);
-        r[0] = Rec3{a.x, a.y, a.z};
-        r[1] = Rec3{a.w, b.x, b.y};
-        r[2] = Rec3{b.z, b.w, d.x};
-      }
-    };
-    const uint32_t len = hi - lo;
-    for (uint32_t base = 0; base < len; base += 64) {
-      const uint32_t cnt = min(64u, len - base);
-      // stage: lane t holds entry t of the batch (walk order: back to front)
-      const bool mine = (uint32_t)lane < cnt;
-      const uint32_t slot = slot_c;
-      const float ccx = pa.z, ccy = pa.w, ccz = pb.x, cop = pb.y;  // raw conic + opacity (flush)
-      uint32_t qmask = 0;
-      if (mine) {
-        s_xy[lane] = make_float4(pa.x, pa.y, pb.z, pb.w);
-        s_co[lane] = fall_coefs(pa.z, pa.w, pb.x, pb.y);
-        const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
-        s_br[lane] = make_float4(pd.x, pa.x - fminf(fmaxf(pa.x, x0), x0 + 15.0f),
-                                 pa.y - fminf(fmaxf(pa.y, y0), y0 + 15.0f), 0.0f);
-        qmask = quadrant_mask(pa.x, pa.y, pa.z, pa.w, pb.x, pd.z, tx, ty);
-      }
-      // issue the next batch's splat loads, the ids after it and the slots after those
-      const int32_t e1 = e0 - (int32_t)(base + 64);
-      slot_c = S1;
-      pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
-      S1 = S2;
-      G1 = point_gid[S2];
-      S2 = plist[pos(e1 - 128)];
-      // the previous batch's records (mapped by its flush into the lanes' LDS rows, slot in word 9):
-      // stored now, behind this batch's loads, so that the wait for those loads at the next staging
-      // does not also wait for just-issued stores (loads and stores share one counter)
-      store_records();
-      // per-slot entry sets; entries no pixel of quadrant k reaches (e >= qlast[k]) sit at the low bits
-      uint64_t M[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        uint64_t mk = __ballot((qmask >> k) & 1u);
-        const int jmin = (int)hi - (int)qlast[k] - (int)base;  // entry j reaches quadrant k iff j >= jmin
-        if (jmin > 0) mk &= jmin >= 64 ? 0ull : ~((1ull << jmin) - 1ull);
-        M[k] = mk;
-      }
-      __builtin_amdgcn_wave_barrier();
-      uint64_t m = (M[0] | M[1]) | (M[2] | M[3]);
-      uint64_t wrote = 0;
-#pragma unroll 1
-      while (m) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        const float4 xr = s_xy[j], co = s_co[j], br = s_br[j];
-        const uint32_t e = hi - 1 - (base + j);
-        float s[GRAD_REC];
-#pragma unroll
-        for (int t = 0; t < GRAD_REC; t++) s[t] = 0.0f;
-#ifdef GS_TIMING
-        t_walked++;
-        t_slots += ((M[0] >> j) & 1ull) + ((M[1] >> j) & 1ull) + ((M[2] >> j) & 1ull) + ((M[3] >> j) & 1ull);
-#endif
-        uint64_t con = 0;  // lanes with a contributing slot
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          if ((M[k] >> j) & 1ull)
-            con |= bwd_slot<EXACT>(p[k], pfx0 + (float)(8 * (k & 1)), pfy0 + (float)(8 * (k >> 1)), xr, co, br, e, s);
-        if (con != 0) {
-          wrote |= 1ull << j;
-          float d, d8;
-          wave_sum9_halfrows(s, hi8, d, d8);
-          asm volatile("" ::"v"(d), "v"(d8));
-          if ((lane & 7) == 0) {
-            uint32_t eo = j * ROW;
-            asm volatile("" : "+s"(eo));
-            lds_float* acc = acc_lane + eo;
-            acc[0] = d;
-            acc[8] = d8;
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      // flush: lane t maps the sums of its entry into the record (zeros for an entry no pixel took),
-      // written back into its LDS row with the slot; stored by the next batch (or after the loop)
-      if (mine) {
-        float S[GRAD_REC];
-        if ((wrote >> lane) & 1ull) {
-          const float4 a0 = *reinterpret_cast<const float4*>(&s_acc[lane][0]);
-          const float4 a1 = *reinterpret_cast<const float4*>(&s_acc[lane][4]);
-          const float4 a2 = *reinterpret_cast<const float4*>(&s_acc[lane][8]);
-          const float4 a3 = *reinterpret_cast<const float4*>(&s_acc[lane][12]);
-          S[0] = a0.x, S[1] = a0.y, S[2] = a0.z, S[3] = a0.w, S[4] = a1.x, S[5] = a1.y, S[6] = a1.z, S[7] = a1.w;
-          S[8] = ((a2.x + a2.y) + (a2.z + a2.w)) + ((a3.x + a3.y) + (a3.z + a3.w));
-        } else {
-#pragma unroll
-          for (int t = 0; t < GRAD_REC; t++) S[t] = 0.0f;
-        }
-        // S3..S7 are the moments of q about the reference point r; with R = mean - r (dx = u + R):
-        // sum q dx = S3 + R.x S8, sum q dx^2 = S5 + 2 R.x S3 + R.x^2 S8, ... in fp64, one rounding to
-        // the record (R = 0, nothing to shift, for a splat centred in the tile)
-        const float2 R = *reinterpret_cast<const float2*>(&s_br[lane].y);
-        const double Rx = R.x, Ry = R.y, q0 = S[8];
-        const float m1x = (float)__builtin_fma(Rx, q0, (double)S[3]), m1y = (float)__builtin_fma(Ry, q0, (double)S[4]);
-        __builtin_amdgcn_sched_barrier(0);
-        const float m2xx = (float)__builtin_fma(Rx, __builtin_fma(Rx, q0, 2.0 * (double)S[3]), (double)S[5]);
-        __builtin_amdgcn_sched_barrier(0);
-        const float m2xy = (float)__builtin_fma(Rx, __builtin_fma(Ry, q0, (double)S[4]),
-                                                __builtin_fma(Ry, (double)S[3], (double)S[6]));
-        __builtin_amdgcn_sched_barrier(0);
-        const float m2yy = (float)__builtin_fma(Ry, __builtin_fma(Ry, q0, 2.0 * (double)S[4]), (double)S[7]);
-        __builtin_amdgcn_sched_barrier(0);
-        float4* row = reinterpret_cast<float4*>(&s_acc[lane][0]);
-        row[0] = make_float4(S[0], S[1], S[2], -ddelx_dx * (ccx * m1x + ccy * m1y));
-        row[1] = make_float4(-ddely_dy * (ccz * m1y + ccy * m1x), -0.5f * m2xx, -0.5f * m2xy, -0.5f * m2yy);
-        // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
-        row[2] = make_float4(S[8] != 0.0f ? S[8] / cop : 0.0f, __uint_as_float(slot), 0.0f, 0.0f);
-      }
-      rec_lanes = cnt;
-      __builtin_amdgcn_wave_barrier();  // the next batch overwrites the staged entries
-    }
-    // the next unit (a value held across the walk would cost a register: 96 VGPRs for 5 waves / SIMD)
-    const uint32_t take = take_unit(grp);
-#ifdef GS_TIMING
-    t_segs++;
-#endif
-    s_cur = __builtin_amdgcn_readfirstlane(take);
-  }
-  // the last unit's records
-  auto store_last = [&]() {
+  uint32_t rec_lanes = 0;  // lanes holding a mapped record in their LDS row (the last flushed batch)
+  auto store_records = [&]() {
     if ((uint32_t)lane < rec_lanes) {
       const float4* row = reinterpret_cast<const float4*>(&s_acc[lane][0]);
       const float4 a = row[0], b = row[1], d = row[2];
@@ -389,22 +201,143 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
       r[2] = Rec3{b.z, b.w, d.x};
     }
   };
-  store_last();
-  GS_BWD_TREC(t_segs, t_walked, t_slots);
+  for (uint32_t base = 0; base < n_eff; base += 64) {
+    const uint32_t cnt = min(64u, n_eff - base);
+    // stage: lane t holds entry t of the batch (walk order: back to front)
+    const bool mine = (uint32_t)lane < cnt;
+    const uint32_t slot = slot_c;
+    const float ccx = pa.z, ccy = pa.w, ccz = pb.x, cop = pb.y;  // raw conic + opacity (flush)
+    uint32_t qmask = 0;
+    if (mine) {
+      s_xy[lane] = make_float4(pa.x, pa.y, pb.z, pb.w);
+      s_co[lane] = fall_coefs(pa.z, pa.w, pb.x, pb.y);
+      const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
+      s_br[lane] = make_float4(pd.x, pa.x - fminf(fmaxf(pa.x, x0), x0 + 15.0f),
+                               pa.y - fminf(fmaxf(pa.y, y0), y0 + 15.0f), 0.0f);
+      qmask = quadrant_mask(pa.x, pa.y, pa.z, pa.w, pb.x, pd.z, tx, ty);
+    }
+    // issue the next batch's splat loads, the ids after it and (ids by slot) the slots after those
+    const int32_t e1 = e0 - (int32_t)(base + 64);
+    slot_c = S1;
+    pa = splat[3 * G1], pb = splat[3 * G1 + 1], pd = splat[3 * G1 + 2];
+    S1 = S2;
+    G1 = point_gid[S2];
+    S2 = plist[pos(e1 - 128)];
+    // the previous batch's records (mapped by its flush into the lanes' LDS rows, slot in word 9):
+    // stored now, behind this batch's loads, so that the wait for those loads at the next staging
+    // does not also wait for just-issued stores (loads and stores share one counter)
+    if (base > 0) store_records();
+    // per-slot entry sets; entries no pixel of quadrant k reaches (e >= qlast[k]) sit at the low bits
+    uint64_t M[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint64_t mk = __ballot((qmask >> k) & 1u);
+      const int jmin = (int)n_eff - (int)qlast[k] - (int)base;  // entry j reaches quadrant k iff j >= jmin
+      if (jmin > 0) mk &= jmin >= 64 ? 0ull : ~((1ull << jmin) - 1ull);
+      M[k] = mk;
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint64_t m = (M[0] | M[1]) | (M[2] | M[3]);
+    uint64_t wrote = 0;
+#pragma unroll 1
+    while (m) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      const float4 xr = s_xy[j], co = s_co[j], br = s_br[j];
+      const uint32_t e = n_eff - 1 - (base + j);
+      float s[GRAD_REC];
+#pragma unroll
+      for (int t = 0; t < GRAD_REC; t++) s[t] = 0.0f;
+#ifdef GS_TIMING
+      t_walked++;
+      t_slots += ((M[0] >> j) & 1ull) + ((M[1] >> j) & 1ull) + ((M[2] >> j) & 1ull) + ((M[3] >> j) & 1ull);
+#endif
+      uint64_t con = 0;  // lanes with a contributing slot
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if ((M[k] >> j) & 1ull)
+          con |= bwd_slot<EXACT>(p[k], pfx0 + (float)(8 * (k & 1)), pfy0 + (float)(8 * (k >> 1)), xr, co, br, e, s);
+      if (con != 0) {
+        wrote |= 1ull << j;
+        float d, d8;
+        wave_sum9_halfrows(s, hi8, d, d8);
+        asm volatile("" ::"v"(d), "v"(d8));
+        if ((lane & 7) == 0) {
+          uint32_t eo = j * ROW;
+          asm volatile("" : "+s"(eo));
+          lds_float* acc = acc_lane + eo;
+          acc[0] = d;
+          acc[8] = d8;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // flush: lane t maps the sums of its entry into the record (zeros for an entry no pixel took),
+    // written back into its LDS row with the slot; stored by the next batch (or after the loop)
+    if (mine) {
+      float S[GRAD_REC];
+      if ((wrote >> lane) & 1ull) {
+        const float4 a0 = *reinterpret_cast<const float4*>(&s_acc[lane][0]);
+        const float4 a1 = *reinterpret_cast<const float4*>(&s_acc[lane][4]);
+        const float4 a2 = *reinterpret_cast<const float4*>(&s_acc[lane][8]);
+        const float4 a3 = *reinterpret_cast<const float4*>(&s_acc[lane][12]);
+        S[0] = a0.x, S[1] = a0.y, S[2] = a0.z, S[3] = a0.w, S[4] = a1.x, S[5] = a1.y, S[6] = a1.z, S[7] = a1.w;
+        S[8] = ((a2.x + a2.y) + (a2.z + a2.w)) + ((a3.x + a3.y) + (a3.z + a3.w));
+      } else {
+#pragma unroll
+        for (int t = 0; t < GRAD_REC; t++) S[t] = 0.0f;
+      }
+      // S3..S7 are the moments of q about the reference point r; with R = mean - r (dx = u + R):
+      // sum q dx = S3 + R.x S8, sum q dx^2 = S5 + 2 R.x S3 + R.x^2 S8, ... in fp64, one rounding to
+      // the record (R = 0, nothing to shift, for a splat centred in the tile)
+      const float2 R = *reinterpret_cast<const float2*>(&s_br[lane].y);
+      const double Rx = R.x, Ry = R.y, q0 = S[8];
+      const float m1x = (float)__builtin_fma(Rx, q0, (double)S[3]), m1y = (float)__builtin_fma(Ry, q0, (double)S[4]);
+      __builtin_amdgcn_sched_barrier(0);
+      const float m2xx = (float)__builtin_fma(Rx, __builtin_fma(Rx, q0, 2.0 * (double)S[3]), (double)S[5]);
+      __builtin_amdgcn_sched_barrier(0);
+      const float m2xy = (float)__builtin_fma(Rx, __builtin_fma(Ry, q0, (double)S[4]),
+                                              __builtin_fma(Ry, (double)S[3], (double)S[6]));
+      __builtin_amdgcn_sched_barrier(0);
+      const float m2yy = (float)__builtin_fma(Ry, __builtin_fma(Ry, q0, 2.0 * (double)S[4]), (double)S[7]);
+      __builtin_amdgcn_sched_barrier(0);
+      float4* row = reinterpret_cast<float4*>(&s_acc[lane][0]);
+      row[0] = make_float4(S[0], S[1], S[2], -ddelx_dx * (ccx * m1x + ccy * m1y));
+      row[1] = make_float4(-ddely_dy * (ccz * m1y + ccy * m1x), -0.5f * m2xx, -0.5f * m2xy, -0.5f * m2yy);
+      // S8 = o sum G dL/dalpha (a contributor has o >= 1/255)
+      row[2] = make_float4(S[8] != 0.0f ? S[8] / cop : 0.0f, __uint_as_float(slot), 0.0f, 0.0f);
+    }
+    rec_lanes = cnt;
+    __builtin_amdgcn_wave_barrier();  // the next batch overwrites the staged entries
+  }
+  store_records();
+  GS_BWD_TREC(tile, n_eff, t_walked, t_slots);
 }
 
-// Per tile (before the backward): the record cut -- 1 + the slot of the tile's last walked
-// instance; records exist only for a tile's first n_eff instances (those its walk reaches, n_eff =
-// its largest n_contrib), and a tile's list is in slot order, so k_sum_records keeps a record of
-// slot s in tile T iff s < tile_cut[T] and the backward writes no zero records for the rest -- and
-// the largest cut.  Also resets the backward's unit queue (the forward built the units).
-constexpr int CUT_THREADS = 256;
-__global__ __launch_bounds__(CUT_THREADS) void k_tile_cut(uint32_t tiles, const uint32_t* __restrict__ tile_max,
-                                                          const uint2* __restrict__ ranges,
-                                                          const uint32_t* __restrict__ point_list,
-                                                          uint32_t* __restrict__ tile_cut, uint32_t* __restrict__ sched) {
-  const uint32_t t = blockIdx.x * CUT_THREADS + threadIdx.x;
-  if (t < ORDER_GROUPS) sched[SCHED_NEXT + SCHED_STRIDE * t] = 0u;
+// Longest-first launch order for the backward.  A tile's walk is as long as its largest
+// n_contrib (the forward's per-quadrant maxima), which varies ~10x across an image, and dense
+// tiles sit together: in index order the last workgroups to start include heavy ones and the
+// grid ends on a long tail.  The forward buckets every tile by that length and ranks it in its
+// bucket of its XCD group (tile_finish); here each thread places one tile at (bucket base + rank)
+// within the group's launch positions, so the heavy tiles start first and the tail is made of
+// light ones (list scheduling, LPT).  The order inside a bucket is arbitrary: a tile's outputs do
+// not depend on when it runs.
+constexpr int ORDER_THREADS = 256;
+// Also (always) each tile's record cut: records exist only for a tile's first n_eff instances
+// (those its walk reaches, n_eff = its largest n_contrib); tile_cut = 1 + the slot of the last
+// of them.  A tile's list is in slot order, so k_sum_records keeps a record of slot s in tile T
+// iff s < tile_cut[T] and the backward writes no zero records for the rest.
+__global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __restrict__ len_hist,
+                                                              const uint32_t* __restrict__ tile_brank, uint32_t gx,
+                                                              uint32_t gy, uint32_t* __restrict__ order,
+                                                              const uint32_t* __restrict__ tile_max,
+                                                              const uint2* __restrict__ ranges,
+                                                              const uint32_t* __restrict__ point_list,
+                                                              uint32_t* __restrict__ tile_cut,
+                                                              uint32_t* __restrict__ cut_max) {
+  __shared__ uint32_t s_base[ORDER_GROUPS][ORDER_BUCKETS];
+  const uint32_t tid = threadIdx.x, t = blockIdx.x * ORDER_THREADS + tid, lane = tid & 63, wid = tid >> 6;
+  const uint32_t tiles = gx * gy;
   uint32_t cut = 0;
   if (t < tiles) {
     const uint4 q = reinterpret_cast<const uint4*>(tile_max)[t];
@@ -413,43 +346,43 @@ __global__ __launch_bounds__(CUT_THREADS) void k_tile_cut(uint32_t tiles, const 
     cut = n_eff ? point_list[r.x + n_eff - 1] + 1u : 0u;
     tile_cut[t] = cut;
   }
-  // the largest cut (all lanes take part in the wave max): k_sum_records stops there -- slots are in
-  // depth order, so past it no tile walked an instance
-  const uint32_t wm = wave_max_u32(cut);
-  if ((threadIdx.x & 63) == 0 && wm) atomicMax(&sched[SCHED_CUT_MAX], wm);
-}
-
-// resident 64-lane workgroups of the backward on this device (its persistent grid)
-template <bool EXACT>
-static uint32_t bwd_seg_waves() {
-  static uint32_t n[2][64] = {};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  uint32_t& w = n[EXACT ? 1 : 0][dev & 63];
-  if (w == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_render_bwd_seg<EXACT>, 64, 0) != hipSuccess ||
-        per_cu <= 0)
-      per_cu = 20;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    w = (uint32_t)per_cu * (uint32_t)cus;
+  {
+    // the largest cut (all lanes take part in the wave max): k_sum_records stops there -- slots
+    // are in depth order, so past it no tile walked an instance
+    const uint32_t wm = wave_max_u32(cut);
+    if (lane == 0 && wm) atomicMax(cut_max, wm);
   }
-  return w;
+  if (!order) return;  // (uniform)
+  const uint32_t br = t < tiles ? tile_brank[t] : 0u;
+  static_assert(ORDER_BUCKETS == 64 && ORDER_GROUPS == 2 * (ORDER_THREADS / 64), "two groups per wave");
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t g = wid + h * (ORDER_THREADS / 64);
+    const uint32_t v = len_hist[g * ORDER_BUCKETS + lane];
+    s_base[g][lane] = wave_incl_scan(v) - v;
+  }
+  lds_barrier();
+  // the j-th tile of group g (longest first) takes launch position 8 j + g
+  if (t < tiles) {
+    const uint32_t g = t % ORDER_GROUPS;
+    order[ORDER_GROUPS * (s_base[g][br >> 22] + (br & 0x3FFFFFu)) + g] = t;
+  }
 }
 
 void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
                 const float* dL_dpix, float* gradrec, hipStream_t st) {
-  (void)P;
-  const uint32_t tiles = (uint32_t)(c.gx * c.gy);
-  GS_LAUNCH("tile_cut", k_tile_cut, dim3((tiles + CUT_THREADS - 1) / CUT_THREADS), dim3(CUT_THREADS), 0, st, tiles,
-            img.tile_max, img.ranges, bin.point_list, img.tile_cut, img.sched);
-  const SegArgs sa{img.fin, bin.ckpt, bin.seg_table, bin.seg_cap, img.sched};
+  const int tiles = c.gx * c.gy;
+  uint32_t* order = img.tile_order;
+  const uint32_t slots = (uint32_t)tiles;
+  GS_LAUNCH("tile_order", k_tile_order, dim3((slots + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
+            img.len_hist, img.tile_brank, (uint32_t)c.gx, (uint32_t)c.gy, order, img.tile_max, img.ranges,
+            bin.point_list, img.tile_cut, img.cut_max);
   if (exact_exp())
-    GS_LAUNCH("render_bwd", k_render_bwd_seg<true>, dim3(bwd_seg_waves<true>()), dim3(64), 0, st, c, img.ranges,
-              bin.point_list, bin.presort_gid, geo.splat, img.n_contrib, img.tile_max, sa, dL_dpix, gradrec);
+    GS_LAUNCH("render_bwd", k_render_bwd_tw<true>, dim3(slots), dim3(64), 0, st, c, img.ranges, bin.point_list,
+              bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order, dL_dpix, gradrec);
   else
-    GS_LAUNCH("render_bwd", k_render_bwd_seg<false>, dim3(bwd_seg_waves<false>()), dim3(64), 0, st, c, img.ranges,
-              bin.point_list, bin.presort_gid, geo.splat, img.n_contrib, img.tile_max, sa, dL_dpix, gradrec);
+    GS_LAUNCH("render_bwd", k_render_bwd_tw<false>, dim3(slots), dim3(64), 0, st, c, img.ranges, bin.point_list,
+              bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order, dL_dpix, gradrec);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -571,7 +504,7 @@ static void launch_sum_records(const GaussianArgs& g, const GeomPtrs& geo, const
                                float* gradrec, uint32_t R, hipStream_t st) {
   GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
             dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
-            img.sched + SCHED_CUT_MAX, gradrec, geo.gsum, (uint32_t)g.P);
+            img.cut_max, gradrec, geo.gsum, (uint32_t)g.P);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -696,7 +696,7 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
       img_layout(c.W, c.H, &im, (char*)img.ranges + (uint64_t)v * is);
       if (I == 0) {
         (void)hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
-        (void)hipMemsetAsync(im.tile_fin, 0, sizeof(uint32_t) * sched_n, st);
+        (void)hipMemsetAsync(im.tile_done, 0, sizeof(uint32_t) * sched_n, st);
         continue;
       }
       (void)hipMemsetAsync(im.ranges, 0, sizeof(uint2) * (size_t)tiles, st);
@@ -706,7 +706,7 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
                        bb.sort_scratch, st, false, false, nullptr, nullptr, nullptr, bb.slot_tile,
                        GS_TILE_SORT_BLOCKS);
       GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024), dim3(256), 0, st, I, &g.counters[CNT_NREND],
-                bb.sorted_tile, im.ranges, im.tile_fin, sched_n, (uint32_t)tiles, 0ull, 0ull);
+                bb.sorted_tile, im.ranges, (uint32_t*)im.tile_done, sched_n, (uint32_t)tiles, 0ull, 0ull);
     }
     return;
   }
@@ -723,7 +723,7 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
                    false, hist0, nullptr, nullptr, nullptr, bin.slot_tile,
                    GS_TILE_SORT_BLOCKS, views, bs);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024, views), dim3(256), 0, st, I, bin.count, bin.sorted_tile,
-            img.ranges, img.tile_fin, sched_n, (uint32_t)tiles, bs, is);
+            img.ranges, (uint32_t*)img.tile_done, sched_n, (uint32_t)tiles, bs, is);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -823,47 +823,31 @@ __device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist,
 GS_TIMING_BUFFER(g_fwd_timing, gs_debug_fwd_timing)
 #endif
 
-// Epilogue of one quadrant wave (whole wave): the tile's largest n_contrib and the backward's units.
-// Lane 0 raises the tile's maximum (one atomicMax, whose return it waits for) and only then counts
-// itself finished (atomicAdd), so when the fourth finisher sees a count of 3 every other wave's
-// maximum is already in; it reads the tile's maximum n_eff back (atomicMax with 0) and queues the
-// tile's backward units in its XCD group's table (the group whose XCD ran this tile's waves): the
-// full SEG-entry segments of [0, n_eff) from the table's front, the partial last one (if any) from
-// its back, so the queue hands out the short units last.
-__device__ __forceinline__ void tile_finish(uint32_t tile, uint32_t wave_last, uint32_t* __restrict__ tile_fin,
-                                            uint32_t* __restrict__ sched, uint2* __restrict__ table, uint32_t cap) {
-  const uint32_t lane = threadIdx.x;
-  uint32_t n1 = 0;  // n_eff + 1 on the tile's fourth finisher, else 0
-  if (lane == 0) {
-    uint32_t* const tf = tile_fin + TILE_FIN_STRIDE * tile;
-    const uint32_t om = atomicMax(&tf[0], wave_last);
-    uint32_t one = 1u;
-    asm volatile("" : "+v"(one) : "v"(om));  // the count is issued after the maximum has landed
-    if (atomicAdd(&tf[1], one) == 3u) n1 = atomicMax(&tf[0], 0u) + 1u;
-  }
-  n1 = __builtin_amdgcn_readfirstlane(n1);
-  if (n1 <= 1u) return;  // (uniform) not the last quadrant, or nothing walked
-  const uint32_t n_eff = n1 - 1u, full = n_eff / SEG, part = n_eff % SEG != 0u ? 1u : 0u;
-  const uint32_t grp = tile % ORDER_GROUPS;
-  uint2* const tab = table + (size_t)grp * cap;
-  uint32_t bf = 0, bp = 0;
-  if (lane == 0) {
-    if (full) bf = atomicAdd(&sched[SCHED_FRONT + SCHED_STRIDE * grp], full);
-    if (part) bp = atomicAdd(&sched[SCHED_BACK + SCHED_STRIDE * grp], 1u);
-  }
-  bf = __builtin_amdgcn_readfirstlane(bf);
-  bp = __builtin_amdgcn_readfirstlane(bp);
-  for (uint32_t j = lane; j < full; j += 64) tab[bf + j] = make_uint2(tile, j);
-  if (part && lane == 0) tab[cap - 1u - bp] = make_uint2(tile, full);
+// Epilogue of one quadrant wave (one lane): one 64-bit atomic per wave adds 1 (finished waves, low
+// 3 bits) plus a one-hot bit of the quadrant's walk-length class (bit 8 + class).  The tile's
+// fourth finisher gets the other three from the returned value, with no fence: the highest set
+// bit of the sum is the tile's longest class (or one above it, when classes coincide and carry),
+// which is all the longest-first order needs.  It takes a rank in that bucket; k_tile_order turns
+// (bucket, rank) into the backward's launch order.
+__device__ __forceinline__ void tile_finish(uint32_t tile, uint32_t grp, uint32_t wave_last,
+                                            uint64_t* __restrict__ tile_done, uint32_t* __restrict__ len_hist,
+                                            uint32_t* __restrict__ tile_brank) {
+  // length classes on a log scale, four per octave
+  const uint32_t cls = min((uint32_t)(4.0f * __log2f((float)wave_last + 1.0f)), 47u);
+  const uint64_t mine = (1ull << (8 + cls)) + 1ull;
+  const uint64_t old = atomicAdd((unsigned long long*)&tile_done[tile], (unsigned long long)mine);
+  if ((old & 7ull) != 3ull) return;
+  const uint32_t top = 63u - (uint32_t)__builtin_clzll((old + mine) >> 8);  // 0 .. 49
+  const uint32_t b = (uint32_t)ORDER_BUCKETS - 1u - top;                    // descending length
+  tile_brank[tile] = b << 22 | atomicAdd(&len_hist[grp * ORDER_BUCKETS + b], 1u);
 }
 
-// fin = (C0, C1, C2, T_final) for the backward's segment starts; out = C + T_final bg
 __device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q, bool inside, const FwdPix& px,
-                                          float* __restrict__ out, float4* __restrict__ fin,
+                                          float* __restrict__ out, float* __restrict__ final_T,
                                           uint32_t* __restrict__ n_contrib) {
   if (inside) {
     const size_t pix = (size_t)q.py * c.W + q.px, HW = (size_t)c.W * c.H;
-    fin[pix] = make_float4(px.C0, px.C1, px.C2, px.T);
+    final_T[pix] = px.T;
     n_contrib[pix] = px.last;
     out[pix] = px.C0 + px.T * c.bg[0];
     out[HW + pix] = px.C1 + px.T * c.bg[1];
@@ -876,8 +860,7 @@ __device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q,
 // are done (a workgroup per tile would wait for its slowest quadrant: 203 -> 188 us at C3 when this
 // went in).  Workgroup b takes the (b / 32)-th tile of XCD group b % 8 (xcd_tile), quadrant
 // (b / 8) % 4, so the four quadrant waves of a tile share the workgroup-to-XCD round robin (b % 8)
-// and their repeated entry loads hit one L2.  At every multiple of SEG entries it reaches, the wave
-// stores its pixels' (T, C) for the backward's depth segments (BinPtrs::ckpt).
+// and their repeated entry loads hit one L2.
 // (Tried and not kept: the next batch's ids / records prefetched one batch ahead, 168 -> 179 us --
 // the loads past the stop are wasted; 32-entry batches, 174 -> 195 us.)
 constexpr int FWDQ_NB = 64;  // entries staged per round (one per lane)
@@ -888,9 +871,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
                                                      const uint32_t* __restrict__ point_list,
                                                      const uint32_t* __restrict__ point_gid,
                                                      const float4* __restrict__ splat, float* __restrict__ out,
-                                                     ImgPtrs img, float4* __restrict__ ckpt,
-                                                     uint2* __restrict__ table, uint32_t cap,
-                                                     const uint32_t* __restrict__ err, uint32_t* __restrict__ err_host) {
+                                                     ImgPtrs img, const uint32_t* __restrict__ err,
+                                                     uint32_t* __restrict__ err_host) {
   __shared__ float4 s_ent[3 * FWDQ_NBS];
   __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
   if (threadIdx.x < 3)  // the dummy entry: position 0, opacity 0 (never contributes)
@@ -914,7 +896,6 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
   const uint32_t n = (*err & ERR_INVALID) ? 0u : range.y - range.x;
   const char* ent = reinterpret_cast<const char*>(s_ent);
   const float qx = (float)(tx * GS_TILE + 8 * (wid & 1)), qy = (float)(ty * GS_TILE + 8 * (wid >> 1));
-  float4* const ck = ckpt + ((size_t)(range.x / SEG) << 8) + 64 * wid + lane;
   FwdPix px;
   px.done = __builtin_amdgcn_ballot_w64(!inside);
   for (uint32_t base = 0; base < n; base += FWDQ_NB) {
@@ -934,15 +915,6 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
           16u * lane;
     const uint32_t qcnt = (uint32_t)__popcll(m);
     if (lane < 2 * FWD_ILP) s_qlist[qcnt + lane] = 16u * FWDQ_NB;
-    // a segment boundary the backward may start from (this quadrant still runs: its largest
-    // n_contrib may lie behind it).  Stored once this batch's loads have landed: loads and stores
-    // share one wait counter, so a store issued ahead of them would hold their wait until its
-    // write completes (measured: before the staging loads, render_fwd 172 -> 242 us at SEG 128)
-    if (base != 0 && base % SEG == 0) {
-      // non-temporal: read once, by the backward; kept out of the L2 that caches the splat records
-      typedef float v4f __attribute__((ext_vector_type(4)));
-      __builtin_nontemporal_store(v4f{px.T, px.C0, px.C1, px.C2}, reinterpret_cast<v4f*>(ck + ((size_t)(base / SEG) << 8)));
-    }
     __builtin_amdgcn_wave_barrier();
 #ifdef GS_TIMING
     t_batches++;
@@ -951,13 +923,12 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
     fwd_walk<EXACT, FWDQ_NBS>(ent, s_qlist, qcnt, (float)q.px, (float)q.py, px);
     __builtin_amdgcn_wave_barrier();  // the next round overwrites the staged entries
   }
-  // the tile's bookkeeping first: its atomics return values this wave waits for, and loads and
-  // stores share one wait counter -- issued after the pixel stores, the waits would also hold the
-  // wave (and its slot) until those stores completed
+  fwd_store(c, q, inside, px, out, img.final_T, img.n_contrib);
   const uint32_t wmax = wave_max_u32(px.last);
-  tile_finish(tile, wmax, img.tile_fin, img.sched, table, cap);
-  if (lane == 0) img.tile_max[4 * tile + wid] = wmax;
-  fwd_store(c, q, inside, px, out, img.fin, img.n_contrib);
+  if (lane == 0) {
+    img.tile_max[4 * tile + wid] = wmax;
+    tile_finish(tile, tile % ORDER_GROUPS, wmax, img.tile_done, img.len_hist, img.tile_brank);
+  }
 #ifdef GS_TIMING
   timing_record(g_fwd_timing, t_start, tile, (uint32_t)wid, t_batches, t_walked);
 #endif
@@ -969,12 +940,10 @@ void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
   const int blocks = (int)xcd_span((uint32_t)tiles) * 32;
   if (exact_exp())
     GS_LAUNCH("render_fwd", k_render_fwd_q<true>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, out_color, img, bin.ckpt, bin.seg_table, bin.seg_cap,
-              &geo.counters[CNT_ERR], err_host);
+              bin.presort_gid, geo.splat, out_color, img, &geo.counters[CNT_ERR], err_host);
   else
     GS_LAUNCH("render_fwd", k_render_fwd_q<false>, dim3(blocks), dim3(64), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, out_color, img, bin.ckpt, bin.seg_table, bin.seg_cap,
-              &geo.counters[CNT_ERR], err_host);
+              bin.presort_gid, geo.splat, out_color, img, &geo.counters[CNT_ERR], err_host);
 }
 
 // ------------------------------------------------------------------------------------------

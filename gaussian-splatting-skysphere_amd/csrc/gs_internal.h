@@ -7,12 +7,10 @@
 //                                    clamped u8 | depth-sort keys/vals x2 u32 (keys_a: depth keys
 //                                    written by preprocess) | offsets u32 |
 //                                    scan partials | sort scratch | counters
-//   binning   (per instance, I)      tile keys/vals x2 u32 | presort_gid u32 | sort scratch |
-//                                    segment-boundary states float4 x 256 per SEG instances |
-//                                    backward units uint2 (I / SEG + tiles + 1)
-//   image     (per pixel / tile)     ranges uint2 | fin float4 (final colour, T) | n_contrib u32 |
-//                                    tile_max u32 x4 (largest n_contrib of each 8x8 quadrant) |
-//                                    tile_cut u32 | tile_fin u32 x2 per tile + SCHED words
+//   binning   (per instance, I)      tile keys/vals x2 u32 | presort_gid u32 | sort scratch
+//   image     (per pixel / tile)     ranges uint2 | final_T f32 | n_contrib u32 | tile_max u32 x4
+//                                    (largest n_contrib of each 8x8 quadrant) | tile_order u32 |
+//                                    tile_cut u32 | tile_done u64 + length buckets | bucket rank u32
 //   gradient  (per instance, I)      9 f32 per (Gaussian, tile) instance (backward scratch)
 #pragma once
 #include <stddef.h>
@@ -259,25 +257,7 @@ struct BinPtrs {
                          // first pass reads it and writes keys_b)
   uint32_t* count;       // [0]: the view's instance count bounded by the buffer's capacity (the duplicate
                          // writes it; the tile sort and k_ranges read it from this buffer)
-  // segment-boundary pixel states (T, C0, C1, C2) the forward's quadrant waves store at list
-  // positions SEG j (j >= 1) of a tile: entry [(range.x / SEG + j) * 256 + 64 quadrant + lane]
-  // (distinct for every (tile, j): range.x / SEG + j <= (range.y - 1) / SEG < I / SEG + 1)
-  float4* ckpt;
-  // the backward's units (tile, segment), one table of seg_cap entries per XCD group (tile % 8): full
-  // segments from its front, partial ones from its back
-  uint2* seg_table;
-  uint32_t seg_cap;
 };
-
-// Depth segments of the backward (k_render_bwd_seg): a tile's list is walked in units of SEG
-// entries, each started from the pixel states the forward stored at the unit's far end.
-#ifndef GS_SEG
-#define GS_SEG 128
-#endif
-constexpr uint32_t SEG = GS_SEG;
-static_assert(SEG % 64 == 0, "segments are whole 64-entry batches");
-inline size_t seg_ckpts(size_t I) { return I / SEG + 1; }
-inline size_t seg_units(size_t I, size_t tiles) { return I / SEG + tiles + 1; }
 
 
 // (Tried in round 2 and not kept: the forward's quadrant waves storing each staged entry's 48-B splat
@@ -303,13 +283,8 @@ inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base) {
   size_t o_pg = take(In * 4), o_st = take(In * 4);
   size_t o_ss = take(sort_scratch_words(In) * 4);
   size_t o_cn = take(64);
-  size_t o_ck = take(seg_ckpts(In) * 256 * 16);
-  size_t o_su = take(seg_units(In, (size_t)tiles) * 8 * 8);
   if (out && base) {
     out->count = (uint32_t*)(base + o_cn);
-    out->ckpt = (float4*)(base + o_ck);
-    out->seg_table = (uint2*)(base + o_su);
-    out->seg_cap = (uint32_t)seg_units(In, (size_t)tiles);
     out->keys_a = (uint32_t*)(base + o_ka);
     out->vals_a = (uint32_t*)(base + o_va);
     out->keys_b = (uint32_t*)(base + o_kb);
@@ -326,29 +301,22 @@ inline size_t bin_layout(size_t I, int tiles, BinPtrs* out, char* base) {
 
 struct ImgPtrs {
   uint2* ranges;
-  float4* fin;           // per pixel: (C0, C1, C2, T_final), the composited colour without background
+  float* final_T;
   uint32_t* n_contrib;
   uint32_t* tile_max;
-  uint32_t* tile_cut;    // per tile: 1 + the slot of its last walked instance (0: none), k_tile_cut
-  uint32_t* tile_fin;    // per tile: [2 t] largest n_contrib of the finished quadrant waves, [2 t + 1]
-                         // their count (zeroed by k_ranges, with the SCHED words after them)
-  uint32_t* sched;       // = tile_fin + 2 tiles: SCHED_* words
+  uint32_t* tile_order;  // backward launch order (k_tile_order)
+  uint32_t* tile_cut;    // per tile: 1 + the slot of its last walked instance (0: none), k_tile_order
+  uint64_t* tile_done;   // per tile: finished quadrant waves + their length bits (zeroed by k_ranges),
+  uint32_t* len_hist;    //   then ORDER_GROUPS x ORDER_BUCKETS walk-length bucket counts
+  uint32_t* tile_brank;  // bucket << 22 | rank within the bucket, per tile
+  uint32_t* cut_max;     // the largest tile_cut (after len_hist; zeroed with it): no instance slot at
+                         // or past it has a gradient record
 };
-// words of ImgPtrs::sched, per XCD group g (tile % ORDER_GROUPS): backward units queued from the front
-// (full segments) / back (partial) of the group's unit table, the backward's take counter; then the
-// largest tile_cut (no instance slot at or past it has a record).  Every counter has a 128-B line of
-// its own (word SCHED_* + SCHED_STRIDE g): atomics on one line from many waves serialise -- with
-// the 25 counters packed into one line, render_bwd took 2,100 us and render_fwd 243 us at C3, one
-// line each: 348 / 179 us.
-constexpr int SCHED_STRIDE = 32;
-constexpr int SCHED_FRONT = 0, SCHED_BACK = 8 * SCHED_STRIDE, SCHED_NEXT = 16 * SCHED_STRIDE,
-              SCHED_CUT_MAX = 24 * SCHED_STRIDE, SCHED_WORDS = 25 * SCHED_STRIDE;
-#ifndef GS_TF_STRIDE
-#define GS_TF_STRIDE 2
-#endif
-constexpr uint32_t TILE_FIN_STRIDE = GS_TF_STRIDE;  // words per tile of tile_fin ([0] max, [1] count)
-// scheduling words zeroed per binning (k_ranges)
-inline uint32_t sched_words(uint32_t tiles) { return TILE_FIN_STRIDE * tiles + SCHED_WORDS; }
+
+// Backward launch order: tiles bucketed by walk length (largest n_contrib), longest first.
+constexpr int ORDER_BUCKETS = 64;
+// scheduling words zeroed per binning (k_ranges): tile_done, len_hist, cut_max
+inline uint32_t sched_words(uint32_t tiles);
 
 // The forward's quadrant waves are laid out in ORDER_GROUPS groups: group g = tile % 8 fills
 // workgroups g, g + 8, g + 16, ..., which the dispatcher sends to one XCD (workgroup b runs on XCD
@@ -358,6 +326,7 @@ inline uint32_t sched_words(uint32_t tiles) { return TILE_FIN_STRIDE * tiles + S
 // neighbouring tiles in both directions share one L2, made both renders slower: render_fwd 174 ->
 // 184 us, render_bwd 404 -> 417 us.)
 constexpr int ORDER_GROUPS = 8;
+inline uint32_t sched_words(uint32_t tiles) { return 2u * tiles + ORDER_GROUPS * ORDER_BUCKETS + 1u; }
 // tiles per group (the last groups may hold one fewer)
 __host__ __device__ inline uint32_t xcd_span(uint32_t tiles) { return (tiles + ORDER_GROUPS - 1) / ORDER_GROUPS; }
 // the k-th tile of group g (~0u past its end)
@@ -377,16 +346,20 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   size_t npix = (size_t)W * H;
   if (tiles == 0) tiles = 1;
   if (npix == 0) npix = 1;
-  size_t o_r = take(tiles * 8), o_f = take(npix * 16), o_n = take(npix * 4), o_m = take(tiles * 16),
-         o_c = take(tiles * 4), o_d = take((size_t)sched_words((uint32_t)tiles) * 4);
+  size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16),
+         o_o = take(tiles * 4), o_c = take(tiles * 4), o_d = take((size_t)sched_words((uint32_t)tiles) * 4),
+         o_b = take(tiles * 4);
   if (out && base) {
     out->ranges = (uint2*)(base + o_r);
-    out->fin = (float4*)(base + o_f);
+    out->final_T = (float*)(base + o_t);
     out->n_contrib = (uint32_t*)(base + o_n);
     out->tile_max = (uint32_t*)(base + o_m);
+    out->tile_order = (uint32_t*)(base + o_o);
     out->tile_cut = (uint32_t*)(base + o_c);
-    out->tile_fin = (uint32_t*)(base + o_d);
-    out->sched = out->tile_fin + TILE_FIN_STRIDE * tiles;
+    out->tile_done = (uint64_t*)(base + o_d);
+    out->len_hist = (uint32_t*)(out->tile_done + tiles);
+    out->cut_max = out->len_hist + ORDER_GROUPS * ORDER_BUCKETS;
+    out->tile_brank = (uint32_t*)(base + o_b);
   }
   return off;
 }

@@ -1,12 +1,10 @@
-"""Critical path of the backward render: per-wave start / end stamps of one launch.
+"""Critical path of k_render_bwd_tw: per-wave start / end stamps of one backward launch.
 
-Needs a library built with -DGS_BWD_TIMING (make -C gaussian-splatting-skysphere_amd BUILD=build_timing
-EXTRA=-DGS_BWD_TIMING) and GSRAST_LIB pointing at it.  Runs the batch-1 loop (bench.py's single_view
-shape), then one more iteration with the stamp buffer cleared, and reports for the persistent
-segmented kernel (k_render_bwd_seg): the launch's span, when its waves end (the drain), the resident
-waves over time, the units and entries each wave took, per-XCD spans.  The stamps are
-s_memrealtime (100 MHz).  Round 4's one-wave-per-tile kernel (k_render_bwd_tw) was measured with the
-previous version of this script (git history; profiles/r05_bwd_timing_c3_v0.json).
+Needs a library built with -DGS_TIMING (make -C gaussian-splatting-skysphere_amd BUILD=build_timing
+EXTRA=-DGS_TIMING) and GSRAST_LIB pointing at it.  Runs the batch-1 loop (bench.py's single_view
+shape), then one more iteration with the stamp buffer cleared, and reports: the launch's span against
+its longest wave, the resident-wave profile over time, the tail, per-XCD spans, and how a wave's
+duration follows its walk (entries walked, slots evaluated).  The stamps are s_memrealtime (100 MHz).
 """
 import argparse
 import ctypes
@@ -54,7 +52,9 @@ def step():
 for _ in range(20):
     step()
 torch.cuda.synchronize()
-slots = 1 << 16  # the timing buffer's capacity (BWD_TIMING_MAX waves)
+gx, gy = (W + 15) // 16, (H + 15) // 16
+tiles = gx * gy
+slots = 8 * ((tiles + 7) // 8) + 8
 reports = []
 for rep in range(a.reps):
     assert lib.gs_debug_bwd_timing(None, 0, 1) == 0
@@ -74,31 +74,63 @@ for rep in range(a.reps):
     s_us = (t0 - base) / 100.0  # 100 MHz -> us
     e_us = (t1 - base) / 100.0
     dur = e_us - s_us
-    units = (d[:, 2] >> 32).astype(np.int64)  # backward units (tile, depth segment) the wave walked
+    n_eff = (d[:, 2] & 0xFFFFFFFF).astype(np.int64)
     walked = (d[:, 4] >> 32).astype(np.int64)
     nslots = (d[:, 4] & 0xFFFFFFFF).astype(np.int64)
     xcc = (d[:, 3] >> 32).astype(np.int64) & 0xF
+    hw = (d[:, 3] & 0xFFFFFFFF).astype(np.int64)
     span = e_us.max()
+    il = int(np.argmax(dur))
+    order = np.argsort(dur)[::-1]
+    # resident waves over time (1 us bins)
     nb = int(np.ceil(span)) + 1
     occ = np.zeros(nb)
     for s, e in zip(s_us, e_us):
         occ[int(s):int(np.ceil(e))] += 1
+    # least-squares duration model: a + b walked + c slots
+    X = np.stack([np.ones_like(dur), walked, nslots], 1)
+    coef, *_ = np.linalg.lstsq(X, dur, rcond=None)
+    active = walked > 0
+    # per-XCD spans
     per_xcd = {}
     for x in range(8):
         m = xcc == x
         if m.any():
-            per_xcd[int(x)] = {"waves": int(m.sum()), "last_end": round(float(e_us[m].max()), 1),
-                               "units": int(units[m].sum()), "entries": int(walked[m].sum())}
-    frac_run = {f"{f:.2f}": int(((s_us <= f * span) & (e_us > f * span)).sum()) for f in (0.5, 0.7, 0.8, 0.9, 0.95)}
+            per_xcd[int(x)] = {"waves": int(m.sum()), "first_start": round(float(s_us[m].min()), 1),
+                               "last_end": round(float(e_us[m].max()), 1), "sum_dur": round(float(dur[m].sum()), 0),
+                               "entries": int(walked[m].sum())}
+    # SIMD / CU identity (gfx9 HW_ID: simd 5:4, cu 11:8, sh 12, se 15:13)
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 15
+    se = (hw >> 13) & 7
+    sh = (hw >> 12) & 1
+    cu_key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    simd_key = cu_key * 4 + simd
+    simd_busy_end = {}
+    for k, e in zip(simd_key, e_us):
+        simd_busy_end[int(k)] = max(simd_busy_end.get(int(k), 0.0), float(e))
+    ends = np.array(sorted(simd_busy_end.values()))
+    # waves still running at fractions of the span
+    frac_run = {f"{f:.1f}": int(((s_us <= f * span) & (e_us > f * span)).sum()) for f in (0.5, 0.7, 0.8, 0.9, 0.95)}
     rep_d = {
         "workload": a.workload, "rep": rep, "event_us": round(ev_us, 1), "span_us": round(float(span), 1),
-        "waves": int(len(dur)), "units": int(units.sum()), "entries_walked": int(walked.sum()),
-        "slots_evaluated": int(nslots.sum()), "last_start_us": round(float(s_us.max()), 1),
-        "end_pct_of_span": {p: round(float(np.percentile(e_us, p) / span), 3) for p in (1, 10, 50, 90, 99)},
-        "units_per_wave": {p: int(np.percentile(units, p)) for p in (1, 50, 99)},
+        "waves": int(len(dur)), "waves_with_walk": int(active.sum()), "simds_seen": int(len(simd_busy_end)),
+        "longest_wave_us": round(float(dur[il]), 1), "longest_over_span": round(float(dur[il] / span), 3),
+        "longest_wave": {"n_eff": int(n_eff[il]), "walked": int(walked[il]), "slots": int(nslots[il]),
+                         "start_us": round(float(s_us[il]), 1), "xcc": int(xcc[il])},
+        "top10_dur_us": [round(float(dur[i]), 1) for i in order[:10]],
+        "top10_walked": [int(walked[i]) for i in order[:10]],
+        "top10_start_us": [round(float(s_us[i]), 1) for i in order[:10]],
+        "dur_pct": {p: round(float(np.percentile(dur[active], p)), 1) for p in (10, 50, 90, 99)},
+        "walked_pct": {p: int(np.percentile(walked[active], p)) for p in (10, 50, 90, 99)},
+        "max_walked": int(walked.max()), "mean_walked": round(float(walked[active].mean()), 1),
+        "last_start_us": round(float(s_us.max()), 1),
+        "model_us": {"const": round(float(coef[0]), 2), "per_entry": round(float(coef[1]), 4),
+                     "per_slot": round(float(coef[2]), 4)},
         "resident_waves_by_10pct": [round(float(occ[int(i * nb / 10):int((i + 1) * nb / 10)].mean()), 0)
                                     for i in range(10)],
         "running_at_frac_of_span": frac_run,
+        "simd_last_end_pct_of_span": {p: round(float(np.percentile(ends, p) / span), 3) for p in (5, 25, 50, 75, 95)},
         "per_xcd": per_xcd,
     }
     reports.append(rep_d)

@@ -1,0 +1,9 @@
+#!/bin/bash
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p $OUT; cd $R
+SV_ARGS="--steps 60" timeout -k 10 500 bash tools/sv_ab.sh build build_s64 build_s256 build_r4 > $OUT/r05_sv_ab6.txt 2>&1 || { cat $OUT/r05_sv_ab6.txt; exit 1; }
+cat $OUT/r05_sv_ab6.txt
+TAG=steal timeout -k 10 300 bash tools/r05_timing.sh || exit 1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/r05_gpu_tests_v2.txt 2>&1; rc=$?
+tail -15 $OUT/r05_gpu_tests_v2.txt
+exit $rc
