@@ -315,6 +315,8 @@ struct ImgPtrs {
 
 // Backward launch order: tiles bucketed by walk length (largest n_contrib), longest first.
 constexpr int ORDER_BUCKETS = 64;
+// (The forward's completion counters -- 16 tiles' tile_done words per 128-B line, the 512 len_hist
+// counts in 16 lines -- padded to one line each measured the same: render_fwd 171.5 / 171.9 us.)
 // scheduling words zeroed per binning (k_ranges): tile_done, len_hist, cut_max
 inline uint32_t sched_words(uint32_t tiles);
 
