@@ -744,6 +744,18 @@ def train_step_bench(sc, cam, deg, dev, steps, densify):
     dt = (time.perf_counter() - t) / steps
     out["fused_item"] = {"iters_s": round(1.0 / dt, 2), "ms_per_iter": round(1e3 * dt, 4)}
     del model
+    # the same loop with the per-Gaussian backward fused into the Adam step (train_step(fuse_adam=True),
+    # gs_backward_gaussians_adam): bit-identical parameters and moments, no stored gradients
+    model = ts.TrainModel(sc, dev, fused=True)
+    for _ in range(3):
+        ts.train_step(model, settings, gt, fused=True, loss_item=True, fuse_adam=True)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        ts.train_step(model, settings, gt, fused=True, loss_item=True, fuse_adam=True)
+    dt = (time.perf_counter() - t) / steps
+    out["fused_adam_item"] = {"iters_s": round(1.0 / dt, 2), "ms_per_iter": round(1e3 * dt, 4)}
+    del model
     for fused in (True, False):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()

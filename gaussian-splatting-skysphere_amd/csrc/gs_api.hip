@@ -1,3 +1,5 @@
+#include <dlfcn.h>
+
 #include <atomic>
 #include <cstdlib>
 // gs_api.hip -- C ABI (include/gsrast.h): argument validation, buffer layout, stage orchestration,
@@ -85,6 +87,28 @@ void trace_end(const char* name, hipStream_t st) {
     e = hipStreamSynchronize(st);
     if (e != hipSuccess) set_error("kernel %s failed: %s", name, hipGetErrorString(e));
   }
+}
+
+static std::atomic<int> g_launch_log{-1};  // -1: not yet read from GSRAST_LAUNCH_LOG
+static std::mutex g_launch_mu;
+static std::vector<const void*> g_launched;
+
+static int launch_log_on() {
+  int v = g_launch_log.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("GSRAST_LAUNCH_LOG");
+    v = (e && atoi(e) != 0) ? 1 : 0;
+    g_launch_log.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+
+void launch_record(const void* k) {
+  if (!launch_log_on()) return;
+  std::lock_guard<std::mutex> lk(g_launch_mu);
+  for (const void* x : g_launched)
+    if (x == k) return;
+  g_launched.push_back(k);
 }
 
 static bool check_hip(hipError_t e, const char* what) {
@@ -1146,6 +1170,48 @@ int gs_backward_gaussians_range(int P, int first, int count, int D, int M, const
                                  dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, accumulate, wait_event, debug, stream);
 }
 
+int gs_backward_gaussians_adam(int P, int D, int M, const float* means3D, const float* shs_dc, const float* shs_rest,
+                               const float* scales, float scale_modifier, const float* rotations,
+                               const gs_view_grad* view, float* const* params_host, float* const* exp_avg_host,
+                               float* const* exp_avg_sq_host, const double* lr_host, const long long* step_host,
+                               const double* weight_decay_host, double beta1, double beta2, double eps, int maximize,
+                               int debug, void* stream) {
+  clear_error(debug);
+  if (P < 0) return set_error("P must be >= 0"), 1;
+  if (P == 0) return 0;
+  if (D < 0 || D > 3 || M != 16) return set_error("fused Adam backward: 16 SH coefficients, degree 0..3 only"), 1;
+  if (!means3D || !shs_dc || !shs_rest || !scales || !rotations || !view || !params_host || !exp_avg_host ||
+      !exp_avg_sq_host || !lr_host || !step_host)
+    return set_error("missing required input pointer"), 1;
+  if (!view->viewmatrix || !view->projmatrix || !view->campos || !view->geom_buffer)
+    return set_error("view: missing pointer"), 1;
+  if (view->image_width <= 0 || view->image_height <= 0) return set_error("view: bad image size"), 1;
+  for (int k = 0; k < 6; k++) {
+    if (!params_host[k] || !exp_avg_host[k] || !exp_avg_sq_host[k]) return set_error("missing tensor pointer"), 1;
+    if (step_host[k] < 1) return set_error("adam: step must be >= 1"), 1;
+  }
+  if (means3D != params_host[DT_XYZ]) return set_error("means3D must be the xyz parameter (params_host[0])"), 1;
+  if (((uintptr_t)params_host[DT_ROT]) & 15) return set_error("rotation parameter must be 16-byte aligned"), 1;
+  GaussianArgs g{P, D, M, means3D, shs_dc, nullptr, nullptr, scales, rotations, nullptr, scale_modifier};
+  g.shs_rest = shs_rest;
+  if ((((uintptr_t)shs_dc) | ((uintptr_t)shs_rest)) & 15) return set_error("split SH rows must be 16-byte aligned"), 1;
+  FusedAdamArgs a{};
+  for (int k = 0; k < 6; k++) {
+    a.p[k] = params_host[k];
+    a.m[k] = exp_avg_host[k];
+    a.v[k] = exp_avg_sq_host[k];
+    adam_scalars(lr_host[k], step_host[k], beta1, beta2, &a.nss[k], &a.bc2s[k]);
+    a.wd[k] = weight_decay_host ? (float)weight_decay_host[k] : 0.0f;
+  }
+  a.k = adam_consts(beta1, beta2, eps, maximize != 0);
+  GeomPtrs geo;
+  geom_layout((size_t)P, &geo, (char*)view->geom_buffer);
+  CameraArgs c = make_camera(nullptr, view->image_width, view->image_height, view->viewmatrix, view->projmatrix,
+                             view->campos, view->tan_fovx, view->tan_fovy, 0);
+  bwd_gaussians_adam(g, c, geo, a, (hipStream_t)stream);
+  return t_failed ? 1 : 0;
+}
+
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
                     void* stream) {
   clear_error(0);
@@ -1168,6 +1234,30 @@ int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, voi
 
 unsigned gs_debug_set_scan_spin_limit(unsigned limit) {
   return gs::g_spin_limit.exchange(limit, std::memory_order_relaxed);
+}
+
+/* ---- launched-kernel log (tests: every kernel in the code object is launched by some test) ---- */
+int gs_debug_launch_log(int enable) {
+  const int prev = gs::launch_log_on();
+  gs::g_launch_log.store(enable ? 1 : 0, std::memory_order_relaxed);
+  return prev;
+}
+
+long long gs_debug_launched_kernels(char* buf, long long cap) {
+  std::string out;
+  {
+    std::lock_guard<std::mutex> lk(gs::g_launch_mu);
+    for (const void* k : gs::g_launched) {
+      Dl_info info;
+      if (dladdr(k, &info) && info.dli_sname && info.dli_saddr == k)
+        out += info.dli_sname;
+      else
+        out += "?";
+      out += '\n';
+    }
+  }
+  if (buf && cap > (long long)out.size()) memcpy(buf, out.c_str(), out.size() + 1);
+  return (long long)out.size();
 }
 
 /* ---- numerics mode of the render loops ---- */

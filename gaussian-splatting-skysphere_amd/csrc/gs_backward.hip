@@ -713,6 +713,87 @@ __device__ __forceinline__ void gput(float* p, size_t k, float v, uint32_t acc, 
   p[k] = (acc & bit) ? p[k] + v : v;
 }
 
+// One visible Gaussian's gradients from its record sum (upstream's preprocess backward, order
+// identical to oracle/gs_oracle.c): the screen-space terms, conic -> cov2D -> cov3D / mean, the
+// projection, SH (DEG >= 0: dL/dsh into `row`, see sh_backward) and scale / rotation.  Each result
+// goes to `sink` as soon as it is formed (the stores of the plain path stay where they were, which
+// keeps the values' live ranges -- and the kernels' register counts -- short).
+template <int DEG, bool REG, class Sink>
+__device__ __forceinline__ void preprocess_bwd_visible(int i, const GaussianArgs& g, const CameraArgs& c,
+                                                       const uint8_t* __restrict__ clamped,
+                                                       const float* __restrict__ gsum, float* row, bool want_sr,
+                                                       Sink& sink) {
+  // the Gaussian's per-tile records, summed by k_sum_records (index order: coalesced here)
+  const float* rec = gsum + (size_t)i * GRAD_REC;
+  float a[GRAD_REC];
+#pragma unroll
+  for (int k = 0; k < GRAD_REC; k++) a[k] = rec[k];
+  const float dcol[3] = {a[0], a[1], a[2]};
+  const float dm2x = a[3], dm2y = a[4];
+  const float dcon0 = a[5], dcon1 = a[6], dcon2 = a[7];
+  sink.color(dcol);
+  sink.mean2d(dm2x, dm2y);
+  sink.opacity(a[8]);
+  const float px = g.means3D[3 * i], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
+  float cov3[6];
+  if (g.cov3D) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) cov3[k] = g.cov3D[6 * i + k];
+  } else {
+    cov3d(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
+          g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], cov3);
+  }
+  float dcv[6], dmean[3];
+  camera_grads(c, px, py, pz, cov3, dcon0, dcon1, dcon2, dm2x, dm2y, dcv, dmean);
+  sink.cov3d(dcv);
+  if (DEG >= 0) {
+    float shm[3];
+    const float vx = px - c.campos[0], vy = py - c.campos[1], vz = pz - c.campos[2];
+    sh_backward<(DEG < 0 ? 0 : DEG), REG>(row, g.M, vx, vy, vz, clamped[i], dcol, shm);
+    dmean[0] = dmean[0] + shm[0];
+    dmean[1] = dmean[1] + shm[1];
+    dmean[2] = dmean[2] + shm[2];
+  }
+  sink.mean3d(dmean);
+  if (!g.cov3D && want_sr) {
+    float ds[3], dr[4];
+    cov3d_backward(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
+                   g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], dcv, ds, dr);
+    sink.scale_rot(ds, dr);
+  }
+}
+
+// the plain path's sink: the caller's gradient outputs, written or (GS_ACC_* bits) added
+struct StoreSink {
+  const GradOut& out;
+  const int i;
+  __device__ void color(const float* d) {
+    if (out.dcolor)
+      for (int k = 0; k < 3; k++) gput(out.dcolor, 3 * i + k, d[k], out.acc, GS_ACC_COLORS);
+  }
+  __device__ void mean2d(float x, float y) {
+    gput(out.dmean2D, 3 * i, x, out.acc, GS_ACC_MEANS2D);
+    gput(out.dmean2D, 3 * i + 1, y, out.acc, GS_ACC_MEANS2D);
+    gput(out.dmean2D, 3 * i + 2, 0.0f, out.acc, GS_ACC_MEANS2D);
+  }
+  __device__ void opacity(float d) { gput(out.dopacity, i, d, out.acc, GS_ACC_OPACITY); }
+  __device__ void cov3d(const float* d) {
+    if (out.dcov3D)
+#pragma unroll
+      for (int k = 0; k < 6; k++) gput(out.dcov3D, 6 * i + k, d[k], out.acc, GS_ACC_COV3D);
+  }
+  __device__ void mean3d(const float* d) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) gput(out.dmean3D, 3 * i + k, d[k], out.acc, GS_ACC_MEANS3D);
+  }
+  __device__ void scale_rot(const float* ds, const float* dr) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) gput(out.dscale, 3 * i + k, ds[k], out.acc, GS_ACC_SCALES);
+#pragma unroll
+    for (int k = 0; k < 4; k++) gput(out.drot, 4 * i + k, dr[k], out.acc, GS_ACC_ROTATIONS);
+  }
+};
+
 template <int DEG, bool REG = false>
 __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g, const CameraArgs& c,
                                                    const uint32_t* __restrict__ tiles,
@@ -752,58 +833,8 @@ __device__ __forceinline__ void preprocess_bwd_one(int i, const GaussianArgs& g,
       for (int k = 0; k < 4; k++) out.drot[4 * i + k] = 0.f;
     return;
   }
-  // the Gaussian's per-tile records, summed by k_sum_records (index order: coalesced here)
-  const float* rec = gsum + (size_t)i * GRAD_REC;
-  float a[GRAD_REC];
-#pragma unroll
-  for (int k = 0; k < GRAD_REC; k++) a[k] = rec[k];
-  const float dcol[3] = {a[0], a[1], a[2]};
-  const float dm2x = a[3], dm2y = a[4];
-  const float dcon0 = a[5], dcon1 = a[6], dcon2 = a[7];
-  if (out.dcolor) {
-    gput(out.dcolor, 3 * i, dcol[0], acc, GS_ACC_COLORS);
-    gput(out.dcolor, 3 * i + 1, dcol[1], acc, GS_ACC_COLORS);
-    gput(out.dcolor, 3 * i + 2, dcol[2], acc, GS_ACC_COLORS);
-  }
-  gput(out.dmean2D, 3 * i, dm2x, acc, GS_ACC_MEANS2D);
-  gput(out.dmean2D, 3 * i + 1, dm2y, acc, GS_ACC_MEANS2D);
-  gput(out.dmean2D, 3 * i + 2, 0.0f, acc, GS_ACC_MEANS2D);
-  gput(out.dopacity, i, a[8], acc, GS_ACC_OPACITY);
-
-  const float px = g.means3D[3 * i], py = g.means3D[3 * i + 1], pz = g.means3D[3 * i + 2];
-  float cov3[6];
-  if (g.cov3D) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) cov3[k] = g.cov3D[6 * i + k];
-  } else {
-    cov3d(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
-          g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], cov3);
-  }
-  float dcv[6], dmean[3];
-  camera_grads(c, px, py, pz, cov3, dcon0, dcon1, dcon2, dm2x, dm2y, dcv, dmean);
-  if (out.dcov3D)
-#pragma unroll
-    for (int k = 0; k < 6; k++) gput(out.dcov3D, 6 * i + k, dcv[k], acc, GS_ACC_COV3D);
-  if (DEG >= 0) {
-    float shm[3];
-    const float vx = px - c.campos[0], vy = py - c.campos[1], vz = pz - c.campos[2];
-    sh_backward<(DEG < 0 ? 0 : DEG), REG>(row, g.M, vx, vy, vz, clamped[i], dcol, shm);
-    dmean[0] = dmean[0] + shm[0];
-    dmean[1] = dmean[1] + shm[1];
-    dmean[2] = dmean[2] + shm[2];
-  }
-  gput(out.dmean3D, 3 * i, dmean[0], acc, GS_ACC_MEANS3D);
-  gput(out.dmean3D, 3 * i + 1, dmean[1], acc, GS_ACC_MEANS3D);
-  gput(out.dmean3D, 3 * i + 2, dmean[2], acc, GS_ACC_MEANS3D);
-  if (!g.cov3D && out.dscale && out.drot) {
-    float ds[3], dr[4];
-    cov3d_backward(g.scales[3 * i], g.scales[3 * i + 1], g.scales[3 * i + 2], g.scale_modifier, g.rotations[4 * i],
-                   g.rotations[4 * i + 1], g.rotations[4 * i + 2], g.rotations[4 * i + 3], dcv, ds, dr);
-#pragma unroll
-    for (int k = 0; k < 3; k++) gput(out.dscale, 3 * i + k, ds[k], acc, GS_ACC_SCALES);
-#pragma unroll
-    for (int k = 0; k < 4; k++) gput(out.drot, 4 * i + k, dr[k], acc, GS_ACC_ROTATIONS);
-  }
+  StoreSink sink{out, i};
+  preprocess_bwd_visible<DEG, REG>(i, g, c, clamped, gsum, row, out.dscale && out.drot, sink);
 }
 
 // colours precomputed (no SH gradient)
@@ -936,6 +967,202 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd_stage(GaussianArgs g, Ca
       dst4[f] = *reinterpret_cast<const float4*>(&s_rows[r * SH_STAGE_ROW + 4 * (f - r * Q)]);
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// The per-Gaussian half of one view's backward fused with the optimizer step of GaussianModel's six
+// parameter groups (gs_backward_gaussians_adam, the opt-in train step of gs_train_step).
+//
+// The unfused train step writes every Gaussian's 59-float gradient row (k_preprocess_bwd_stage,
+// 236 MB at 1M Gaussians) and reads it back in k_adam.  Here the workgroup's 256 Gaussians get
+// their gradients in registers (xyz, opacity, scaling, rotation) and in LDS (the SH rows, staged as
+// in k_preprocess_bwd_stage), apply the adjoint of render()'s activations to the raw parameters
+// and run Adam on them directly: the gradient rows never touch HBM.  Same floats as the stage
+// kernel followed by k_adam in its activated modes (the same device functions, operation for
+// operation): parameters and moments are bit-identical to the unfused step (test_train_step.py).
+// M = 16 split SH rows, 16-B aligned, any active degree; scales / rotations activated.
+// ------------------------------------------------------------------------------------------
+struct RegSink {
+  float dop, dmean[3] = {0.f, 0.f, 0.f}, ds[3] = {0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f};
+  __device__ void color(const float*) {}
+  __device__ void mean2d(float, float) {}  // written by the view's k_mean2d_grad (gs_backward_render)
+  __device__ void opacity(float d) { dop = d; }
+  __device__ void cov3d(const float*) {}
+  __device__ void mean3d(const float* d) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) dmean[k] = d[k];
+  }
+  __device__ void scale_rot(const float* s, const float* r) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) ds[k] = s[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) dr[k] = r[k];
+  }
+};
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// The Adam step of one float4 of a workgroup's features_dc / features_rest block: the gradients
+// come from the staged dL/dsh rows (column `off` + col of row r, the identity adjoint of the SH
+// concatenation).  Loads of p, m, v for the whole batch are issued before any update so that
+// the batch's HBM latency overlaps (the stores could alias the loads as far as the compiler knows).
+template <int NB, int W>  // NB float4s per thread per batch, W floats per Gaussian row of the tensor
+__device__ __forceinline__ void adam_sh_block(const FusedAdamArgs& a, int tk, int i0, int nG, int t,
+                                              const float* s_rows) {
+  constexpr int OFF = W == 3 ? 0 : 3;
+  const int n = nG * W, n4 = n >> 2;
+  float* p = a.p[tk] + (size_t)i0 * W;
+  float* m = a.m[tk] + (size_t)i0 * W;
+  float* v = a.v[tk] + (size_t)i0 * W;
+  const float nss = a.nss[tk], bc2s = a.bc2s[tk], wd = a.wd[tk];
+  for (int f0 = t; f0 < n4; f0 += 256 * NB) {
+    v4f P[NB], M[NB], V[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const int f = f0 + 256 * b;
+      if (f < n4) {
+        P[b] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p) + f);
+        M[b] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(m) + f);
+        V[b] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(v) + f);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const int f = f0 + 256 * b;
+      if (f < n4) {
+        int e = 4 * f, r = e / W, col = e - r * W;
+        float pp[4] = {P[b].x, P[b].y, P[b].z, P[b].w}, mm[4] = {M[b].x, M[b].y, M[b].z, M[b].w},
+              vv[4] = {V[b].x, V[b].y, V[b].z, V[b].w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          adam_update(pp[j], s_rows[r * SH_STAGE_ROW + OFF + col], mm[j], vv[j], a.k, nss, bc2s, wd);
+          if (++col == W) col = 0, r++;
+        }
+        __builtin_nontemporal_store((v4f){pp[0], pp[1], pp[2], pp[3]}, reinterpret_cast<v4f*>(p) + f);
+        __builtin_nontemporal_store((v4f){mm[0], mm[1], mm[2], mm[3]}, reinterpret_cast<v4f*>(m) + f);
+        __builtin_nontemporal_store((v4f){vv[0], vv[1], vv[2], vv[3]}, reinterpret_cast<v4f*>(v) + f);
+      }
+    }
+  }
+  // tail of a partial last block (n not a multiple of 4)
+  for (int e = 4 * n4 + t; e < n; e += 256) {
+    const int r = e / W;
+    float pe = p[e], me = m[e], ve = v[e];
+    adam_update(pe, s_rows[r * SH_STAGE_ROW + OFF + (e - r * W)], me, ve, a.k, nss, bc2s, wd);
+    p[e] = pe, m[e] = me, v[e] = ve;
+  }
+}
+
+template <int DEG>
+__global__ __launch_bounds__(256) void k_preprocess_bwd_adam(GaussianArgs g, CameraArgs c,
+                                                             const uint32_t* __restrict__ tiles,
+                                                             const uint8_t* __restrict__ clamped,
+                                                             const float* __restrict__ gsum, FusedAdamArgs a) {
+  constexpr int KF = 48, Q = KF / 4;  // M == 16 rows; the active degree DEG uses the first 3 (DEG + 1)^2
+  constexpr int K3 = 3 * (DEG + 1) * (DEG + 1);
+  __shared__ __attribute__((aligned(16))) float s_rows[256 * SH_STAGE_ROW];
+  const int i0 = blockIdx.x * 256, t = (int)threadIdx.x, i = i0 + t;
+  const int nG = g.P - i0 < 256 ? g.P - i0 : 256;
+  stage_sh_rows48<true>(g, i0, nG, s_rows);
+  // the lane's own rows of xyz (plain), opacity (sigmoid), scaling (exp), rotation (normalize):
+  // p / m / v loaded up front, in flight with the SH rows' staging loads
+  const bool live = i < g.P;
+  const size_t i3 = 3 * (size_t)(live ? i : 0), i4 = 4 * (size_t)(live ? i : 0), io = live ? i : 0;
+  float px[3], mx[3], vx[3], ps[3], ms[3], vs[3], po, mo, vo;
+  v4f pq, mq, vq;
+  if (live) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      px[k] = __builtin_nontemporal_load(a.p[DT_XYZ] + i3 + k);
+      mx[k] = __builtin_nontemporal_load(a.m[DT_XYZ] + i3 + k);
+      vx[k] = __builtin_nontemporal_load(a.v[DT_XYZ] + i3 + k);
+      ps[k] = __builtin_nontemporal_load(a.p[DT_SCALING] + i3 + k);
+      ms[k] = __builtin_nontemporal_load(a.m[DT_SCALING] + i3 + k);
+      vs[k] = __builtin_nontemporal_load(a.v[DT_SCALING] + i3 + k);
+    }
+    po = __builtin_nontemporal_load(a.p[DT_OPACITY] + io);
+    mo = __builtin_nontemporal_load(a.m[DT_OPACITY] + io);
+    vo = __builtin_nontemporal_load(a.v[DT_OPACITY] + io);
+    pq = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(a.p[DT_ROT] + i4));
+    mq = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(a.m[DT_ROT] + i4));
+    vq = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(a.v[DT_ROT] + i4));
+  }
+  lds_barrier();
+  if (live) {
+    float row[KF];
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const float4 r4 = *reinterpret_cast<const float4*>(&s_rows[t * SH_STAGE_ROW + 4 * q]);
+      row[4 * q] = r4.x, row[4 * q + 1] = r4.y, row[4 * q + 2] = r4.z, row[4 * q + 3] = r4.w;
+    }
+    RegSink gr;
+    gr.dop = 0.0f;
+    if (tiles[i] == 0) {  // invisible: every gradient is zero (the Adam step still runs on them)
+#pragma unroll
+      for (int k = 0; k < KF; k++) row[k] = 0.0f;
+    } else {
+      preprocess_bwd_visible<DEG, true>(i, g, c, clamped, gsum, row, true, gr);
+#pragma unroll
+      for (int k = K3; k < KF; k++) row[k] = 0.0f;  // coefficients past the active degree: zero gradient
+    }
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+      *reinterpret_cast<float4*>(&s_rows[t * SH_STAGE_ROW + 4 * q]) =
+          make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+    const float gq_in[4] = {gr.dr[0], gr.dr[1], gr.dr[2], gr.dr[3]}, q[4] = {pq.x, pq.y, pq.z, pq.w};
+    float gq[4];
+    normalize_adjoint(gq_in, q, gq);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      adam_update(px[k], gr.dmean[k], mx[k], vx[k], a.k, a.nss[DT_XYZ], a.bc2s[DT_XYZ], a.wd[DT_XYZ]);
+      adam_update(ps[k], exp_adjoint(gr.ds[k], ps[k]), ms[k], vs[k], a.k, a.nss[DT_SCALING], a.bc2s[DT_SCALING],
+                  a.wd[DT_SCALING]);
+    }
+    adam_update(po, sigmoid_adjoint(gr.dop, po), mo, vo, a.k, a.nss[DT_OPACITY], a.bc2s[DT_OPACITY],
+                a.wd[DT_OPACITY]);
+    float rq[4] = {pq.x, pq.y, pq.z, pq.w}, rm[4] = {mq.x, mq.y, mq.z, mq.w}, rv[4] = {vq.x, vq.y, vq.z, vq.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      adam_update(rq[k], gq[k], rm[k], rv[k], a.k, a.nss[DT_ROT], a.bc2s[DT_ROT], a.wd[DT_ROT]);
+    pq = (v4f){rq[0], rq[1], rq[2], rq[3]};
+    mq = (v4f){rm[0], rm[1], rm[2], rm[3]};
+    vq = (v4f){rv[0], rv[1], rv[2], rv[3]};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      __builtin_nontemporal_store(px[k], a.p[DT_XYZ] + i3 + k);
+      __builtin_nontemporal_store(mx[k], a.m[DT_XYZ] + i3 + k);
+      __builtin_nontemporal_store(vx[k], a.v[DT_XYZ] + i3 + k);
+      __builtin_nontemporal_store(ps[k], a.p[DT_SCALING] + i3 + k);
+      __builtin_nontemporal_store(ms[k], a.m[DT_SCALING] + i3 + k);
+      __builtin_nontemporal_store(vs[k], a.v[DT_SCALING] + i3 + k);
+    }
+    __builtin_nontemporal_store(po, a.p[DT_OPACITY] + io);
+    __builtin_nontemporal_store(mo, a.m[DT_OPACITY] + io);
+    __builtin_nontemporal_store(vo, a.v[DT_OPACITY] + io);
+    __builtin_nontemporal_store(pq, reinterpret_cast<v4f*>(a.p[DT_ROT] + i4));
+    __builtin_nontemporal_store(mq, reinterpret_cast<v4f*>(a.m[DT_ROT] + i4));
+    __builtin_nontemporal_store(vq, reinterpret_cast<v4f*>(a.v[DT_ROT] + i4));
+  }
+  lds_barrier();
+  // features_dc / features_rest: the workgroup's contiguous blocks (16-B aligned: 256 rows of 12 /
+  // 180 B), coalesced float4s, dL/dsh from the staged rows
+  adam_sh_block<1, 3>(a, DT_FDC, i0, nG, t, s_rows);
+  adam_sh_block<6, 45>(a, DT_FREST, i0, nG, t, s_rows);
+}
+
+void bwd_gaussians_adam(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const FusedAdamArgs& a,
+                        hipStream_t st) {
+  if (g.P <= 0) return;
+  const dim3 grid((g.P + 255) / 256), block(256);
+#define GS_PBWD_ADAM(D) \
+  GS_LAUNCH("preprocess_bwd_adam", k_preprocess_bwd_adam<D>, grid, block, 0, st, g, c, geo.tiles, geo.clamped, geo.gsum, a)
+  switch (g.D) {
+    case 0: GS_PBWD_ADAM(0); break;
+    case 1: GS_PBWD_ADAM(1); break;
+    case 2: GS_PBWD_ADAM(2); break;
+    default: GS_PBWD_ADAM(3); break;
+  }
+#undef GS_PBWD_ADAM
 }
 
 // ------------------------------------------------------------------------------------------

@@ -34,10 +34,14 @@ __device__ __forceinline__ void lds_barrier() {
 // ------------------------------------------------------------------------------------------
 void trace_begin(const char* name, hipStream_t st);
 void trace_end(const char* name, hipStream_t st);
+// the set of kernels launched since load (GSRAST_LAUNCH_LOG=1 / gs_debug_launch_log; tests list it
+// against the code object's kernels)
+void launch_record(const void* kernel_handle);
 
 #define GS_LAUNCH(name, kern, grid, block, shm, st, ...)              \
   do {                                                                \
     ::gs::trace_begin(name, st);                                      \
+    ::gs::launch_record(reinterpret_cast<const void*>(kern));         \
     hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__);      \
     ::gs::trace_end(name, st);                                        \
   } while (0)

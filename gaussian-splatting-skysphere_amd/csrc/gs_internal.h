@@ -16,6 +16,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <cmath>
+
 #include "../../include/gsrast.h"  // GS_ACC_* bits
 #include "gs_common.h"
 #include "gs_sortscan.h"
@@ -488,6 +490,63 @@ void photometric_forward(int planes, int H, int W, const float* win11, const flo
 void photometric_backward(int planes, int H, int W, const float* win11, const float* img, const float* gt,
                           const float* dmaps, float lambda, const float* grad, float* dimg, hipStream_t st);
 constexpr int ADAM_MAX_TENSORS = 16;  // parameter tensors per Adam launch
+// ---- Adam (torch.optim.Adam semantics), shared by k_adam and the fused per-Gaussian backward ----
+struct AdamConsts {
+  float w1, w2, b2, eps;  // 1 - b1, 1 - b2, b2, eps (rounded to float from the Python doubles)
+  int maximize;
+};
+inline AdamConsts adam_consts(double beta1, double beta2, double eps, bool maximize) {
+  return AdamConsts{(float)(1.0 - beta1), (float)(1.0 - beta2), (float)beta2, (float)eps, maximize ? 1 : 0};
+}
+// per tensor: -lr / (1 - b1^t) and sqrt(1 - b2^t), in double on the host as torch's Adam forms them
+// from the Python step, then rounded to float
+inline void adam_scalars(double lr, long long step, double beta1, double beta2, float* neg_step_size,
+                         float* bc2_sqrt) {
+  const double t = (double)step;
+  const double bc1 = 1.0 - std::pow(beta1, t), bc2 = 1.0 - std::pow(beta2, t);
+  *neg_step_size = (float)(-(lr / bc1));
+  *bc2_sqrt = (float)std::sqrt(bc2);
+}
+// Operation order of torch's foreach Adam on the device (torch/optim/adam.py _multi_tensor_adam,
+// ATen lerp / addcmul / addcdiv functors, compiled with FMA contraction): scalars rounded to float
+// from the Python doubles, each tensor op rounded to float.
+__device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, const AdamConsts& a, float nss,
+                                            float bc2s, float wd) {
+  if (a.maximize) g = -g;
+  if (wd != 0.0f) g = __builtin_fmaf(wd, p, g);  // grad.add(param, alpha=weight_decay)
+  m = __builtin_fmaf(a.w1, g - m, m);             // exp_avg.lerp_(grad, 1 - beta1), weight < 0.5 branch
+  v = __builtin_fmaf(a.w2 * g, g, v * a.b2);      // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+  const float denom = sqrtf(v) / bc2s + a.eps;    // (sqrt(v) / sqrt(bc2)) + eps
+  p = __builtin_fmaf(nss, m / denom, p);          // param.addcdiv_(m, denom, -lr / bc1)
+}
+// Adjoints of GaussianModel's activations (gaussian_model.py:95-115; k_activate_bwd's expressions,
+// operation for operation), from the raw parameter values
+__device__ __forceinline__ float sigmoid_adjoint(float g, float praw) {
+  const float y = 1.0f / (1.0f + expf(-praw));
+  return g * (1.0f - y) * y;
+}
+__device__ __forceinline__ float exp_adjoint(float g, float praw) { return g * expf(praw); }
+// q / max(|q|, 1e-12) (F.normalize): the quaternion's adjoint
+__device__ __forceinline__ void normalize_adjoint(const float* gq, const float* q, float* out) {
+  const float len = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const float n = fmaxf(len, 1e-12f);
+  const float dot = gq[0] * q[0] + gq[1] * q[1] + gq[2] * q[2] + gq[3] * q[3];
+  const float c = len > 1e-12f ? dot / (n * n) / len : 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; j++) out[j] = gq[j] / n - c * q[j];
+}
+// the six parameter groups of GaussianModel (xyz, f_dc, f_rest, opacity, scaling, rotation) for the
+// fused per-Gaussian backward + Adam step (gs_backward_gaussians_adam)
+struct FusedAdamArgs {
+  float* p[6];
+  float* m[6];
+  float* v[6];
+  float nss[6], bc2s[6], wd[6];
+  AdamConsts k;
+};
+// one view's per-Gaussian half fused with the Adam step (g: M == 16 split SH rows, 16-B aligned)
+void bwd_gaussians_adam(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const FusedAdamArgs& a,
+                        hipStream_t st);
 // how k_adam forms a tensor's gradient from its source g (gs_adam_step_activated)
 enum AdamGrad { AG_PLAIN = 0, AG_SH_DC = 1, AG_SH_REST = 2, AG_SIGMOID = 3, AG_EXP = 4, AG_NORMALIZE = 5 };
 void adam_step(int count, float* const* params, const float* const* grads, float* const* exp_avg,

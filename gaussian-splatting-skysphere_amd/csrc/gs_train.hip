@@ -6,7 +6,7 @@
 //                       as torch's Adam (amsgrad off, no weight decay):
 //                         m = m + (1 - b1) (g - m);  v = b2 v + (1 - b2) g^2
 //                         p = p - (lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps)
-//                       in torch's operation order (see adam_one).
+//                       in torch's operation order (see adam_update, gs_internal.h).
 //   k_densify_stats     train.py:114-115 + gaussian_model.py:405-407 in one pass:
 //                         vis = radii > 0; max_r[vis] = max(max_r, radii)
 //                         accum[vis] += |grad2D[vis, :2]|;  denom[vis] += 1
@@ -40,9 +40,9 @@ struct AdamLaunch {
   float bc2_sqrt[ADAM_MAX_TENSORS];       // sqrt(1 - b2^t)
   float wd[ADAM_MAX_TENSORS];
   int mode[ADAM_MAX_TENSORS];  // AdamGrad: how the tensor's gradient is formed from g
-  int count, maximize;
+  int count;
   int sh_row, sh_rest;    // AG_SH_*: floats per row of the SH gradient source (3M) and of f_rest (3(M - 1))
-  float w1, w2, b2, eps;  // 1 - b1, 1 - b2, b2, eps
+  AdamConsts k;
 };
 
 // The element's gradient, from a gradient source g (base pointer) and the raw parameter values
@@ -60,38 +60,13 @@ __device__ __forceinline__ float act_grad1(const AdamLaunch& a, int k, const flo
       const uint64_t gi = e / (uint64_t)a.sh_rest;
       return g[gi * a.sh_row + 3 + (e - gi * a.sh_rest)];
     }
-    case AG_SIGMOID: {
-      const float y = 1.0f / (1.0f + expf(-praw));
-      return g[e] * (1.0f - y) * y;
-    }
+    case AG_SIGMOID:
+      return sigmoid_adjoint(g[e], praw);
     case AG_EXP:
-      return g[e] * expf(praw);
+      return exp_adjoint(g[e], praw);
     default:
       return g[e];
   }
-}
-
-// AG_NORMALIZE: the quaternion e .. e + 3 (one Gaussian's row)
-__device__ __forceinline__ void normalize_adjoint(const float* gq, const float* q, float* out) {
-  const float len = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-  const float n = fmaxf(len, 1e-12f);
-  const float dot = gq[0] * q[0] + gq[1] * q[1] + gq[2] * q[2] + gq[3] * q[3];
-  const float c = len > 1e-12f ? dot / (n * n) / len : 0.0f;
-#pragma unroll
-  for (int j = 0; j < 4; j++) out[j] = gq[j] / n - c * q[j];
-}
-
-// Operation order of torch's foreach Adam on the device (torch/optim/adam.py _multi_tensor_adam,
-// ATen lerp / addcmul / addcdiv functors, compiled with FMA contraction): scalars rounded to float
-// from the Python doubles, each tensor op rounded to float.
-__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamLaunch& a, float nss,
-                                         float bc2s, float wd) {
-  if (a.maximize) g = -g;
-  if (wd != 0.0f) g = __builtin_fmaf(wd, p, g);  // grad.add(param, alpha=weight_decay)
-  m = __builtin_fmaf(a.w1, g - m, m);             // exp_avg.lerp_(grad, 1 - beta1), weight < 0.5 branch
-  v = __builtin_fmaf(a.w2 * g, g, v * a.b2);      // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
-  const float denom = sqrtf(v) / bc2s + a.eps;    // (sqrt(v) / sqrt(bc2)) + eps
-  p = __builtin_fmaf(nss, m / denom, p);          // param.addcdiv_(m, denom, -lr / bc1)
 }
 
 __global__ __launch_bounds__(256) void k_adam(AdamLaunch a, uint64_t total_chunks) {
@@ -139,7 +114,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamLaunch a, uint64_t total_chunk
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       float pe = P[e], me = M[e], ve = V[e];
-      adam_one(pe, G[e], me, ve, a, ss, ib, wd);
+      adam_update(pe, G[e], me, ve, a.k, ss, ib, wd);
       P[e] = pe, M[e] = me, V[e] = ve;
     }
     __builtin_nontemporal_store(P, reinterpret_cast<v4f*>(p));
@@ -154,7 +129,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamLaunch a, uint64_t total_chunk
     } else {
       for (int j = 0; j < cnt; j++) G[j] = mode == AG_PLAIN ? g[j] : act_grad1(a, k, a.g[k], i + j, p[j]);
     }
-    for (int j = 0; j < cnt; j++) adam_one(p[j], G[j], m[j], v[j], a, ss, ib, wd);
+    for (int j = 0; j < cnt; j++) adam_update(p[j], G[j], m[j], v[j], a.k, ss, ib, wd);
   }
 }
 
@@ -188,22 +163,14 @@ void adam_step(int count, float* const* params, const float* const* grads, float
       a.n[j] = (uint64_t)numel[k];
       chunks += (a.n[j] + 3) / 4;
       a.end[j] = chunks;
-      // bias corrections in double on the host, as torch's Adam forms them from the Python step
-      const double t = (double)step[k];
-      const double bc1 = 1.0 - std::pow(beta1, t), bc2 = 1.0 - std::pow(beta2, t);
-      a.neg_step_size[j] = (float)(-(lr[k] / bc1));
-      a.bc2_sqrt[j] = (float)std::sqrt(bc2);
+      adam_scalars(lr[k], step[k], beta1, beta2, &a.neg_step_size[j], &a.bc2_sqrt[j]);
       a.wd[j] = weight_decay ? (float)weight_decay[k] : 0.0f;
       a.mode[j] = modes ? modes[k] : AG_PLAIN;
     }
     if (!a.count) continue;
     a.sh_row = 3 * sh_coeffs;
     a.sh_rest = 3 * (sh_coeffs - 1);
-    a.w1 = (float)(1.0 - beta1);
-    a.w2 = (float)(1.0 - beta2);
-    a.b2 = (float)beta2;
-    a.eps = (float)eps;
-    a.maximize = maximize ? 1 : 0;
+    a.k = adam_consts(beta1, beta2, eps, maximize);
     GS_LAUNCH("adam", k_adam, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, st, a, chunks);
   }
 }

@@ -299,16 +299,17 @@ class _RasterizeGaussians(torch.autograd.Function):
         # when every parameter gradient the call needs goes to it: only the per-tile half and
         # dL_dmeans2D run now, the per-Gaussian half later for all of its views in one pass
         deferrer = _deferring_owner(ctx)
-        if deferrer is not None and ctx.sh_rest is not None:
+        if deferrer is not None and ctx.sh_rest is not None and not getattr(deferrer, "accepts_sh_split", False):
             raise RuntimeError("sh_split: not supported with a deferring gradient bucket")
         if deferrer is not None:
+            M = (1 + ctx.sh_rest.size(1)) if ctx.sh_rest is not None else (sh.size(1) if sh.ndimension() == 3 else 0)
             dm2 = _C.backward_render(s.bg, view, proj, s.campos, s.tanfovx, s.tanfovy, grad_out_color.contiguous(),
-                                     means3D.size(0), s.sh_degree, sh.size(1) if sh.ndimension() == 3 else 0,
+                                     means3D.size(0), s.sh_degree, M,
                                      geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, ctx.needs_input_grad[1],
                                      s.debug)
             deferrer.defer_view(ctx, dict(means3D=means3D, sh=sh, colors=colors_precomp, scales=scales,
                                           rotations=rotations, cov3D=cov3Ds_precomp, scale_modifier=s.scale_modifier,
-                                          degree=s.sh_degree, debug=s.debug),
+                                          degree=s.sh_degree, debug=s.debug, sh_rest=ctx.sh_rest),
                                 (view, proj, s.campos, s.tanfovx, s.tanfovy, s.image_width, s.image_height,
                                  geomBuffer))
             return (None, dm2) + (None,) * 10

@@ -124,10 +124,18 @@ SIGNATURES = {
          _c_f, _c_f, _c_i, _c_p, _c_p, _c_ll, _c_p, _c_p, _c_p, ctypes.POINTER(_c_ll), _c_i, _c_p],
     ),
     "gs_binning_layout_count": (_c_ll, [_c_sz, _c_i, _c_i]),
+    # ABI v15: one view's per-Gaussian backward half fused with the six groups' Adam step
+    "gs_backward_gaussians_adam": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, ctypes.POINTER(ViewGrad), _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_p, _c_d, _c_d, _c_d, _c_i, _c_i, _c_p],
+    ),
     "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),
     "gs_knn_mean_dist2": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p]),
     "gs_set_exact_exp": (_c_i, [_c_i]),
+    "gs_debug_launch_log": (_c_i, [_c_i]),
+    "gs_debug_launched_kernels": (_c_ll, [ctypes.c_char_p, _c_ll]),
     "gs_ssim_partial_count": (_c_sz, [_c_i, _c_i, _c_i]),
     "gs_ssim_forward": (_c_i, [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_ssim_backward": (_c_i, [_c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),

@@ -75,6 +75,23 @@ class FusedAdam(torch.optim.Optimizer):
                         decoupled_weight_decay=decoupled_weight_decay)
         super().__init__(params, defaults)
 
+    def _advance(self, p):
+        """The parameter's Adam state (created as torch creates it), its step count incremented:
+        (exp_avg, exp_avg_sq, step after this update)."""
+        state = self.state[p]
+        if len(state) == 0:
+            state["step"] = torch.tensor(0.0, dtype=torch.float32)
+            state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        step_t = state["step"]
+        if torch.is_tensor(step_t):
+            step_t += 1
+            t = int(step_t.item())
+        else:
+            t = int(step_t) + 1
+            state["step"] = torch.tensor(float(t), dtype=torch.float32)
+        return state["exp_avg"], state["exp_avg_sq"], t
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -102,23 +119,8 @@ class FusedAdam(torch.optim.Optimizer):
                     raise TypeError("FusedAdam: grad must be float32 on the parameter's device")
                 if not grad.is_contiguous():
                     grad = grad.contiguous()
-                state = self.state[p]
-                if len(state) == 0:
-                    state["step"] = torch.tensor(0.0, dtype=torch.float32)
-                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                m, v = state["exp_avg"], state["exp_avg_sq"]
-                _check_f32_dense(m, "FusedAdam exp_avg")
-                _check_f32_dense(v, "FusedAdam exp_avg_sq")
-                if m.numel() != p.numel() or v.numel() != p.numel():
-                    raise ValueError("FusedAdam: optimizer state does not match the parameter size")
-                step_t = state["step"]
-                if torch.is_tensor(step_t):
-                    step_t += 1
-                    t = int(step_t.item())
-                else:
-                    t = int(step_t) + 1
-                    state["step"] = torch.tensor(float(t), dtype=torch.float32)
+                m, v = self._checked_state(p)
+                t = self._advance(p)[2]
                 batches.setdefault((p.device, key_h), []).append((p, grad, m, v, lr, t, wd))
         for (dev, (b1, b2, eps, maximize)), items in batches.items():
             st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -161,19 +163,8 @@ class FusedAdam(torch.optim.Optimizer):
                 elif src.shape != p.shape:
                     raise ValueError(f"FusedAdam: {mode} gradient source shape {tuple(src.shape)} != param "
                                      f"{tuple(p.shape)}")
-                state = self.state[p]
-                if len(state) == 0:
-                    state["step"] = torch.tensor(0.0, dtype=torch.float32)
-                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                m, v = state["exp_avg"], state["exp_avg_sq"]
-                step_t = state["step"]
-                if torch.is_tensor(step_t):
-                    step_t += 1
-                    t = int(step_t.item())
-                else:
-                    t = int(step_t) + 1
-                    state["step"] = torch.tensor(float(t), dtype=torch.float32)
+                m, v = self._checked_state(p)
+                t = self._advance(p)[2]
                 batches.setdefault((p.device, key_h), []).append((p, src, m, v, lr, t, wd, self._MODES[mode]))
         for (dev, (b1, b2, eps, maximize)), items in batches.items():
             st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -192,6 +183,86 @@ class FusedAdam(torch.optim.Optimizer):
                     _native.check(_lib.gs_adam_step_activated(
                         n, cast(P), cast(G), cast(modes), int(sh_coeffs), cast(M), cast(V), cast(numel), cast(lr),
                         cast(steps), cast(wd), b1, b2, eps, int(maximize), st), "adam step (activated)")
+
+    def _checked_state(self, p):
+        """(exp_avg, exp_avg_sq) of p, created if absent, checked dense fp32 of p's size (a state
+        loaded from a checkpoint may not be)."""
+        state = self.state[p]
+        if len(state) == 0:
+            state["step"] = torch.tensor(0.0, dtype=torch.float32)
+            state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        m, v = state["exp_avg"], state["exp_avg_sq"]
+        _check_f32_dense(m, "FusedAdam exp_avg")
+        _check_f32_dense(v, "FusedAdam exp_avg_sq")
+        if m.numel() != p.numel() or v.numel() != p.numel():
+            raise ValueError("FusedAdam: optimizer state does not match the parameter size")
+        return m, v
+
+    @torch.no_grad()
+    def step_fused_backward(self, params, inputs: dict, view) -> None:
+        """The per-Gaussian half of one view's backward fused with step_activated (one HIP launch,
+        gs_backward_gaussians_adam): `params` are GaussianModel's six raw parameters in group
+        order (xyz, features_dc, features_rest, opacity, scaling, rotation), `inputs` / `view` the
+        deferred rasterizer backward of that view (diff_gaussian_rasterization's deferral
+        protocol: the call's Gaussian inputs and (viewmatrix, projmatrix, campos, tan_fovx,
+        tan_fovy, W, H, geomBuffer), after its per-tile half).  Same floats as the unfused backward
+        followed by step_activated in the modes plain / features_dc / features_rest / sigmoid / exp /
+        normalize, and no gradient is stored (.grad of the six stays as it is)."""
+        from diff_gaussian_rasterization import _C
+
+        if len(params) != 6:
+            raise ValueError("step_fused_backward: the six GaussianModel parameters in group order")
+        where = {id(p): g for g in self.param_groups for p in g["params"]}
+        xyz, dc, rest, op, sc, rot = params
+        P = xyz.shape[0]
+        shapes = ((P, 3), (P, 1, 3), (P, 15, 3), (P, 1), (P, 3), (P, 4))
+        hyper = set()
+        ms, vs, lrs, steps, wds = [], [], [], [], []
+        for p, want in zip(params, shapes):
+            g = where.get(id(p))
+            if g is None:
+                raise ValueError("step_fused_backward: a parameter is not in this optimizer")
+            _check_f32_dense(p, "FusedAdam param")
+            if tuple(p.shape) != want:
+                raise ValueError(f"step_fused_backward: parameter of shape {tuple(p.shape)}, expected {want} "
+                                 "(16 SH coefficients)")
+            b1, b2 = g["betas"]
+            hyper.add((float(b1), float(b2), float(g["eps"]), bool(g.get("maximize", False))))
+            m, v = self._checked_state(p)
+            ms.append(m)
+            vs.append(v)
+            lrs.append(float(g["lr"]))
+            wds.append(float(g.get("weight_decay", 0.0)))
+        if len(hyper) != 1:
+            raise ValueError("step_fused_backward: the six groups must share betas, eps and maximize")
+        if rot.data_ptr() % 16:
+            raise ValueError("step_fused_backward: the rotation parameter must be 16-byte aligned")
+        mean3, sh, sh_rest = inputs["means3D"], inputs["sh"], inputs.get("sh_rest")
+        if mean3.data_ptr() != xyz.data_ptr() or sh_rest is None or sh.data_ptr() != dc.data_ptr() or \
+                sh_rest.data_ptr() != rest.data_ptr():
+            raise ValueError("step_fused_backward: the deferred view must have read xyz and the split SH rows "
+                             "(features_dc / features_rest) of these parameters")
+        scales, rots = inputs["scales"], inputs["rotations"]
+        dev = xyz.device
+        vm, pm, cp, tx, ty, W, H, geom = view
+        vm, pm = _C._f32(vm, "viewmatrix", dev, host_ok=True), _C._f32(pm, "projmatrix", dev, host_ok=True)
+        cp = _C._f32(cp, "campos", dev, host_ok=True)
+        vg = _native.ViewGrad(vm.data_ptr(), pm.data_ptr(), cp.data_ptr(), float(tx), float(ty), int(W), int(H),
+                              geom.data_ptr())
+        for p in params:
+            steps.append(self._advance(p)[2])
+        (b1, b2, eps, maximize), = hyper
+        arr = lambda ts: ctypes.cast((ctypes.c_void_p * 6)(*[t.data_ptr() for t in ts]), ctypes.c_void_p)  # noqa: E731
+        with torch.cuda.device(dev):
+            _native.check(_lib.gs_backward_gaussians_adam(
+                P, int(inputs["degree"]), 16, _ptr(xyz), _ptr(dc), _ptr(rest), _ptr(scales),
+                float(inputs["scale_modifier"]), _ptr(rots), ctypes.byref(vg), arr(params), arr(ms), arr(vs),
+                ctypes.cast((ctypes.c_double * 6)(*lrs), ctypes.c_void_p),
+                ctypes.cast((ctypes.c_longlong * 6)(*steps), ctypes.c_void_p),
+                ctypes.cast((ctypes.c_double * 6)(*wds), ctypes.c_void_p), b1, b2, eps, int(maximize),
+                int(bool(inputs.get("debug", False))), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                "backward + adam step (fused)")
 
     @staticmethod
     def _launch(items, b1, b2, eps, maximize, dev, st):

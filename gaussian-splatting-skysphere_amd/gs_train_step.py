@@ -27,7 +27,8 @@ import torch
 
 import gs_loss
 import gs_train
-from diff_gaussian_rasterization import GaussianRasterizer, bounded_status
+from diff_gaussian_rasterization import GaussianRasterizer, bounded_status, register_gradient_sink, \
+    unregister_gradient_sink
 
 # OptimizationParams defaults (/root/reference/arguments/__init__.py:74-83)
 POSITION_LR_INIT = 0.00016
@@ -86,12 +87,46 @@ class TrainModel:
                 torch.exp(self._scaling), torch.nn.functional.normalize(self._rotation))
 
 
+class _AdamBackward:
+    """Gradient-sink owner of the fused-Adam train step (train_step(fuse_adam=True)).  Armed on
+    the step's rasterizer inputs (xyz and the activated leaves), it receives the view's
+    per-Gaussian backward through diff_gaussian_rasterization's deferral protocol (`defers`,
+    `defer_view`: only the per-tile half and dL/dmeans2D run inside loss.backward()); train_step
+    then runs that half fused with the optimizer step (FusedAdam.step_fused_backward) where
+    train.py steps the optimizer, after loss.item() and the densification statistics."""
+
+    defers = True
+    accepts_sh_split = True
+
+    def __init__(self):
+        self.tensors, self.pending = [], None
+
+    def arm(self, tensors):
+        for t in tensors:
+            register_gradient_sink(t, self)
+        self.tensors = list(tensors)
+
+    def disarm(self):
+        for t in self.tensors:
+            unregister_gradient_sink(t)
+        self.tensors, self.pending = [], None
+
+    def claim(self, t):
+        return None  # not deferred (a backward that needs another input's gradient): plain autograd
+
+    def defer_view(self, ctx, inputs, view):
+        if self.pending is not None:
+            raise RuntimeError("train_step(fuse_adam=True): more than one rasterizer backward in one step")
+        self.pending = (inputs, view)
+
+
 def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | None = None, split_sh: bool = True,
-           binning_capacity: int | None = None):
+           binning_capacity: int | None = None, sink_owner=None):
     """gaussian_renderer.render() for the default pipe (SH and covariance in the rasterizer).
     act_leaves (a list): the activated inputs are made autograd leaves (their adjoint then runs in
     FusedAdam.step_activated) and appended to it as (shs, opacity, scales, rotations).
-    binning_capacity: a bounded forward (no host wait; HIP-graph capturable), see train_step."""
+    binning_capacity: a bounded forward (no host wait; HIP-graph capturable), see train_step.
+    sink_owner: armed on xyz and the activated leaves before the rasterizer call (_AdamBackward)."""
     sh_split = None
     if act_leaves is not None and not split_sh:
         acts = gs_train.activate_values(model._features_dc, model._features_rest, model._opacity, model._scaling,
@@ -118,6 +153,8 @@ def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | N
         means3D, shs, opacity, scales, rotations = gs_train.render_inputs(model)
     else:
         means3D, shs, opacity, scales, rotations = model.torch_render_inputs()
+    if sink_owner is not None:
+        sink_owner.arm([means3D, shs, opacity, scales, rotations])
     # __init__.py:26 (zeros_like(...) + 0, then retain_grad): the screen-space gradient carrier as a
     # leaf; the rasterizer never reads its values (only its .grad is written), so no fill launch
     screenspace_points = torch.empty_like(means3D, requires_grad=True)
@@ -136,7 +173,7 @@ def _torch_densification_stats(model: TrainModel, viewspace, radii):
 
 def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool = True, densify_stats: bool = True,
                lambda_dssim: float = LAMBDA_DSSIM, fused_adjoint: bool = True, split_sh: bool = True,
-               loss_item: bool = False, binning_capacity: int | None = None):
+               loss_item: bool = False, binning_capacity: int | None = None, fuse_adam: bool = False):
     """One iteration (module docstring).  Returns the loss tensor, or with loss_item=True the
     reference's per-iteration `loss.item()` (train.py:99, its progress-bar EMA): a host read-back
     that waits for the forward and backward, taken where train.py takes it (before the statistics
@@ -149,38 +186,57 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
     invalid: the flags land in the device's bounded status, which train_step reads at the
     loss.item() sync point (loss_item=True) and raises there -- the iteration that overflowed, not
     a later one, and before its optimizer step.  Without loss_item the caller polls
-    bounded_status() after its own sync."""
+    bounded_status() after its own sync.
+    fuse_adam (with fused, fused_adjoint, split_sh and 16 SH coefficients): the per-Gaussian half of
+    the backward runs fused with the Adam step, in one pass over the Gaussians where train.py runs
+    optimizer.step() (_AdamBackward, FusedAdam.step_fused_backward): no gradient of the six
+    parameters is ever stored; parameters and moments bit-identical to the unfused step, the
+    screen-space carrier's .grad (the densification statistics' input) as there."""
     acts = [] if (fused and fused_adjoint) else None
-    image, viewspace, radii = render(model, settings, fused, acts, split_sh, binning_capacity)
-    if fused:  # the whole loss expression in one fused forward / backward (gs_loss.photometric_loss)
-        loss, Ll1 = gs_loss.photometric_loss(image, gt_image, lambda_dssim)
-    else:
-        Ll1 = gs_loss.l1_loss(image, gt_image)
-        loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - gs_loss.ssim(image, gt_image))
-    loss.backward()
-    value = None
-    if loss_item:
-        # train.py:99 reads loss.item() here, after the backward and before the statistics and the
-        # optimizer step (train.py:115-128): an iteration whose bounded forward overflowed raises
-        # now, before any parameter, moment or statistic is updated from its invalid gradients
-        value = loss.item()
-        if binning_capacity is not None:
-            bounded_status()
-    with torch.no_grad():
-        if densify_stats:
-            if fused:
-                gs_train.add_densification_stats(model, viewspace, radii)
-            else:
-                _torch_densification_stats(model, viewspace, radii)
-        if acts:
-            shs, opac, scales, rots = acts
-            model.optimizer.step_activated(
-                {model._features_dc: ("features_dc", shs.grad), model._features_rest: ("features_rest", shs.grad),
-                 model._opacity: ("sigmoid", opac.grad), model._scaling: ("exp", scales.grad),
-                 model._rotation: ("normalize", rots.grad)}, sh_coeffs=shs.shape[1])
+    owner = None
+    if fuse_adam and acts is not None and split_sh and model._features_rest.shape[1] == 15:
+        owner = _AdamBackward()
+    try:
+        image, viewspace, radii = render(model, settings, fused, acts, split_sh, binning_capacity, owner)
+        if fused:  # the whole loss expression in one fused forward / backward (gs_loss.photometric_loss)
+            loss, Ll1 = gs_loss.photometric_loss(image, gt_image, lambda_dssim)
         else:
-            model.optimizer.step()
-        model.optimizer.zero_grad(set_to_none=True)
+            Ll1 = gs_loss.l1_loss(image, gt_image)
+            loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - gs_loss.ssim(image, gt_image))
+        loss.backward()
+        value = None
+        if loss_item:
+            # train.py:99 reads loss.item() here, after the backward and before the statistics and
+            # the optimizer step (train.py:115-128): an iteration whose bounded forward overflowed
+            # raises now, before any parameter, moment or statistic is updated from its invalid
+            # gradients
+            value = loss.item()
+            if binning_capacity is not None:
+                bounded_status()
+        with torch.no_grad():
+            if densify_stats:
+                if fused:
+                    gs_train.add_densification_stats(model, viewspace, radii)
+                else:
+                    _torch_densification_stats(model, viewspace, radii)
+            if owner is not None and owner.pending is not None:
+                inputs, view = owner.pending
+                owner.pending = None
+                model.optimizer.step_fused_backward(
+                    [model._xyz, model._features_dc, model._features_rest, model._opacity, model._scaling,
+                     model._rotation], inputs, view)
+            elif acts:
+                shs, opac, scales, rots = acts
+                model.optimizer.step_activated(
+                    {model._features_dc: ("features_dc", shs.grad), model._features_rest: ("features_rest", shs.grad),
+                     model._opacity: ("sigmoid", opac.grad), model._scaling: ("exp", scales.grad),
+                     model._rotation: ("normalize", rots.grad)}, sh_coeffs=shs.shape[1])
+            else:
+                model.optimizer.step()
+            model.optimizer.zero_grad(set_to_none=True)
+    finally:
+        if owner is not None:
+            owner.disarm()
     return value if loss_item else loss
 
 

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 14  /* v14: gs_forward_counted + gs_binning_layout_count (v13: depth slabs removed) */
+#define GSRAST_ABI_VERSION 15  /* v15: gs_backward_gaussians_adam (v14: gs_forward_counted + gs_binning_layout_count) */
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -329,6 +329,16 @@ int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const 
 size_t gs_knn_scratch_bytes(int P);
 int gs_knn_mean_dist2(int P, const float* points, float* out, void* scratch, void* stream);
 
+/* ---- launched-kernel log (ABI v15, test support) ----
+ * gs_debug_launch_log(enable): record the distinct kernels this library launches from now on (the
+ *   initial state comes from GSRAST_LAUNCH_LOG=1); returns the previous state.
+ * gs_debug_launched_kernels: the recorded kernels' mangled symbol names (the names of the code
+ *   object's kernel descriptors without ".kd"), one per line; returns the text's length and copies it,
+ *   NUL-terminated, when buf holds more than that.  tests/test_zz_kernel_coverage.py checks that every
+ *   kernel of the code object is launched by some GPU test. */
+int gs_debug_launch_log(int enable);
+long long gs_debug_launched_kernels(char* buf, long long cap);
+
 /* ---- numerics mode of the render loops (process-wide) ----
  * exact != 0: the render kernels evaluate exp2 with a deterministic polynomial that the CPU oracle
  * mirrors, so the whole forward is bit-identical to the oracle.  exact == 0 (default): the
@@ -392,6 +402,29 @@ int gs_adam_step_activated(int count, float* const* params_host, const float* co
                            float* const* exp_avg_sq_host, const long long* numel_host, const double* lr_host,
                            const long long* step_host, const double* weight_decay_host, double beta1, double beta2,
                            double eps, int maximize, void* stream);
+
+/* gs_backward_gaussians_adam (ABI v15): one view's per-Gaussian backward half fused with the Adam
+ * step of GaussianModel's six parameter groups (train.py:93 loss.backward() + train.py:123-124
+ * optimizer.step() of one iteration, gaussian_model.py:154-163 groups; the opt-in fused train step
+ * of gs_train_step).  Call after the view's gs_backward_render (its dL_dmeans2D, which the
+ * densification statistics read, comes from there).  Same floats as gs_backward_accumulate_split
+ * (accumulate 0) followed by gs_adam_step_activated in the modes plain / features_dc /
+ * features_rest / sigmoid / exp / normalize: every Gaussian's parameters and moments are
+ * bit-identical to that pair, and no gradient is stored.
+ * M == 16 split SH rows (shs_dc / shs_rest 16-byte aligned), active degree D 0..3 (coefficients
+ * past it get zero gradients, as in gs_backward_accumulate_split); scales /
+ * rotations are the activated render() inputs the forward read, means3D is params_host[0].
+ * params / exp_avg / exp_avg_sq: HOST arrays of 6 DEVICE pointers in group order xyz [P,3],
+ * f_dc [P,1,3], f_rest [P,15,3], opacity [P,1], scaling [P,3], rotation [P,4] (raw parameters,
+ * rotation 16-byte aligned); lr / step / weight_decay per group as gs_adam_step (weight_decay_host
+ * may be NULL).  The Adam update runs in place while the kernel reads the parameters: nothing else
+ * may read or write them on another stream until the call's work completes. */
+int gs_backward_gaussians_adam(int P, int D, int M, const float* means3D, const float* shs_dc, const float* shs_rest,
+                               const float* scales, float scale_modifier, const float* rotations,
+                               const gs_view_grad* view, float* const* params_host, float* const* exp_avg_host,
+                               float* const* exp_avg_sq_host, const double* lr_host, const long long* step_host,
+                               const double* weight_decay_host, double beta1, double beta2, double eps, int maximize,
+                               int debug, void* stream);
 
 /* ---- render() inputs from GaussianModel's raw parameters  <-  get_features / get_opacity /
  *      get_scaling / get_rotation (/root/reference/scene/gaussian_model.py:95-115, read at

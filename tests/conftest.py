@@ -3,6 +3,9 @@ import sys
 
 import pytest
 
+# record every kernel the library launches in this process (tests/test_zz_kernel_coverage.py)
+os.environ.setdefault("GSRAST_LAUNCH_LOG", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "gaussian-splatting-skysphere_amd")
 for p in (ROOT, PKG, os.path.join(ROOT, "tests")):
@@ -14,13 +17,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); parity tests through the C ABI")
     config.addinivalue_line("markers", "spawn_first: starts child processes on the GPU; runs before any other test, "
                                        "while this process has not touched the GPU")
+    config.addinivalue_line("markers", "last: runs after every other test of the session")
     # autograd accumulating one leaf's gradient from backwards on several streams (multi-stream
     # views without a GradBucket): an error, not a warning, so no test relies on it
     config.addinivalue_line("filterwarnings", "error:The AccumulateGrad node's stream does not match:UserWarning")
 
 
 def pytest_collection_modifyitems(config, items):
-    items.sort(key=lambda it: 0 if it.get_closest_marker("spawn_first") else 1)  # stable: keeps the rest in order
+    # stable: keeps the rest in order; the kernel-coverage check runs after everything else
+    items.sort(key=lambda it: 0 if it.get_closest_marker("spawn_first") else 2 if it.get_closest_marker("last") else 1)
 
 
 @pytest.fixture(scope="session")

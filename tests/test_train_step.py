@@ -220,6 +220,9 @@ def test_bounded_overflow_in_a_captured_step_raises_in_the_loop(device):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     bounded_status()
+    # the warm-up's loss would keep its autograd graph (and the leaves' AccumulateGrad nodes, made on
+    # the warm-up stream) alive into the capture, which runs on the capture stream
+    static.clear()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         step()
@@ -234,3 +237,54 @@ def test_bounded_overflow_in_a_captured_step_raises_in_the_loop(device):
     static["loss"].item()
     with pytest.raises(RuntimeError, match="binning capacity"):
         bounded_status()
+
+
+@pytest.mark.parametrize("active_degree", [3, 1])
+def test_fused_adam_train_step_bitwise_equal_unfused(device, active_degree, monkeypatch):
+    """train_step(fuse_adam=True): the per-Gaussian backward fused with the Adam step
+    (gs_backward_gaussians_adam) against the default step (backward, then FusedAdam.step_activated)
+    over three iterations: every parameter, both Adam moments, the step counts and the densification
+    statistics bit-identical, the same loss.item() values -- at the full SH degree and at an active
+    degree below the 16 stored coefficients (train.py's oneupSHdegree schedule)."""
+    import gs_train
+    import gs_train_step as ts
+
+    sc, settings, gt = _setup(device)
+    settings = settings._replace(sh_degree=active_degree)
+    runs = []
+    for fuse in (False, True):
+        m = ts.TrainModel(sc, device, fused=True)
+        if fuse:  # the fused step must not fall back to the unfused optimizer update
+            def refuse(*a, **k):
+                raise AssertionError("fused step fell back to step_activated")
+            monkeypatch.setattr(gs_train.FusedAdam, "step_activated", refuse)
+        losses = [ts.train_step(m, settings, gt, loss_item=True, fuse_adam=fuse) for _ in range(3)]
+        torch.cuda.synchronize()
+        monkeypatch.undo()
+        steps = [float(m.optimizer.state[g["params"][0]]["step"]) for g in m.optimizer.param_groups]
+        runs.append((losses, _state(m), steps, [t.clone() for t in (m.max_radii2D, m.xyz_gradient_accum, m.denom)],
+                     m))
+    (la, sa, ta, da, ma), (lb, sb, tb, db, mb) = runs
+    assert la == lb and ta == tb == [3.0] * 6
+    for k, (a, b) in enumerate(zip(sa, sb)):
+        assert torch.equal(a, b), k
+    for a, b in zip(da, db):
+        assert torch.equal(a, b)
+    assert mb.denom.sum() > 0
+    for name in ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"):
+        assert getattr(mb, name).grad is None, name
+
+
+def test_fused_adam_train_step_releases_its_sinks(device):
+    """After a fused-Adam step the rasterizer inputs are no longer gradient sinks: a plain autograd
+    backward through the model's xyz afterwards gets its own .grad."""
+    import gs_train_step as ts
+    from diff_gaussian_rasterization import _sink_owner
+
+    sc, settings, gt = _setup(device, P=500)
+    m = ts.TrainModel(sc, device, fused=True)
+    ts.train_step(m, settings, gt, fuse_adam=True)
+    assert _sink_owner(m._xyz) is None
+    img, _, _ = ts.render(m, settings, fused=True)
+    img.sum().backward()
+    assert m._xyz.grad is not None and m._xyz.grad.abs().sum() > 0
