@@ -241,14 +241,17 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
 
 
 def train_step_views(model: TrainModel, bucket, views, lambda_dssim: float = LAMBDA_DSSIM, densify_stats: bool = True,
-                     average: bool = False):
+                     average: bool = False, sharded=None):
     """One view-parallel optimizer step (gs_view_parallel): this rank's views
     `views` = [(settings, gt_image)] each run render -> L1 + SSIM -> backward with the fused glue,
     their raw-parameter gradients accumulate in `bucket` (a gs_view_parallel.GradBucket over the six
     parameters, lazy_zero=False: the activation backward accumulates too), ONE all-reduce sums the
     bucket over the ranks (every rank holds the same sum), then every rank runs the same Adam step,
     so the replicas stay bit-identical.  Densification statistics stay per rank until
-    gs_view_parallel.reduce_densify_stats at densify time.  Returns the rank's losses."""
+    gs_view_parallel.reduce_densify_stats at densify time.  sharded (a gs_view_parallel.ShardedAdam
+    over the bucket and model.optimizer): reduce-scatter -> sharded Adam -> all-gather in place of the
+    all-reduce and the replicated step (call its gather_state() before densify).  Returns the rank's
+    losses."""
     bucket.zero_grad()
     losses = []
     for settings, gt in views:
@@ -259,6 +262,9 @@ def train_step_views(model: TrainModel, bucket, views, lambda_dssim: float = LAM
             with torch.no_grad():
                 gs_train.add_densification_stats(model, viewspace, radii)
         losses.append(loss)
+    if sharded is not None:
+        sharded.step(average=average)
+        return losses
     bucket.allreduce(average=average)
     with torch.no_grad():
         model.optimizer.step()

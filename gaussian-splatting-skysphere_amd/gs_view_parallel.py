@@ -15,6 +15,7 @@ train.py:118-121): gradient accumulators and denominators are summed, max_radii2
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Iterable, List, Optional, Sequence
 
 import torch
@@ -318,6 +319,213 @@ class GradBucket:
                     work = None
                 flat.div_(dist.get_world_size(group))
         return work if async_op else flat
+
+
+class ShardedAdam:
+    """The optimizer step of view-parallel training as reduce-scatter -> sharded Adam -> all-gather
+    (ZeRO-1 style) instead of all-reduce -> replicated Adam, in Gaussian-row chunks.
+
+    Rows [0, Pm) (Pm = P rounded down to a multiple of the world size N) are cut into `chunks` row
+    ranges whose sizes are multiples of N; in chunk c every rank owns an equal slice of S_c rows.  Per
+    chunk, for every parameter of the bucket: the gradient rows are reduce-scattered (each rank gets
+    the summed rows of its slice), the rank runs the Adam update on its slice only (FusedAdam's
+    kernel, the parameter's own lr / step / moments), and the updated rows are all-gathered in place
+    into every replica.  The < N tail rows [Pm, P) are all-reduced and updated by every rank.  With a
+    deferred per-Gaussian backward pending (GradBucket(defer=True)), chunk c's pass runs on the
+    current stream while chunk c-1's collectives and update run on a side stream.
+
+    Same values as GradBucket.allreduce + FusedAdam.step: every element is the same sum of the ranks'
+    gradients (bit-identical at N = 2, where a sum of two is one rounding in any order; at N > 2 the
+    ring's association may differ from the all-reduce's) and the same Adam arithmetic.  The moment
+    tensors in optimizer.state stay full-size, but only the rows a rank owns are current:
+    gather_state() all-gathers them, and must run before anything reads whole moments (densify_and_prune,
+    state_dict); the row plan follows P afterwards.  Bytes on the wire per step equal the all-reduce's
+    (an all-reduce IS a reduce-scatter + an all-gather); the Adam work per rank is 1/N of it."""
+
+    def __init__(self, optimizer, bucket: GradBucket, group=None, chunks: int = 4, update=None):
+        self.opt, self.bucket, self.group = optimizer, bucket, group
+        self.chunks = max(1, int(chunks))
+        self._update = update  # (items, b1, b2, eps, maximize) -> None; default: FusedAdam's HIP kernel
+        self._comm = None
+        self._bufs = {}
+
+    def _world(self):
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(self.group), dist.get_rank(self.group)
+        return 1, 0
+
+    def plan(self, P: int):
+        """[(b, e, S)]: the chunks' row ranges over [0, Pm) (e - b == N S) and Pm."""
+        N, _ = self._world()
+        Pm = (P // N) * N
+        units = Pm // N
+        C = max(1, min(self.chunks, units))
+        cuts = [N * (units * c // C) for c in range(C + 1)]
+        return [(cuts[c], cuts[c + 1], (cuts[c + 1] - cuts[c]) // N) for c in range(C) if cuts[c + 1] > cuts[c]], Pm
+
+    def _groups(self):
+        out = []
+        where = {id(p): g for g in self.opt.param_groups for p in g["params"]}
+        for p in self.bucket.params:
+            g = where.get(id(p))
+            if g is None:
+                raise ValueError("ShardedAdam: a bucket parameter is not in the optimizer")
+            out.append(g)
+        return out
+
+    def _run_update(self, items, hyper, dev):
+        b1, b2, eps, maximize = hyper
+        if self._update is not None:
+            return self._update(items, b1, b2, eps, maximize)
+        import gs_train
+
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        gs_train.FusedAdam._launch(items, b1, b2, eps, maximize, dev, st)
+
+    def _collective_ctx(self, dev):
+        if dist.get_backend(self.group) == "nccl":
+            return dist._coalescing_manager(self.group, device=dev, async_ops=True)
+        return None
+
+    @torch.no_grad()
+    def step(self, average: bool = False) -> None:
+        """One optimizer step from the bucket's gradients (replaces bucket.allreduce() +
+        optimizer.step()).  The current stream waits for the step's collectives at the end."""
+        b = self.bucket
+        b._check_bound()
+        params = b.params
+        P = params[0].shape[0]
+        if any(p.dim() == 0 or p.shape[0] != P for p in params):
+            raise ValueError("ShardedAdam: every bucket parameter must have the same row count")
+        N, r = self._world()
+        groups = self._groups()
+        hyper = {(float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), bool(g.get("maximize", False)))
+                 for g in groups}
+        if len(hyper) != 1:
+            raise ValueError("ShardedAdam: the parameter groups must share betas, eps and maximize")
+        hyper = hyper.pop()
+        for g in groups:
+            if g.get("amsgrad", False) or g.get("decoupled_weight_decay", False):
+                raise NotImplementedError("ShardedAdam: amsgrad / decoupled weight decay are not supported")
+        moments = [self._state(p) for p in params]
+        steps = [self.opt._advance(p)[2] for p in params]
+        lrs = [float(g["lr"]) for g in groups]
+        wds = [float(g.get("weight_decay", 0.0)) for g in groups]
+        chunks, Pm = self.plan(P)
+        dev = b.flat.device
+        on_dev = b.flat.is_cuda
+        deferred = bool(b._deferred)
+        if deferred:
+            inputs, views, outs, acc = b._claim_deferred()
+            b._zero_unwritten()
+        else:
+            b.finalize()
+        cur = torch.cuda.current_stream(dev) if on_dev else None
+        if on_dev and self._comm is None:
+            self._comm = torch.cuda.Stream(dev)
+        comm = self._comm
+        rows = [p.grad.view(P, -1) for p in params]  # gradient rows (bucket views)
+        data = [p.detach().view(P, -1) for p in params]
+        mv = [(m.view(P, -1), v.view(P, -1)) for m, v in moments]
+        works = []
+        last = len(chunks) - 1
+        for c, (lo, hi, S) in enumerate(chunks + ([(Pm, Pm, 0)] if not chunks else [])):
+            end = P if c == max(last, 0) else hi  # the last chunk's pass also covers the tail rows
+            if deferred:
+                b._deferred_pass(inputs, views, outs, acc, first=lo, count=end - lo)
+            if on_dev:
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                comm.wait_event(ev)
+            with (torch.cuda.stream(comm) if on_dev else _nullctx()):
+                items = []
+                if S > 0:
+                    shard = self._buf(c, rows, S, dev)
+                    cm = self._collective_ctx(dev) if on_dev else None
+                    with (cm if cm is not None else _nullctx()):
+                        for k, g in enumerate(rows):
+                            dist.reduce_scatter_tensor(shard[k].view(-1), g[lo:hi].reshape(-1), group=self.group)
+                    if cm is not None:
+                        cm.wait()
+                    a, z = lo + r * S, lo + (r + 1) * S
+                    for k in range(len(params)):
+                        if average:
+                            shard[k].div_(N)
+                        items.append((data[k][a:z], shard[k], mv[k][0][a:z], mv[k][1][a:z], lrs[k], steps[k], wds[k]))
+                if c == max(last, 0) and Pm < P:  # the tail: all-reduced, updated by every rank
+                    for k, g in enumerate(rows):
+                        t = g[Pm:P]
+                        dist.all_reduce(t, group=self.group)
+                        if average:
+                            t.div_(N)
+                        items.append((data[k][Pm:P], t, mv[k][0][Pm:P], mv[k][1][Pm:P], lrs[k], steps[k], wds[k]))
+                if items:
+                    self._run_update(items, hyper, dev)
+                if S > 0:
+                    cm = self._collective_ctx(dev) if on_dev else None
+                    with (cm if cm is not None else _nullctx()):
+                        for k in range(len(params)):
+                            dist.all_gather_into_tensor(data[k][lo:hi].reshape(-1), data[k][a:z].reshape(-1),
+                                                        group=self.group)
+                    if cm is not None:
+                        works.append(cm)
+        if deferred:
+            b._retire_deferred(inputs, views)
+        for w in works:
+            w.wait()
+        if on_dev:
+            cur.wait_stream(comm)
+            b.written(cur)
+
+    def _state(self, p):
+        """(exp_avg, exp_avg_sq) of p, created as torch's Adam creates them, checked full-size"""
+        st = self.opt.state[p]
+        if len(st) == 0:
+            st["step"] = torch.tensor(0.0, dtype=torch.float32)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        m, v = st["exp_avg"], st["exp_avg_sq"]
+        for t in (m, v):
+            if t.shape != p.shape or t.dtype != torch.float32 or not t.is_contiguous() or t.device != p.device:
+                raise ValueError("ShardedAdam: optimizer state must be contiguous float32 of the parameter's shape")
+        return m, v
+
+    def _buf(self, c, rows, S, dev):
+        key = (c, S, tuple(g.shape[1] for g in rows), str(dev))
+        buf = self._bufs.get(key)
+        if buf is None:
+            if len(self._bufs) > 64:
+                self._bufs.clear()
+            buf = self._bufs[key] = [torch.empty((S, g.shape[1]), dtype=torch.float32, device=dev) for g in rows]
+        return buf
+
+    @torch.no_grad()
+    def gather_state(self) -> None:
+        """Make every rank's Adam moments whole (all-gather of the owned rows of exp_avg /
+        exp_avg_sq, chunk by chunk): call before densify_and_prune or state_dict()."""
+        N, r = self._world()
+        if N == 1:
+            return
+        params = self.bucket.params
+        P = params[0].shape[0]
+        chunks, _ = self.plan(P)
+        for p in params:
+            st = self.opt.state.get(p)
+            if not st:
+                continue
+            for t in (st["exp_avg"], st["exp_avg_sq"]):
+                rows = t.view(P, -1)
+                for lo, hi, S in chunks:
+                    a, z = lo + r * S, lo + (r + 1) * S
+                    dist.all_gather_into_tensor(rows[lo:hi].reshape(-1), rows[a:z].reshape(-1), group=self.group)
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
 
 
 def _same_inputs(a, b) -> bool:

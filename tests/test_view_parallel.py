@@ -1,5 +1,6 @@
 """View-parallel exchange (gs_view_parallel) on CPU with gloo, world_size 2: one flat bucket
 all-reduce of the 59-float/Gaussian gradient set, densify-statistics reduction, view sharding."""
+import math
 import os
 import socket
 
@@ -181,3 +182,134 @@ def test_sync_from_rank0_and_check_replicas_gloo_world2():
         assert p.exitcode == 0
     for rank, t, same, differ in res:
         assert (t == 1.0).all() and same and not differ
+
+
+def _np_adam(items, b1, b2, eps, maximize):
+    """Adam on CPU rows for the sharding test (numpy float32 ufuncs: one rounding per op, so every
+    element's result is independent of how the rows are sliced); the GPU path is FusedAdam's kernel."""
+    import numpy as np
+
+    f = np.float32
+    for p, g, m, v, lr, t, wd in items:
+        pn, gn, mn, vn = (x.numpy() for x in (p, g, m, v))
+        gg = -gn if maximize else gn.copy()
+        if wd:
+            gg += f(wd) * pn
+        mn += f(1 - b1) * (gg - mn)
+        vn *= f(b2)
+        vn += f(1 - b2) * gg * gg
+        denom = np.sqrt(vn) / f(math.sqrt(1 - b2 ** t)) + f(eps)
+        pn += f(-lr / (1 - b1 ** t)) * (mn / denom)
+
+
+def _sharded_worker(rank, world, port, P, chunks, out_q):
+    """Two replicas per rank from the same init: one steps through GradBucket.allreduce + Adam on all
+    rows, the other through ShardedAdam (reduce-scatter, Adam on the rank's rows, all-gather); three
+    steps, a densify-like resize (prune + append rows of params and moments, new P with a tail), two
+    more steps."""
+    import gs_train
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        widths = [(3,), (1, 3), (15, 3), (1,), (3,), (4,)]
+        lrs = [1.6e-4, 2.5e-3, 1.25e-4, 5e-2, 5e-3, 1e-3]
+
+        def make(P):
+            g = torch.Generator().manual_seed(5)
+            ps = [torch.nn.Parameter(torch.randn((P,) + w, generator=g)) for w in widths]
+            opt = gs_train.FusedAdam([{"params": [p], "lr": lr} for p, lr in zip(ps, lrs)], lr=0.0, eps=1e-15)
+            return ps, opt, vp.GradBucket(ps)
+
+        pa, oa, ba = make(P)
+        pb, ob, bb = make(P)
+        sh = vp.ShardedAdam(ob, bb, chunks=chunks, update=_np_adam)
+
+        def grads(step, ps, bucket):
+            g = torch.Generator().manual_seed(100 * step + rank)
+            bucket.zero_grad()
+            for p in ps:
+                p.grad.copy_(torch.randn(p.shape, generator=g))
+
+        def step_a(step):
+            grads(step, pa, ba)
+            ba.allreduce()
+            items = []
+            for p, grp in zip(pa, oa.param_groups):
+                st = oa.state[p]
+                if not st:
+                    st.update(step=torch.tensor(0.0), exp_avg=torch.zeros_like(p), exp_avg_sq=torch.zeros_like(p))
+                t = oa._advance(p)[2]
+                items.append((p.detach(), p.grad, st["exp_avg"], st["exp_avg_sq"], grp["lr"], t, 0.0))
+            _np_adam(items, 0.9, 0.999, 1e-15, False)
+
+        def step_b(step):
+            grads(step, pb, bb)
+            sh.step()
+
+        for s_ in range(3):
+            step_a(s_)
+            step_b(s_)
+        sh.gather_state()
+
+        def resize(ps, opt, bucket):  # keep 3 of every 4 rows, append 6 copies of the first rows
+            keep = torch.arange(ps[0].shape[0]) % 4 != 1
+            new = []
+            for i, p in enumerate(ps):
+                st = opt.state.pop(p)
+                f = lambda t: torch.cat([t[keep], t[:6]]).contiguous()  # noqa: E731
+                q = torch.nn.Parameter(f(p.detach()))
+                st["exp_avg"], st["exp_avg_sq"] = f(st["exp_avg"]), f(st["exp_avg_sq"])
+                opt.state[q] = st
+                opt.param_groups[i]["params"][0] = q
+                new.append(q)
+            bucket.rebind(new)
+            return new
+
+        pa[:] = resize(pa, oa, ba)
+        pb[:] = resize(pb, ob, bb)
+        for s_ in range(3, 5):
+            step_a(s_)
+            step_b(s_)
+        sh.gather_state()
+
+        def dump(ps, opt):
+            return [t.detach().numpy().copy() for p in ps for t in (p, opt.state[p]["exp_avg"], opt.state[p]["exp_avg_sq"])]
+
+        out_q.put((rank, dump(pa, oa), dump(pb, ob), [float(ob.state[p]["step"]) for p in pb], pb[0].shape[0],
+                   sh.plan(pb[0].shape[0])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("P,chunks", [(37, 3), (64, 4), (1, 2)])
+def test_sharded_adam_equals_allreduce_gloo_world2(P, chunks):
+    """ShardedAdam (reduce-scatter -> Adam on the rank's row slices -> all-gather, in row chunks, with
+    the odd tail all-reduced) against GradBucket.allreduce + Adam on every row, world 2 (gloo, CPU):
+    parameters and both moments bit-identical on both ranks after 3 steps, a resize of every
+    parameter and moment (rows pruned and appended, as densify_and_prune does; gather_state first) and
+    2 more steps."""
+    import numpy as np
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, P, chunks, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, a, b, steps, Pn, plan = q.get(timeout=120)
+        res[r] = (a, b, steps, Pn, plan)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        a, b, steps, Pn, plan = res[r]
+        assert steps == [5.0] * 6
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(b, res[0][1]):
+            np.testing.assert_array_equal(x, y)
+    if P >= 4:
+        assert len(res[0][4][0]) > 1  # the step ran in several chunks

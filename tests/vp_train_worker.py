@@ -93,6 +93,58 @@ def gloo2():
     dist.destroy_process_group()
 
 
+def gloo2_sharded():
+    """Two replicas per rank from the same scene: A steps through the bucket all-reduce + FusedAdam,
+    B through gs_view_parallel.ShardedAdam (reduce-scatter -> FusedAdam on the rank's row slices ->
+    all-gather, 3 row chunks); three steps, reduce_densify_stats, gather_state, densify_and_prune (same
+    seeded draws for A and B, rank 0's broadcast), two more steps.  A and B bit-identical on every rank
+    and B identical across the ranks."""
+    import gs_train_step as ts
+    import gs_view_parallel as vp
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    sc, settings, gts = setup(dev, rank)
+    mine = [(settings[v], gts[v]) for v in vp.shard_views(4, rank, world)]
+    runs = []
+    for sharded in (False, True):
+        m = ts.TrainModel(sc, dev, fused=True)
+        bucket = vp.GradBucket([m._xyz, m._features_dc, m._features_rest, m._opacity, m._scaling, m._rotation])
+        sh = vp.ShardedAdam(m.optimizer, bucket, chunks=3) if sharded else None
+        for _ in range(3):
+            ts.train_step_views(m, bucket, mine, sharded=sh)
+        vp.reduce_densify_stats(m.xyz_gradient_accum, m.denom, m.max_radii2D)
+        g = torch.Generator(device=dev).manual_seed(7)
+        boost = (torch.rand((m.P, 1), generator=g, device=dev) < 0.05).float() * 1e-2
+        m.xyz_gradient_accum += boost * m.denom
+        if sh is not None:
+            sh.gather_state()
+        torch.manual_seed(1000 + rank)
+        P0 = m.P
+        ts.densify(m, extent=0.5)
+        for _ in range(2):
+            ts.train_step_views(m, bucket, mine, sharded=sh)
+        if sh is not None:
+            sh.gather_state()
+        torch.cuda.synchronize()
+        runs.append(([t.clone() for t in model_tensors(m)], P0, m.P,
+                     [float(m.optimizer.state[g_["params"][0]]["step"]) for g_ in m.optimizer.param_groups]))
+        bucket.close()
+    (ta, p0a, pa, sa), (tb, p0b, pb, sb) = runs
+    same = len(ta) == len(tb) and all(torch.equal(x, y) for x, y in zip(ta, tb))
+    replicas = vp.check_replicas(tb)
+    if rank == 0:
+        ok = same and replicas and pa == pb and pa != p0a and sa == sb == [5.0] * 6
+        msg = ("OK " if ok else "FAIL ") + (f"sharded == all-reduce {same}; sharded replicas equal {replicas}; "
+                                            f"P {p0a} -> {pa} / {pb}; steps {sa} / {sb}")
+        with open(os.environ["GS_VP_OUT"], "w") as f:
+            f.write(msg + "\n")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def nccl1():
     import gs_train_step as ts
     import gs_view_parallel as vp
@@ -102,11 +154,12 @@ def nccl1():
     sc, settings, gts = setup(dev, 0)
     views = [(settings[v], gts[v]) for v in range(2)]
 
-    def run():
+    def run(sharded=False):
         m = ts.TrainModel(sc, dev, fused=True)
         b = vp.GradBucket([m._xyz, m._features_dc, m._features_rest, m._opacity, m._scaling, m._rotation])
+        sh = vp.ShardedAdam(m.optimizer, b, chunks=3) if sharded else None
         for _ in range(2):
-            ts.train_step_views(m, b, views)
+            ts.train_step_views(m, b, views, sharded=sh)
         torch.cuda.synchronize()
         b.close()
         return [t.clone() for t in model_tensors(m)]
@@ -120,14 +173,17 @@ def nccl1():
     got = run()
     dist.all_reduce = orig
     same = all(torch.equal(a, b) for a, b in zip(ref, got))
+    # the sharded step through RCCL (reduce-scatter / all-gather at world 1, coalesced per chunk)
+    sharded_same = all(torch.equal(a, b) for a, b in zip(ref, run(sharded=True)))
     # the chunked all-reduce (RCCL coalesced groups per Gaussian-row range, on a side stream,
     # overlapping the deferred per-Gaussian pass) against the bucket's one-shot finalize
     chunk_same = chunked_vs_finalize(sc, settings, dev)
     backend = dist.get_backend()
     dist.destroy_process_group()
-    ok = same and len(calls) == 2 and backend == "nccl" and chunk_same
+    ok = same and len(calls) == 2 and backend == "nccl" and chunk_same and sharded_same
     msg = ("OK " if ok else "FAIL ") + (f"backend {backend}; all-reduces {len(calls)}; bitwise equal to no-group "
-                                        f"{same}; chunked all-reduce equal to finalize {chunk_same}")
+                                        f"{same}; chunked all-reduce equal to finalize {chunk_same}; sharded step "
+                                        f"equal {sharded_same}")
     with open(os.environ["GS_VP_OUT"], "w") as f:
         f.write(msg + "\n")
 
@@ -158,4 +214,4 @@ def chunked_vs_finalize(sc, settings, dev):
 
 
 if __name__ == "__main__":
-    {"gloo2": gloo2, "nccl1": nccl1}[sys.argv[1]]()
+    {"gloo2": gloo2, "gloo2_sharded": gloo2_sharded, "nccl1": nccl1}[sys.argv[1]]()
