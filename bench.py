@@ -146,6 +146,9 @@ def main():
     ap.add_argument("--step-events", action="store_true",
                     help="diagnostic: record a HIP event after every timed step (no host syncs) and report the "
                          "per-step times of the timed region in deciles")
+    ap.add_argument("--regions", type=int, default=5,
+                    help="timed regions of --steps steps each; `value` is the median region's rate, every "
+                         "region's rate is reported (`regions_iters_s`)")
     ap.add_argument("--sustain-s", type=float, default=2.0,
                     help="after the timed steps, keep stepping for this long (untimed for `value`) and report "
                          "the sustained rate too")
@@ -315,27 +318,35 @@ def main():
         step()
     torch.cuda.synchronize()
     torch.cuda.reset_peak_memory_stats(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    if args.step_events:
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-        evs[0].record()
-        for k in range(args.steps):
-            step()
-            evs[k + 1].record()
-    else:
-        for _ in range(args.steps):
-            step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    # `regions` timed regions of exactly K steps each, every one bracketed by a barrier and a device
+    # sync (max over ranks); `value` is the median region (host-bound configurations such as C2 vary
+    # from region to region with the box's host load; every region is reported)
+    region_s = []
+    for reg in range(max(1, args.regions)):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if args.step_events and reg == 0:
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+            evs[0].record()
+            for k in range(args.steps):
+                step()
+                evs[k + 1].record()
+        else:
+            for _ in range(args.steps):
+                step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        region_s.append(el)
+    elapsed = sorted(region_s)[len(region_s) // 2]
     peak_hbm = torch.cuda.max_memory_allocated(dev)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     # sustained rate: keep stepping for ~--sustain-s (a longer region than the K timed steps,
     # which last only tens of ms; the same step, reported beside `value`, not instead of it)
@@ -570,6 +581,7 @@ def main():
         "ms_per_view": round(ms_per_view, 4),
         "step_roofline": step_roofline,
         "sustained": sustained,
+        "regions_iters_s": [round((n_views or world * len(my_views)) * args.steps / r_, 2) for r_ in region_s],
         "streams": len(streams),
         "fused_front": fused_front,
         "serial_one_stream": serial,

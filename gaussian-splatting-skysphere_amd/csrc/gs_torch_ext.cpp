@@ -10,8 +10,10 @@
 // It does not link libgsrast.so: _native.load() has already loaded it RTLD_GLOBAL, and init()
 // resolves the entry points from that one copy (its per-device state -- bounded status, ordering
 // flags, numerics mode -- stays shared with the ctypes path).  Same exception texts as _C.py.
-// Plain calls only: prepared views, bounded forwards, gradient sinks and the split backward halves
-// stay on the ctypes path.  The forward reads its instance count back after queueing every launch
+// Every call of the training paths goes through here: the eager forward, the bounded forward
+// (binning capacity), prepared views, the backward with gradient sinks / a wait event, and the split
+// backward halves; the ctypes bridge keeps only the debug exports, the want_all backward of the
+// upstream-named entry and the CPU-less error paths.  The forward reads its instance count back after queueing every launch
 // (gs_forward_counted, binning buffer sized from the last count), so neither the device nor the host
 // idles across the host round trip that upstream's resize callbacks need between the two halves.
 #include <ATen/hip/HIPContext.h>
@@ -38,6 +40,7 @@ struct Fns {
   decltype(&gs_forward_render) render = nullptr;
   decltype(&gs_forward_counted) counted = nullptr;
   decltype(&gs_forward_render_bounded) render_bounded = nullptr;
+  decltype(&gs_forward_bounded) fwd_bounded = nullptr;
   decltype(&gs_forward_preprocess_views) pre_views = nullptr;
   decltype(&gs_forward_preprocess_views_bounded) pre_views_bounded = nullptr;
   decltype(&gs_forward_bin_views) bin_views = nullptr;
@@ -71,6 +74,7 @@ void init() {
   resolve(F.render, "gs_forward_render");
   resolve(F.counted, "gs_forward_counted");
   resolve(F.render_bounded, "gs_forward_render_bounded");
+  resolve(F.fwd_bounded, "gs_forward_bounded");
   resolve(F.pre_views, "gs_forward_preprocess_views");
   resolve(F.pre_views_bounded, "gs_forward_preprocess_views_bounded");
   resolve(F.bin_views, "gs_forward_bin_views");
@@ -261,6 +265,38 @@ py::tuple forward(const at::Tensor& background, const at::Tensor& means3D, const
   return py::make_tuple((int64_t)nr, out_color, radii, geom, binning, img);
 }
 
+// _C.rasterize_gaussians with a binning capacity: the whole forward enqueued without a host wait
+// (gs_forward_bounded); num_rendered is returned as the capacity
+py::tuple forward_bounded(const at::Tensor& background, const at::Tensor& means3D,
+                          const c10::optional<at::Tensor>& colors, const c10::optional<at::Tensor>& opacity,
+                          const c10::optional<at::Tensor>& scales, const c10::optional<at::Tensor>& rotations,
+                          double scale_modifier, const c10::optional<at::Tensor>& cov3D, const at::Tensor& viewmatrix,
+                          const at::Tensor& projmatrix, double tan_fovx, double tan_fovy, int64_t H, int64_t W,
+                          const c10::optional<at::Tensor>& sh, int64_t degree, const at::Tensor& campos,
+                          bool prefiltered, bool debug, const c10::optional<at::Tensor>& sh_rest, int64_t capacity) {
+  Inputs x(background, means3D, colors, opacity, scales, rotations, cov3D, viewmatrix, projmatrix, sh, campos, true,
+           sh_rest);
+  const auto u8 = at::TensorOptions().dtype(at::kByte).device(x.dev);
+  const auto f32o = at::TensorOptions().dtype(at::kFloat).device(x.dev);
+  if (x.P == 0) {
+    return py::make_tuple(0, at::zeros({3, H, W}, f32o), at::zeros({0}, f32o.dtype(at::kInt)), at::empty({0}, u8),
+                          at::empty({0}, u8), at::empty({0}, u8));
+  }
+  c10::DeviceGuard guard(x.dev);
+  at::Tensor out_color = at::empty({3, H, W}, f32o);
+  at::Tensor radii = at::empty({x.P}, f32o.dtype(at::kInt));
+  at::Tensor geom = at::empty({(int64_t)F.geom_bytes((int)x.P)}, u8);
+  at::Tensor binning = at::empty({(int64_t)F.binning_bytes((long long)capacity, (int)W, (int)H)}, u8);
+  at::Tensor img = at::empty({(int64_t)F.image_bytes((int)W, (int)H)}, u8);
+  check(F.fwd_bounded((int)x.P, (int)degree, (int)x.M, fp(x.bg), (int)W, (int)H, fp(x.means3D), fp(x.sh),
+                      fp(x.sh_rest), fp(x.colors), fp(x.opacity), fp(x.scales), (float)scale_modifier,
+                      fp(x.rotations), fp(x.cov3D), fp(x.view), fp(x.proj), fp(x.campos), (float)tan_fovx,
+                      (float)tan_fovy, (int)prefiltered, radii.data_ptr<int>(), geom.data_ptr(), (long long)capacity,
+                      binning.data_ptr(), img.data_ptr(), out_color.data_ptr<float>(), (int)debug, stream_of(x.dev)),
+        "rasterize_gaussians (bounded)");
+  return py::make_tuple(capacity, out_color, radii, geom, binning, img);
+}
+
 // _C.binning_layout_count: the instance count the binning buffer is laid out for (R, or the capacity
 // of a gs_forward_counted buffer)
 long long layout_count(long long R, const at::Tensor& binning, int64_t W, int64_t H) {
@@ -271,7 +307,9 @@ long long layout_count(long long R, const at::Tensor& binning, int64_t W, int64_
   return L;
 }
 
-// _C.backward_impl with want_all=False, no gradient sinks and no wait event
+// _C.backward_impl with want_all=False.  sinks: {name: (buffer, accumulate)} -- that gradient is
+// written into (accumulate: added to) the caller's buffer, returned in its place (gradient buckets);
+// wait_event: a hipEvent_t the stream waits for before the gradient-writing kernel (0: none)
 py::tuple backward(const at::Tensor& background, const at::Tensor& means3D, const at::Tensor& radii,
                    const c10::optional<at::Tensor>& colors, const c10::optional<at::Tensor>& scales,
                    const c10::optional<at::Tensor>& rotations, double scale_modifier,
@@ -279,7 +317,7 @@ py::tuple backward(const at::Tensor& background, const at::Tensor& means3D, cons
                    double tan_fovx, double tan_fovy, const at::Tensor& dL_dout_color,
                    const c10::optional<at::Tensor>& sh, int64_t degree, const at::Tensor& campos,
                    const at::Tensor& geom, int64_t R, const at::Tensor& binning, const at::Tensor& img, bool debug,
-                   const c10::optional<at::Tensor>& sh_rest) {
+                   const c10::optional<at::Tensor>& sh_rest, const py::dict& sinks, int64_t wait_event) {
   Inputs x(background, means3D, colors, c10::nullopt, scales, rotations, cov3D, viewmatrix, projmatrix, sh, campos,
            false, sh_rest);
   const int64_t P = x.P, M = x.M;
@@ -287,15 +325,32 @@ py::tuple backward(const at::Tensor& background, const at::Tensor& means3D, cons
   const int64_t H = dL_dout_color.size(1), W = dL_dout_color.size(2);
   const bool has_sr = x.scales.defined() && x.rotations.defined() && !x.cov3D.defined();
   const bool need_sr = x.scales.defined() && x.rotations.defined();
+  unsigned acc = 0;
+  // a computed gradient with a sink goes to the sink's buffer (GS_ACC bit `bit` when accumulating)
+  auto sunk = [&](const char* name, int bit, int64_t numel, at::Tensor& out) -> bool {
+    if (sinks.empty() || !sinks.contains(name)) return false;
+    py::tuple t = sinks[name].cast<py::tuple>();
+    at::Tensor buf = t[0].cast<at::Tensor>();
+    TORCH_CHECK(buf.scalar_type() == at::kFloat && buf.device() == x.dev && buf.is_contiguous() &&
+                    buf.numel() == numel,
+                "gradient sink for ", name, ": expected a contiguous float32 buffer of ", numel, " elements on ",
+                x.dev.str());
+    out = buf;
+    if (t[1].cast<bool>()) acc |= 1u << bit;
+    return true;
+  };
   // upstream order: means2D, colors, opacity, means3D, cov3D, sh, scales, rotations
-  at::Tensor g_m2 = at::empty({P, 3}, f32o), g_op = at::empty({P, 1}, f32o), g_m3 = at::empty({P, 3}, f32o);
-  at::Tensor g_col = x.colors.defined() ? at::empty({P, 3}, f32o) : at::Tensor();
-  at::Tensor g_cov = x.cov3D.defined() ? at::empty({P, 6}, f32o) : at::Tensor();
-  at::Tensor g_sh = x.sh.defined() ? at::empty({P, M, 3}, f32o) : at::Tensor();
-  at::Tensor g_sc, g_rot;
+  at::Tensor g_m2, g_op, g_m3, g_col, g_cov, g_sh, g_sc, g_rot;
+  if (!sunk("means2D", 0, 3 * P, g_m2)) g_m2 = at::empty({P, 3}, f32o);
+  if (x.colors.defined() && !sunk("colors", 1, 3 * P, g_col)) g_col = at::empty({P, 3}, f32o);
+  if (!sunk("opacity", 2, P, g_op)) g_op = at::empty({P, 1}, f32o);
+  if (!sunk("means3D", 3, 3 * P, g_m3)) g_m3 = at::empty({P, 3}, f32o);
+  if (x.cov3D.defined() && !sunk("cov3D", 4, 6 * P, g_cov)) g_cov = at::empty({P, 6}, f32o);
+  if (x.sh.defined() && !sunk("sh", 5, 3 * M * P, g_sh)) g_sh = at::empty({P, M, 3}, f32o);
   if (need_sr) {
-    g_sc = has_sr ? at::empty({P, 3}, f32o) : at::zeros({P, 3}, f32o);
-    g_rot = has_sr ? at::empty({P, 4}, f32o) : at::zeros({P, 4}, f32o);
+    if (!(has_sr && sunk("scales", 6, 3 * P, g_sc))) g_sc = has_sr ? at::empty({P, 3}, f32o) : at::zeros({P, 3}, f32o);
+    if (!(has_sr && sunk("rotations", 7, 4 * P, g_rot)))
+      g_rot = has_sr ? at::empty({P, 4}, f32o) : at::zeros({P, 4}, f32o);
   }
   auto opt = [](const at::Tensor& t) -> py::object { return t.defined() ? py::cast(t) : py::none(); };
   auto result = [&]() {
@@ -315,7 +370,7 @@ py::tuple backward(const at::Tensor& background, const at::Tensor& means3D, cons
                            radii.data_ptr<int>(), geom.data_ptr(), (long long)R, binning.data_ptr(), img.data_ptr(),
                            fp(dpix), scratch.data_ptr(), g_m2.data_ptr<float>(), g_op.data_ptr<float>(),
                            g_m3.data_ptr<float>(), (float*)vp(g_cov), (float*)vp(g_sh), (float*)vp(sc_out),
-                           (float*)vp(rot_out), 0u, nullptr, (int)debug, st),
+                           (float*)vp(rot_out), acc, reinterpret_cast<void*>(wait_event), (int)debug, st),
           "rasterize_gaussians_backward");
     return result();
   }
@@ -324,8 +379,8 @@ py::tuple backward(const at::Tensor& background, const at::Tensor& means3D, cons
                    fp(x.proj), fp(x.campos), (float)tan_fovx, (float)tan_fovy, radii.data_ptr<int>(), geom.data_ptr(),
                    (long long)R, binning.data_ptr(), img.data_ptr(), fp(dpix), scratch.data_ptr(),
                    g_m2.data_ptr<float>(), (float*)vp(g_col), g_op.data_ptr<float>(), g_m3.data_ptr<float>(),
-                   (float*)vp(g_cov), (float*)vp(g_sh), (float*)vp(sc_out), (float*)vp(rot_out), 0u, nullptr,
-                   (int)debug, st),
+                   (float*)vp(g_cov), (float*)vp(g_sh), (float*)vp(sc_out), (float*)vp(rot_out), acc,
+                   reinterpret_cast<void*>(wait_event), (int)debug, st),
         "rasterize_gaussians_backward");
   return result();
 }
@@ -577,6 +632,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "host fast path of diff_gaussian_rasterization._C over libgsrast.so (see gs_torch_ext.cpp)";
   m.def("init", &init);
   m.def("forward", &forward);
+  m.def("forward_bounded", &forward_bounded);
   m.def("backward", &backward);
   m.def("preprocess_views", &preprocess_views);
   m.def("forward_prepared", &forward_prepared);

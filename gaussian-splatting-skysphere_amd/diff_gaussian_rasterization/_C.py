@@ -222,6 +222,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     if _EXT is not None and prepared is not None and capacity is None and sh_rest is None and means3D.is_cuda:
         return _EXT.forward_prepared(background, means3D, viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy),
                                      int(image_height), int(image_width), campos, bool(debug), tuple(prepared))
+    if _EXT is not None and prepared is None and capacity is not None and means3D.is_cuda:
+        return _EXT.forward_bounded(background, means3D, colors, opacity, scales, rotations, float(scale_modifier),
+                                    cov3D_precomp, viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy),
+                                    int(image_height), int(image_width), sh, int(degree), campos, bool(prefiltered),
+                                    bool(debug), sh_rest, int(capacity))
     if _EXT is not None and prepared is None and capacity is None and means3D.is_cuda:
         out = _EXT.forward(background, means3D, colors, opacity, scales, rotations, float(scale_modifier),
                            cov3D_precomp, viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy), int(image_height),
@@ -337,11 +342,11 @@ def backward_impl(background, means3D, radii, colors, scales, rotations, scale_m
     wait_event: torch.cuda.Event the stream waits for before the kernel that writes the gradients
     (a sink shared with views on other streams).  sh_rest: split SH rows as rasterize_gaussians;
     the `sh` gradient is then that of the concatenation, [P, M, 3]."""
-    if _EXT is not None and not want_all and not sinks and wait_event is None and means3D.is_cuda:
+    if _EXT is not None and not want_all and means3D.is_cuda:
         return _EXT.backward(background, means3D, radii, colors, scales, rotations, float(scale_modifier),
                              cov3D_precomp, viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy), dL_dout_color,
                              sh, int(degree), campos, geomBuffer, int(R), binningBuffer, imageBuffer, bool(debug),
-                             sh_rest)
+                             sh_rest, sinks or {}, wait_event.cuda_event if wait_event is not None else 0)
     x = _Inputs(background, means3D, colors, None, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
                 campos, need_opacity=False, sh_rest=sh_rest)
     P, dev = x.P, x.device
