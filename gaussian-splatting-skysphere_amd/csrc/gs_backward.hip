@@ -71,8 +71,8 @@ __device__ __forceinline__ uint64_t bwd_slot(BwdSlot& q, float pfx, float pfy, c
                                          const float4 br, uint32_t e, float* s) {
   const float bl = br.x;
   const float dx = xr.x - pfx, dy = xr.y - pfy;
-  const float pw = falloff_log2(co, dx, dy);  // log2(e) * power
-  const float oG = co.w * exp2_m<EXACT>(pw);
+  const float pw = falloff_log2_m<EXACT>(co, dx, dy);  // log2(e) * power (fast: + log2 o)
+  const float oG = opac_gauss<EXACT>(co, pw);
   // same decision as the forward (k_render_fwd_q): alpha = min(0.99, o G) >= 1/255 <=> o G >= 1/255
   const bool c_walk = e < q.last, c_alpha = oG >= 1.0f / 255.0f, c_pw = !EXACT || pw <= 0.0f;
   const bool con = c_walk && c_pw && c_alpha;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(CameraArgs c, const uint2*
     uint32_t qmask = 0;
     if (mine) {
       s_xy[lane] = make_float4(pa.x, pa.y, pb.z, pb.w);
-      s_co[lane] = fall_coefs(pa.z, pa.w, pb.x, pb.y);
+      s_co[lane] = fall_coefs_m<EXACT>(pa.z, pa.w, pb.x, pb.y);
       const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
       s_br[lane] = make_float4(pd.x, pa.x - fminf(fmaxf(pa.x, x0), x0 + 15.0f),
                                pa.y - fminf(fmaxf(pa.y, y0), y0 + 15.0f), 0.0f);

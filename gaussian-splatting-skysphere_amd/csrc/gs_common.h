@@ -138,11 +138,31 @@ __device__ __forceinline__ float falloff_log2(float4 k, float dx, float dy) {
   const float t = __builtin_fmaf(k.z, dy, b);
   return __builtin_fmaf(dy, t, a2);
 }
-__device__ __forceinline__ f2 falloff_log2_pk(float4 k, float dx, f2 dy) {
-  const float a2 = (k.x * dx) * dx;
+// By numerics mode (gs_set_exact_exp).  EXACT: as above, alpha = min(0.99, o 2^t) with the oracle's
+// operation order.  Fast: the opacity enters the exponent -- the staged fourth coefficient is
+// log2(o) (v_log_f32; -inf for o = 0) and the first product becomes an FMA with it, so
+// alpha = min(0.99, 2^(t + log2 o)) costs no multiply per pixel (the forward's walk and the
+// backward's slots evaluate the same expression, so their per-entry decisions agree; the fast
+// mode's deviation from o 2^t stays below the oracle's near-threshold margins, relative < 1e-6 of
+// alpha where it can decide).
+template <bool EXACT>
+__device__ __forceinline__ float4 fall_coefs_m(float cxx, float cxy, float cyy, float opacity) {
+  return make_float4(cxx * K_HALF_LOG2E, cxy * K_LOG2E, cyy * K_HALF_LOG2E,
+                     EXACT ? opacity : __builtin_amdgcn_logf(opacity));
+}
+template <bool EXACT>
+__device__ __forceinline__ float falloff_log2_m(float4 k, float dx, float dy) {
+  if constexpr (EXACT) return falloff_log2(k, dx, dy);
+  const float a2 = __builtin_fmaf(k.x * dx, dx, k.w);
   const float b = k.y * dx;
-  const f2 t = pk_fma((f2)(k.z), dy, (f2)(b));
-  return pk_fma(dy, t, (f2)(a2));
+  const float t = __builtin_fmaf(k.z, dy, b);
+  return __builtin_fmaf(dy, t, a2);
+}
+// o G = o 2^t from the exponent falloff_log2_m returned (fast: the opacity is already in it)
+template <bool EXACT>
+__device__ __forceinline__ float opac_gauss(float4 k, float t) {
+  if constexpr (EXACT) return k.w * exp2_m<true>(t);
+  else return exp2_m<false>(t);
 }
 
 // m = 4x4 world_view_transform / full_proj_transform, row-major flattening of the torch tensor

@@ -159,6 +159,11 @@ constexpr int CNT_I = 1, CNT_ERR = 2, CNT_NREND = 4, CNT_V = 5, CNT_LB_TILE = 9;
 // advanced by every forward's counter finalize: the look-back scans' epochs (k_scan_lb) differ
 // between HIP-graph replays
 constexpr int CNT_SEQ = 13;
+// the depth sort's fused row scans (RowScan): arrivals and scanners past their wait, zeroed by the
+// counter finalize of every forward
+constexpr int CNT_ARRIVE = 6;
+// the same pair for the tile sort, in the binning buffer's count words (zeroed by the duplicate)
+constexpr int BIN_ARRIVE = 4;
 // error flags in counters[CNT_ERR]: 1 prefiltered cull, 4 look-back timeout, 8 instance count overflow,
 // 16 more instances than the binning buffer's capacity (gs_forward_bounded)
 constexpr uint32_t ERR_PREFILTERED = 1u, ERR_LOOKBACK = 4u, ERR_INSTANCES = 8u, ERR_CAPACITY = 16u;
