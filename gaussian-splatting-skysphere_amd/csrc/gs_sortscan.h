@@ -637,6 +637,12 @@ static inline void launch_scatter(int bits, uint32_t nb, hipStream_t st, const u
 #define GS_SCATTER(B)                                                                                       \
   GS_LAUNCH("radix_scatter", (k_radix_scatter<AUX, B>), dim3(nb, views), dim3(SORT_THREADS), 0, st, kin, vin, \
             kout, vout, nd, n_max, shift, chunk, nb, hist, row_total, drop, ain, aout, vstride)
+  if constexpr (AUX) {
+    // a second value stream travels only with the 32-bit depth keys (four 8-bit passes): no other
+    // width is instantiated
+    GS_SCATTER(8);
+    return;
+  }
   switch (bits) {
     case 8: GS_SCATTER(8); break;
     case 7: GS_SCATTER(7); break;
@@ -651,7 +657,7 @@ static inline void launch_scatter(int bits, uint32_t nb, hipStream_t st, const u
 }
 
 // aux0 / aux_a / aux_b (optional): a second value stream in input order (aux0) that travels with
-// the keys; pass p writes aux_a (p even) or aux_b (p odd), so the result is in aux_b after an even
+// the keys (32-bit keys only: every pass then has 8-bit digits, the only aux scatter built); pass p writes aux_a (p even) or aux_b (p odd), so the result is in aux_b after an even
 // number of passes and in aux_a after an odd one.
 // hist0_ready: the caller already wrote the first pass's [digit][block] counts into scratch.
 // drop_first: the first pass reads n_max keys (host count) and drops those equal to DEPTH_DROP;

@@ -11,11 +11,11 @@
 // resolves the entry points from that one copy (its per-device state -- bounded status, ordering
 // flags, numerics mode -- stays shared with the ctypes path).  Same exception texts as _C.py.
 // Every call of the training paths goes through here: the eager forward, the bounded forward
-// (binning capacity), prepared views, the backward with gradient sinks / a wait event, and the split
-// backward halves; the ctypes bridge keeps only the debug exports, the want_all backward of the
-// upstream-named entry and the CPU-less error paths.  The forward reads its instance count back after queueing every launch
-// (gs_forward_counted, binning buffer sized from the last count), so neither the device nor the host
-// idles across the host round trip that upstream's resize callbacks need between the two halves.
+// (binning capacity), prepared views, the backward with gradient sinks / a wait event, and the
+// split backward halves; the ctypes bridge keeps the debug exports and the want_all backward of the
+// upstream-named entry.  The forward reads its instance count back after queueing every launch
+// (gs_forward_counted, binning buffer sized from the last count), so neither the device nor the
+// host idles across the host round trip that upstream's resize callbacks need between the halves.
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>

@@ -239,7 +239,7 @@ def test_bounded_overflow_in_a_captured_step_raises_in_the_loop(device):
         bounded_status()
 
 
-@pytest.mark.parametrize("active_degree", [3, 1])
+@pytest.mark.parametrize("active_degree", [3, 2, 1, 0])
 def test_fused_adam_train_step_bitwise_equal_unfused(device, active_degree, monkeypatch):
     """train_step(fuse_adam=True): the per-Gaussian backward fused with the Adam step
     (gs_backward_gaussians_adam) against the default step (backward, then FusedAdam.step_activated)

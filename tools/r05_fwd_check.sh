@@ -1,6 +1,11 @@
+# round 5: full GPU suite (kernel coverage last), batch-1 A/B of the base build against the
+# current one, train-step kernel profile, default bench line
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_train_step.py -x -q --timeout 150 --timeout-method thread > gpurun_out/r05_parity_fwdq.txt 2>&1 || { tail -30 gpurun_out/r05_parity_fwdq.txt; exit 1; }
-tail -2 gpurun_out/r05_parity_fwdq.txt
-SV_ARGS="" bash tools/sv_ab.sh build_base build
-timeout -k 10 300 python -u tools/train_step_kernels.py > gpurun_out/r05_tsk.json 2>&1
+timeout -k 10 480 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/r05_gpu_tests.txt 2>&1
+rc=$?
+tail -3 gpurun_out/r05_gpu_tests.txt
+[ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r05_gpu_tests.txt | head -20; exit 1; }
+SV_ARGS="" bash tools/sv_ab.sh build_base build || exit 1
+timeout -k 10 200 python -u tools/train_step_kernels.py > gpurun_out/r05_tsk.json 2>&1 || exit 1
+timeout -k 10 400 python -u bench.py > gpurun_out/r05_bench.json 2> gpurun_out/r05_bench.err
