@@ -202,7 +202,7 @@ def _np_adam(items, b1, b2, eps, maximize):
         pn += f(-lr / (1 - b1 ** t)) * (mn / denom)
 
 
-def _sharded_worker(rank, world, port, P, chunks, out_q):
+def _sharded_worker(rank, world, port, P, chunks, out_q, average=False):
     """Two replicas per rank from the same init: one steps through GradBucket.allreduce + Adam on all
     rows, the other through ShardedAdam (reduce-scatter, Adam on the rank's rows, all-gather); three
     steps, a densify-like resize (prune + append rows of params and moments, new P with a tail), two
@@ -233,7 +233,7 @@ def _sharded_worker(rank, world, port, P, chunks, out_q):
 
         def step_a(step):
             grads(step, pa, ba)
-            ba.allreduce()
+            ba.allreduce(average=average)
             items = []
             for p, grp in zip(pa, oa.param_groups):
                 st = oa.state[p]
@@ -245,7 +245,7 @@ def _sharded_worker(rank, world, port, P, chunks, out_q):
 
         def step_b(step):
             grads(step, pb, bb)
-            sh.step()
+            sh.step(average=average)
 
         for s_ in range(3):
             step_a(s_)
@@ -282,8 +282,8 @@ def _sharded_worker(rank, world, port, P, chunks, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("P,chunks", [(37, 3), (64, 4), (1, 2)])
-def test_sharded_adam_equals_allreduce_gloo_world2(P, chunks):
+@pytest.mark.parametrize("P,chunks,average", [(37, 3, False), (64, 4, False), (1, 2, False), (50, 2, True)])
+def test_sharded_adam_equals_allreduce_gloo_world2(P, chunks, average):
     """ShardedAdam (reduce-scatter -> Adam on the rank's row slices -> all-gather, in row chunks, with
     the odd tail all-reduced) against GradBucket.allreduce + Adam on every row, world 2 (gloo, CPU):
     parameters and both moments bit-identical on both ranks after 3 steps, a resize of every
@@ -294,7 +294,7 @@ def test_sharded_adam_equals_allreduce_gloo_world2(P, chunks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, P, chunks, q)) for r in range(2)]
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, P, chunks, q, average)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
