@@ -441,12 +441,12 @@ class ShardedAdam:
                 items = []
                 if S > 0:
                     shard = self._buf(c, rows, S, dev)
-                    cm = self._collective_ctx(dev) if on_dev else None
-                    with (cm if cm is not None else _nullctx()):
+                    ctx = self._collective_ctx(dev) if on_dev else None
+                    with (ctx if ctx is not None else _nullctx()) as cm:
                         for k, g in enumerate(rows):
                             dist.reduce_scatter_tensor(shard[k].view(-1), g[lo:hi].reshape(-1), group=self.group)
                     if cm is not None:
-                        cm.wait()
+                        cm.wait()  # (the side stream waits for the coalesced group)
                     a, z = lo + r * S, lo + (r + 1) * S
                     for k in range(len(params)):
                         if average:
@@ -462,8 +462,8 @@ class ShardedAdam:
                 if items:
                     self._run_update(items, hyper, dev)
                 if S > 0:
-                    cm = self._collective_ctx(dev) if on_dev else None
-                    with (cm if cm is not None else _nullctx()):
+                    ctx = self._collective_ctx(dev) if on_dev else None
+                    with (ctx if ctx is not None else _nullctx()) as cm:
                         for k in range(len(params)):
                             dist.all_gather_into_tensor(data[k][lo:hi].reshape(-1), data[k][a:z].reshape(-1),
                                                         group=self.group)
