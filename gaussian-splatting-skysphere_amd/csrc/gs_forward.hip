@@ -435,7 +435,10 @@ void fwd_order(int P, const GeomPtrs& geo, hipStream_t st, uint32_t* host_counts
   // view's passes in one set of launches (blockIdx.y = view)
   // passes 2-4 scan their histogram rows in their counting launch (the counter finalize above zeroes
   // the words before they run)
-  const RowScanCtx rs{&geo.counters[CNT_ARRIVE], &geo.counters[CNT_ERR], vstride, scan_spin_limit()};
+  // (the fused row scans wait only for workgroups dispatched before them, which wait for nothing:
+  // they keep the full spin bound even when a test shortens the look-back scans' waits, since a row
+  // scan cut short would hand the scatter offsets that are not a permutation)
+  const RowScanCtx rs{&geo.counters[CNT_ARRIVE], &geo.counters[CNT_ERR], vstride, LB_SPIN_LIMIT};
   if (lb_tiles(n) <= LB_STATIC_MAX) {
     radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
                      geo.sort_scratch, st, /*drop_first=*/true, /*hist0_ready=*/true, nullptr, nullptr, nullptr,
@@ -732,7 +735,7 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, bin.count, I, tbits, bin.sort_scratch, st,
                    false, hist0, nullptr, nullptr, nullptr, bin.slot_tile,
                    GS_TILE_SORT_BLOCKS, views, bs,
-                   RowScanCtx{bin.count + BIN_ARRIVE, &geo.counters[CNT_ERR], gs, scan_spin_limit()});
+                   RowScanCtx{bin.count + BIN_ARRIVE, &geo.counters[CNT_ERR], gs, LB_SPIN_LIMIT});
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024, views), dim3(256), 0, st, I, bin.count, bin.sorted_tile,
             img.ranges, (uint32_t*)img.tile_done, sched_n, (uint32_t)tiles, bs, is);
 }
