@@ -83,7 +83,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(Src src, const uin
 }
 
 // single workgroup (1024 lanes): exclusive scan of partial[0..nb) in place; total -> *total_out
-static __global__ __launch_bounds__(1024) void k_scan_partials(uint32_t* partial, uint32_t nb, uint32_t* total_out) {
+// (a template, like every kernel of this header: vague linkage, so the TUs that include it share one
+// exported kernel handle -- the launch log resolves it by name)
+template <int = 0>
+__global__ __launch_bounds__(1024) void k_scan_partials(uint32_t* partial, uint32_t nb, uint32_t* total_out) {
   __shared__ uint32_t sh[16];
   const uint32_t lane = __lane_id(), wid = threadIdx.x >> 6;
   uint32_t carry = 0;
@@ -141,7 +144,7 @@ inline void scan_exclusive(Src src, Dst dst, const uint32_t* n_dev, uint32_t n_m
   ScanPlan p = scan_plan(n_max);
   GS_LAUNCH("scan_reduce", (k_scan_reduce<Src>), dim3(p.nb), dim3(SCAN_THREADS), 0, st, src, n_dev, n_max,
             p.chunk, partial);
-  GS_LAUNCH("scan_partials", k_scan_partials, dim3(1), dim3(1024), 0, st, partial, p.nb, total_out);
+  GS_LAUNCH("scan_partials", k_scan_partials<>, dim3(1), dim3(1024), 0, st, partial, p.nb, total_out);
   GS_LAUNCH("scan_down", (k_scan_down<Src, Dst>), dim3(p.nb), dim3(SCAN_THREADS), 0, st, src, dst, n_dev, n_max,
             p.chunk, partial);
 }
@@ -514,7 +517,8 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __r
 
 // Row scan of the [digit][block] histogram: workgroup d turns row d into exclusive per-block
 // offsets (within digit d) and writes the row total; the scatter adds the digit base itself.
-static __global__ __launch_bounds__(SORT_THREADS) void k_radix_rowscan(uint32_t* __restrict__ hist, uint32_t nb,
+template <int = 0>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_rowscan(uint32_t* __restrict__ hist, uint32_t nb,
                                                                         uint32_t* __restrict__ row_total,
                                                                         uint64_t vstride) {
   __shared__ uint32_t sh[4];
@@ -697,7 +701,7 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
       if (!(hist0_ready && shift == 0))
         GS_LAUNCH("radix_hist", (k_radix_hist<NoFin, NoRowScan>), dim3(p.nb, views), dim3(SORT_THREADS), 0, st, kin_p,
                   nd, n_max, shift, bits, p.chunk, p.nb, hist, drop, vstride, NoFin(), NoRowScan());
-      GS_LAUNCH("radix_rowscan", k_radix_rowscan, dim3(RADIX, views), dim3(SORT_THREADS), 0, st, hist, p.nb,
+      GS_LAUNCH("radix_rowscan", k_radix_rowscan<>, dim3(RADIX, views), dim3(SORT_THREADS), 0, st, hist, p.nb,
                 row_total, vstride);
     }
     const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
