@@ -250,9 +250,8 @@ long long gs_binning_layout_count(size_t bytes, int W, int H) {
   return lo;
 }
 size_t gs_grad_buffer_bytes(long long num_rendered) {
-  // the records of every instance, and a second set for the split tiles' bottom halves
   const size_t R = (size_t)(num_rendered > 0 ? num_rendered : 1);
-  return 2 * grad_rec_floats(R) * sizeof(float);
+  return align_up(R * GRAD_REC * sizeof(float));
 }
 
 // Pinned, device-mapped host words: kernels store into them directly (vector stores through the
@@ -991,7 +990,7 @@ static int backward_impl(int P, int D, int M, const float* background, int W, in
   GaussianArgs g{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, scale_modifier,
                  shs_rest};
   float* gradrec = (float*)grad_buffer;
-  if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, (uint32_t)num_rendered, st);
+  if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, st);
   // dL_dcov3D is filled whenever the caller passes it: upstream writes it for scale/rotation
   // inputs too (the covariance gradient the scale / rotation chain starts from)
   GradOut out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
@@ -1085,7 +1084,7 @@ int gs_backward_render(int P, int D, int M, const float* background, int W, int 
   img_layout(W, H, &img, (char*)image_buffer);
   GaussianArgs g{P, D, M, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1.0f};
   float* gradrec = (float*)grad_buffer;
-  if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, (uint32_t)num_rendered, st);
+  if (num_rendered > 0) bwd_render(P, c, geo, bin, img, dL_dout_color, gradrec, st);
   bwd_records(g, geo, bin, img, gradrec, (uint32_t)num_rendered, num_rendered > 0, dL_dmeans2D, accumulate, st);
   if (!t_failed && check_order_flags(false)) return 1;
   return t_failed ? 1 : 0;

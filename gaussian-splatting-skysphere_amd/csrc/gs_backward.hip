@@ -122,8 +122,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(CameraArgs c, const uint2*
                                                                     const uint32_t* __restrict__ tile_max,
                                                                     const uint32_t* __restrict__ tile_order,
                                                                     const float* __restrict__ dL_dpix,
-                                                                    float* __restrict__ gradrec,
-                                                                    float* __restrict__ gradrec2) {
+                                                                    float* __restrict__ gradrec) {
   __shared__ float4 s_xy[64];  // (x, y, r, g)
   __shared__ float4 s_co[64];  // falloff coefficients + opacity (fall_coefs)
   __shared__ float4 s_br[64];  // (b, mean - r: x, y, -), r the moments' reference point (bwd_slot)
@@ -132,14 +131,8 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(CameraArgs c, const uint2*
   constexpr int ROW = 16;
   __shared__ __attribute__((aligned(16))) float s_acc[64][ROW];
   GS_BWD_T0();
-  const uint32_t unit = __builtin_amdgcn_readfirstlane(tile_order ? tile_order[blockIdx.x] : blockIdx.x);
-  if (unit == ~0u) return;  // a hole of the XCD-group launch order
-  // a split tile's wave takes the top (half 1: quadrants 0, 1) or the bottom (half 2: quadrants
-  // 2, 3) 8 pixel rows and writes its records into the first or the second record set; both walk
-  // the tile's whole list, so both sets hold a record (zeros where the half has no pixel) for every
-  // walked slot, which k_sum_records adds (top + bottom)
-  const uint32_t tile = unit & 0x3FFFFFFFu, half = unit >> 30;
-  float* const recs = half == 2 ? gradrec2 : gradrec;
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(tile_order ? tile_order[blockIdx.x] : blockIdx.x);
+  if (tile == ~0u) return;  // a hole of the XCD-group launch order
   const int tx = (int)(tile % (uint32_t)c.gx), ty = (int)(tile / (uint32_t)c.gx);
   const int lane = threadIdx.x;
   const uint2 range = ranges[tile];
@@ -202,7 +195,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(CameraArgs c, const uint2*
     if ((uint32_t)lane < rec_lanes) {
       const float4* row = reinterpret_cast<const float4*>(&s_acc[lane][0]);
       const float4 a = row[0], b = row[1], d = row[2];
-      Rec3* r = reinterpret_cast<Rec3*>(recs + (size_t)__float_as_uint(d.y) * GRAD_REC);
+      Rec3* r = reinterpret_cast<Rec3*>(gradrec + (size_t)__float_as_uint(d.y) * GRAD_REC);
       r[0] = Rec3{a.x, a.y, a.z};
       r[1] = Rec3{a.w, b.x, b.y};
       r[2] = Rec3{b.z, b.w, d.x};
@@ -241,7 +234,6 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(CameraArgs c, const uint2*
       uint64_t mk = __ballot((qmask >> k) & 1u);
       const int jmin = (int)n_eff - (int)qlast[k] - (int)base;  // entry j reaches quadrant k iff j >= jmin
       if (jmin > 0) mk &= jmin >= 64 ? 0ull : ~((1ull << jmin) - 1ull);
-      if (half != 0 && (uint32_t)(k >> 1) != half - 1u) mk = 0;  // (uniform) the other half's quadrants
       M[k] = mk;
     }
     __builtin_amdgcn_wave_barrier();
@@ -337,9 +329,6 @@ constexpr int ORDER_THREADS = 256;
 // (those its walk reaches, n_eff = its largest n_contrib); tile_cut = 1 + the slot of the last
 // of them.  A tile's list is in slot order, so k_sum_records keeps a record of slot s in tile T
 // iff s < tile_cut[T] and the backward writes no zero records for the rest.
-// The heaviest tiles are split: in each group, the longest whole buckets that fit the budget
-// split_per_group(tiles) (S_g tiles) run as two half waves each, at launch positions 2 j and 2 j + 1
-// (j < S_g); the group's other tiles follow at S_g + j.  Unused positions of bwd_units are holes.
 __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __restrict__ len_hist,
                                                               const uint32_t* __restrict__ tile_brank, uint32_t gx,
                                                               uint32_t gy, uint32_t* __restrict__ order,
@@ -347,10 +336,8 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __
                                                               const uint2* __restrict__ ranges,
                                                               const uint32_t* __restrict__ point_list,
                                                               uint32_t* __restrict__ tile_cut,
-                                                              uint32_t* __restrict__ cut_max,
-                                                              uint32_t* __restrict__ tile_split) {
+                                                              uint32_t* __restrict__ cut_max) {
   __shared__ uint32_t s_base[ORDER_GROUPS][ORDER_BUCKETS];
-  __shared__ uint32_t s_nsplit[ORDER_GROUPS];
   const uint32_t tid = threadIdx.x, t = blockIdx.x * ORDER_THREADS + tid, lane = tid & 63, wid = tid >> 6;
   const uint32_t tiles = gx * gy;
   uint32_t cut = 0;
@@ -367,61 +354,37 @@ __global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const uint32_t* __
     const uint32_t wm = wave_max_u32(cut);
     if (lane == 0 && wm) atomicMax(cut_max, wm);
   }
-  if (!order) {  // (uniform) no launch order: no split tile
-    if (t < tiles) tile_split[t] = 0u;
-    return;
-  }
+  if (!order) return;  // (uniform)
   const uint32_t br = t < tiles ? tile_brank[t] : 0u;
-  const uint32_t budget = split_per_group(tiles);
   static_assert(ORDER_BUCKETS == 64 && ORDER_GROUPS == 2 * (ORDER_THREADS / 64), "two groups per wave");
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     const uint32_t g = wid + h * (ORDER_THREADS / 64);
     const uint32_t v = len_hist[g * ORDER_BUCKETS + lane];
-    const uint32_t incl = wave_incl_scan(v);
-    s_base[g][lane] = incl - v;
-    // the tiles of the longest whole buckets within the budget (incl grows with the lane)
-    const uint32_t ns = wave_max_u32(incl <= budget ? incl : 0u);
-    if (lane == 0) s_nsplit[g] = ns;
+    s_base[g][lane] = wave_incl_scan(v) - v;
   }
   lds_barrier();
-  // the j-th tile of group g (longest first) takes launch position 8 j + g (8 (2 j + h) + g for the
-  // halves of a split one, 8 (S_g + j) + g after them)
+  // the j-th tile of group g (longest first) takes launch position 8 j + g
   if (t < tiles) {
     const uint32_t g = t % ORDER_GROUPS;
-    const uint32_t j = s_base[g][br >> 22] + (br & 0x3FFFFFu), ns = s_nsplit[g];
-    if (j < ns) {
-      order[ORDER_GROUPS * (2 * j) + g] = t | (1u << 30);
-      order[ORDER_GROUPS * (2 * j + 1) + g] = t | (2u << 30);
-    } else {
-      order[ORDER_GROUPS * (ns + j) + g] = t;
-    }
-    tile_split[t] = j < ns ? 1u : 0u;
-  }
-  // holes: group g's positions past its tiles and halves
-  const uint32_t units = bwd_units(tiles);
-  for (uint32_t p = blockIdx.x * ORDER_THREADS + tid; p < units; p += gridDim.x * ORDER_THREADS) {
-    const uint32_t g = p % ORDER_GROUPS, q = p / ORDER_GROUPS;
-    const uint32_t n_g = g < tiles ? (tiles - g + ORDER_GROUPS - 1) / ORDER_GROUPS : 0u;
-    if (q >= n_g + s_nsplit[g]) order[p] = ~0u;
+    order[ORDER_GROUPS * (s_base[g][br >> 22] + (br & 0x3FFFFFu)) + g] = t;
   }
 }
 
 void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
-                const float* dL_dpix, float* gradrec, uint32_t R, hipStream_t st) {
+                const float* dL_dpix, float* gradrec, hipStream_t st) {
   const int tiles = c.gx * c.gy;
   uint32_t* order = img.tile_order;
-  const uint32_t units = bwd_units((uint32_t)tiles);
-  GS_LAUNCH("tile_order", k_tile_order, dim3((tiles + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
+  const uint32_t slots = (uint32_t)tiles;
+  GS_LAUNCH("tile_order", k_tile_order, dim3((slots + ORDER_THREADS - 1) / ORDER_THREADS), dim3(ORDER_THREADS), 0, st,
             img.len_hist, img.tile_brank, (uint32_t)c.gx, (uint32_t)c.gy, order, img.tile_max, img.ranges,
-            bin.point_list, img.tile_cut, img.cut_max, img.tile_split);
-  float* const gradrec2 = grad_second(gradrec, R);
+            bin.point_list, img.tile_cut, img.cut_max);
   if (exact_exp())
-    GS_LAUNCH("render_bwd", k_render_bwd_tw<true>, dim3(units), dim3(64), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order, dL_dpix, gradrec, gradrec2);
+    GS_LAUNCH("render_bwd", k_render_bwd_tw<true>, dim3(slots), dim3(64), 0, st, c, img.ranges, bin.point_list,
+              bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order, dL_dpix, gradrec);
   else
-    GS_LAUNCH("render_bwd", k_render_bwd_tw<false>, dim3(units), dim3(64), 0, st, c, img.ranges, bin.point_list,
-              bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order, dL_dpix, gradrec, gradrec2);
+    GS_LAUNCH("render_bwd", k_render_bwd_tw<false>, dim3(slots), dim3(64), 0, st, c, img.ranges, bin.point_list,
+              bin.presort_gid, geo.splat, img.final_T, img.n_contrib, img.tile_max, order, dL_dpix, gradrec);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -452,9 +415,7 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
                                                                    const uint32_t* __restrict__ slot_tile,
                                                                    const uint32_t* __restrict__ tile_cut,
                                                                    const uint32_t* __restrict__ cut_max,
-                                                                   const uint32_t* __restrict__ tile_split,
                                                                    const float* __restrict__ gradrec,
-                                                                   const float* __restrict__ gradrec2,
                                                                    float* __restrict__ gsum, uint32_t P) {
   __shared__ double s_acc[SUMREC_WAVES][64][GRAD_REC];
   __shared__ unsigned long long s_mark[SUMREC_WAVES];
@@ -480,29 +441,28 @@ __global__ __launch_bounds__(64 * SUMREC_WAVES) void k_sum_records(const uint32_
   // records of the next chunk are loaded one chunk ahead (their HBM latency overlaps this chunk)
   float vn[GRAD_REC];
   unsigned long long hn;  // lanes of the next chunk that hold a record
-  // a slot's record (a split tile's: top half + bottom half, in that order)
-  auto load_slot = [&](uint32_t kk, float* v) -> bool {
+  {
+    const uint32_t kk = S0 + lane;
 #pragma unroll
-    for (int c = 0; c < GRAD_REC; c++) v[c] = 0.0f;
-    if (kk >= S1) return false;
-    const uint32_t tk = slot_tile[kk];
-    if (kk >= tile_cut[tk]) return false;
-    load_rec(gradrec + (size_t)kk * GRAD_REC, v);
-    if (tile_split[tk]) {
-      float w[GRAD_REC];
-      load_rec(gradrec2 + (size_t)kk * GRAD_REC, w);
-#pragma unroll
-      for (int c = 0; c < GRAD_REC; c++) v[c] = v[c] + w[c];
-    }
-    return true;
-  };
-  hn = __ballot(load_slot(S0 + lane, vn));
+    for (int c = 0; c < GRAD_REC; c++) vn[c] = 0.0f;
+    const bool h = kk < S1 && kk < tile_cut[slot_tile[kk]];
+    if (h) load_rec(gradrec + (size_t)kk * GRAD_REC, vn);
+    hn = __ballot(h);
+  }
   for (uint32_t base = S0; base < S1; base += 64) {
     float v[GRAD_REC];
 #pragma unroll
     for (int c = 0; c < GRAD_REC; c++) v[c] = vn[c];
     const unsigned long long hc = hn;
-    if (base + 64 < S1) hn = __ballot(load_slot(base + 64 + lane, vn));  // past a tile's cut: zeros (no load)
+    if (base + 64 < S1) {
+      // records past their tile's cut were never written: zeros (no load)
+      const uint32_t kn = base + 64 + lane;
+#pragma unroll
+      for (int c = 0; c < GRAD_REC; c++) vn[c] = 0.0f;
+      const bool h = kn < S1 && kn < tile_cut[slot_tile[kn]];
+      if (h) load_rec(gradrec + (size_t)kn * GRAD_REC, vn);
+      hn = __ballot(h);
+    }
     if (hc == 0) {
       // no record in the chunk (every slot behind its tile's walk, as for most of a dense
       // scene's instances): only count the owners that start in it
@@ -546,7 +506,7 @@ static void launch_sum_records(const GaussianArgs& g, const GeomPtrs& geo, const
                                float* gradrec, uint32_t R, hipStream_t st) {
   GS_LAUNCH("sum_records", k_sum_records, dim3((g.P + 64 * SUMREC_WAVES - 1) / (64 * SUMREC_WAVES)),
             dim3(64 * SUMREC_WAVES), 0, st, geo.counters, geo.offsets, geo.sorted_gid, bin.slot_tile, img.tile_cut,
-            img.cut_max, img.tile_split, gradrec, grad_second(gradrec, R), geo.gsum, (uint32_t)g.P);
+            img.cut_max, gradrec, geo.gsum, (uint32_t)g.P);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -399,8 +399,6 @@ struct CounterFinalize {
       counters[CNT_ERR] = err;
       counters[CNT_I] = 0u;
       counters[CNT_LB_TILE] = 0u;
-      counters[CNT_ARRIVE] = 0u;
-      counters[CNT_ARRIVE + 1] = 0u;
       counters[CNT_SEQ] = counters[CNT_SEQ] + 1u;
       if (host) {
         host[0] = (uint32_t)I;
@@ -433,23 +431,17 @@ void fwd_order(int P, const GeomPtrs& geo, hipStream_t st, uint32_t* host_counts
   // depth sort of the Gaussians with instances: the first pass reads all P keys in index order
   // and drops the DEPTH_DROP ones (compaction), the later passes sort the V survivors; every
   // view's passes in one set of launches (blockIdx.y = view)
-  // passes 2-4 scan their histogram rows in their counting launch (the counter finalize above zeroes
-  // the words before they run)
-  // (the fused row scans wait only for workgroups dispatched before them, which wait for nothing:
-  // they keep the full spin bound even when a test shortens the look-back scans' waits, since a row
-  // scan cut short would hand the scatter offsets that are not a permutation)
-  const RowScanCtx rs{&geo.counters[CNT_ARRIVE], &geo.counters[CNT_ERR], vstride, LB_SPIN_LIMIT};
   if (lb_tiles(n) <= LB_STATIC_MAX) {
     radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
                      geo.sort_scratch, st, /*drop_first=*/true, /*hist0_ready=*/true, nullptr, nullptr, nullptr,
-                     nullptr, GS_DEPTH_SORT_BLOCKS, views, vstride, rs);
+                     nullptr, GS_DEPTH_SORT_BLOCKS, views, vstride);
   } else {
     // larger scenes: the tile counts travel with the keys through the sort (read in index order by
     // the first pass), and the 3-launch scan reads them in depth order, coalesced (C5, 5M: the
     // per-rank gather and the ticketed look-back took 197 us)
     radix_sort_pairs(geo.keys_a, geo.vals_a, geo.keys_b, geo.vals_b, true, &geo.counters[CNT_V], n, 32,
                      geo.sort_scratch, st, /*drop_first=*/true, /*hist0_ready=*/true, geo.tiles, geo.rtiles_a,
-                     geo.rtiles_b, nullptr, GS_DEPTH_SORT_BLOCKS, views, vstride, rs);
+                     geo.rtiles_b, nullptr, GS_DEPTH_SORT_BLOCKS, views, vstride);
   }
   for (int v = 0; v < views; v++) {
     GeomPtrs g = geo;
@@ -555,11 +547,7 @@ __global__ __launch_bounds__(DUP_THREADS) void k_duplicate_lb(
   const uint32_t V = counters[CNT_V];
   // I: the binning buffer's capacity (= the count, unless the buffer was sized ahead of it)
   I = min(I, counters[CNT_NREND]);
-  if (b == 0 && tid == 0) {
-    n_copy[0] = I;  // for the tile sort and k_ranges (kernels after this one)
-    n_copy[BIN_ARRIVE] = 0u;  // the tile sort's fused row scans start from zero
-    n_copy[BIN_ARRIVE + 1] = 0u;
-  }
+  if (b == 0 && tid == 0) n_copy[0] = I;  // for the tile sort and k_ranges (kernels after this one)
   const uint32_t k0 = b * DUP_SLOTS;
   const uint32_t k1 = k0 < I ? min(k0 + DUP_SLOTS, I) : k0;
   if (counters[CNT_ERR] & ERR_INVALID) {
@@ -731,11 +719,9 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
             bin.presort_gid, img.ranges, hist0 ? bin.sort_scratch : nullptr, (1u << radix_first_bits(tbits)) - 1u,
             bin.count, gs, bs, is);
   // the device count bounds the sort (I is the buffers' capacity, which may exceed it)
-  // the second pass scans its histogram rows in its counting launch (the duplicate zeroes the words)
   radix_sort_pairs(bin.keys_a, bin.vals_a, bin.keys_b, bin.vals_b, true, bin.count, I, tbits, bin.sort_scratch, st,
                    false, hist0, nullptr, nullptr, nullptr, bin.slot_tile,
-                   GS_TILE_SORT_BLOCKS, views, bs,
-                   RowScanCtx{bin.count + BIN_ARRIVE, &geo.counters[CNT_ERR], gs, LB_SPIN_LIMIT});
+                   GS_TILE_SORT_BLOCKS, views, bs);
   GS_LAUNCH("ranges", k_ranges, dim3((I + 1023) / 1024, views), dim3(256), 0, st, I, bin.count, bin.sorted_tile,
             img.ranges, (uint32_t*)img.tile_done, sched_n, (uint32_t)tiles, bs, is);
 }
@@ -743,15 +729,15 @@ void fwd_bin_views(int views, int P, uint32_t I, const CameraArgs& c, const Geom
 // ------------------------------------------------------------------------------------------
 // render forward
 // ------------------------------------------------------------------------------------------
-// A quadrant wave stages the batch entries that meet its quadrant, compacted in list order (entry
-// k of the wave's list at record k), as three 16-B LDS records at byte offsets 16 k, 16 (NB + k),
-// 16 (2 NB + k):
+// Entries are staged as three 16-B LDS records at one byte offset o (o, o + 16 NB, o + 32 NB for
+// a batch of NB entries):
 //   (x, y, r, g) | falloff coefficients + opacity | (b, bits(entry index + 1), -, -)
-// so the walk reads entry k at fixed offsets from one address per trip: no list indirection, no
-// dependent LDS round trip per trip (was: a list of record offsets read 16 B at a time ahead of the
-// records, 77 -> 73 VALU per 4 entries and one LDS wait less per trip).
+// and each quadrant wave's dense list holds the offsets (u32), read FWD_ILP = 4 at a time with one
+// 16-B LDS read: a list entry costs no address arithmetic, no unpacking and no dependent list read.
 // (8 entries per trip: 60 -> 74 VGPRs, 8 -> 6 waves per SIMD, render_fwd 174 -> 189 us)
-constexpr int FWD_ILP = 4;  // entries per trip
+constexpr int FWD_ILP = 4;  // a multiple of 4 (whole 16-B list reads)
+static_assert(FWD_ILP % 4 == 0, "list groups are read 16 B at a time");
+
 struct FwdPix {
   float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
   uint32_t last = 0;
@@ -762,23 +748,34 @@ struct FwdPix {
 // with 2 FWD_ILP offsets of a staged dummy entry of opacity 0 (alpha 0 at every pixel), so the walk
 // needs no per-entry end-of-list test (175.8 -> 172.6 us at C3).
 template <bool EXACT, int NB>
-__device__ __forceinline__ void fwd_walk(const float4* ent, uint32_t qcnt, float pfx, float pfy, FwdPix& px) {
+__device__ __forceinline__ void fwd_walk(const char* ent, const uint32_t* qlist, uint32_t qcnt, float pfx, float pfy,
+                                         FwdPix& px) {
   // FWD_ILP entries per trip: their power / exp / alpha chains are independent (ILP); the
-  // compositing is then applied entry by entry in list order, exactly as one at a time.
+  // compositing is then applied entry by entry in list order, exactly as one at a time.  The
+  // next group's offsets are read one trip ahead (one dependent LDS round trip per trip).
+  constexpr int NQ = FWD_ILP / 4;
+  uint4 wn[NQ];
+#pragma unroll
+  for (int r = 0; r < NQ; r++) wn[r] = *reinterpret_cast<const uint4*>(&qlist[4 * r]);
   for (uint32_t k = 0; k < qcnt; k += FWD_ILP) {
-    const float4* e = ent + k;
+    uint32_t o[FWD_ILP];
+#pragma unroll
+    for (int r = 0; r < NQ; r++) {
+      o[4 * r] = wn[r].x, o[4 * r + 1] = wn[r].y, o[4 * r + 2] = wn[r].z, o[4 * r + 3] = wn[r].w;
+      wn[r] = *reinterpret_cast<const uint4*>(&qlist[k + FWD_ILP + 4 * r]);
+    }
     float pw[FWD_ILP], al[FWD_ILP];
 #pragma unroll
     for (int u = 0; u < FWD_ILP; u++) {
-      const float4 xr = e[u];
-      const float4 co = e[NB + u];
+      const float4 xr = *reinterpret_cast<const float4*>(ent + o[u]);
+      const float4 co = *reinterpret_cast<const float4*>(ent + o[u] + 16 * NB);
       pw[u] = falloff_log2_m<EXACT>(co, xr.x - pfx, xr.y - pfy);  // log2(e) * power (fast: + log2 o)
       al[u] = fminf(0.99f, opac_gauss<EXACT>(co, pw[u]));
     }
 #pragma unroll
     for (int u = 0; u < FWD_ILP; u++) {
-      const float4 xr = e[u];
-      const float2 bl = *reinterpret_cast<const float2*>(&e[2 * NB + u]);
+      const float4 xr = *reinterpret_cast<const float4*>(ent + o[u]);
+      const float2 bl = *reinterpret_cast<const float2*>(ent + o[u] + 32 * NB);
       const float rr = xr.z, rg = xr.w, rb = bl.x;
       // branch-free compositing (selects instead of divergent ifs); the per-entry decisions are
       // lane masks combined on the scalar unit (ballot / inverse ballot), so the VALU does the
@@ -867,16 +864,20 @@ __device__ __forceinline__ void fwd_store(const CameraArgs& c, const QuadPix& q,
 // (Tried and not kept: the next batch's ids / records prefetched one batch ahead, 168 -> 179 us --
 // the loads past the stop are wasted; 32-entry batches, 174 -> 195 us.)
 constexpr int FWDQ_NB = 64;  // entries staged per round (one per lane)
-// record stride of the staged batch: the batch plus the padding's FWD_ILP dummy entries
-constexpr int FWDQ_NBS = FWDQ_NB + FWD_ILP;
+// record stride of the staged batch: one more than the batch for the padding's dummy entry
+constexpr int FWDQ_NBS = FWDQ_NB + 1;
 template <bool EXACT>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_render_fwd_q(CameraArgs c, const uint2* __restrict__ ranges,
+__global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* __restrict__ ranges,
                                                      const uint32_t* __restrict__ point_list,
                                                      const uint32_t* __restrict__ point_gid,
                                                      const float4* __restrict__ splat, float* __restrict__ out,
                                                      ImgPtrs img, const uint32_t* __restrict__ err,
                                                      uint32_t* __restrict__ err_host) {
   __shared__ float4 s_ent[3 * FWDQ_NBS];
+  __shared__ __attribute__((aligned(16))) uint32_t s_qlist[FWDQ_NB + 2 * FWD_ILP];
+  if (threadIdx.x < 3)  // the dummy entry: position 0, opacity 0 (never contributes; fast: log2 0 = -inf)
+    s_ent[threadIdx.x * FWDQ_NBS + FWDQ_NB] =
+        make_float4(0.0f, 0.0f, 0.0f, (EXACT || threadIdx.x != 1) ? 0.0f : -__builtin_inff());
   const uint32_t b = blockIdx.x;
   const uint32_t tile = xcd_tile(b & 7, b >> 5, c.gx, c.gy);
   if (tile == ~0u) return;  // (grid padded to whole groups of 8 tiles)
@@ -894,42 +895,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_
   const uint2 range = ranges[tile];
   // a sort / scan look-back that timed out (reported by the host) leaves no valid list: render none
   const uint32_t n = (*err & ERR_INVALID) ? 0u : range.y - range.x;
+  const char* ent = reinterpret_cast<const char*>(s_ent);
   const float qx = (float)(tx * GS_TILE + 8 * (wid & 1)), qy = (float)(ty * GS_TILE + 8 * (wid >> 1));
   FwdPix px;
   px.done = __builtin_amdgcn_ballot_w64(!inside);
   for (uint32_t base = 0; base < n; base += FWDQ_NB) {
     if (px.done == ~0ull) break;
     bool meets = false;
-    float4 a, bb, d;
     if (lane < (uint32_t)FWDQ_NB && base + lane < n) {
       const uint32_t gid = point_gid[point_list[range.x + base + lane]];
-      a = splat[3 * gid], bb = splat[3 * gid + 1], d = splat[3 * gid + 2];
+      const float4 a = splat[3 * gid], bb = splat[3 * gid + 1], d = splat[3 * gid + 2];
+      s_ent[lane] = make_float4(a.x, a.y, bb.z, bb.w);
+      s_ent[FWDQ_NBS + lane] = fall_coefs_m<EXACT>(a.z, a.w, bb.x, bb.y);
+      s_ent[2 * FWDQ_NBS + lane] = make_float4(d.x, __uint_as_float(base + lane + 1), 0.0f, 0.0f);
       meets = d.z >= 0.0f && ellipse_meets_rect(a.x, a.y, a.z, a.w, bb.x, d.z, qx, qx + 7.0f, qy, qy + 7.0f);
     }
-    // the entries meeting the quadrant, compacted in list order; then FWD_ILP dummy entries
-    // (position 0, opacity 0 -- fast: log2 0 = -inf -- never contributing), so the walk's last trip
-    // needs no per-entry end-of-list test (175.8 -> 172.6 us at C3)
     const uint64_t m = __ballot(meets);
+    if (meets)
+      s_qlist[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+          16u * lane;
     const uint32_t qcnt = (uint32_t)__popcll(m);
-    if (meets) {
-      const uint32_t at =
-          __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      s_ent[at] = make_float4(a.x, a.y, bb.z, bb.w);
-      s_ent[FWDQ_NBS + at] = fall_coefs_m<EXACT>(a.z, a.w, bb.x, bb.y);
-      s_ent[2 * FWDQ_NBS + at] = make_float4(d.x, __uint_as_float(base + lane + 1), 0.0f, 0.0f);
-    }
-    if (lane < FWD_ILP) {
-      const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      s_ent[qcnt + lane] = z;
-      s_ent[FWDQ_NBS + qcnt + lane] = make_float4(0.0f, 0.0f, 0.0f, EXACT ? 0.0f : -__builtin_inff());
-      s_ent[2 * FWDQ_NBS + qcnt + lane] = z;
-    }
+    if (lane < 2 * FWD_ILP) s_qlist[qcnt + lane] = 16u * FWDQ_NB;
     __builtin_amdgcn_wave_barrier();
 #ifdef GS_TIMING
     t_batches++;
     t_walked += qcnt;
 #endif
-    fwd_walk<EXACT, FWDQ_NBS>(s_ent, qcnt, (float)q.px, (float)q.py, px);
+    fwd_walk<EXACT, FWDQ_NBS>(ent, s_qlist, qcnt, (float)q.px, (float)q.py, px);
     __builtin_amdgcn_wave_barrier();  // the next round overwrites the staged entries
   }
   fwd_store(c, q, inside, px, out, img.final_T, img.n_contrib);

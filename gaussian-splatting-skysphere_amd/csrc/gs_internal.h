@@ -159,11 +159,6 @@ constexpr int CNT_I = 1, CNT_ERR = 2, CNT_NREND = 4, CNT_V = 5, CNT_LB_TILE = 9;
 // advanced by every forward's counter finalize: the look-back scans' epochs (k_scan_lb) differ
 // between HIP-graph replays
 constexpr int CNT_SEQ = 13;
-// the depth sort's fused row scans (RowScan): arrivals and scanners past their wait, zeroed by the
-// counter finalize of every forward
-constexpr int CNT_ARRIVE = 6;
-// the same pair for the tile sort, in the binning buffer's count words (zeroed by the duplicate)
-constexpr int BIN_ARRIVE = 4;
 // error flags in counters[CNT_ERR]: 1 prefiltered cull, 4 look-back timeout, 8 instance count overflow,
 // 16 more instances than the binning buffer's capacity (gs_forward_bounded)
 constexpr uint32_t ERR_PREFILTERED = 1u, ERR_LOOKBACK = 4u, ERR_INSTANCES = 8u, ERR_CAPACITY = 16u;
@@ -311,8 +306,7 @@ struct ImgPtrs {
   float* final_T;
   uint32_t* n_contrib;
   uint32_t* tile_max;
-  uint32_t* tile_order;  // backward launch order (k_tile_order): tile | half << 30 per wave (bwd_units)
-  uint32_t* tile_split;  // per tile: 1 if the backward splits it into two half waves (k_tile_order)
+  uint32_t* tile_order;  // backward launch order (k_tile_order)
   uint32_t* tile_cut;    // per tile: 1 + the slot of its last walked instance (0: none), k_tile_order
   uint64_t* tile_done;   // per tile: finished quadrant waves + their length bits (zeroed by k_ranges),
   uint32_t* len_hist;    //   then ORDER_GROUPS x ORDER_BUCKETS walk-length bucket counts
@@ -339,14 +333,6 @@ constexpr int ORDER_GROUPS = 8;
 inline uint32_t sched_words(uint32_t tiles) { return 2u * tiles + ORDER_GROUPS * ORDER_BUCKETS + 1u; }
 // tiles per group (the last groups may hold one fewer)
 __host__ __device__ inline uint32_t xcd_span(uint32_t tiles) { return (tiles + ORDER_GROUPS - 1) / ORDER_GROUPS; }
-// The backward splits the heaviest tiles of each XCD group into two waves (top and bottom 8-pixel
-// halves): at most this many per group, taken as whole walk-length buckets from the longest down, so
-// whether a tile splits depends only on the bucket counts (deterministic, k_tile_order)
-__host__ __device__ inline uint32_t split_per_group(uint32_t tiles) { return xcd_span(tiles) / 16; }
-// backward launch positions (waves): every tile once, plus the split budget's second halves
-__host__ __device__ inline uint32_t bwd_units(uint32_t tiles) {
-  return ORDER_GROUPS * (xcd_span(tiles) + split_per_group(tiles));
-}
 // the k-th tile of group g (~0u past its end)
 __host__ __device__ inline uint32_t xcd_tile(uint32_t g, uint32_t k, uint32_t gx, uint32_t gy) {
   const uint32_t t = ORDER_GROUPS * k + g;
@@ -365,8 +351,8 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
   if (tiles == 0) tiles = 1;
   if (npix == 0) npix = 1;
   size_t o_r = take(tiles * 8), o_t = take(npix * 4), o_n = take(npix * 4), o_m = take(tiles * 16),
-         o_o = take((size_t)bwd_units((uint32_t)tiles) * 4), o_c = take(tiles * 4),
-         o_d = take((size_t)sched_words((uint32_t)tiles) * 4), o_b = take(tiles * 4), o_s = take(tiles * 4);
+         o_o = take(tiles * 4), o_c = take(tiles * 4), o_d = take((size_t)sched_words((uint32_t)tiles) * 4),
+         o_b = take(tiles * 4);
   if (out && base) {
     out->ranges = (uint2*)(base + o_r);
     out->final_T = (float*)(base + o_t);
@@ -378,7 +364,6 @@ inline size_t img_layout(int W, int H, ImgPtrs* out, char* base) {
     out->len_hist = (uint32_t*)(out->tile_done + tiles);
     out->cut_max = out->len_hist + ORDER_GROUPS * ORDER_BUCKETS;
     out->tile_brank = (uint32_t*)(base + o_b);
-    out->tile_split = (uint32_t*)(base + o_s);
   }
   return off;
 }
@@ -450,11 +435,8 @@ void fwd_render(const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, co
                 hipStream_t st, uint32_t* err_host = nullptr);
 void mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
                   hipStream_t st);
-// gradient records: R of GRAD_REC floats, then (split tiles' bottom halves) R more at grad_second
-inline size_t grad_rec_floats(size_t R) { return align_up((R ? R : 1) * GRAD_REC * sizeof(float)) / sizeof(float); }
-inline float* grad_second(float* gradrec, uint32_t R) { return gradrec + grad_rec_floats(R); }
 void bwd_render(int P, const CameraArgs& c, const GeomPtrs& geo, const BinPtrs& bin, const ImgPtrs& img,
-                const float* dL_dpix, float* gradrec, uint32_t R, hipStream_t st);
+                const float* dL_dpix, float* gradrec, hipStream_t st);
 struct GradOut {
   float* dmean2D;   // [P, 3]
   float* dcolor;    // [P, 3] or null

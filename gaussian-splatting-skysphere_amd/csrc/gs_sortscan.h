@@ -414,71 +414,15 @@ __device__ __forceinline__ void radix_row_scan(uint32_t* row, uint32_t nb, uint3
   if (threadIdx.x == 0) *row_total = carry;
 }
 
-// The row scan fused into the histogram launch (RowScan::active): RADIX extra workgroups after the
-// nb counting ones (blockIdx.x = nb + d scans digit d's row).  A counting workgroup publishes its
-// column with one release add to `arrive`; a scanning workgroup waits (acquire loads, bounded) until
-// all nb have arrived, then scans its row.  The scanning workgroups come last in the grid, so every
-// counting workgroup has been dispatched before any of them waits: the waits cannot block the work
-// they wait for.  The last scanner to start resets both words for the next pass (they start at 0:
-// zeroed by the kernel that precedes the sort in the forward).  A wait that exceeds the spin limit
-// sets err bit 4 (ERR_LOOKBACK: the list is invalid, nothing hangs).  Saves the separate row-scan
-// launch of the pass.
-struct RowScan {
-  static constexpr bool active = true;
-  uint32_t* row_total;
-  uint32_t* arrive;  // [0] arrivals, [1] scanners past their wait (per view: vptr)
-  uint32_t* err;     // the view's error flags (view v's: err_vstride v bytes further)
-  uint64_t err_vstride;
-  uint32_t spin_limit;
-};
-struct NoRowScan {
-  static constexpr bool active = false;
-  uint32_t *row_total = nullptr, *arrive = nullptr, *err = nullptr;
-  uint64_t err_vstride = 0;
-  uint32_t spin_limit = 0;
-};
-// the RowScan words of a sort: its error flags and their view stride, and the spin limit
-struct RowScanCtx {
-  uint32_t* arrive = nullptr;  // null: separate row-scan launches
-  uint32_t* err = nullptr;
-  uint64_t err_vstride = 0;
-  uint32_t spin_limit = 0;
-};
-
-template <class Fin = NoFin, class Scan = NoRowScan>
+template <class Fin = NoFin>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __restrict__ keys, const uint32_t* n_dev,
                                                              uint32_t n_max, int shift, int bits, uint32_t chunk,
                                                              uint32_t nb, uint32_t* __restrict__ hist, bool drop,
-                                                             uint64_t vstride, Fin fin = Fin(), Scan scan = Scan()) {
+                                                             uint64_t vstride, Fin fin = Fin()) {
   __shared__ uint32_t h[RADIX];
   if constexpr (Fin::active) {
     if (blockIdx.x == nb) {  // (uniform) the extra workgroup runs beside the counting ones
       fin(blockIdx.y);
-      return;
-    }
-  }
-  if constexpr (Scan::active) {
-    if (blockIdx.x >= nb) {  // (uniform) a scanning workgroup: digit blockIdx.x - nb
-      uint32_t* arrive = vptr(scan.arrive, vstride);
-      if (threadIdx.x == 0) {
-        uint32_t spins = 0;
-        while (__hip_atomic_load(arrive, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < nb) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > scan.spin_limit) {
-            atomicOr((uint32_t*)((char*)scan.err + (uint64_t)blockIdx.y * scan.err_vstride), 4u);
-            break;
-          }
-        }
-        // the last scanner past its wait resets the words (no counting workgroup or scanner reads
-        // them after this)
-        if (__hip_atomic_fetch_add(arrive + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == RADIX - 1) {
-          __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(arrive + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      __syncthreads();
-      const uint32_t d = blockIdx.x - nb;
-      radix_row_scan(vptr(hist, vstride) + (size_t)d * nb, nb, vptr(scan.row_total, vstride) + d, h);
       return;
     }
   }
@@ -505,14 +449,6 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const uint32_t* __r
   }
   lds_barrier();
   hist[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
-  if constexpr (Scan::active) {
-    // every wave's column store complete (the barrier's workgroup-scope fence waits for none on
-    // gfx950), then published device-wide by one release add (its L2 write-back covers them)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(vptr(scan.arrive, vstride), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 // Row scan of the [digit][block] histogram: workgroup d turns row d into exclusive per-block
@@ -674,7 +610,7 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
                                     bool hist0_ready = false, const uint32_t* aux0 = nullptr,
                                     uint32_t* aux_a = nullptr, uint32_t* aux_b = nullptr,
                                     const uint32_t* keys_in0 = nullptr, uint32_t max_blocks = SORT_MAX_BLOCKS,
-                                    int views = 1, uint64_t vstride = 0, RowScanCtx rs = RowScanCtx()) {
+                                    int views = 1, uint64_t vstride = 0) {
   SortPlan p = sort_plan(n_max, max_blocks);
   uint32_t* hist = scratch;
   const size_t hist_n = (size_t)RADIX * p.nb;
@@ -691,19 +627,11 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
     const uint32_t* nd = drop ? nullptr : n_dev;
     // keys_in0: the first pass reads its keys from there (kept), not from keys_a
     const uint32_t* kin_p = (shift == 0 && keys_in0) ? keys_in0 : kin;
-    // arrive (a device word pair, zero at the sort's start): a pass that counts here scans its rows
-    // in the same launch (RowScan); a first pass counted elsewhere (hist0_ready) keeps the launch
-    if (!(hist0_ready && shift == 0) && rs.arrive) {
-      GS_LAUNCH("radix_hist", (k_radix_hist<NoFin, RowScan>), dim3(p.nb + RADIX, views), dim3(SORT_THREADS), 0, st,
-                kin_p, nd, n_max, shift, bits, p.chunk, p.nb, hist, drop, vstride, NoFin(),
-                RowScan{row_total, rs.arrive, rs.err, rs.err_vstride, rs.spin_limit});
-    } else {
-      if (!(hist0_ready && shift == 0))
-        GS_LAUNCH("radix_hist", (k_radix_hist<NoFin, NoRowScan>), dim3(p.nb, views), dim3(SORT_THREADS), 0, st, kin_p,
-                  nd, n_max, shift, bits, p.chunk, p.nb, hist, drop, vstride, NoFin(), NoRowScan());
-      GS_LAUNCH("radix_rowscan", k_radix_rowscan<>, dim3(RADIX, views), dim3(SORT_THREADS), 0, st, hist, p.nb,
-                row_total, vstride);
-    }
+    if (!(hist0_ready && shift == 0))
+      GS_LAUNCH("radix_hist", k_radix_hist<NoFin>, dim3(p.nb, views), dim3(SORT_THREADS), 0, st, kin_p, nd, n_max,
+                shift, bits, p.chunk, p.nb, hist, drop, vstride, NoFin());
+    GS_LAUNCH("radix_rowscan", k_radix_rowscan<>, dim3(RADIX, views), dim3(SORT_THREADS), 0, st, hist, p.nb,
+              row_total, vstride);
     const uint32_t* vsrc = (shift == 0 && vals_identity) ? nullptr : vin;
     if (aux0) {
       launch_scatter<true>(bits, p.nb, st, kin_p, vsrc, kout, vout, nd, n_max, shift, p.chunk, hist, row_total, drop, ain,
