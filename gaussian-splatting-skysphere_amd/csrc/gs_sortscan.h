@@ -581,17 +581,17 @@ static inline void launch_scatter(int bits, uint32_t nb, hipStream_t st, const u
     // a second value stream travels only with the 32-bit depth keys (four 8-bit passes): no other
     // width is instantiated
     GS_SCATTER(8);
-    return;
-  }
-  switch (bits) {
-    case 8: GS_SCATTER(8); break;
-    case 7: GS_SCATTER(7); break;
-    case 6: GS_SCATTER(6); break;
-    case 5: GS_SCATTER(5); break;
-    case 4: GS_SCATTER(4); break;
-    case 3: GS_SCATTER(3); break;
-    case 2: GS_SCATTER(2); break;
-    default: GS_SCATTER(1); break;
+  } else {
+    switch (bits) {
+      case 8: GS_SCATTER(8); break;
+      case 7: GS_SCATTER(7); break;
+      case 6: GS_SCATTER(6); break;
+      case 5: GS_SCATTER(5); break;
+      case 4: GS_SCATTER(4); break;
+      case 3: GS_SCATTER(3); break;
+      case 2: GS_SCATTER(2); break;
+      default: GS_SCATTER(1); break;
+    }
   }
 #undef GS_SCATTER
 }

@@ -490,3 +490,57 @@ def test_prepared_views_equal_single_view_calls(device):
     with pytest.raises(RuntimeError, match="used once"):
         rasts[0](means3D=sc.means3D, means2D=m2, opacities=sc.opacities, shs=sc.shs, scales=sc.scales,
                  rotations=sc.rotations, prepared=pre[0])
+
+
+@pytest.mark.parametrize("deg", [-1, 0, 1, 2], ids=["colors", "sh0", "sh1", "sh2"])
+def test_prepared_deferred_views_every_degree(device, deg):
+    """prepare_views (gs_forward_preprocess_views) and the deferred per-Gaussian half
+    (gs_backward_gaussians) for precomputed colours and SH degrees 0-2 (degree 3: the tests above):
+    three views' images, radii and gradient sums bit-identical to plain per-view calls whose
+    gradients autograd sums with += in view order."""
+    import gs_view_parallel as vp
+    from diff_gaussian_rasterization import GaussianRasterizer, prepare_views
+
+    W, H = 160, 120
+    cams = gs_scenes.circle_cameras(3, 6.0, W, H)
+    sc = gs_scenes.random_gaussians(5000, max(deg, 0), seed=31, ball_radius=2.0).to(device)
+    rasts = [GaussianRasterizer(gs_scenes.raster_settings_for(c, max(deg, 0), device=device)) for c in cams]
+    dpix = [gs_scenes.dl_dimage(H, W, seed=60 + v).to(device) for v in range(3)]
+    colors = torch.rand((sc.P, 3), generator=torch.Generator().manual_seed(3)).to(device)
+    feat = colors if deg < 0 else sc.shs
+
+    def leaves():
+        return [t.clone().requires_grad_(True) for t in (sc.means3D, feat, sc.opacities, sc.scales, sc.rotations)]
+
+    def call(r, p, m2, prepared=None):
+        kw = dict(colors_precomp=p[1]) if deg < 0 else dict(shs=p[1])
+        return r(means3D=p[0], means2D=m2, opacities=p[2], scales=p[3], rotations=p[4], prepared=prepared, **kw)
+
+    ref, outs_ref = None, []
+    for r, dp in zip(rasts, dpix):
+        p = leaves()
+        m2 = torch.zeros_like(p[0], requires_grad=True)
+        img, radii = call(r, p, m2)
+        img.backward(dp)
+        outs_ref.append((img.detach().clone(), radii.clone(), m2.grad.clone()))
+        g = [t.grad for t in p]
+        ref = [x.clone() for x in g] if ref is None else [a + b for a, b in zip(ref, g)]
+    p = leaves()
+    b = vp.GradBucket(p, lazy_zero=True, defer=True)
+    b.zero_grad()
+    kw = dict(colors_precomp=p[1]) if deg < 0 else dict(shs=p[1])
+    pre = prepare_views(rasts, p[0], p[2], scales=p[3], rotations=p[4], **kw)
+    outs = []
+    for r, pv, dp in zip(rasts, pre, dpix):
+        m2 = torch.zeros_like(p[0], requires_grad=True)
+        img, radii = call(r, p, m2, pv)
+        img.backward(dp)
+        outs.append((img.detach().clone(), radii.clone(), m2))
+    b.finalize()
+    torch.cuda.synchronize()
+    for (ia, ra, ma), (ib, rb, m2) in zip(outs_ref, outs):
+        assert torch.equal(ia, ib) and torch.equal(ra, rb) and torch.equal(ma, m2.grad)
+        assert (ra > 0).any()
+    for k, (t, x) in enumerate(zip(p, ref)):
+        assert torch.equal(t.grad, x), k
+    b.close()
