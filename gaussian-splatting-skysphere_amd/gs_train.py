@@ -85,8 +85,16 @@ class FusedAdam(torch.optim.Optimizer):
             state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
         step_t = state["step"]
         if torch.is_tensor(step_t):
-            step_t += 1
-            t = int(step_t.item())
+            if step_t.device.type == "cpu" and step_t.dim() == 0 and not step_t.requires_grad:
+                # the CPU step counter in place through numpy (shares the storage): 0.4 us instead of
+                # 7 us for a torch add + item() -- an optimizer step that follows the iteration's
+                # loss.item() sync runs these on the device's critical path
+                a = step_t.numpy()
+                a[()] += 1
+                t = int(a)
+            else:
+                step_t += 1
+                t = int(step_t.item())
         else:
             t = int(step_t) + 1
             state["step"] = torch.tensor(float(t), dtype=torch.float32)

@@ -214,17 +214,23 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
             if binning_capacity is not None:
                 bounded_status()
         with torch.no_grad():
-            if densify_stats:
-                if fused:
-                    gs_train.add_densification_stats(model, viewspace, radii)
-                else:
-                    _torch_densification_stats(model, viewspace, radii)
-            if owner is not None and owner.pending is not None:
+            fused_step = owner is not None and owner.pending is not None
+            if fused_step:
+                # the fused backward + Adam first: the statistics (train.py:115-116) read only the
+                # screen-space gradient and the radii, which it does not touch, and the device gets
+                # its longest kernel right after the loss.item() sync
                 inputs, view = owner.pending
                 owner.pending = None
                 model.optimizer.step_fused_backward(
                     [model._xyz, model._features_dc, model._features_rest, model._opacity, model._scaling,
                      model._rotation], inputs, view)
+            if densify_stats:
+                if fused:
+                    gs_train.add_densification_stats(model, viewspace, radii)
+                else:
+                    _torch_densification_stats(model, viewspace, radii)
+            if fused_step:
+                pass  # (the optimizer step ran above, fused with the per-Gaussian backward)
             elif acts:
                 shs, opac, scales, rots = acts
                 model.optimizer.step_activated(
