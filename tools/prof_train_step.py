@@ -17,6 +17,8 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--warmup", type=int, default=3)
 ap.add_argument("--torch-glue", action="store_true")
 ap.add_argument("--no-split-sh", action="store_true")
+ap.add_argument("--loss-item", action="store_true", help="train.py's per-iteration loss.item()")
+ap.add_argument("--fuse-adam", action="store_true", help="train_step(fuse_adam=True)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 cam = gs_scenes.identity_camera(1920, 1080)
@@ -25,10 +27,12 @@ settings = gs_scenes.raster_settings_for(cam, 3, device=dev)
 gt = torch.rand((3, 1080, 1920), generator=torch.Generator().manual_seed(2)).to(dev)
 model = ts.TrainModel(sc, dev, fused=not a.torch_glue)
 for _ in range(a.warmup):
-    ts.train_step(model, settings, gt, fused=not a.torch_glue, split_sh=not a.no_split_sh)
+    ts.train_step(model, settings, gt, fused=not a.torch_glue, split_sh=not a.no_split_sh, loss_item=a.loss_item,
+                  fuse_adam=a.fuse_adam)
 torch.cuda.synchronize()
 t = time.perf_counter()
 for _ in range(a.steps):
-    ts.train_step(model, settings, gt, fused=not a.torch_glue, split_sh=not a.no_split_sh)
+    ts.train_step(model, settings, gt, fused=not a.torch_glue, split_sh=not a.no_split_sh, loss_item=a.loss_item,
+                  fuse_adam=a.fuse_adam)
 torch.cuda.synchronize()
 print(f"train step {1e3 * (time.perf_counter() - t) / a.steps:.3f} ms")
