@@ -209,6 +209,11 @@ class FusedAdam(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step_fused_backward(self, params, inputs: dict, view) -> None:
+        """prepare_fused_backward(...)() (below)."""
+        self.prepare_fused_backward(params, inputs, view)()
+
+    @torch.no_grad()
+    def prepare_fused_backward(self, params, inputs: dict, view):
         """The per-Gaussian half of one view's backward fused with step_activated (one HIP launch,
         gs_backward_gaussians_adam): `params` are GaussianModel's six raw parameters in group
         order (xyz, features_dc, features_rest, opacity, scaling, rotation), `inputs` / `view` the
@@ -216,7 +221,10 @@ class FusedAdam(torch.optim.Optimizer):
         protocol: the call's Gaussian inputs and (viewmatrix, projmatrix, campos, tan_fovx,
         tan_fovy, W, H, geomBuffer), after its per-tile half).  Same floats as the unfused backward
         followed by step_activated in the modes plain / features_dc / features_rest / sigmoid / exp /
-        normalize, and no gradient is stored (.grad of the six stays as it is)."""
+        normalize, and no gradient is stored (.grad of the six stays as it is).
+        Returns the launch: every check and argument is done here, so a caller that must read the
+        loss first (train.py:99 before :127) prepares before that host sync and launches after it;
+        the step counts advance at the launch."""
         from diff_gaussian_rasterization import _C
 
         if len(params) != 6:
@@ -258,19 +266,24 @@ class FusedAdam(torch.optim.Optimizer):
         cp = _C._f32(cp, "campos", dev, host_ok=True)
         vg = _native.ViewGrad(vm.data_ptr(), pm.data_ptr(), cp.data_ptr(), float(tx), float(ty), int(W), int(H),
                               geom.data_ptr())
-        for p in params:
-            steps.append(self._advance(p)[2])
         (b1, b2, eps, maximize), = hyper
         arr = lambda ts: ctypes.cast((ctypes.c_void_p * 6)(*[t.data_ptr() for t in ts]), ctypes.c_void_p)  # noqa: E731
-        with torch.cuda.device(dev):
-            _native.check(_lib.gs_backward_gaussians_adam(
-                P, int(inputs["degree"]), 16, _ptr(xyz), _ptr(dc), _ptr(rest), _ptr(scales),
+        steps_c = (ctypes.c_longlong * 6)()
+        args = [P, int(inputs["degree"]), 16, _ptr(xyz), _ptr(dc), _ptr(rest), _ptr(scales),
                 float(inputs["scale_modifier"]), _ptr(rots), ctypes.byref(vg), arr(params), arr(ms), arr(vs),
-                ctypes.cast((ctypes.c_double * 6)(*lrs), ctypes.c_void_p),
-                ctypes.cast((ctypes.c_longlong * 6)(*steps), ctypes.c_void_p),
+                ctypes.cast((ctypes.c_double * 6)(*lrs), ctypes.c_void_p), ctypes.cast(steps_c, ctypes.c_void_p),
                 ctypes.cast((ctypes.c_double * 6)(*wds), ctypes.c_void_p), b1, b2, eps, int(maximize),
-                int(bool(inputs.get("debug", False))), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
-                "backward + adam step (fused)")
+                int(bool(inputs.get("debug", False))), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)]
+        keep = (vm, pm, cp, geom, vg, inputs)  # alive until the launch
+
+        def launch():
+            for k, p in enumerate(params):
+                steps_c[k] = self._advance(p)[2]
+            with torch.cuda.device(dev):
+                _native.check(_lib.gs_backward_gaussians_adam(*args), "backward + adam step (fused)")
+            assert keep  # (the closure holds the arguments' tensors until the launch)
+
+        return launch
 
     @staticmethod
     def _launch(items, b1, b2, eps, maximize, dev, st):

@@ -204,6 +204,15 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
             Ll1 = gs_loss.l1_loss(image, gt_image)
             loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - gs_loss.ssim(image, gt_image))
         loss.backward()
+        # the fused backward + Adam's launch is prepared before the loss.item() host sync (its checks
+        # and arguments), so the device waits only for the launch itself after the sync
+        fused_launch = None
+        if owner is not None and owner.pending is not None:
+            inputs, view = owner.pending
+            owner.pending = None
+            fused_launch = model.optimizer.prepare_fused_backward(
+                [model._xyz, model._features_dc, model._features_rest, model._opacity, model._scaling,
+                 model._rotation], inputs, view)
         value = None
         if loss_item:
             # train.py:99 reads loss.item() here, after the backward and before the statistics and
@@ -214,22 +223,17 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
             if binning_capacity is not None:
                 bounded_status()
         with torch.no_grad():
-            fused_step = owner is not None and owner.pending is not None
-            if fused_step:
+            if fused_launch is not None:
                 # the fused backward + Adam first: the statistics (train.py:115-116) read only the
                 # screen-space gradient and the radii, which it does not touch, and the device gets
                 # its longest kernel right after the loss.item() sync
-                inputs, view = owner.pending
-                owner.pending = None
-                model.optimizer.step_fused_backward(
-                    [model._xyz, model._features_dc, model._features_rest, model._opacity, model._scaling,
-                     model._rotation], inputs, view)
+                fused_launch()
             if densify_stats:
                 if fused:
                     gs_train.add_densification_stats(model, viewspace, radii)
                 else:
                     _torch_densification_stats(model, viewspace, radii)
-            if fused_step:
+            if fused_launch is not None:
                 pass  # (the optimizer step ran above, fused with the per-Gaussian backward)
             elif acts:
                 shs, opac, scales, rots = acts
