@@ -535,67 +535,72 @@ __device__ __forceinline__ QuadPix quad_pixel(int tx, int ty, int wid, int lane)
 // Conservative culling of (splat, pixel-rectangle) pairs.  A pixel p can only contribute if
 // alpha >= 1/255, i.e. q(p - m) <= 2 ln(255 o) with q(d) = cxx dx^2 + 2 cxy dx dy + cyy dy^2
 // (power = -q/2).  preprocess stores lim = 2 ln(255 o) (1 + 1e-3) + 1e-3 (or -1 when o < 1/255);
-// the minimum of q over the rectangle of pixel centres is found exactly (convex quadratic: at
-// the centre if inside, else on an edge) and compared with lim.  The margins absorb rounding,
-// so a culled pair never contributes: results are unchanged, only work is skipped.
-__device__ __forceinline__ float q_form(float cx, float cy, float cz, float dx, float dy) {
-  return cx * dx * dx + 2.0f * cy * dx * dy + cz * dy * dy;
+// the minimum of q over the rectangle of pixel centres is compared with lim.  The margins absorb
+// rounding, so a culled pair never contributes: results are unchanged, only work is skipped.
+//
+// The minimum (convex quadratic, minimum at d = 0): 0 when the centre lies in the rectangle, else
+// on an edge that faces the centre (at a constrained minimum d* on edge x = e the KKT multiplier
+// mu >= 0 with grad q(d*) = (mu, 0) and convexity give mu (0 - e) < 0, so e > 0 for the low edge
+// -- the centre lies beyond it).  So per axis ONE edge is evaluated: the facing one when the centre
+// lies outside that axis's range, and otherwise an arbitrary one, harmless since any point of the
+// rectangle is >= the minimum.  On the edge x = e the 1-D minimiser dy = -cxy e / cyy is clamped to
+// the edge; rcp for 1 / cyy (the minimiser only needs to be close: q is flat there, second order).
+__device__ __forceinline__ float q_form(float cx, float cy2, float cz, float dx, float dy) {
+  return __builtin_fmaf(dx, __builtin_fmaf(cx, dx, cy2 * dy), (cz * dy) * dy);
+}
+
+struct EllipseCull {
+  float cx, cy2, cz, kx, ky;  // conic (cxy doubled), edge minimiser slopes -cxy / cxx, -cxy / cyy
+  bool degenerate;            // not positive definite on the axes: never culled
+};
+__device__ __forceinline__ EllipseCull ellipse_cull(float cx, float cy, float cz) {
+  EllipseCull e;
+  e.cx = cx, e.cy2 = 2.0f * cy, e.cz = cz;
+  e.degenerate = !(cx > 0.0f && cz > 0.0f);
+  e.kx = -cy * __builtin_amdgcn_rcpf(cx);
+  e.ky = -cy * __builtin_amdgcn_rcpf(cz);
+  return e;
+}
+// min of q over [dxl, dxh] x [dyl, dyh] (offsets from the centre) <= lim; the centre-inside case
+// is the caller's (q = 0 there)
+__device__ __forceinline__ bool rect_min_within(const EllipseCull& e, float dxl, float dxh, float dyl, float dyh,
+                                                float lim) {
+  const float dxe = dxl > 0.0f ? dxl : dxh, dye = dyl > 0.0f ? dyl : dyh;
+  const float a = q_form(e.cx, e.cy2, e.cz, dxe, fminf(fmaxf(dxe * e.ky, dyl), dyh));
+  const float b = q_form(e.cx, e.cy2, e.cz, fminf(fmaxf(dye * e.kx, dxl), dxh), dye);
+  return fminf(a, b) <= lim;
 }
 __device__ __forceinline__ bool ellipse_meets_rect(float mx, float my, float cx, float cy, float cz, float lim,
                                                    float x0, float x1, float y0, float y1) {
   if (!(lim >= 0.0f)) return false;
   const float dxl = x0 - mx, dxh = x1 - mx, dyl = y0 - my, dyh = y1 - my;
-  if (dxl <= 0.0f && dxh >= 0.0f && dyl <= 0.0f && dyh >= 0.0f) return true;
-  if (!(cx > 0.0f && cz > 0.0f)) return true;  // degenerate conic: do not cull
-  const float icx = 1.0f / cx, icz = 1.0f / cz;
-  float best = q_form(cx, cy, cz, dxl, fminf(fmaxf(-cy * dxl * icz, dyl), dyh));
-  best = fminf(best, q_form(cx, cy, cz, dxh, fminf(fmaxf(-cy * dxh * icz, dyl), dyh)));
-  best = fminf(best, q_form(cx, cy, cz, fminf(fmaxf(-cy * dyl * icx, dxl), dxh), dyl));
-  best = fminf(best, q_form(cx, cy, cz, fminf(fmaxf(-cy * dyh * icx, dxl), dxh), dyh));
-  return best <= lim;
+  const bool inside = dxl <= 0.0f && dxh >= 0.0f && dyl <= 0.0f && dyh >= 0.0f;
+  const EllipseCull e = ellipse_cull(cx, cy, cz);
+  return inside || e.degenerate || rect_min_within(e, dxl, dxh, dyl, dyh, lim);
 }
 
-// bit w set if the splat can contribute to a pixel of 8x8 quadrant w of tile (tx, ty)
+// bit w set if the splat can contribute to a pixel of 8x8 quadrant w of tile (tx, ty); the
+// column / row offsets and the edge slopes are shared by the four rectangles
 __device__ __forceinline__ uint32_t quadrant_mask(float mx, float my, float cx, float cy, float cz, float lim, int tx,
                                                   int ty) {
   if (!(lim >= 0.0f)) return 0u;
   const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
+  const EllipseCull e = ellipse_cull(cx, cy, cz);
+  if (e.degenerate) return 0xFu;
+  float xl[2], xh[2], yl[2], yh[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    xl[h] = (x0 + 8.0f * h) - mx, xh[h] = (x0 + 8.0f * h + 7.0f) - mx;
+    yl[h] = (y0 + 8.0f * h) - my, yh[h] = (y0 + 8.0f * h + 7.0f) - my;
+  }
   uint32_t m = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) {
-    const float qx = x0 + 8.0f * (w & 1), qy = y0 + 8.0f * (w >> 1);
-    m |= ellipse_meets_rect(mx, my, cx, cy, cz, lim, qx, qx + 7.0f, qy, qy + 7.0f) ? (1u << w) : 0u;
+    const int c = w & 1, r = w >> 1;
+    const bool inside = xl[c] <= 0.0f && xh[c] >= 0.0f && yl[r] <= 0.0f && yh[r] >= 0.0f;
+    m |= (inside || rect_min_within(e, xl[c], xh[c], yl[r], yh[r], lim)) ? (1u << w) : 0u;
   }
   return m;
-}
-
-// bit h set if the splat can contribute to a pixel of the 8-wide column half h of the tile
-__device__ __forceinline__ uint32_t half_mask(float mx, float my, float cx, float cy, float cz, float lim, int tx,
-                                              int ty) {
-  if (!(lim >= 0.0f)) return 0u;
-  const float x0 = (float)(tx * GS_TILE), y0 = (float)(ty * GS_TILE);
-  uint32_t m = 0;
-  m |= ellipse_meets_rect(mx, my, cx, cy, cz, lim, x0, x0 + 7.0f, y0, y0 + 15.0f) ? 1u : 0u;
-  m |= ellipse_meets_rect(mx, my, cx, cy, cz, lim, x0 + 8.0f, x0 + 15.0f, y0, y0 + 15.0f) ? 2u : 0u;
-  return m;
-}
-
-// each staging wave publishes, per quadrant, the 64-bit set of its entries meeting that quadrant
-__device__ __forceinline__ void publish_masks(uint32_t qmask, uint64_t (*s_mask)[4], int tid) {
-  const uint64_t b0 = __ballot(qmask & 1u), b1 = __ballot(qmask & 2u), b2 = __ballot(qmask & 4u),
-                 b3 = __ballot(qmask & 8u);
-  if ((tid & 63) == 0) {
-    s_mask[tid >> 6][0] = b0;
-    s_mask[tid >> 6][1] = b1;
-    s_mask[tid >> 6][2] = b2;
-    s_mask[tid >> 6][3] = b3;
-  }
-}
-
-__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
 }
 
 }  // namespace gs
