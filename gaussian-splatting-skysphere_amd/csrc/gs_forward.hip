@@ -931,7 +931,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_q(CameraArgs c, const uint2* 
     tile_finish(tile, tile % ORDER_GROUPS, wmax, img.tile_done, img.len_hist, img.tile_brank);
   }
 #ifdef GS_TIMING
-  timing_record(g_fwd_timing, t_start, tile, (uint32_t)wid, t_batches, t_walked);
+  timing_record(g_fwd_timing, t_start, tile, (uint32_t)wid | n << 2, t_batches, t_walked);
 #endif
 }
 

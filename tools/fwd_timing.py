@@ -25,6 +25,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c3")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--out", default="")
+ap.add_argument("--raw", default="", help="also write each rep's per-wave arrays to RAW.<rep>.npz")
 a = ap.parse_args()
 P, deg, W, H = WL[a.workload]
 dev = torch.device("cuda:0")
@@ -70,6 +71,11 @@ for rep in range(a.reps):
     s_us = (t0 - base) / 100.0
     e_us = (t1 - base) / 100.0
     dur = e_us - s_us
+    if a.raw:
+        np.savez_compressed(f"{a.raw}.{rep}.npz", start=s_us, end=e_us, tile=(d[:, 2] >> 32).astype(np.int64),
+                            quad=(d[:, 2] & 3).astype(np.int64), n=((d[:, 2] & 0xFFFFFFFF) >> 2).astype(np.int64),
+                            batches=(d[:, 4] >> 32).astype(np.int64), walked=(d[:, 4] & 0xFFFFFFFF).astype(np.int64),
+                            xcc=(d[:, 3] >> 32).astype(np.int64), hw=(d[:, 3] & 0xFFFFFFFF).astype(np.int64))
     batches = (d[:, 4] >> 32).astype(np.int64)
     walked = (d[:, 4] & 0xFFFFFFFF).astype(np.int64)
     span = e_us.max()
