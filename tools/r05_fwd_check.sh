@@ -13,6 +13,6 @@ if [ $rc -ne 0 ]; then
     grep -E "FAILED|Error|assert" gpurun_out/r05_gpu_tests.txt | head -20; exit 1
   fi
 fi
-SV_ARGS="" bash tools/sv_ab.sh build_base build || exit 1
+SV_ARGS="" bash tools/sv_ab.sh ${BASE:-build} build || exit 1
 timeout -k 10 200 python -u tools/train_step_kernels.py > gpurun_out/r05_tsk.json 2>&1 || exit 1
 timeout -k 10 400 python -u bench.py > gpurun_out/r05_bench.json 2> gpurun_out/r05_bench.err
