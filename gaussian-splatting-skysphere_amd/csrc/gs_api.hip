@@ -1206,6 +1206,7 @@ int gs_backward_gaussians_adam(int P, int D, int M, const float* means3D, const 
   a.k = adam_consts(beta1, beta2, eps, maximize != 0);
   GeomPtrs geo;
   geom_layout((size_t)P, &geo, (char*)view->geom_buffer);
+  a.err = &geo.counters[CNT_ERR];
   CameraArgs c = make_camera(nullptr, view->image_width, view->image_height, view->viewmatrix, view->projmatrix,
                              view->campos, view->tan_fovx, view->tan_fovy, 0);
   bwd_gaussians_adam(g, c, geo, a, (hipStream_t)stream);

@@ -1063,6 +1063,9 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd_adam(GaussianArgs g, Cam
   constexpr int KF = 48, Q = KF / 4;  // M == 16 rows; the active degree DEG uses the first 3 (DEG + 1)^2
   constexpr int K3 = 3 * (DEG + 1) * (DEG + 1);
   __shared__ __attribute__((aligned(16))) float s_rows[256 * SH_STAGE_ROW];
+  // an invalid forward (capacity overflow, look-back timeout, culled prefiltered point): no update
+  // (the host raises when it reads the flags; the step counts are committed only after that)
+  if (*a.err != 0u) return;  // (uniform)
   const int i0 = blockIdx.x * 256, t = (int)threadIdx.x, i = i0 + t;
   const int nG = g.P - i0 < 256 ? g.P - i0 : 256;
   stage_sh_rows48<true>(g, i0, nG, s_rows);

@@ -543,6 +543,9 @@ struct FusedAdamArgs {
   float* v[6];
   float nss[6], bc2s[6], wd[6];
   AdamConsts k;
+  // the view's forward error flags (counters[CNT_ERR]): non-zero -> the update is skipped, so a
+  // step launched before the host has read them leaves an invalid view's parameters untouched
+  const uint32_t* err;
 };
 // one view's per-Gaussian half fused with the Adam step (g: M == 16 split SH rows, 16-B aligned)
 void bwd_gaussians_adam(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const FusedAdamArgs& a,

@@ -75,6 +75,11 @@ class FusedAdam(torch.optim.Optimizer):
                         decoupled_weight_decay=decoupled_weight_decay)
         super().__init__(params, defaults)
 
+    def _peek_step(self, p):
+        """The step count p's next update uses (state unchanged; the state exists: _checked_state)."""
+        step_t = self.state[p]["step"]
+        return (int(step_t.item()) if torch.is_tensor(step_t) else int(step_t)) + 1
+
     def _advance(self, p):
         """The parameter's Adam state (created as torch creates it), its step count incremented:
         (exp_avg, exp_avg_sq, step after this update)."""
@@ -276,12 +281,24 @@ class FusedAdam(torch.optim.Optimizer):
                 int(bool(inputs.get("debug", False))), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)]
         keep = (vm, pm, cp, geom, vg, inputs)  # alive until the launch
 
-        def launch():
+        def launch(defer_commit: bool = False):
+            """Advances the step counts and launches.  defer_commit: launches with the next step
+            counts but returns a commit() that advances them, for a caller that reads the view's
+            forward status after the launch -- the kernel skips the update of a view whose forward
+            recorded an error, so a caller that raises then leaves parameters, moments and step
+            counts as they were (and commits after its check otherwise)."""
             for k, p in enumerate(params):
-                steps_c[k] = self._advance(p)[2]
+                steps_c[k] = self._peek_step(p) if defer_commit else self._advance(p)[2]
             with torch.cuda.device(dev):
                 _native.check(_lib.gs_backward_gaussians_adam(*args), "backward + adam step (fused)")
             assert keep  # (the closure holds the arguments' tensors until the launch)
+            if defer_commit:
+                def commit():
+                    for k, p in enumerate(params):
+                        if self._advance(p)[2] != steps_c[k]:
+                            raise RuntimeError("step_fused_backward: a step count moved between launch and commit")
+                return commit
+            return None
 
         return launch
 

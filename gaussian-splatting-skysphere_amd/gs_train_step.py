@@ -171,6 +171,17 @@ def _torch_densification_stats(model: TrainModel, viewspace, radii):
     model.denom[vis] += 1
 
 
+_PINNED = {}
+
+
+def _pinned_scalar(device):
+    """A pinned host float32 scalar per device (the fused step's early loss read-back)."""
+    b = _PINNED.get(device)
+    if b is None:
+        b = _PINNED[device] = torch.empty((), dtype=torch.float32, pin_memory=True)
+    return b
+
+
 def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool = True, densify_stats: bool = True,
                lambda_dssim: float = LAMBDA_DSSIM, fused_adjoint: bool = True, split_sh: bool = True,
                loss_item: bool = False, binning_capacity: int | None = None, fuse_adam: bool = False):
@@ -203,9 +214,16 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
         else:
             Ll1 = gs_loss.l1_loss(image, gt_image)
             loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - gs_loss.ssim(image, gt_image))
+        early = None
+        if loss_item and owner is not None:
+            # fused Adam: the loss value is copied out right after the loss kernel and read through an
+            # event, so the host's sync does not wait for the backward and the optimizer step queued
+            # behind it (below)
+            buf = _pinned_scalar(loss.device)
+            buf.copy_(loss.detach().reshape(()), non_blocking=True)
+            early = (buf, torch.cuda.Event())
+            early[1].record()
         loss.backward()
-        # the fused backward + Adam's launch is prepared before the loss.item() host sync (its checks
-        # and arguments), so the device waits only for the launch itself after the sync
         fused_launch = None
         if owner is not None and owner.pending is not None:
             inputs, view = owner.pending
@@ -214,6 +232,25 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
                 [model._xyz, model._features_dc, model._features_rest, model._opacity, model._scaling,
                  model._rotation], inputs, view)
         value = None
+        if early is not None and fused_launch is not None:
+            # train.py:99 (loss.item()) before :127 (optimizer.step()): the fused backward + Adam is
+            # launched BEFORE the host reads the loss and the forward's status, with its step counts
+            # committed only after that check -- the kernel skips the update of a view whose forward
+            # recorded an error, so an overflowing bounded iteration raises here with parameters,
+            # moments, step counts and statistics untouched, as the reference order guarantees
+            with torch.no_grad():
+                commit = fused_launch(defer_commit=True)
+            early[1].synchronize()
+            value = float(early[0].item())
+            if binning_capacity is not None:
+                bounded_status()
+            commit()
+            fused_launch = None
+            with torch.no_grad():
+                if densify_stats:
+                    gs_train.add_densification_stats(model, viewspace, radii)
+                model.optimizer.zero_grad(set_to_none=True)
+            return value
         if loss_item:
             # train.py:99 reads loss.item() here, after the backward and before the statistics and
             # the optimizer step (train.py:115-128): an iteration whose bounded forward overflowed

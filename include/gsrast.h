@@ -418,7 +418,10 @@ int gs_adam_step_activated(int count, float* const* params_host, const float* co
  * f_dc [P,1,3], f_rest [P,15,3], opacity [P,1], scaling [P,3], rotation [P,4] (raw parameters,
  * rotation 16-byte aligned); lr / step / weight_decay per group as gs_adam_step (weight_decay_host
  * may be NULL).  The Adam update runs in place while the kernel reads the parameters: nothing else
- * may read or write them on another stream until the call's work completes. */
+ * may read or write them on another stream until the call's work completes.  A view whose forward
+ * recorded an error (its geometry buffer's flags: capacity overflow, look-back timeout, culled
+ * prefiltered point) is not updated, so a caller may launch this before reading the forward's status
+ * and keep its step counts unchanged when that raises. */
 int gs_backward_gaussians_adam(int P, int D, int M, const float* means3D, const float* shs_dc, const float* shs_rest,
                                const float* scales, float scale_modifier, const float* rotations,
                                const gs_view_grad* view, float* const* params_host, float* const* exp_avg_host,

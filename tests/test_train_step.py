@@ -191,6 +191,50 @@ def test_bounded_train_step_raises_at_its_own_loss_item(device):
         assert torch.equal(x, y)
 
 
+def test_fused_adam_bounded_overflow_raises_with_state_untouched(device):
+    """The fused-Adam step launches its backward + Adam before the host reads the loss and the
+    forward's status (train_step's early read-back); an overflowing bounded iteration must still
+    raise at its own loss.item() with parameters, moments, step counts and statistics untouched:
+    the kernel skips the update of a view whose forward recorded an error and the step counts are
+    committed only after the check.  The next (fitting) iteration then equals the plain step's."""
+    import gs_train_step as ts
+    from diff_gaussian_rasterization import bounded_status, last_num_rendered
+
+    sc, settings, gt = _setup(device)
+    a, b = ts.TrainModel(sc, device), ts.TrainModel(sc, device)
+    ts.train_step(a, settings, gt, loss_item=True, fuse_adam=True)
+    n = last_num_rendered()
+    ts.train_step(b, settings, gt, loss_item=True, fuse_adam=True, binning_capacity=n + 64)
+    names = ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
+
+    def snapshot(m):
+        torch.cuda.synchronize()
+        st = m.optimizer.state_dict()["state"]
+        moments = {(i, k): v.clone() for i, s in st.items() for k, v in s.items() if torch.is_tensor(v) and v.dim()}
+        steps = {(i, k): float(v) for i, s in st.items() for k, v in s.items() if not torch.is_tensor(v) or not v.dim()}
+        return ({n_: getattr(m, n_).detach().clone() for n_ in names}, moments, steps,
+                [t.clone() for t in (m.max_radii2D, m.xyz_gradient_accum, m.denom)])
+
+    before = snapshot(b)
+    with pytest.raises(RuntimeError, match="binning capacity"):
+        ts.train_step(b, settings, gt, loss_item=True, fuse_adam=True, binning_capacity=n // 4)
+    assert bounded_status() == (0, 0)
+    after = snapshot(b)
+    for n_ in names:
+        assert torch.equal(before[0][n_], after[0][n_]), n_
+    assert before[1].keys() == after[1].keys() and before[2] == after[2]
+    for k in before[1]:
+        assert torch.equal(before[1][k], after[1][k]), k
+    for x, y in zip(before[3], after[3]):
+        assert torch.equal(x, y)
+    # the model continues as if the failed iteration had not happened
+    la = ts.train_step(a, settings, gt, loss_item=True, fuse_adam=True)
+    lb = ts.train_step(b, settings, gt, loss_item=True, fuse_adam=True, binning_capacity=n + 64)
+    assert la == lb
+    for n_ in names:
+        assert torch.equal(getattr(a, n_), getattr(b, n_)), n_
+
+
 def test_bounded_overflow_in_a_captured_step_raises_in_the_loop(device):
     """render -> L1 + SSIM -> backward with a bounded forward, captured once into a HIP graph
     (torch.cuda.CUDAGraph) and replayed in a training loop that polls bounded_status() at its
