@@ -23,6 +23,8 @@ densification statistics, percent_dense and active_sh_degree.  The learning-rate
 """
 from __future__ import annotations
 
+import threading
+
 import torch
 
 import gs_loss
@@ -171,14 +173,18 @@ def _torch_densification_stats(model: TrainModel, viewspace, radii):
     model.denom[vis] += 1
 
 
-_PINNED = {}
+_PINNED = threading.local()
 
 
 def _pinned_scalar(device):
-    """A pinned host float32 scalar per device (the fused step's early loss read-back)."""
-    b = _PINNED.get(device)
+    """A pinned host float32 scalar per thread and device (the fused step's early loss read-back;
+    per thread: two threads' steps must not share the copy target)."""
+    cache = getattr(_PINNED, "bufs", None)
+    if cache is None:
+        cache = _PINNED.bufs = {}
+    b = cache.get(device)
     if b is None:
-        b = _PINNED[device] = torch.empty((), dtype=torch.float32, pin_memory=True)
+        b = cache[device] = torch.empty((), dtype=torch.float32, pin_memory=True)
     return b
 
 
