@@ -586,6 +586,10 @@ def main():
         "fused_front": fused_front,
         "serial_one_stream": serial,
         "kernels": kernels,
+        # how `kernels` (and single_view's kernel_us_per_iter) are timed: HIP events around each
+        # launch on its stream, so a short kernel's figure includes its dispatch gap; the
+        # kernel-only durations are rocprofv3's (profiles/*rocprof*.csv, bench.py --profile-pass-only)
+        "kernels_timing": "hip events per launch (dispatch gap included)",
         "train_step": train,
         "init_knn": knn,
         **({"step_ms_deciles": step_deciles} if step_deciles else {}),
