@@ -243,7 +243,10 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
             # launched BEFORE the host reads the loss and the forward's status, with its step counts
             # committed only after that check -- the kernel skips the update of a view whose forward
             # recorded an error, so an overflowing bounded iteration raises here with parameters,
-            # moments, step counts and statistics untouched, as the reference order guarantees
+            # moments, step counts and statistics untouched, as the reference order guarantees.
+            # (A read-back forward raises its own errors in its call, except a look-back timeout of
+            # its sorts -- never observed -- which the next call raises: that step's update is then
+            # skipped while its step counts advance.)
             with torch.no_grad():
                 commit = fused_launch(defer_commit=True)
             early[1].synchronize()
