@@ -1176,6 +1176,20 @@ int gs_backward_gaussians_adam(int P, int D, int M, const float* means3D, const 
                                float* const* exp_avg_sq_host, const double* lr_host, const long long* step_host,
                                const double* weight_decay_host, double beta1, double beta2, double eps, int maximize,
                                int debug, void* stream) {
+  return gs_backward_gaussians_adam_stats(P, D, M, means3D, shs_dc, shs_rest, scales, scale_modifier, rotations, view,
+                                          params_host, exp_avg_host, exp_avg_sq_host, lr_host, step_host,
+                                          weight_decay_host, beta1, beta2, eps, maximize, nullptr, nullptr, 0, nullptr,
+                                          nullptr, nullptr, debug, stream);
+}
+
+int gs_backward_gaussians_adam_stats(int P, int D, int M, const float* means3D, const float* shs_dc,
+                                     const float* shs_rest, const float* scales, float scale_modifier,
+                                     const float* rotations, const gs_view_grad* view, float* const* params_host,
+                                     float* const* exp_avg_host, float* const* exp_avg_sq_host, const double* lr_host,
+                                     const long long* step_host, const double* weight_decay_host, double beta1,
+                                     double beta2, double eps, int maximize, const int* radii, const float* grad2d,
+                                     int grad_stride, float* max_radii2D, float* grad_accum, float* denom, int debug,
+                                     void* stream) {
   clear_error(debug);
   if (P < 0) return set_error("P must be >= 0"), 1;
   if (P == 0) return 0;
@@ -1204,6 +1218,14 @@ int gs_backward_gaussians_adam(int P, int D, int M, const float* means3D, const 
     a.wd[k] = weight_decay_host ? (float)weight_decay_host[k] : 0.0f;
   }
   a.k = adam_consts(beta1, beta2, eps, maximize != 0);
+  const bool any_stat = radii || grad2d || max_radii2D || grad_accum || denom;
+  if (any_stat) {
+    if (!radii || !grad2d || !max_radii2D || !grad_accum || !denom)
+      return set_error("densify stats: all five pointers or none"), 1;
+    if (grad_stride < 2) return set_error("densify stats: grad_stride must be >= 2"), 1;
+    a.radii = radii, a.grad2d = grad2d, a.gstride = grad_stride;
+    a.max_r = max_radii2D, a.accum = grad_accum, a.denom = denom;
+  }
   GeomPtrs geo;
   geom_layout((size_t)P, &geo, (char*)view->geom_buffer);
   a.err = &geo.counters[CNT_ERR];

@@ -1147,6 +1147,8 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd_adam(GaussianArgs g, Cam
     __builtin_nontemporal_store(pq, reinterpret_cast<v4f*>(a.p[DT_ROT] + i4));
     __builtin_nontemporal_store(mq, reinterpret_cast<v4f*>(a.m[DT_ROT] + i4));
     __builtin_nontemporal_store(vq, reinterpret_cast<v4f*>(a.v[DT_ROT] + i4));
+    // train.py:115-116 in the same pass (k_densify_stats's arithmetic; skipped with the update)
+    if (a.max_r) densify_stat_one(i, a.radii, a.grad2d, a.gstride, a.max_r, a.accum, a.denom);
   }
   lds_barrier();
   // features_dc / features_rest: the workgroup's contiguous blocks (16-B aligned: 256 rows of 12 /

@@ -535,6 +535,18 @@ __device__ __forceinline__ void normalize_adjoint(const float* gq, const float* 
 #pragma unroll
   for (int j = 0; j < 4; j++) out[j] = gq[j] / n - c * q[j];
 }
+// train.py:115-116 (gaussian_model.py:405-407) for Gaussian i: k_densify_stats's body, shared with
+// the fused backward + Adam step so both write the same floats
+__device__ __forceinline__ void densify_stat_one(int i, const int* __restrict__ radii, const float* __restrict__ grad2d,
+                                                 int gstride, float* __restrict__ max_r, float* __restrict__ accum,
+                                                 float* __restrict__ denom) {
+  const int r = radii[i];
+  if (r <= 0) return;
+  max_r[i] = fmaxf(max_r[i], (float)r);
+  const float gx = grad2d[(size_t)gstride * i], gy = grad2d[(size_t)gstride * i + 1];
+  accum[i] += sqrtf(gx * gx + gy * gy);
+  denom[i] += 1.0f;
+}
 // the six parameter groups of GaussianModel (xyz, f_dc, f_rest, opacity, scaling, rotation) for the
 // fused per-Gaussian backward + Adam step (gs_backward_gaussians_adam)
 struct FusedAdamArgs {
@@ -546,6 +558,11 @@ struct FusedAdamArgs {
   // the view's forward error flags (counters[CNT_ERR]): non-zero -> the update is skipped, so a
   // step launched before the host has read them leaves an invalid view's parameters untouched
   const uint32_t* err;
+  // optional densification statistics of the view (max_r == nullptr: none), densify_stat_one
+  const int* radii;
+  const float* grad2d;
+  int gstride;
+  float *max_r, *accum, *denom;
 };
 // one view's per-Gaussian half fused with the Adam step (g: M == 16 split SH rows, 16-B aligned)
 void bwd_gaussians_adam(const GaussianArgs& g, const CameraArgs& c, const GeomPtrs& geo, const FusedAdamArgs& a,

@@ -138,12 +138,7 @@ __global__ __launch_bounds__(256) void k_densify_stats(int P, const int* __restr
                                                        float* __restrict__ accum, float* __restrict__ denom) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= P) return;
-  const int r = radii[i];
-  if (r <= 0) return;
-  max_r[i] = fmaxf(max_r[i], (float)r);
-  const float gx = grad2d[(size_t)gstride * i], gy = grad2d[(size_t)gstride * i + 1];
-  accum[i] += sqrtf(gx * gx + gy * gy);
-  denom[i] += 1.0f;
+  densify_stat_one(i, radii, grad2d, gstride, max_r, accum, denom);
 }
 
 void adam_step(int count, float* const* params, const float* const* grads, float* const* exp_avg,

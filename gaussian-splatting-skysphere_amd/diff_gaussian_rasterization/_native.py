@@ -130,6 +130,12 @@ SIGNATURES = {
         [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, ctypes.POINTER(ViewGrad), _c_p, _c_p, _c_p, _c_p, _c_p,
          _c_p, _c_d, _c_d, _c_d, _c_i, _c_i, _c_p],
     ),
+    # ABI v16: the same plus the view's densification statistics in that pass
+    "gs_backward_gaussians_adam_stats": (
+        _c_i,
+        [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, ctypes.POINTER(ViewGrad), _c_p, _c_p, _c_p, _c_p, _c_p,
+         _c_p, _c_d, _c_d, _c_d, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p],
+    ),
     "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),
     "gs_knn_mean_dist2": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p]),

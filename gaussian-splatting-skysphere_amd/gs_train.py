@@ -213,12 +213,12 @@ class FusedAdam(torch.optim.Optimizer):
         return m, v
 
     @torch.no_grad()
-    def step_fused_backward(self, params, inputs: dict, view) -> None:
+    def step_fused_backward(self, params, inputs: dict, view, stats=None) -> None:
         """prepare_fused_backward(...)() (below)."""
-        self.prepare_fused_backward(params, inputs, view)()
+        self.prepare_fused_backward(params, inputs, view, stats)()
 
     @torch.no_grad()
-    def prepare_fused_backward(self, params, inputs: dict, view):
+    def prepare_fused_backward(self, params, inputs: dict, view, stats=None):
         """The per-Gaussian half of one view's backward fused with step_activated (one HIP launch,
         gs_backward_gaussians_adam): `params` are GaussianModel's six raw parameters in group
         order (xyz, features_dc, features_rest, opacity, scaling, rotation), `inputs` / `view` the
@@ -227,6 +227,9 @@ class FusedAdam(torch.optim.Optimizer):
         tan_fovy, W, H, geomBuffer), after its per-tile half).  Same floats as the unfused backward
         followed by step_activated in the modes plain / features_dc / features_rest / sigmoid / exp /
         normalize, and no gradient is stored (.grad of the six stays as it is).
+        stats: (max_radii2D, xyz_gradient_accum, denom, radii, viewspace_grad) -- the view's
+        densification statistics (densify_stats, train.py:115-116) in the same pass
+        (gs_backward_gaussians_adam_stats), the same floats as densify_stats after the step.
         Returns the launch: every check and argument is done here, so a caller that must read the
         loss first (train.py:99 before :127) prepares before that host sync and launches after it;
         the step counts advance at the launch."""
@@ -272,14 +275,22 @@ class FusedAdam(torch.optim.Optimizer):
         vg = _native.ViewGrad(vm.data_ptr(), pm.data_ptr(), cp.data_ptr(), float(tx), float(ty), int(W), int(H),
                               geom.data_ptr())
         (b1, b2, eps, maximize), = hyper
+        if stats is not None:
+            max_r, accum, denom, radii, vgrad = stats
+            _check_densify_stats(max_r, accum, denom, radii, vgrad)
+            if radii.shape[0] != P:
+                raise ValueError(f"step_fused_backward: statistics of {radii.shape[0]} Gaussians, expected {P}")
+            stat_args = [_ptr(radii), _ptr(vgrad), vgrad.shape[1], _ptr(max_r), _ptr(accum), _ptr(denom)]
+        else:
+            stat_args = [None, None, 0, None, None, None]
         arr = lambda ts: ctypes.cast((ctypes.c_void_p * 6)(*[t.data_ptr() for t in ts]), ctypes.c_void_p)  # noqa: E731
         steps_c = (ctypes.c_longlong * 6)()
         args = [P, int(inputs["degree"]), 16, _ptr(xyz), _ptr(dc), _ptr(rest), _ptr(scales),
                 float(inputs["scale_modifier"]), _ptr(rots), ctypes.byref(vg), arr(params), arr(ms), arr(vs),
                 ctypes.cast((ctypes.c_double * 6)(*lrs), ctypes.c_void_p), ctypes.cast(steps_c, ctypes.c_void_p),
-                ctypes.cast((ctypes.c_double * 6)(*wds), ctypes.c_void_p), b1, b2, eps, int(maximize),
+                ctypes.cast((ctypes.c_double * 6)(*wds), ctypes.c_void_p), b1, b2, eps, int(maximize), *stat_args,
                 int(bool(inputs.get("debug", False))), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)]
-        keep = (vm, pm, cp, geom, vg, inputs)  # alive until the launch
+        keep = (vm, pm, cp, geom, vg, inputs, stats)  # alive until the launch
 
         def launch(defer_commit: bool = False):
             """Advances the step counts and launches.  defer_commit: launches with the next step
@@ -290,7 +301,7 @@ class FusedAdam(torch.optim.Optimizer):
             for k, p in enumerate(params):
                 steps_c[k] = self._peek_step(p) if defer_commit else self._advance(p)[2]
             with torch.cuda.device(dev):
-                _native.check(_lib.gs_backward_gaussians_adam(*args), "backward + adam step (fused)")
+                _native.check(_lib.gs_backward_gaussians_adam_stats(*args), "backward + adam step (fused)")
             assert keep  # (the closure holds the arguments' tensors until the launch)
             if defer_commit:
                 def commit():
@@ -322,16 +333,8 @@ def densify_stats(max_radii2D: torch.Tensor, grad_accum: torch.Tensor, denom: to
     """In place, for every i with radii[i] > 0 (train.py:115, gaussian_model.py:405-407):
     max_radii2D[i] = max(max_radii2D[i], radii[i]); grad_accum[i] += ||viewspace_grad[i, :2]||;
     denom[i] += 1."""
+    _check_densify_stats(max_radii2D, grad_accum, denom, radii, viewspace_grad)
     P = radii.shape[0]
-    for t, name in ((max_radii2D, "max_radii2D"), (grad_accum, "xyz_gradient_accum"), (denom, "denom")):
-        _check_f32_dense(t, name)
-        if t.numel() != P:
-            raise ValueError(f"{name}: expected {P} entries, got {t.numel()}")
-    _check_f32_dense(viewspace_grad, "viewspace grad")
-    if viewspace_grad.dim() != 2 or viewspace_grad.shape[0] != P or viewspace_grad.shape[1] < 2:
-        raise ValueError(f"viewspace grad: expected [{P}, >=2], got {tuple(viewspace_grad.shape)}")
-    if radii.dtype != torch.int32 or not radii.is_cuda or not radii.is_contiguous():
-        raise TypeError("radii: expected a contiguous int32 device tensor (the rasterizer's output)")
     if P == 0:
         return
     dev = radii.device
@@ -342,6 +345,19 @@ def densify_stats(max_radii2D: torch.Tensor, grad_accum: torch.Tensor, denom: to
                                             ctypes.c_void_p(max_radii2D.data_ptr()),
                                             ctypes.c_void_p(grad_accum.data_ptr()),
                                             ctypes.c_void_p(denom.data_ptr()), st), "densify stats")
+
+
+def _check_densify_stats(max_radii2D, grad_accum, denom, radii, viewspace_grad) -> None:
+    P = radii.shape[0]
+    for t, name in ((max_radii2D, "max_radii2D"), (grad_accum, "xyz_gradient_accum"), (denom, "denom")):
+        _check_f32_dense(t, name)
+        if t.numel() != P:
+            raise ValueError(f"{name}: expected {P} entries, got {t.numel()}")
+    _check_f32_dense(viewspace_grad, "viewspace grad")
+    if viewspace_grad.dim() != 2 or viewspace_grad.shape[0] != P or viewspace_grad.shape[1] < 2:
+        raise ValueError(f"viewspace grad: expected [{P}, >=2], got {tuple(viewspace_grad.shape)}")
+    if radii.dtype != torch.int32 or not radii.is_cuda or not radii.is_contiguous():
+        raise TypeError("radii: expected a contiguous int32 device tensor (the rasterizer's output)")
 
 
 def add_densification_stats(gaussians, viewspace_point_tensor: torch.Tensor, radii: torch.Tensor) -> None:

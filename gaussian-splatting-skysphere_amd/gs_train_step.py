@@ -234,9 +234,14 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
         if owner is not None and owner.pending is not None:
             inputs, view = owner.pending
             owner.pending = None
+            stats = None
+            if densify_stats:  # train.py:115-116 in the fused pass (gs_backward_gaussians_adam_stats)
+                if viewspace.grad is None:
+                    raise RuntimeError("train_step: the screen-space carrier has no gradient after backward")
+                stats = (model.max_radii2D, model.xyz_gradient_accum, model.denom, radii, viewspace.grad)
             fused_launch = model.optimizer.prepare_fused_backward(
                 [model._xyz, model._features_dc, model._features_rest, model._opacity, model._scaling,
-                 model._rotation], inputs, view)
+                 model._rotation], inputs, view, stats)
         value = None
         if early is not None and fused_launch is not None:
             # train.py:99 (loss.item()) before :127 (optimizer.step()): the fused backward + Adam is
@@ -256,8 +261,6 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
             commit()
             fused_launch = None
             with torch.no_grad():
-                if densify_stats:
-                    gs_train.add_densification_stats(model, viewspace, radii)
                 model.optimizer.zero_grad(set_to_none=True)
             return value
         if loss_item:
@@ -270,11 +273,10 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
                 bounded_status()
         with torch.no_grad():
             if fused_launch is not None:
-                # the fused backward + Adam first: the statistics (train.py:115-116) read only the
-                # screen-space gradient and the radii, which it does not touch, and the device gets
-                # its longest kernel right after the loss.item() sync
+                # the fused backward + Adam, with the statistics (train.py:115-116) in its pass: they
+                # read only the screen-space gradient and the radii, which the update does not touch
                 fused_launch()
-            if densify_stats:
+            elif densify_stats:
                 if fused:
                     gs_train.add_densification_stats(model, viewspace, radii)
                 else:

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 15  /* v15: gs_backward_gaussians_adam (v14: gs_forward_counted + gs_binning_layout_count) */
+#define GSRAST_ABI_VERSION 16  /* v16: gs_backward_gaussians_adam_stats (v15: gs_backward_gaussians_adam; v14: gs_forward_counted + gs_binning_layout_count) */
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -428,6 +428,23 @@ int gs_backward_gaussians_adam(int P, int D, int M, const float* means3D, const 
                                float* const* exp_avg_sq_host, const double* lr_host, const long long* step_host,
                                const double* weight_decay_host, double beta1, double beta2, double eps, int maximize,
                                int debug, void* stream);
+
+/* gs_backward_gaussians_adam_stats (ABI v16): gs_backward_gaussians_adam plus the view's
+ * densification statistics (train.py:115-116, gaussian_model.py:405-407, i.e. gs_densify_stats) in
+ * the same pass: for every i with radii[i] > 0, max_radii2D[i] = max(max_radii2D[i], radii[i]),
+ * grad_accum[i] += |grad2d[i * grad_stride + 0..1]|, denom[i] += 1 -- the same floats as
+ * gs_densify_stats.  grad2d is the view's dL/dmeans2D (its gs_backward_render output, grad_stride
+ * >= 2 floats per row), radii the forward's.  The five stats pointers are all given or all NULL (NULL:
+ * exactly gs_backward_gaussians_adam).  A view whose forward recorded an error updates neither its
+ * parameters nor its statistics. */
+int gs_backward_gaussians_adam_stats(int P, int D, int M, const float* means3D, const float* shs_dc,
+                                     const float* shs_rest, const float* scales, float scale_modifier,
+                                     const float* rotations, const gs_view_grad* view, float* const* params_host,
+                                     float* const* exp_avg_host, float* const* exp_avg_sq_host, const double* lr_host,
+                                     const long long* step_host, const double* weight_decay_host, double beta1,
+                                     double beta2, double eps, int maximize, const int* radii, const float* grad2d,
+                                     int grad_stride, float* max_radii2D, float* grad_accum, float* denom, int debug,
+                                     void* stream);
 
 /* ---- render() inputs from GaussianModel's raw parameters  <-  get_features / get_opacity /
  *      get_scaling / get_rotation (/root/reference/scene/gaussian_model.py:95-115, read at

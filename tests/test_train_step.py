@@ -302,6 +302,8 @@ def test_fused_adam_train_step_bitwise_equal_unfused(device, active_degree, monk
             def refuse(*a, **k):
                 raise AssertionError("fused step fell back to step_activated")
             monkeypatch.setattr(gs_train.FusedAdam, "step_activated", refuse)
+            # ... nor run the statistics as their own launch (they are in the fused pass, ABI 16)
+            monkeypatch.setattr(gs_train, "densify_stats", refuse)
         losses = [ts.train_step(m, settings, gt, loss_item=True, fuse_adam=fuse) for _ in range(3)]
         torch.cuda.synchronize()
         monkeypatch.undo()
@@ -317,6 +319,27 @@ def test_fused_adam_train_step_bitwise_equal_unfused(device, active_degree, monk
     assert mb.denom.sum() > 0
     for name in ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"):
         assert getattr(mb, name).grad is None, name
+
+
+@pytest.mark.parametrize("loss_item", [True, False])
+def test_fused_adam_train_step_without_stats_leaves_them(device, loss_item):
+    """train_step(fuse_adam=True, densify_stats=False) (past densify_until_iter): the fused pass
+    updates the parameters as with statistics and leaves max_radii2D / xyz_gradient_accum / denom
+    untouched; with statistics, denom counts the visible Gaussians (radii > 0) of each step."""
+    import gs_train_step as ts
+
+    sc, settings, gt = _setup(device)
+    ma, mb = ts.TrainModel(sc, device, fused=True), ts.TrainModel(sc, device, fused=True)
+    for _ in range(2):
+        ts.train_step(ma, settings, gt, loss_item=loss_item, fuse_adam=True, densify_stats=False)
+        ts.train_step(mb, settings, gt, loss_item=loss_item, fuse_adam=True, densify_stats=True)
+    torch.cuda.synchronize()
+    for t in (ma.max_radii2D, ma.xyz_gradient_accum, ma.denom):
+        assert int(torch.count_nonzero(t)) == 0
+    for a, b in zip(_state(ma), _state(mb)):
+        assert torch.equal(a, b)
+    assert mb.denom.sum() > 0 and float(mb.denom.max()) <= 2.0
+    assert torch.equal(mb.denom.reshape(-1) > 0, mb.max_radii2D.reshape(-1) > 0)
 
 
 def test_fused_adam_train_step_releases_its_sinks(device):
