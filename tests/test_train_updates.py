@@ -51,7 +51,23 @@ def test_adam_abi_validation_without_gpu():
     rc = lib.gs_densify_stats(5, None, None, 1, None, None, None, None)
     assert rc != 0 and "grad_stride" in _native.last_error()
     assert lib.gs_densify_stats(0, None, None, 3, None, None, None, None) == 0
-    del ctypes
+    # the fused step's statistics (ABI 16): all five pointers or none, checked before any launch
+    # (the other arguments are placeholders that are only range-checked on the host here)
+    fake = [ctypes.c_void_p(0x10000 * (k + 1)) for k in range(6)]
+    arr = lambda: ctypes.cast((ctypes.c_void_p * 6)(*fake), ctypes.c_void_p)  # noqa: E731
+    steps = ctypes.cast((ctypes.c_longlong * 6)(*[1] * 6), ctypes.c_void_p)
+    lrs = ctypes.cast((ctypes.c_double * 6)(*[1e-3] * 6), ctypes.c_void_p)
+    vg = _native.ViewGrad(0x1000, 0x2000, 0x3000, 0.5, 0.5, 8, 8, 0x4000)
+    base = [5, 3, 16, fake[0], fake[1], fake[2], ctypes.c_void_p(0x9000), 1.0, ctypes.c_void_p(0xA000),
+            ctypes.byref(vg), arr(), arr(), arr(), lrs, steps, None, 0.9, 0.999, 1e-15, 0]
+    some = [ctypes.c_void_p(0xB000), None, 2, None, None, None]
+    assert lib.gs_backward_gaussians_adam_stats(*base, *some, 0, None) != 0
+    assert "all five pointers or none" in _native.last_error()
+    every = [ctypes.c_void_p(0xB000 + 0x100 * k) for k in range(6)]
+    every[2] = 1
+    assert lib.gs_backward_gaussians_adam_stats(*base, *every, 0, None) != 0
+    assert "grad_stride" in _native.last_error()
+    assert lib.gs_backward_gaussians_adam_stats(0, *base[1:], *some, 0, None) == 0  # P == 0: nothing to do
 
 
 def _make_params(device, sizes, seed=0):
