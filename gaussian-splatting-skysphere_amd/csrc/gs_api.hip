@@ -215,6 +215,21 @@ bool exact_exp() {
 namespace gs {
 static std::atomic<uint32_t> g_spin_limit{LB_SPIN_LIMIT};
 uint32_t scan_spin_limit() { return g_spin_limit.load(std::memory_order_relaxed); }
+
+// row waits installed by gs_set_row_waits, per host thread, until the next forward preprocess
+static thread_local RowWait t_row_waits[GS_MAX_ROW_WAITS];
+static thread_local int t_row_wait_count = 0;
+int take_row_waits(RowWait* out, int max) {
+  const int n = t_row_wait_count < max ? t_row_wait_count : max;
+  for (int k = 0; k < n; k++) out[k] = t_row_waits[k];
+  t_row_wait_count = 0;
+  return n;
+}
+bool stream_wait(hipStream_t st, hipEvent_t ev) {
+  const hipError_t e = hipStreamWaitEvent(st, ev, 0);
+  if (e != hipSuccess) set_error("row wait: hipStreamWaitEvent failed: %s", hipGetErrorString(e));
+  return e == hipSuccess;
+}
 uint32_t next_scan_epoch() {
   static std::atomic<uint32_t> e{0};
   return (e.fetch_add(1, std::memory_order_relaxed) % ((1u << 30) - 1u)) + 1u;
@@ -927,6 +942,33 @@ int gs_bounded_status(unsigned* flags, long long* instances) {
   if (flags) *flags = f;
   if (instances) *instances = inst;
   return bounded_status_error(f, inst) ? 1 : 0;
+}
+
+size_t gs_geom_flags_offset(int P) {
+  // the layout's offsets from a dummy base address (nothing is dereferenced)
+  alignas(256) static char base[256];
+  GeomPtrs geo;
+  geom_layout((size_t)(P > 0 ? P : 1), &geo, base);
+  return (size_t)((uintptr_t)geo.counters - (uintptr_t)base) + CNT_ERR * sizeof(uint32_t);
+}
+
+int gs_forward_order_status(void) {
+  clear_error(0);
+  return check_order_flags(true) ? 1 : 0;
+}
+
+int gs_set_row_waits(int n, const int* bounds, void* const* events) {
+  clear_error(0);
+  t_row_wait_count = 0;
+  if (n == 0) return 0;
+  if (n < 0 || n > GS_MAX_ROW_WAITS) return set_error("row waits: 0..%d chunks (got %d)", GS_MAX_ROW_WAITS, n), 1;
+  if (!bounds || !events) return set_error("row waits: missing bounds / events"), 1;
+  if (bounds[0] != 0) return set_error("row waits: the first chunk must start at row 0"), 1;
+  for (int k = 0; k < n; k++)
+    if (bounds[k + 1] <= bounds[k]) return set_error("row waits: chunk bounds must increase"), 1;
+  for (int k = 0; k < n; k++) t_row_waits[k] = RowWait{bounds[k + 1], (hipEvent_t)events[k]};
+  t_row_wait_count = n;
+  return 0;
 }
 
 long long gs_rasterize_forward(int P, int D, int M, const float* background, int W, int H, const float* means3D,

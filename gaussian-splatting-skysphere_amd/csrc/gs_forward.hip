@@ -176,7 +176,7 @@ __device__ __forceinline__ uint32_t preprocess_one(int i, const GaussianArgs& g,
 
 // The workgroup's tile total and count of Gaussians with instances (+ a prefiltered cull) -> its
 // WgTotals slot; the first depth-sort histogram launch sums the slots (CounterFinalize).
-__device__ __forceinline__ void workgroup_totals(uint32_t area, bool culled, WgTotals* wg) {
+__device__ __forceinline__ void workgroup_totals(uint32_t area, bool culled, WgTotals* wg, uint32_t b) {
   __shared__ uint32_t s_sum[4], s_vis[4];
   uint32_t vis = area ? 1u : 0u;
   const uint64_t cm = __ballot(culled);
@@ -195,7 +195,7 @@ __device__ __forceinline__ void workgroup_totals(uint32_t area, bool culled, WgT
     const uint32_t v4 = s_vis[0] | s_vis[1] | s_vis[2] | s_vis[3];
     const uint32_t nv = (s_vis[0] & 0x7FFFFFFFu) + (s_vis[1] & 0x7FFFFFFFu) + (s_vis[2] & 0x7FFFFFFFu) +
                         (s_vis[3] & 0x7FFFFFFFu);
-    store_wg_totals(wg, nv, tot, (v4 >> 31) != 0);
+    store_wg_totals(wg, b, nv, tot, (v4 >> 31) != 0);
   }
 }
 
@@ -210,14 +210,14 @@ __global__ __launch_bounds__(256) void k_preprocess(GaussianArgs g, CameraArgs c
                                                     uint32_t* __restrict__ depth_key,
                                                     uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
                                                     WgTotals* __restrict__ wg) {
-  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  const int b = (int)blockIdx.x + g.blk0, i = b * 256 + (int)threadIdx.x;
   uint32_t area = 0, dbits = 0;
   bool culled = false;
   if (i < g.P) {
     area = preprocess_one<DEG>(i, g, c, radii, splat, binrec, dbits, tiles, clamped, culled);
     depth_key[i] = area ? dbits : DEPTH_DROP;
   }
-  workgroup_totals(area, culled, wg);
+  workgroup_totals(area, culled, wg, (uint32_t)b);
 }
 
 // The split-SH preprocess: k_preprocess's body with the split row loader (preprocess_one SPLIT).
@@ -226,18 +226,51 @@ __global__ __launch_bounds__(256) void k_preprocess_split(
     GaussianArgs g, CameraArgs c, int* __restrict__ radii, float4* __restrict__ splat, float4* __restrict__ binrec,
     uint32_t* __restrict__ depth_key, uint32_t* __restrict__ tiles, uint8_t* __restrict__ clamped,
     WgTotals* __restrict__ wg) {
-  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  const int b = (int)blockIdx.x + g.blk0, i = b * 256 + (int)threadIdx.x;
   uint32_t area = 0, dbits = 0;
   bool culled = false;
   if (i < g.P) {
     area = preprocess_one<DEG, true>(i, g, c, radii, splat, binrec, dbits, tiles, clamped, culled);
     depth_key[i] = area ? dbits : DEPTH_DROP;
   }
-  workgroup_totals(area, culled, wg);
+  workgroup_totals(area, culled, wg, (uint32_t)b);
 }
 
-void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st) {
-  dim3 grid((g.P + 255) / 256), block(256);
+// The preprocess grid, launched whole or -- with row waits installed on this thread
+// (gs_set_row_waits) -- in row chunks: before chunk k the stream waits for event k, and chunk k
+// launches the workgroups whose last row lies below its end, so every row a workgroup reads is
+// behind all the waits of the chunks it spans (e.g. the all-gather of a sharded optimizer step's
+// row chunk, gs_view_parallel.ShardedAdam).  Same workgroups, same outputs as one launch.
+template <class Launch>
+static void launch_row_chunks(const GaussianArgs& g, hipStream_t st, Launch&& launch) {
+  const int nb = (g.P + 255) / 256;
+  RowWait w[GS_MAX_ROW_WAITS];
+  const int n = take_row_waits(w, GS_MAX_ROW_WAITS);
+  int b0 = 0;
+  for (int k = 0; k < n && b0 < nb; k++) {
+    if (w[k].ev && !stream_wait(st, w[k].ev)) return;
+    const int b1 = w[k].hi >= g.P ? nb : w[k].hi / 256;
+    if (b1 > b0) {
+      GaussianArgs gc = g;
+      gc.blk0 = b0;
+      launch(gc, dim3(b1 - b0));
+      b0 = b1;
+    }
+  }
+  if (b0 < nb) {
+    GaussianArgs gc = g;
+    gc.blk0 = b0;
+    launch(gc, dim3(nb - b0));
+  }
+}
+
+void fwd_preprocess(const GaussianArgs& g0, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st) {
+  launch_row_chunks(g0, st, [&](const GaussianArgs& g, dim3 grid) { fwd_preprocess_grid(g, c, radii, geo, st, grid); });
+}
+
+void fwd_preprocess_grid(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st,
+                         dim3 grid) {
+  const dim3 block(256);
   if (g.colors) {
     GS_LAUNCH("preprocess", k_preprocess<-1>, grid, block, 0, st, g, c, radii, geo.splat, geo.binrec, geo.keys_a, geo.tiles,
               geo.clamped, geo.wg_tot);
@@ -282,7 +315,7 @@ void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, cons
 // per-view workgroup totals go to each view's WgTotals slots as in k_preprocess.
 template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess_views(GaussianArgs g, PreViews pv) {
-  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  const int b = (int)blockIdx.x + g.blk0, i = b * 256 + (int)threadIdx.x;
   for (int v = 0; v < pv.K; v++) {
     const GeomPtrs& geo = pv.geo[v];
     uint32_t area = 0, dbits = 0;
@@ -292,23 +325,25 @@ __global__ __launch_bounds__(256) void k_preprocess_views(GaussianArgs g, PreVie
                                  culled);
       geo.keys_a[i] = area ? dbits : DEPTH_DROP;
     }
-    workgroup_totals(area, culled, geo.wg_tot);
+    workgroup_totals(area, culled, geo.wg_tot, (uint32_t)b);
     lds_barrier();  // workgroup_totals' LDS is reused by the next view
   }
 }
 
-void fwd_preprocess_views(const GaussianArgs& g, const PreViews& pv, hipStream_t st) {
-  dim3 grid((g.P + 255) / 256), block(256);
-  if (g.colors) {
-    GS_LAUNCH("preprocess_views", k_preprocess_views<-1>, grid, block, 0, st, g, pv);
-    return;
-  }
-  switch (g.D) {
-    case 0: GS_LAUNCH("preprocess_views", k_preprocess_views<0>, grid, block, 0, st, g, pv); break;
-    case 1: GS_LAUNCH("preprocess_views", k_preprocess_views<1>, grid, block, 0, st, g, pv); break;
-    case 2: GS_LAUNCH("preprocess_views", k_preprocess_views<2>, grid, block, 0, st, g, pv); break;
-    default: GS_LAUNCH("preprocess_views", k_preprocess_views<3>, grid, block, 0, st, g, pv); break;
-  }
+void fwd_preprocess_views(const GaussianArgs& g0, const PreViews& pv, hipStream_t st) {
+  launch_row_chunks(g0, st, [&](const GaussianArgs& g, dim3 grid) {
+    const dim3 block(256);
+    if (g.colors) {
+      GS_LAUNCH("preprocess_views", k_preprocess_views<-1>, grid, block, 0, st, g, pv);
+      return;
+    }
+    switch (g.D) {
+      case 0: GS_LAUNCH("preprocess_views", k_preprocess_views<0>, grid, block, 0, st, g, pv); break;
+      case 1: GS_LAUNCH("preprocess_views", k_preprocess_views<1>, grid, block, 0, st, g, pv); break;
+      case 2: GS_LAUNCH("preprocess_views", k_preprocess_views<2>, grid, block, 0, st, g, pv); break;
+      default: GS_LAUNCH("preprocess_views", k_preprocess_views<3>, grid, block, 0, st, g, pv); break;
+    }
+  });
 }
 
 // ------------------------------------------------------------------------------------------

@@ -58,6 +58,10 @@ struct GaussianArgs {
   // features_dc [P, 1, 3] and this is features_rest [P, M - 1, 3] (GaussianModel's own tensors,
   // no concatenated copy); only the single-view preprocess and preprocess backward read it
   const float* shs_rest = nullptr;
+  // first workgroup of a launch that covers only part of the rows (the forward preprocess launched
+  // in row chunks behind row waits, gs_set_row_waits): workgroup blockIdx.x + blk0 owns rows
+  // [256 (blockIdx.x + blk0), +256); 0 for every whole-grid launch
+  int blk0 = 0;
 };
 
 // a 12-B row piece loaded with one global_load_dwordx3 (4-B alignment is enough)
@@ -177,8 +181,9 @@ struct WgTotals {
   uint32_t inst;  // tiles touched by the workgroup's Gaussians (<= 256 x tiles of the image)
   uint32_t vis;   // Gaussians with instances | ERR_PREFILTERED << 31
 };
-__device__ __forceinline__ void store_wg_totals(WgTotals* wg, uint32_t nv, uint32_t tot, bool culled_prefiltered) {
-  wg[blockIdx.x] = WgTotals{tot, nv | (culled_prefiltered ? 0x80000000u : 0u)};
+__device__ __forceinline__ void store_wg_totals(WgTotals* wg, uint32_t b, uint32_t nv, uint32_t tot,
+                                                bool culled_prefiltered) {
+  wg[b] = WgTotals{tot, nv | (culled_prefiltered ? 0x80000000u : 0u)};
 }
 
 struct GeomPtrs {
@@ -412,6 +417,19 @@ __device__ __forceinline__ void timing_record(unsigned long long (*buf)[5], unsi
 
 // ---- stages (gs_forward.hip / gs_backward.hip) ----
 void fwd_preprocess(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st);
+void fwd_preprocess_grid(const GaussianArgs& g, const CameraArgs& c, int* radii, const GeomPtrs& geo, hipStream_t st,
+                         dim3 grid);
+// Row waits of this thread (gs_set_row_waits): chunk k covers the rows below `hi` not covered by an
+// earlier chunk and must wait for `ev` (null: nothing to wait for).  take_row_waits() moves them out
+// (the next forward preprocess consumes them); stream_wait() is hipStreamWaitEvent with the error
+// captured (gs_last_error).
+constexpr int GS_MAX_ROW_WAITS = 64;
+struct RowWait {
+  int hi;
+  hipEvent_t ev;
+};
+int take_row_waits(RowWait* out, int max);
+bool stream_wait(hipStream_t st, hipEvent_t ev);
 // compaction, depth sort, instance offsets; the view's totals are finalised by the first histogram
 // launch (written to host_counts when given: [I lo, I hi, V, err]), after which counts_ready is recorded.
 // cap: the binning buffer's instance capacity (more instances: ERR_CAPACITY); sticky (pinned host

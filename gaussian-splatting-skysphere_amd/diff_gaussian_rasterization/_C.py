@@ -211,6 +211,58 @@ def bounded_status():
     return int(flags.value), int(inst.value)
 
 
+# forward error flags (include/gsrast.h; gs_internal.h ERR_*): a view with ERR_INVALID set is skipped
+# by the backward's record sums and by the fused backward + Adam
+ERR_PREFILTERED, ERR_LOOKBACK, ERR_INSTANCES, ERR_CAPACITY = 1, 4, 8, 16
+ERR_INVALID = ERR_LOOKBACK | ERR_CAPACITY
+
+
+def view_flags_word(geom_buffer: torch.Tensor, P: int) -> torch.Tensor:
+    """The int32 word of a view's geometry buffer that holds its forward error flags
+    (gs_geom_flags_offset, ABI v17), as a one-element device tensor view: copy it out behind the
+    forward (non_blocking into pinned memory) to read the view's status at a later sync."""
+    off = int(_lib.gs_geom_flags_offset(int(P)))
+    if geom_buffer.dtype != torch.uint8 or geom_buffer.numel() < off + 4:
+        raise ValueError("view_flags_word: not a geometry buffer of this P")
+    return geom_buffer[off:off + 4].view(torch.int32)
+
+
+class row_waits:
+    """Context manager (extension, ABI v17 gs_set_row_waits): the next forward preprocess on this
+    thread inside the block launches in Gaussian-row chunks, each behind a stream wait on its
+    chunk's event.  waits: [(lo, hi, torch.cuda.Event or None)] covering [0, P) in order.  The
+    waits are cleared on exit whether or not a preprocess consumed them."""
+
+    def __init__(self, waits):
+        self.waits = list(waits or [])
+
+    def __enter__(self):
+        w = self.waits
+        if not w:
+            return self
+        if w[0][0] != 0 or any(w[k][1] != w[k + 1][0] for k in range(len(w) - 1)):
+            raise ValueError("row_waits: chunks must be contiguous from row 0")
+        bounds = (ctypes.c_int * (len(w) + 1))(*([w[0][0]] + [hi for _, hi, _ in w]))
+        evs = (ctypes.c_void_p * len(w))(*[e.cuda_event if e is not None else None for _, _, e in w])
+        self._keep = (bounds, evs)
+        _native.check(_lib.gs_set_row_waits(len(w), ctypes.cast(bounds, ctypes.c_void_p),
+                                            ctypes.cast(evs, ctypes.c_void_p)), "row waits")
+        return self
+
+    def __exit__(self, *exc):
+        if self.waits:
+            _lib.gs_set_row_waits(0, None, None)
+        return False
+
+
+def forward_order_status() -> None:
+    """Take the ordering flags of every queued read-back forward on the current device (waits for
+    their renders; gs_forward_order_status, ABI v17).  Raises RuntimeError when a look-back wait of
+    one of them timed out -- that report is then consumed, not repeated by the next call."""
+    if _lib.gs_forward_order_status() != 0:
+        raise RuntimeError(_native.last_error())
+
+
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
                         prefiltered, debug, prepared=None, sh_rest=None, capacity=None):

@@ -277,6 +277,12 @@ class _RasterizeGaussians(torch.autograd.Function):
                 owner = _sink_owner(inputs[k])
                 if owner is not None:
                     sinks.append((k, name, inputs[k], owner))
+            # an owner that follows its views' forward status (gs_train_step._AdamBackward) gets the
+            # view's geometry buffer now, while its error-flags word can still be copied out
+            # stream-ordered behind this forward
+            for owner in {id(o): o for _k, _n, _t, o in sinks}.values():
+                if hasattr(owner, "forwarded"):
+                    owner.forwarded(geomBuffer, means3D.shape[0])
         ctx.sinks = sinks
         return color, radii
 

@@ -136,6 +136,11 @@ SIGNATURES = {
         [_c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_f, _c_p, ctypes.POINTER(ViewGrad), _c_p, _c_p, _c_p, _c_p, _c_p,
          _c_p, _c_d, _c_d, _c_d, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p],
     ),
+    # ABI v17: a view's forward error-flags word (its offset in the geometry buffer) and the
+    # read-back forwards' ordering status, taken in the caller's own call
+    "gs_geom_flags_offset": (_c_sz, [_c_i]),
+    "gs_forward_order_status": (_c_i, []),
+    "gs_set_row_waits": (_c_i, [_c_i, _c_p, _c_p]),
     "gs_mark_visible": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "gs_knn_scratch_bytes": (_c_sz, [_c_i]),
     "gs_knn_mean_dist2": (_c_i, [_c_i, _c_p, _c_p, _c_p, _c_p]),

@@ -379,9 +379,41 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+_SIDE = {}
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+def row_chunks(P: int, waits):
+    """The row chunks of `waits` ([(lo, hi, event)] contiguous from row 0) at 256-row granularity,
+    as the rasterizer's chunked preprocess launches them (csrc/gs_forward.hip launch_row_chunks):
+    [(lo, hi, event)] where chunk k holds the rows of the 256-row blocks whose last row lies below
+    its end, and must wait for its event and every earlier one."""
+    nb = (P + 255) // 256
+    out, b0 = [], 0
+    for _lo, hi, ev in waits:
+        if b0 >= nb:
+            break
+        b1 = nb if hi >= P else hi // 256
+        if b1 > b0:
+            out.append((256 * b0, min(P, 256 * b1), ev))
+            b0 = b1
+        elif ev is not None:
+            out.append((256 * b0, 256 * b0, ev))  # nothing to launch, but later chunks wait for it too
+    if b0 < nb:
+        out.append((256 * b0, P, None))
+    return out
+
+
 class _Activate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, f_dc, f_rest, opacity_raw, scaling_raw, rotation_raw, with_sh=True):
+    def forward(ctx, f_dc, f_rest, opacity_raw, scaling_raw, rotation_raw, with_sh=True, row_waits=None,
+                waits_out=None):
         P = f_dc.shape[0]
         if f_dc.shape[1:] != (1, 3) or f_rest.dim() != 3 or f_rest.shape[0] != P or f_rest.shape[2] != 3:
             raise ValueError(f"activate: expected features_dc [P,1,3] and features_rest [P,K,3], got "
@@ -399,10 +431,48 @@ class _Activate(torch.autograd.Function):
         opac = torch.empty(tuple(opacity_raw.shape), dtype=torch.float32, device=dev)
         scales = torch.empty((P, 3), dtype=torch.float32, device=dev)
         rots = torch.empty((P, 4), dtype=torch.float32, device=dev)
-        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        with torch.cuda.device(dev):
-            _native.check(_lib.gs_activate_forward(P, 3 * K, _ptr(dc), _ptr(rest), _ptr(o), _ptr(s), _ptr(q),
-                                                   _ptr(shs), _ptr(opac), _ptr(scales), _ptr(rots), st), "activate")
+        if row_waits:
+            # rows become ready chunk by chunk on other streams (a sharded optimizer step's all-gathers):
+            # each chunk is activated on a side stream as soon as its rows are in, and waits_out gets
+            # [(lo, hi, event)] for the rasterizer's chunked preprocess (gs_set_row_waits)
+            cur = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            side.wait_stream(cur)  # the outputs were allocated on the current stream
+            outs = (shs, opac, scales, rots)
+            ins5 = (dc, rest, o, s, q)
+            widths_in = (3, 3 * K, 1, 3, 4)
+            widths_out = (3 * (1 + K), 1, 3, 4)
+            with torch.cuda.device(dev):
+                st = ctypes.c_void_p(side.cuda_stream)
+                for lo, hi, ev in row_chunks(P, row_waits):
+                    if ev is not None:
+                        side.wait_event(ev)
+                    if hi > lo:
+                        pi = [ctypes.c_void_p(t.data_ptr() + 4 * lo * w) for t, w in zip(ins5, widths_in)]
+                        po = [None if t is None else ctypes.c_void_p(t.data_ptr() + 4 * lo * w)
+                              for t, w in zip(outs, widths_out)]
+                        _native.check(_lib.gs_activate_forward(hi - lo, 3 * K, *pi, *po, st), "activate (row chunk)")
+                    done = torch.cuda.Event()
+                    done.record(side)
+                    if waits_out is not None:
+                        waits_out.append((lo, hi, done))
+            for t in outs + ins5:
+                if t is not None:
+                    t.record_stream(side)
+            if waits_out is not None:  # the rasterizer's chunks must be contiguous: merge empty ones
+                merged = []
+                for lo, hi, e in waits_out:
+                    if merged and merged[-1][1] == merged[-1][0]:
+                        merged[-1] = (merged[-1][0], hi, e)
+                    else:
+                        merged.append((lo, hi, e))
+                waits_out[:] = merged
+        else:
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            with torch.cuda.device(dev):
+                _native.check(_lib.gs_activate_forward(P, 3 * K, _ptr(dc), _ptr(rest), _ptr(o), _ptr(s), _ptr(q),
+                                                       _ptr(shs), _ptr(opac), _ptr(scales), _ptr(rots), st),
+                              "activate")
         ctx.P, ctx.K = P, K
         ctx.shapes = (tuple(f_dc.shape), tuple(f_rest.shape), tuple(opacity_raw.shape))
         ctx.set_materialize_grads(False)
@@ -431,7 +501,7 @@ class _Activate(torch.autograd.Function):
                                                         _ptr(drots), _ptr(opac), _ptr(scales), _ptr(q), _ptr(g_dc),
                                                         _ptr(g_rest), _ptr(g_o), _ptr(g_s), _ptr(g_q), st),
                               "activate backward")
-        return g_dc, g_rest, g_o, g_s, g_q
+        return g_dc, g_rest, g_o, g_s, g_q, None, None, None
 
 
 def activate_values(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw, with_sh=True):
@@ -453,16 +523,21 @@ class _NoCtx:
         pass
 
 
-def activate(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw):
+def activate(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw, row_waits=None, waits_out=None):
     """(shs, opacity, scales, rotations) = (cat(dc, rest, 1), sigmoid(o), exp(s), normalize(q)),
-    differentiable; one HIP launch each way (csrc/gs_train.hip k_activate_fwd / k_activate_bwd)."""
-    return _Activate.apply(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw)
+    differentiable; one HIP launch each way (csrc/gs_train.hip k_activate_fwd / k_activate_bwd).
+    row_waits ([(lo, hi, event)] contiguous from row 0): the raw rows become ready chunk by chunk
+    on other streams; each chunk is activated on a side stream once its event fires, and waits_out
+    (a list) receives the chunks' completion events for the rasterizer (row_chunks, _C.row_waits)."""
+    return _Activate.apply(features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw, True, row_waits,
+                           waits_out)
 
 
-def render_inputs(pc):
+def render_inputs(pc, row_waits=None, waits_out=None):
     """The tensors gaussian_renderer.render() reads from a GaussianModel (__init__.py:53-80):
-    (means3D, shs, opacity, scales, rotations)."""
-    shs, opac, scales, rots = activate(pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation)
+    (means3D, shs, opacity, scales, rotations).  row_waits / waits_out: as activate()."""
+    shs, opac, scales, rots = activate(pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation,
+                                       row_waits, waits_out)
     return pc._xyz, shs, opac, scales, rots
 
 
@@ -485,6 +560,12 @@ def densify_and_prune(gaussians, max_grad, min_opacity, extent, max_screen_size,
     the replicas stay bit-identical (their parameters, moments and reduced statistics already are).
     A gs_view_parallel.GradBucket that holds the replaced parameters' gradients is rebound to the new
     parameters."""
+    sharded = getattr(gaussians.optimizer, "_gs_sharded_moments", None)
+    if sharded is not None and sharded.moments_sharded():
+        raise RuntimeError("densify_and_prune: the Adam moments are sharded over the ranks (gs_view_parallel."
+                           "ShardedAdam); call its gather_state() first")
+    if sharded is not None:
+        sharded.sync()  # an overlapped step's all-gathers, before the parameters are read here
     params = [getattr(gaussians, a) for a in _DENS_ATTRS]
     xyz = params[0]
     P = xyz.shape[0]

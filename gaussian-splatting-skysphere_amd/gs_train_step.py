@@ -29,7 +29,7 @@ import torch
 
 import gs_loss
 import gs_train
-from diff_gaussian_rasterization import GaussianRasterizer, bounded_status, register_gradient_sink, \
+from diff_gaussian_rasterization import GaussianRasterizer, _C, bounded_status, register_gradient_sink, \
     unregister_gradient_sink
 
 # OptimizationParams defaults (/root/reference/arguments/__init__.py:74-83)
@@ -101,7 +101,7 @@ class _AdamBackward:
     accepts_sh_split = True
 
     def __init__(self):
-        self.tensors, self.pending = [], None
+        self.tensors, self.pending, self.geom = [], None, None
 
     def arm(self, tensors):
         for t in tensors:
@@ -111,7 +111,14 @@ class _AdamBackward:
     def disarm(self):
         for t in self.tensors:
             unregister_gradient_sink(t)
-        self.tensors, self.pending = [], None
+        self.tensors, self.pending, self.geom = [], None, None
+
+    def forwarded(self, geom, P):
+        """The step's forward (diff_gaussian_rasterization calls this after it): its geometry buffer,
+        whose error-flags word train_step copies out behind the loss."""
+        if self.geom is not None:
+            raise RuntimeError("train_step(fuse_adam=True): more than one rasterizer forward in one step")
+        self.geom = (geom, P)
 
     def claim(self, t):
         return None  # not deferred (a backward that needs another input's gradient): plain autograd
@@ -123,13 +130,19 @@ class _AdamBackward:
 
 
 def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | None = None, split_sh: bool = True,
-           binning_capacity: int | None = None, sink_owner=None):
+           binning_capacity: int | None = None, sink_owner=None, row_waits=None):
     """gaussian_renderer.render() for the default pipe (SH and covariance in the rasterizer).
     act_leaves (a list): the activated inputs are made autograd leaves (their adjoint then runs in
     FusedAdam.step_activated) and appended to it as (shs, opacity, scales, rotations).
     binning_capacity: a bounded forward (no host wait; HIP-graph capturable), see train_step.
-    sink_owner: armed on xyz and the activated leaves before the rasterizer call (_AdamBackward)."""
+    sink_owner: armed on xyz and the activated leaves before the rasterizer call (_AdamBackward).
+    row_waits (fused=True, the autograd activation; [(lo, hi, event)] from row 0): the parameters'
+    rows become ready chunk by chunk on other streams (ShardedAdam's all-gathers of the previous
+    step); the activation and the rasterizer's preprocess run chunk by chunk behind them."""
+    if row_waits and (act_leaves is not None or not fused):
+        raise ValueError("render: row_waits apply to the fused autograd activation only")
     sh_split = None
+    act_waits = []
     if act_leaves is not None and not split_sh:
         acts = gs_train.activate_values(model._features_dc, model._features_rest, model._opacity, model._scaling,
                                         model._rotation)
@@ -152,7 +165,7 @@ def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | N
         act_leaves.extend(acts)
         means3D = model._xyz
     elif fused:
-        means3D, shs, opacity, scales, rotations = gs_train.render_inputs(model)
+        means3D, shs, opacity, scales, rotations = gs_train.render_inputs(model, row_waits, act_waits)
     else:
         means3D, shs, opacity, scales, rotations = model.torch_render_inputs()
     if sink_owner is not None:
@@ -160,9 +173,13 @@ def render(model: TrainModel, settings, fused: bool = True, act_leaves: list | N
     # __init__.py:26 (zeros_like(...) + 0, then retain_grad): the screen-space gradient carrier as a
     # leaf; the rasterizer never reads its values (only its .grad is written), so no fill launch
     screenspace_points = torch.empty_like(means3D, requires_grad=True)
-    image, radii = GaussianRasterizer(raster_settings=settings)(
-        means3D=means3D, means2D=screenspace_points, shs=shs, colors_precomp=None, opacities=opacity, scales=scales,
-        rotations=rotations, cov3D_precomp=None, sh_split=sh_split, binning_capacity=binning_capacity)
+    with _C.row_waits(act_waits):
+        image, radii = GaussianRasterizer(raster_settings=settings)(
+            means3D=means3D, means2D=screenspace_points, shs=shs, colors_precomp=None, opacities=opacity,
+            scales=scales, rotations=rotations, cov3D_precomp=None, sh_split=sh_split,
+            binning_capacity=binning_capacity)
+    if act_waits:  # (the preprocess waited for every chunk; anything after it on this stream sees all rows)
+        torch.cuda.current_stream(means3D.device).wait_event(act_waits[-1][2])
     return image, screenspace_points, radii
 
 
@@ -176,15 +193,16 @@ def _torch_densification_stats(model: TrainModel, viewspace, radii):
 _PINNED = threading.local()
 
 
-def _pinned_scalar(device):
-    """A pinned host float32 scalar per thread and device (the fused step's early loss read-back;
-    per thread: two threads' steps must not share the copy target)."""
+def _pinned_words(device):
+    """Two pinned host words per thread and device: the fused step's early read-back of the loss
+    (float32, word 0) and of the view's forward error flags (int32, word 1); per thread: two
+    threads' steps must not share the copy target."""
     cache = getattr(_PINNED, "bufs", None)
     if cache is None:
         cache = _PINNED.bufs = {}
     b = cache.get(device)
     if b is None:
-        b = cache[device] = torch.empty((), dtype=torch.float32, pin_memory=True)
+        b = cache[device] = torch.zeros((2,), dtype=torch.int32, pin_memory=True)
     return b
 
 
@@ -221,12 +239,13 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
             Ll1 = gs_loss.l1_loss(image, gt_image)
             loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - gs_loss.ssim(image, gt_image))
         early = None
-        if loss_item and owner is not None:
-            # fused Adam: the loss value is copied out right after the loss kernel and read through an
-            # event, so the host's sync does not wait for the backward and the optimizer step queued
-            # behind it (below)
-            buf = _pinned_scalar(loss.device)
-            buf.copy_(loss.detach().reshape(()), non_blocking=True)
+        if loss_item and owner is not None and owner.geom is not None:
+            # fused Adam: the loss value and the view's forward error flags are copied out right after
+            # the loss kernel and read through an event, so the host's sync does not wait for the
+            # backward and the optimizer step queued behind it (below)
+            buf = _pinned_words(loss.device)
+            buf[0:1].view(torch.float32).copy_(loss.detach().reshape(1), non_blocking=True)
+            buf[1:2].copy_(_C.view_flags_word(*owner.geom), non_blocking=True)
             early = (buf, torch.cuda.Event())
             early[1].record()
         loss.backward()
@@ -247,19 +266,27 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
             # train.py:99 (loss.item()) before :127 (optimizer.step()): the fused backward + Adam is
             # launched BEFORE the host reads the loss and the forward's status, with its step counts
             # committed only after that check -- the kernel skips the update of a view whose forward
-            # recorded an error, so an overflowing bounded iteration raises here with parameters,
-            # moments, step counts and statistics untouched, as the reference order guarantees.
-            # (A read-back forward raises its own errors in its call, except a look-back timeout of
-            # its sorts -- never observed -- which the next call raises: that step's update is then
-            # skipped while its step counts advance.)
+            # recorded an error (a nonzero flags word), and the host decides from the same
+            # word, copied out behind the loss: an invalid view (an overflowing bounded forward, or a
+            # look-back timeout in any forward's sorts) raises here with parameters, moments, step
+            # counts and statistics untouched, as the reference order guarantees
             with torch.no_grad():
                 commit = fused_launch(defer_commit=True)
             early[1].synchronize()
-            value = float(early[0].item())
-            if binning_capacity is not None:
-                bounded_status()
+            value = float(early[0][0:1].view(torch.float32).item())
+            vflags = int(early[0][1])
+            if vflags != 0:
+                # the kernel skips on any flag, so no step count moves.  The device-wide reports name the
+                # cause (and are consumed, so the next call does not raise them again)
+                if binning_capacity is not None:
+                    bounded_status()
+                _C.forward_order_status()
+                raise RuntimeError(f"train_step: the view's forward recorded error flags {vflags:#x} (its instance "
+                                   "list is invalid); the optimizer step was skipped")
             commit()
             fused_launch = None
+            if binning_capacity is not None:
+                bounded_status()  # earlier bounded forwards' flags (this view's update stands)
             with torch.no_grad():
                 model.optimizer.zero_grad(set_to_none=True)
             return value
@@ -269,8 +296,16 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
             # raises now, before any parameter, moment or statistic is updated from its invalid
             # gradients
             value = loss.item()
-            if binning_capacity is not None:
-                bounded_status()
+            try:
+                if binning_capacity is not None:
+                    bounded_status()
+                # a look-back timeout in this forward's sorts (read-back forwards report it at the next
+                # rasterizer call): taken now, past the sync, before the optimizer uses the gradients
+                _C.forward_order_status()
+            except RuntimeError:
+                with torch.no_grad():  # the invalid gradients must not reach the next iteration either
+                    model.optimizer.zero_grad(set_to_none=True)
+                raise
         with torch.no_grad():
             if fused_launch is not None:
                 # the fused backward + Adam, with the statistics (train.py:115-116) in its pass: they
@@ -308,13 +343,19 @@ def train_step_views(model: TrainModel, bucket, views, lambda_dssim: float = LAM
     so the replicas stay bit-identical.  Densification statistics stay per rank until
     gs_view_parallel.reduce_densify_stats at densify time.  sharded (a gs_view_parallel.ShardedAdam
     over the bucket and model.optimizer): reduce-scatter -> sharded Adam -> all-gather in place of the
-    all-reduce and the replicated step (call its gather_state() before densify).  Returns the rank's
-    losses."""
+    all-reduce and the replicated step (call its gather_state() before densify).  With
+    ShardedAdam(overlap=True) the previous step's all-gathers are still in flight when this step
+    starts: the first view's activation and preprocess wait for them row chunk by row chunk
+    (take_row_waits, render(row_waits=...)), and every backward waits for the collective stream's
+    zero-fill of the bucket (GradBucket.before_backward).  Returns the rank's losses."""
+    waits = sharded.take_row_waits() if sharded is not None else []
     bucket.zero_grad()
     losses = []
     for settings, gt in views:
-        image, viewspace, radii = render(model, settings, fused=True)
+        image, viewspace, radii = render(model, settings, fused=True, row_waits=waits)
+        waits = []  # (the first view's preprocess waited for every chunk)
         loss, _ = gs_loss.photometric_loss(image, gt, lambda_dssim)
+        bucket.before_backward()
         loss.backward()
         if densify_stats:
             with torch.no_grad():

@@ -64,6 +64,10 @@ class GradBucket:
         # sorts and tile backward passes overlap)
         self._events = {}
         self._last = None
+        # (event, stream, zeroed): the previous step's gradient reads on another stream (ShardedAdam
+        # with overlap: its reduce-scatters, and with zeroed the zero-fill of the rows it consumed)
+        self._foreign = None
+        self._zero_wait = None
         self.params = []
         self._bind(list(params))
 
@@ -121,8 +125,39 @@ class GradBucket:
                 raise RuntimeError("GradBucket: a parameter's .grad was replaced by another tensor; its gradient "
                                    "would bypass the bucket (call rebind() after replacing parameters)")
 
+    def after_foreign_read(self, event, stream, zeroed: bool) -> None:
+        """The step's gradients were read on `stream` (up to `event`), and with `zeroed` the bucket
+        was zero-filled there afterwards (ShardedAdam(overlap=True)): the next zero_grad() then
+        writes nothing and makes no stream wait, and the next step's writers wait for `event` --
+        the rasterizer's sink writes through write_order, any other producer through
+        before_backward() (gs_train_step.train_step_views calls it before each loss.backward())."""
+        self._foreign = (event, stream, bool(zeroed))
+
+    def before_backward(self) -> None:
+        """Before a backward whose gradients reach the bucket outside the sink protocol (autograd's
+        accumulation into the .grad views): the current stream waits for a foreign zero-fill."""
+        ev, self._zero_wait = self._zero_wait, None
+        if ev is not None and self.flat.is_cuda:
+            torch.cuda.current_stream(self.flat.device).wait_event(ev)
+
     def zero_grad(self):
         self._check_bound()
+        foreign, self._foreign = self._foreign, None
+        if foreign is not None:
+            ev, st, zeroed = foreign
+            if self.lazy_zero:
+                self._fresh = {id(p): self.views[id(p)]._version for p in self.params}
+            elif zeroed:
+                self._fresh = {}
+                self._zero_wait = ev
+            else:
+                torch.cuda.current_stream(self.flat.device).wait_event(ev)
+                self.flat.zero_()
+                self._fresh = {}
+                self.written(torch.cuda.current_stream(self.flat.device))
+                return
+            self._last = (ev, st)  # the step's first sink write (on any stream) waits for the reads
+            return
         if self.lazy_zero:
             self._fresh = {id(p): self.views[id(p)]._version for p in self.params}
         else:
@@ -342,12 +377,51 @@ class ShardedAdam:
     state_dict); the row plan follows P afterwards.  Bytes on the wire per step equal the all-reduce's
     (an all-reduce IS a reduce-scatter + an all-gather); the Adam work per rank is 1/N of it."""
 
-    def __init__(self, optimizer, bucket: GradBucket, group=None, chunks: int = 4, update=None):
+    def __init__(self, optimizer, bucket: GradBucket, group=None, chunks: int = 4, update=None,
+                 overlap: bool = False):
         self.opt, self.bucket, self.group = optimizer, bucket, group
         self.chunks = max(1, int(chunks))
         self._update = update  # (items, b1, b2, eps, maximize) -> None; default: FusedAdam's HIP kernel
         self._comm = None
         self._bufs = {}
+        # overlap: step() returns with its all-gathers in flight; their per-chunk events wait for
+        # the next step's consumers (take_row_waits -> the forward's chunked activation and
+        # preprocess, DESIGN.md §7), and the bucket is zero-filled on the collective stream
+        self.overlap = bool(overlap)
+        self._pending = []
+        # the Gaussian count of the step that left every rank's moments current only on its own rows
+        # (None: whole on every rank).  gather_state() clears it; a step at another count, a densify
+        # or a state_dict() in between raise instead of reading stale moment rows.
+        self._sharded_P = None
+        self.opt._gs_sharded_moments = self
+        if hasattr(self.opt, "register_state_dict_pre_hook"):
+            self.opt.register_state_dict_pre_hook(lambda opt: self._check_whole("state_dict()"))
+
+    def moments_sharded(self) -> bool:
+        """True when the moments are current only on each rank's own rows (call gather_state())."""
+        return self._sharded_P is not None
+
+    def _check_whole(self, what: str) -> None:
+        if self._sharded_P is not None:
+            raise RuntimeError(f"ShardedAdam: {what} needs whole Adam moments, but each rank holds only its own rows "
+                               "since the last step: call gather_state() first")
+
+    def take_row_waits(self):
+        """[(lo, hi, event)] of the last overlapped step's all-gathers (rows [lo, hi) of every
+        parameter are whole once `event` has fired), handed to the next forward (gs_train_step.
+        render(row_waits=...)), which then waits for them chunk by chunk; cleared here, so the caller
+        owns the waits.  Empty when nothing is pending."""
+        out, self._pending = self._pending, []
+        return out
+
+    def sync(self) -> None:
+        """The current stream waits for every pending all-gather (before anything reads the
+        parameters outside a row-waited forward)."""
+        pend, self._pending = self._pending, []
+        if pend and self.bucket.flat.is_cuda:
+            cur = torch.cuda.current_stream(self.bucket.flat.device)
+            for _lo, _hi, ev in pend:
+                cur.wait_event(ev)
 
     def _world(self):
         if dist.is_available() and dist.is_initialized():
@@ -392,11 +466,17 @@ class ShardedAdam:
         """One optimizer step from the bucket's gradients (replaces bucket.allreduce() +
         optimizer.step()).  The current stream waits for the step's collectives at the end."""
         b = self.bucket
+        if self._pending:
+            raise RuntimeError("ShardedAdam: the previous step's all-gathers were never waited for (pass "
+                               "take_row_waits() to the next forward, or call sync())")
         b._check_bound()
         params = b.params
         P = params[0].shape[0]
         if any(p.dim() == 0 or p.shape[0] != P for p in params):
             raise ValueError("ShardedAdam: every bucket parameter must have the same row count")
+        if self._sharded_P is not None and self._sharded_P != P:
+            raise RuntimeError(f"ShardedAdam: the Gaussian count changed ({self._sharded_P} -> {P}) while the moments "
+                               "were sharded: call gather_state() before densify_and_prune")
         N, r = self._world()
         groups = self._groups()
         hyper = {(float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), bool(g.get("maximize", False)))
@@ -428,6 +508,9 @@ class ShardedAdam:
         data = [p.detach().view(P, -1) for p in params]
         mv = [(m.view(P, -1), v.view(P, -1)) for m, v in moments]
         works = []
+        overlap = self.overlap and on_dev
+        pending = []
+        zero_ev = None
         last = len(chunks) - 1
         for c, (lo, hi, S) in enumerate(chunks + ([(Pm, Pm, 0)] if not chunks else [])):
             end = P if c == max(last, 0) else hi  # the last chunk's pass also covers the tail rows
@@ -461,6 +544,14 @@ class ShardedAdam:
                         items.append((data[k][Pm:P], t, mv[k][0][Pm:P], mv[k][1][Pm:P], lrs[k], steps[k], wds[k]))
                 if items:
                     self._run_update(items, hyper, dev)
+                if overlap:
+                    # the chunk's gradient rows are consumed (reduce-scattered / all-reduced and
+                    # updated): zero them here, so the next step's zero_grad needs no fill on its stream
+                    for g in rows:
+                        g[lo:end].zero_()
+                    if c == max(last, 0):
+                        zero_ev = torch.cuda.Event()
+                        zero_ev.record(comm)
                 if S > 0:
                     ctx = self._collective_ctx(dev) if on_dev else None
                     with (ctx if ctx is not None else _nullctx()) as cm:
@@ -468,9 +559,24 @@ class ShardedAdam:
                             dist.all_gather_into_tensor(data[k][lo:hi].reshape(-1), data[k][a:z].reshape(-1),
                                                         group=self.group)
                     if cm is not None:
-                        works.append(cm)
+                        if overlap:
+                            cm.wait()  # (the side stream waits for the coalesced group)
+                        else:
+                            works.append(cm)
+                if overlap:
+                    ev = torch.cuda.Event()
+                    ev.record(comm)
+                    pending.append((0 if not pending else pending[-1][1], end, ev))
         if deferred:
             b._retire_deferred(inputs, views)
+        if N > 1:
+            self._sharded_P = P
+        if overlap:
+            # no wait: the next forward waits for each chunk's all-gather (take_row_waits), the next
+            # step's gradient writers for the zero-fill (the bucket's foreign read)
+            self._pending = pending
+            b.after_foreign_read(zero_ev, comm, zeroed=True)
+            return
         for w in works:
             w.wait()
         if on_dev:
@@ -503,7 +609,9 @@ class ShardedAdam:
     def gather_state(self) -> None:
         """Make every rank's Adam moments whole (all-gather of the owned rows of exp_avg /
         exp_avg_sq, chunk by chunk): call before densify_and_prune or state_dict()."""
+        self.sync()
         N, r = self._world()
+        self._sharded_P = None
         if N == 1:
             return
         params = self.bucket.params

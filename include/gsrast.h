@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define GSRAST_ABI_VERSION 16  /* v16: gs_backward_gaussians_adam_stats (v15: gs_backward_gaussians_adam; v14: gs_forward_counted + gs_binning_layout_count) */
+#define GSRAST_ABI_VERSION 17  /* v17: gs_geom_flags_offset, gs_forward_order_status, gs_set_row_waits; v16: gs_backward_gaussians_adam_stats (v15: gs_backward_gaussians_adam; v14: gs_forward_counted + gs_binning_layout_count) */
 
 int gs_abi_version(void);
 const char* gs_last_error(void);
@@ -173,6 +173,30 @@ int gs_forward_render_bounded(int P, const float* background, int image_width, i
  * gs_last_error) when a flag is set.  Only forwards whose kernels have run are seen: call it after
  * a synchronisation point to cover every forward before it. */
 int gs_bounded_status(unsigned* flags, long long* instances);
+/* (ABI v17) Byte offset, inside a geometry buffer laid out for P Gaussians, of the 32-bit word
+ * holding that view's forward error flags (the bits above; 0 for a valid view).  Every kernel of
+ * the forward that records an error stores it there, and the backward's record sums and the fused
+ * backward + Adam read it (an invalid view adds nothing / is skipped).  A caller copies the word
+ * out stream-ordered behind the forward to decide, at its next sync, whether that view's update
+ * happened (gs_train_step: the fused step's step counts). */
+size_t gs_geom_flags_offset(int P);
+/* (ABI v17) The ordering flags of every forward queued on the current device whose render has been
+ * queued (read-back forwards: a look-back wait of their sorts that timed out): waits for their
+ * render kernels, takes the flags (each forward is reported once) and returns non-zero with the
+ * message in gs_last_error when one timed out.  Without this call the next forward or backward
+ * reports them; a caller that has already seen a view's flags word name ERR_LOOKBACK consumes the
+ * report here, in its own call. */
+int gs_forward_order_status(void);
+/* (ABI v17) Row waits for the next forward preprocess of the calling thread (any forward entry
+ * point: counted, two-call, bounded, split, or the K-view gs_forward_preprocess_views): chunk k
+ * covers the Gaussian rows [bounds[k], bounds[k + 1]) (bounds[0] == 0, increasing) and `events[k]`
+ * is a hipEvent_t recorded when those rows' inputs are ready (null: none).  The preprocess then
+ * launches in row chunks, each behind hipStreamWaitEvent on its chunk's event, so it starts on the
+ * first rows while later rows are still being written on another stream -- the all-gather of a
+ * sharded optimizer step (gs_view_parallel.ShardedAdam: parameters updated by row chunk).  Outputs
+ * are those of the whole-grid launch.  The waits are consumed by that preprocess; n = 0 clears
+ * them.  This mirrors no upstream entry point (upstream has no optimizer sharding). */
+int gs_set_row_waits(int n, const int* bounds, void* const* events);
 
 /* ---- the binning of K prepared views at once (ABI v11) ----
  * After gs_forward_preprocess_views(_bounded): duplicate + tile sort + tile ranges of all K views as

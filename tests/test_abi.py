@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, s), f"libgsrast.so does not export {s}"
     assert set(syms) == set(_native.SIGNATURES), set(syms) ^ set(_native.SIGNATURES)
     want = int(re.search(r"#define GSRAST_ABI_VERSION (\d+)", open(os.path.join(ROOT, "include", "gsrast.h")).read()).group(1))
-    assert want == 16 and lib.gs_abi_version() == want
+    assert want == 17 and lib.gs_abi_version() == want
 
 
 def test_graft_build_checks_the_header_abi():

@@ -106,6 +106,26 @@ def test_two_rank_sharded_adam_equals_allreduce_across_densify(tmp_path):
 
 
 @pytest.mark.spawn_first
+def test_two_rank_deferred_sharded_adam_equals_allreduce(tmp_path):
+    """bench.py's step shape (activated leaves, GradBucket(lazy_zero=True, defer=True): the
+    per-Gaussian half runs once per optimizer step) through ShardedAdam, whose deferred pass runs in
+    row chunks on the compute stream while the previous chunk's reduce-scatter / update /
+    all-gather run on the side stream -- and with overlap=True, the all-gathers left in flight into
+    the next step's chunked preprocess (2 ranks, gloo, one GPU): four steps bit-identical to the
+    bucket all-reduce + replicated FusedAdam, and identical across the ranks."""
+    out = tmp_path / "vp_deferred.txt"
+    env = dict(os.environ, GS_VP_OUT=str(out), HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "vp_train_worker.py"),
+           "gloo2_deferred"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, f"workers failed ({r.returncode}):\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    res = out.read_text()
+    print(res)
+    assert res.startswith("OK"), res
+
+
+@pytest.mark.spawn_first
 def test_rccl_world1_bucket_allreduce_equals_single_process(tmp_path):
     """The RCCL path (torch.distributed backend "nccl" = RCCL on ROCm) at world size 1: the view-
     parallel train step with its bucket all-reduce issued through RCCL equals the same steps without

@@ -235,6 +235,90 @@ def test_fused_adam_bounded_overflow_raises_with_state_untouched(device):
         assert torch.equal(getattr(a, n_), getattr(b, n_)), n_
 
 
+def _full_snapshot(m):
+    names = ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
+    torch.cuda.synchronize()
+    st = m.optimizer.state_dict()["state"]
+    moments = {(i, k): v.clone() for i, s in st.items() for k, v in s.items() if torch.is_tensor(v) and v.dim()}
+    steps = {(i, k): float(v) for i, s in st.items() for k, v in s.items() if not torch.is_tensor(v) or not v.dim()}
+    return ({n_: getattr(m, n_).detach().clone() for n_ in names}, moments, steps,
+            [t.clone() for t in (m.max_radii2D, m.xyz_gradient_accum, m.denom)])
+
+
+def _assert_same_snapshot(before, after):
+    for n_ in before[0]:
+        assert torch.equal(before[0][n_], after[0][n_]), n_
+    assert before[1].keys() == after[1].keys() and before[2] == after[2]
+    for k in before[1]:
+        assert torch.equal(before[1][k], after[1][k]), k
+    for x, y in zip(before[3], after[3]):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("fuse_adam", [True, False])
+def test_lookback_timeout_raises_in_its_own_step_with_state_untouched(device, fuse_adam):
+    """A read-back forward whose offsets scan's look-back wait times out (forced with
+    gs_debug_set_scan_spin_limit(0)) does not raise in its own rasterizer call; train_step(loss_item=
+    True) must raise in that iteration (train.py:99, before :127) with parameters, moments, step
+    counts and statistics untouched -- with the fused backward + Adam launched before the loss
+    read-back, the view's flags word (copied out behind the loss) is what tells the host that the
+    kernel skipped the update.  The report is consumed: the next iterations run clean and equal a
+    model that never saw the failed one."""
+    import gs_train_step as ts
+    from diff_gaussian_rasterization import _native
+
+    lib = _native.load()
+    sc, settings, gt = _setup(device)  # 3000 Gaussians: two look-back tiles in the offsets scan
+    a, b = ts.TrainModel(sc, device), ts.TrainModel(sc, device)
+    ts.train_step(a, settings, gt, loss_item=True, fuse_adam=fuse_adam)
+    ts.train_step(b, settings, gt, loss_item=True, fuse_adam=fuse_adam)
+    before = _full_snapshot(b)
+    prev = lib.gs_debug_set_scan_spin_limit(0)
+    try:
+        with pytest.raises(RuntimeError, match="look-back wait"):
+            ts.train_step(b, settings, gt, loss_item=True, fuse_adam=fuse_adam)
+    finally:
+        lib.gs_debug_set_scan_spin_limit(prev)
+    _assert_same_snapshot(before, _full_snapshot(b))
+    for _ in range(2):
+        la = ts.train_step(a, settings, gt, loss_item=True, fuse_adam=fuse_adam)
+        lb = ts.train_step(b, settings, gt, loss_item=True, fuse_adam=fuse_adam)
+        assert la == lb
+    _assert_same_snapshot(_full_snapshot(a), _full_snapshot(b))
+
+
+def test_fused_adam_commit_follows_its_own_view_not_earlier_flags(device, monkeypatch):
+    """Another bounded forward that overflows while this step is in flight (queued after this step's
+    forward checked the device's bounded status, here: from inside the step's loss call) leaves its
+    flags in the device-wide status.  The fused-Adam step's own view is valid, so its update must be
+    committed -- its flags word is clean -- and the foreign flags reported after the commit:
+    parameters, moments and step counts stay consistent (equal to a model stepped as often)."""
+    import gs_loss
+    import gs_train_step as ts
+    from diff_gaussian_rasterization import bounded_status, last_num_rendered
+
+    sc, settings, gt = _setup(device)
+    a, b = ts.TrainModel(sc, device), ts.TrainModel(sc, device)
+    ts.train_step(a, settings, gt, loss_item=True, fuse_adam=True)
+    n = last_num_rendered()
+    ts.train_step(b, settings, gt, loss_item=True, fuse_adam=True, binning_capacity=n + 64)
+    c = ts.TrainModel(sc, device)
+    orig = gs_loss.photometric_loss
+
+    def loss_with_foreign_overflow(*args, **kw):
+        monkeypatch.setattr(gs_loss, "photometric_loss", orig)
+        with torch.no_grad():  # an overflowing bounded render of another model, never polled by its caller
+            ts.render(c, settings, fused=True, binning_capacity=n // 4)
+        return orig(*args, **kw)
+
+    monkeypatch.setattr(gs_loss, "photometric_loss", loss_with_foreign_overflow)
+    with pytest.raises(RuntimeError, match="binning capacity"):
+        ts.train_step(b, settings, gt, loss_item=True, fuse_adam=True, binning_capacity=n + 64)
+    assert bounded_status() == (0, 0)
+    ts.train_step(a, settings, gt, loss_item=True, fuse_adam=True)
+    _assert_same_snapshot(_full_snapshot(a), _full_snapshot(b))
+
+
 def test_bounded_overflow_in_a_captured_step_raises_in_the_loop(device):
     """render -> L1 + SSIM -> backward with a bounded forward, captured once into a HIP graph
     (torch.cuda.CUDAGraph) and replayed in a training loop that polls bounded_status() at its
@@ -283,17 +367,19 @@ def test_bounded_overflow_in_a_captured_step_raises_in_the_loop(device):
         bounded_status()
 
 
-@pytest.mark.parametrize("active_degree", [3, 2, 1, 0])
-def test_fused_adam_train_step_bitwise_equal_unfused(device, active_degree, monkeypatch):
+@pytest.mark.parametrize("active_degree,P", [(3, 3000), (2, 3000), (1, 3000), (0, 3000), (3, 2999)])
+def test_fused_adam_train_step_bitwise_equal_unfused(device, active_degree, P, monkeypatch):
     """train_step(fuse_adam=True): the per-Gaussian backward fused with the Adam step
     (gs_backward_gaussians_adam) against the default step (backward, then FusedAdam.step_activated)
     over three iterations: every parameter, both Adam moments, the step counts and the densification
     statistics bit-identical, the same loss.item() values -- at the full SH degree and at an active
-    degree below the 16 stored coefficients (train.py's oneupSHdegree schedule)."""
+    degree below the 16 stored coefficients (train.py's oneupSHdegree schedule).  P = 2999 leaves a
+    last workgroup of 183 rows: 549 / 8235 floats of features_dc / features_rest, not multiples of 4,
+    so the SH update's scalar tail runs too (3000: 184 rows, float4s only)."""
     import gs_train
     import gs_train_step as ts
 
-    sc, settings, gt = _setup(device)
+    sc, settings, gt = _setup(device, P=P)
     settings = settings._replace(sh_degree=active_degree)
     runs = []
     for fuse in (False, True):

@@ -313,3 +313,74 @@ def test_sharded_adam_equals_allreduce_gloo_world2(P, chunks, average):
             np.testing.assert_array_equal(x, y)
     if P >= 4:
         assert len(res[0][4][0]) > 1  # the step ran in several chunks
+
+
+def _guard_worker(rank, world, port, out_q):
+    """ShardedAdam's sharded-moments guard: after a step every rank's moments are current only on its
+    own rows, so state_dict(), densify_and_prune and a step at another Gaussian count must raise
+    until gather_state() makes them whole again."""
+    import types
+
+    import gs_train
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {}
+    try:
+        g = torch.Generator().manual_seed(5)
+        ps = [torch.nn.Parameter(torch.randn((37,) + w, generator=g)) for w in [(3,), (4,)]]
+        opt = gs_train.FusedAdam([{"params": [p], "lr": 1e-3} for p in ps], lr=0.0, eps=1e-15)
+        bucket = vp.GradBucket(ps)
+        sh = vp.ShardedAdam(opt, bucket, chunks=2, update=_np_adam, overlap=True)
+        bucket.zero_grad()
+        for p in ps:
+            p.grad.fill_(1.0)
+        sh.step()
+        res["sharded_after_step"] = sh.moments_sharded()
+        res["no_waits_on_cpu"] = sh.take_row_waits() == []  # (overlap needs device streams)
+
+        def raises(fn, text):
+            try:
+                fn()
+            except RuntimeError as e:
+                return text in str(e)
+            return False
+
+        res["state_dict_raises"] = raises(opt.state_dict, "gather_state")
+        model = types.SimpleNamespace(optimizer=opt)
+        res["densify_raises"] = raises(lambda: gs_train.densify_and_prune(model, 2e-4, 0.005, 1.0, 20), "gather_state")
+        # a Gaussian count change while sharded (a densify without gather_state) is refused at the next step
+        new = [torch.nn.Parameter(p.detach()[:30].clone()) for p in ps]
+        for i, (p, q) in enumerate(zip(ps, new)):
+            st = opt.state.pop(p)
+            st["exp_avg"], st["exp_avg_sq"] = st["exp_avg"][:30].clone(), st["exp_avg_sq"][:30].clone()
+            opt.state[q] = st
+            opt.param_groups[i]["params"][0] = q
+        bucket.rebind(new)
+        bucket.zero_grad()
+        res["step_raises"] = raises(sh.step, "Gaussian count changed")
+        sh.gather_state()
+        res["whole_after_gather"] = not sh.moments_sharded() and isinstance(opt.state_dict(), dict)
+        bucket.zero_grad()
+        sh.step()  # at the new count, after gather_state
+        res["steps"] = [float(opt.state[p]["step"]) for p in new]
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_adam_refuses_stale_moments_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_guard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        got = res[r]
+        assert got.pop("steps") == [2.0, 2.0]
+        assert all(got.values()), got

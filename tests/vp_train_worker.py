@@ -94,11 +94,13 @@ def gloo2():
 
 
 def gloo2_sharded():
-    """Two replicas per rank from the same scene: A steps through the bucket all-reduce + FusedAdam,
+    """Three replicas per rank from the same scene: A steps through the bucket all-reduce + FusedAdam,
     B through gs_view_parallel.ShardedAdam (reduce-scatter -> FusedAdam on the rank's row slices ->
-    all-gather, 3 row chunks); three steps, reduce_densify_stats, gather_state, densify_and_prune (same
-    seeded draws for A and B, rank 0's broadcast), two more steps.  A and B bit-identical on every rank
-    and B identical across the ranks."""
+    all-gather, 3 row chunks), C through ShardedAdam(overlap=True) (the all-gathers left in flight:
+    the next step's activation and preprocess wait for them chunk by chunk, the bucket is zero-filled
+    on the collective stream); three steps, reduce_densify_stats, gather_state, densify_and_prune (same
+    seeded draws, rank 0's broadcast), two more steps.  A, B and C bit-identical on every rank and B,
+    C identical across the ranks."""
     import gs_train_step as ts
     import gs_view_parallel as vp
 
@@ -109,10 +111,10 @@ def gloo2_sharded():
     sc, settings, gts = setup(dev, rank)
     mine = [(settings[v], gts[v]) for v in vp.shard_views(4, rank, world)]
     runs = []
-    for sharded in (False, True):
+    for mode in ("allreduce", "sharded", "overlap"):
         m = ts.TrainModel(sc, dev, fused=True)
         bucket = vp.GradBucket([m._xyz, m._features_dc, m._features_rest, m._opacity, m._scaling, m._rotation])
-        sh = vp.ShardedAdam(m.optimizer, bucket, chunks=3) if sharded else None
+        sh = vp.ShardedAdam(m.optimizer, bucket, chunks=3, overlap=mode == "overlap") if mode != "allreduce" else None
         for _ in range(3):
             ts.train_step_views(m, bucket, mine, sharded=sh)
         vp.reduce_densify_stats(m.xyz_gradient_accum, m.denom, m.max_radii2D)
@@ -132,13 +134,76 @@ def gloo2_sharded():
         runs.append(([t.clone() for t in model_tensors(m)], P0, m.P,
                      [float(m.optimizer.state[g_["params"][0]]["step"]) for g_ in m.optimizer.param_groups]))
         bucket.close()
-    (ta, p0a, pa, sa), (tb, p0b, pb, sb) = runs
+    (ta, p0a, pa, sa), (tb, p0b, pb, sb), (tc, p0c, pc, sc_) = runs
     same = len(ta) == len(tb) and all(torch.equal(x, y) for x, y in zip(ta, tb))
-    replicas = vp.check_replicas(tb)
+    same_o = len(ta) == len(tc) and all(torch.equal(x, y) for x, y in zip(ta, tc))
+    replicas = vp.check_replicas(tb) and vp.check_replicas(tc)
     if rank == 0:
-        ok = same and replicas and pa == pb and pa != p0a and sa == sb == [5.0] * 6
-        msg = ("OK " if ok else "FAIL ") + (f"sharded == all-reduce {same}; sharded replicas equal {replicas}; "
-                                            f"P {p0a} -> {pa} / {pb}; steps {sa} / {sb}")
+        ok = same and same_o and replicas and pa == pb == pc and pa != p0a and sa == sb == sc_ == [5.0] * 6
+        msg = ("OK " if ok else "FAIL ") + (f"sharded == all-reduce {same}; overlapped sharded == all-reduce {same_o}; "
+                                            f"sharded replicas equal {replicas}; P {p0a} -> {pa} / {pb} / {pc}; "
+                                            f"steps {sa} / {sb} / {sc_}")
+        with open(os.environ["GS_VP_OUT"], "w") as f:
+            f.write(msg + "\n")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def gloo2_deferred():
+    """bench.py's step shape on two gloo ranks (one GPU): the activated inputs are the leaves, a
+    GradBucket(lazy_zero=True, defer=True) takes every view's per-Gaussian half for one pass at the
+    optimizer step.  A: bucket.allreduce() + FusedAdam.step(); B: ShardedAdam (the deferred pass in
+    row chunks, each chunk's reduce-scatter / update / all-gather on the side stream); C: the same
+    with overlap=True (the next step's first forward waits for the all-gathers chunk by chunk through
+    _C.row_waits).  Four steps; A, B, C bit-identical, B and C identical across the ranks."""
+    import gs_scenes
+    import gs_train
+    import gs_view_parallel as vp
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    sc, settings, _ = setup(dev, rank)
+    d = sc.to(dev)
+    mine = [settings[v] for v in vp.shard_views(4, rank, world)]
+    dpix = [gs_scenes.dl_dimage(H, W, seed=90 + v).to(dev) for v in range(4)]
+    mine_d = [dpix[v] for v in vp.shard_views(4, rank, world)]
+    lrs = [1.6e-4, 2.5e-3, 5e-2, 5e-3, 1e-3]
+    runs = []
+    for mode in ("allreduce", "sharded", "overlap"):
+        params = [t.clone().requires_grad_(True) for t in (d.means3D, d.shs, d.opacities, d.scales, d.rotations)]
+        opt = gs_train.FusedAdam([{"params": [p], "lr": lr} for p, lr in zip(params, lrs)], lr=0.0, eps=1e-15)
+        bucket = vp.GradBucket(params, lazy_zero=True, defer=True)
+        sh = vp.ShardedAdam(opt, bucket, chunks=3, overlap=mode == "overlap") if mode != "allreduce" else None
+        for _ in range(4):
+            waits = sh.take_row_waits() if sh is not None else []
+            bucket.zero_grad()
+            for s_, dp in zip(mine, mine_d):
+                m2 = torch.empty_like(params[0], requires_grad=True)
+                with _C.row_waits(waits):
+                    img, _ = GaussianRasterizer(s_)(means3D=params[0], means2D=m2, opacities=params[2],
+                                                    shs=params[1], scales=params[3], rotations=params[4])
+                waits = []
+                img.backward(dp)
+            if sh is None:
+                bucket.allreduce()
+                opt.step()
+            else:
+                sh.step()
+        if sh is not None:
+            sh.gather_state()
+        torch.cuda.synchronize()
+        runs.append([t.detach().clone() for p in params for t in (p, opt.state[p]["exp_avg"], opt.state[p]["exp_avg_sq"])])
+        bucket.close()
+    same_b = all(torch.equal(x, y) for x, y in zip(runs[0], runs[1]))
+    same_c = all(torch.equal(x, y) for x, y in zip(runs[0], runs[2]))
+    replicas = vp.check_replicas(runs[1]) and vp.check_replicas(runs[2])
+    if rank == 0:
+        ok = same_b and same_c and replicas
+        msg = ("OK " if ok else "FAIL ") + (f"deferred sharded == all-reduce {same_b}; overlapped {same_c}; "
+                                            f"replicas equal {replicas}")
         with open(os.environ["GS_VP_OUT"], "w") as f:
             f.write(msg + "\n")
     dist.barrier()
@@ -157,9 +222,11 @@ def nccl1():
     def run(sharded=False):
         m = ts.TrainModel(sc, dev, fused=True)
         b = vp.GradBucket([m._xyz, m._features_dc, m._features_rest, m._opacity, m._scaling, m._rotation])
-        sh = vp.ShardedAdam(m.optimizer, b, chunks=3) if sharded else None
+        sh = vp.ShardedAdam(m.optimizer, b, chunks=3, overlap=sharded == "overlap") if sharded else None
         for _ in range(2):
             ts.train_step_views(m, b, views, sharded=sh)
+        if sh is not None:
+            sh.sync()
         torch.cuda.synchronize()
         b.close()
         return [t.clone() for t in model_tensors(m)]
@@ -173,8 +240,10 @@ def nccl1():
     got = run()
     dist.all_reduce = orig
     same = all(torch.equal(a, b) for a, b in zip(ref, got))
-    # the sharded step through RCCL (reduce-scatter / all-gather at world 1, coalesced per chunk)
+    # the sharded step through RCCL (reduce-scatter / all-gather at world 1, coalesced per chunk),
+    # and with the all-gathers overlapped into the next step
     sharded_same = all(torch.equal(a, b) for a, b in zip(ref, run(sharded=True)))
+    sharded_same = sharded_same and all(torch.equal(a, b) for a, b in zip(ref, run(sharded="overlap")))
     # the chunked all-reduce (RCCL coalesced groups per Gaussian-row range, on a side stream,
     # overlapping the deferred per-Gaussian pass) against the bucket's one-shot finalize
     chunk_same = chunked_vs_finalize(sc, settings, dev)
@@ -214,4 +283,4 @@ def chunked_vs_finalize(sc, settings, dev):
 
 
 if __name__ == "__main__":
-    {"gloo2": gloo2, "gloo2_sharded": gloo2_sharded, "nccl1": nccl1}[sys.argv[1]]()
+    {"gloo2": gloo2, "gloo2_sharded": gloo2_sharded, "gloo2_deferred": gloo2_deferred, "nccl1": nccl1}[sys.argv[1]]()
