@@ -161,6 +161,10 @@ def main():
     ap.add_argument("--allreduce-chunks", type=int, default=4,
                     help="N > 1: the deferred per-Gaussian pass runs in this many Gaussian-row ranges and each "
                          "range's gradient rows are all-reduced (RCCL, side stream) as soon as they are written")
+    ap.add_argument("--vp-train-steps", type=int, default=10,
+                    help="timed optimizer steps of the view-parallel training measurement (`view_parallel_train`: "
+                         "gs_train_step.train_step_views with the fused glue through ShardedAdam(overlap=True), the "
+                         "bucket all-reduce + replicated Adam, and the exchange-free step, at every N); 0 = skip")
     ap.add_argument("--no-graph", action="store_true",
                     help="skip the HIP-graph measurement (the same step with bounded binning buffers, captured "
                          "once into a torch.cuda.CUDAGraph and replayed; N = 1)")
@@ -533,6 +537,11 @@ def main():
     if world == 1 and not args.no_train_step and not n_views:
         train = train_step_bench(sc, cam, deg, dev, args.train_steps, args.workload == "c5")
 
+    vp_train = None
+    if args.vp_train_steps > 0:
+        vp_train = vp_train_bench(sc, cams, my_views, deg, dev, args.vp_train_steps, max(2, args.warmup // 3), world,
+                                  args.allreduce_chunks)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sc, cam, deg, W, H, dpix.cpu(), args.cpu_threads, args.cpu_runs)
@@ -591,6 +600,7 @@ def main():
         # kernel-only durations are rocprofv3's (profiles/*rocprof*.csv, bench.py --profile-pass-only)
         "kernels_timing": "hip events per launch (dispatch gap included)",
         "train_step": train,
+        "view_parallel_train": vp_train,
         "init_knn": knn,
         **({"step_ms_deciles": step_deciles} if step_deciles else {}),
         "cpu_baseline": cpu,
@@ -599,6 +609,71 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def vp_train_bench(sc, cams, my_views, deg, dev, steps, warmup, world, chunks):
+    """View-parallel TRAINING steps: gs_train_step.train_step_views --
+    every view of the rank through render -> L1 + SSIM -> backward into the rank's GradBucket
+    (fused glue), then the optimizer step over the ranks -- timed per optimizer step, barrier +
+    sync on both sides, max over ranks, in three modes:
+      sharded:   ShardedAdam(overlap=True): reduce-scatter -> Adam on the rank's rows -> all-gather,
+                 in row chunks on a side stream, the all-gathers running into the next step's
+                 chunked activation / preprocess (the last step's are waited for inside the region);
+      allreduce: one bucket all-reduce (RCCL) + the replicated FusedAdam step;
+      local:     the same step without any collective (each rank on its own gradients: the cost of
+                 the step with a free exchange).
+    exposed_exchange_us = (mode - local) per step.  At N = 1 there is no process group: the three
+    modes run the same kernels (sharded = one shard of every row)."""
+    import gs_train_step as ts
+
+    settings = [gs_scenes.raster_settings_for(cams[v], deg, device=dev) for v in my_views]
+    H, W = settings[0].image_height, settings[0].image_width
+    gts = [torch.rand((3, H, W), generator=torch.Generator().manual_seed(100 + v)).to(dev) for v in my_views]
+    views = list(zip(settings, gts))
+    names = ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
+
+    def timed(mode):
+        m = ts.TrainModel(sc, dev)
+        bucket = vp.GradBucket([getattr(m, n) for n in names])
+        sh = vp.ShardedAdam(m.optimizer, bucket, chunks=chunks, overlap=True) if mode == "sharded" else None
+
+        def one():
+            ts.train_step_views(m, bucket, views, sharded=sh, exchange=mode != "local")
+
+        for _ in range(warmup):
+            one()
+        if sh is not None:
+            sh.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        if sh is not None:
+            sh.sync()  # the last step's all-gathers belong to it
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        bucket.close()
+        del m, bucket, sh
+        torch.cuda.empty_cache()
+        return el
+
+    els = {mode: timed(mode) for mode in ("local", "allreduce", "sharded")}
+    nv = world * len(views)
+    out = {"views_per_rank_per_step": len(views), "steps": steps, "chunks": chunks,
+           "glue": "fused (render_inputs activation, photometric_loss, densify stats, FusedAdam)"}
+    for mode, el in els.items():
+        out[mode] = {"iters_s": round(nv * steps / el, 2), "ms_per_step": round(1e3 * el / steps, 4)}
+        if mode != "local":
+            out[mode]["exposed_exchange_us"] = round(1e6 * (el - els["local"]) / steps, 1)
+    return out
 
 
 def single_view_bench(bucket, rast, params, dpix, steps, lib):

@@ -334,7 +334,7 @@ def train_step(model: TrainModel, settings, gt_image: torch.Tensor, fused: bool 
 
 
 def train_step_views(model: TrainModel, bucket, views, lambda_dssim: float = LAMBDA_DSSIM, densify_stats: bool = True,
-                     average: bool = False, sharded=None):
+                     average: bool = False, sharded=None, exchange: bool = True):
     """One view-parallel optimizer step (gs_view_parallel): this rank's views
     `views` = [(settings, gt_image)] each run render -> L1 + SSIM -> backward with the fused glue,
     their raw-parameter gradients accumulate in `bucket` (a gs_view_parallel.GradBucket over the six
@@ -347,7 +347,9 @@ def train_step_views(model: TrainModel, bucket, views, lambda_dssim: float = LAM
     ShardedAdam(overlap=True) the previous step's all-gathers are still in flight when this step
     starts: the first view's activation and preprocess wait for them row chunk by row chunk
     (take_row_waits, render(row_waits=...)), and every backward waits for the collective stream's
-    zero-fill of the bucket (GradBucket.before_backward).  Returns the rank's losses."""
+    zero-fill of the bucket (GradBucket.before_backward).  exchange=False (a measurement baseline,
+    bench.py `view_parallel_train`): no collective, every rank steps on its own gradients -- the
+    step's cost with a free exchange; the replicas diverge.  Returns the rank's losses."""
     waits = sharded.take_row_waits() if sharded is not None else []
     bucket.zero_grad()
     losses = []
@@ -364,7 +366,10 @@ def train_step_views(model: TrainModel, bucket, views, lambda_dssim: float = LAM
     if sharded is not None:
         sharded.step(average=average)
         return losses
-    bucket.allreduce(average=average)
+    if exchange:
+        bucket.allreduce(average=average)
+    else:
+        bucket.finalize()
     with torch.no_grad():
         model.optimizer.step()
     return losses

@@ -508,6 +508,7 @@ class ShardedAdam:
         data = [p.detach().view(P, -1) for p in params]
         mv = [(m.view(P, -1), v.view(P, -1)) for m, v in moments]
         works = []
+        local = not (dist.is_available() and dist.is_initialized())
         overlap = self.overlap and on_dev
         pending = []
         zero_ev = None
@@ -522,7 +523,10 @@ class ShardedAdam:
                 comm.wait_event(ev)
             with (torch.cuda.stream(comm) if on_dev else _nullctx()):
                 items = []
-                if S > 0:
+                if S > 0 and local:  # no process group (one replica): the rows are the rank's shard
+                    shard = [g[lo:hi] for g in rows]
+                    a, z = lo, hi
+                elif S > 0:
                     shard = self._buf(c, rows, S, dev)
                     ctx = self._collective_ctx(dev) if on_dev else None
                     with (ctx if ctx is not None else _nullctx()) as cm:
@@ -531,6 +535,7 @@ class ShardedAdam:
                     if cm is not None:
                         cm.wait()  # (the side stream waits for the coalesced group)
                     a, z = lo + r * S, lo + (r + 1) * S
+                if S > 0:
                     for k in range(len(params)):
                         if average:
                             shard[k].div_(N)
@@ -538,7 +543,8 @@ class ShardedAdam:
                 if c == max(last, 0) and Pm < P:  # the tail: all-reduced, updated by every rank
                     for k, g in enumerate(rows):
                         t = g[Pm:P]
-                        dist.all_reduce(t, group=self.group)
+                        if not local:
+                            dist.all_reduce(t, group=self.group)
                         if average:
                             t.div_(N)
                         items.append((data[k][Pm:P], t, mv[k][0][Pm:P], mv[k][1][Pm:P], lrs[k], steps[k], wds[k]))
@@ -552,7 +558,7 @@ class ShardedAdam:
                     if c == max(last, 0):
                         zero_ev = torch.cuda.Event()
                         zero_ev.record(comm)
-                if S > 0:
+                if S > 0 and not local:
                     ctx = self._collective_ctx(dev) if on_dev else None
                     with (ctx if ctx is not None else _nullctx()) as cm:
                         for k in range(len(params)):
