@@ -111,6 +111,8 @@ void launch_record(const void* k) {
   g_launched.push_back(k);
 }
 
+void host_error(const char* msg) { set_error("%s", msg); }
+
 static bool check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) set_error("%s failed: %s", what, hipGetErrorString(e));
   return e == hipSuccess;

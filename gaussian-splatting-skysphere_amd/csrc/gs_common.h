@@ -37,6 +37,8 @@ void trace_end(const char* name, hipStream_t st);
 // the set of kernels launched since load (GSRAST_LAUNCH_LOG=1 / gs_debug_launch_log; tests list it
 // against the code object's kernels)
 void launch_record(const void* kernel_handle);
+// a host-side error of the current call (the message lands in gs_last_error; the call fails)
+void host_error(const char* msg);
 
 #define GS_LAUNCH(name, kern, grid, block, shm, st, ...)              \
   do {                                                                \

@@ -611,6 +611,11 @@ static inline bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t
                                     uint32_t* aux_a = nullptr, uint32_t* aux_b = nullptr,
                                     const uint32_t* keys_in0 = nullptr, uint32_t max_blocks = SORT_MAX_BLOCKS,
                                     int views = 1, uint64_t vstride = 0) {
+  if (aux0 && end_bit != 32) {
+    // only the 8-bit aux scatter is built (launch_scatter<true>): a second value stream needs 32-bit keys
+    host_error("radix_sort_pairs: a second value stream travels only with 32-bit keys (four 8-bit passes)");
+    return false;
+  }
   SortPlan p = sort_plan(n_max, max_blocks);
   uint32_t* hist = scratch;
   const size_t hist_n = (size_t)RADIX * p.nb;

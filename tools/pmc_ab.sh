@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes of the render kernels for several library builds (batch-1 loop, tools/prof_single.py).
-#   bash tools/r05_pmc_ab.sh build build_r4 ...      -> gpurun_out/pmcab_<build>_<pass>/
+#   bash tools/pmc_ab.sh build build_r4 ...      -> gpurun_out/pmcab_<build>_<pass>/
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p $OUT
 export TMPDIR=/tmp
