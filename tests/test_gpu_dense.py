@@ -26,6 +26,7 @@ import torch
 
 import dense_ref
 import gs_scenes
+import parity_report
 
 pytestmark = pytest.mark.gpu
 
@@ -38,6 +39,7 @@ def _check(got, ref, name, keep, frac=RTOL):
     ref = ref.detach().double().cpu().numpy()[keep]
     scale = float(np.abs(ref).max(initial=0.0))
     d = np.abs(got - ref)
+    parity_report.record(name, got, ref, RTOL, frac)
     bad = d > RTOL * np.abs(ref) + frac * scale
     print(f"{name}: max|d| {d.max(initial=0.0):.3e}  max|ref| {scale:.3e}")
     assert not bad.any(), f"{name}: {int(bad.sum())}/{bad.size} beyond tol, max|d| {d.max():.3e}, max|ref| {scale:.3e}"

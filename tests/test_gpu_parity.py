@@ -25,6 +25,7 @@ import pytest
 import torch
 
 import gs_scenes
+import parity_report
 
 pytestmark = pytest.mark.gpu
 
@@ -57,6 +58,7 @@ def _tol_check(gpu, ref, name, rtol=RTOL, frac=RTOL):
     assert gpu.shape == ref.shape, (name, gpu.shape, ref.shape)
     scale = max(np.abs(ref).max(), 1e-30)
     tol = rtol * np.abs(ref) + frac * scale
+    parity_report.record(name, gpu, ref, rtol, frac)
     bad = np.abs(gpu - ref) > tol
     if bad.any():
         idx = np.argwhere(bad)[:5]
@@ -362,10 +364,12 @@ def _large_splat_scene(anisotropy):
 def test_large_and_elongated_splats(oracle, device):
     """Skysphere-like mix: many small splats plus large ones spanning dozens of tiles and several
     duplicate workgroups (row spans over many tile rows, segments crossing workgroups, long
-    per-Gaussian record runs).  The covariance-chain gradients get 1e-4 of their max: large
-    splats' per-pixel dL/dconic terms cancel across hundreds of tiles, the GPU sums them in fp32
-    wave trees (the oracle in fp64), and the conic -> covariance chain amplifies the ~1e-7
-    relative difference (see test_needle_splats_conditioning for the extreme case)."""
+    per-Gaussian record runs).  Every gradient, the covariance chain included, at the 1e-5
+    contract (round 6: measured max 4.9e-6 of the max, drotations, tests/parity_report.py; the
+    bound was 1e-4 through round 5): large splats' per-pixel dL/dconic terms cancel across hundreds
+    of tiles, the GPU sums them in fp32 wave trees (the oracle in fp64), and the conic ->
+    covariance chain amplifies the ~1e-7 relative difference (test_needle_splats_conditioning is
+    the extreme case)."""
     cam, sc = _large_splat_scene(anisotropy=3.0)
     W, H = cam.image_width, cam.image_height
     bg = np.array([0.1, 0.2, 0.3], np.float32)
@@ -378,17 +382,20 @@ def test_large_and_elongated_splats(oracle, device):
     img, _, leaves = _gpu_run(cam, sc, device, bg, dpix)
     np.testing.assert_array_equal(img.detach().cpu().numpy(), ofw["color"])
     gr = oracle.backward(osc, dpix)
-    _check_backward(gr, leaves, chain_frac=1e-4)
+    _check_backward(gr, leaves)
     _check_chain_noise(leaves, gr, oracle.backward_f32_acc(osc, dpix))
 
 
 def test_needle_splats_conditioning(oracle, device):
     """Needles (60:1 and more) make conic -> covariance -> scale/rotation/mean an ill-conditioned
     chain: the fp32 per-pixel sums of dL/dconic (GPU: fp32 wave trees; oracle: fp64) agree to
-    ~1e-6 relative, and the chain amplifies that to ~1e-3 relative in the covariance-derived
-    gradients (upstream's fp32 atomics have the same property).  Forward stays bit-exact;
-    dmeans2D / dopacity / dsh keep the 1e-5 bound; dmeans3D / dscales / drotations are held
-    to 2e-3 of their max."""
+    ~1e-6 relative, and the chain amplifies that in the covariance-derived gradients (upstream's
+    fp32 atomics have the same property).  Forward stays bit-exact; dmeans2D / dopacity / dsh keep
+    the 1e-5 bound; dmeans3D / dscales / drotations are held to 5e-5 of their max (round 6: measured
+    2.3e-5, drotations; the bound was 2e-3 through round 5).  Against the independent fp64 dense
+    reference, which also rounds no per-pixel term to fp32, the same needles sit at up to 8.9e-4 of
+    the max (test_gpu_dense.py::test_hip_vs_dense_large_and_needle_splats, bound 1e-3): that
+    distance is the fp32 per-pixel terms through the ill-conditioned chain, not the summation."""
     cam, sc = _large_splat_scene(anisotropy=60.0)
     W, H = cam.image_width, cam.image_height
     bg = np.array([0.1, 0.2, 0.3], np.float32)
@@ -404,8 +411,8 @@ def test_needle_splats_conditioning(oracle, device):
     _tol_check(g("opacities"), gr["dopacity"], "dopacity")
     _tol_check(g("shs"), gr["dsh"], "dsh")
     for k, rk in (("means3D", "dmeans3D"), ("scales", "dscales"), ("rotations", "drotations")):
-        _tol_check(g(k), gr[rk], rk, rtol=1e-5, frac=2e-3)
-    # the 2e-3 above is the conditioning, not the device: an fp32 order of the oracle's own sums
+        _tol_check(g(k), gr[rk], rk, rtol=1e-5, frac=5e-5)
+    # the 5e-5 above is the conditioning, not the device: an fp32 order of the oracle's own sums
     # moves these gradients as far (and the device stays within NOISE_FACTOR of that)
     noise = _check_chain_noise(leaves, gr, oracle.backward_f32_acc(osc, dpix))
     assert max(d32 / s for _, d32, s in noise.values()) > 1e-5  # the chain really is ill-conditioned here
@@ -716,8 +723,9 @@ def test_randomized_configurations_vs_oracle(oracle, device, seed):
     """Randomized cameras (off-axis poses, FoV 35-80 deg, ragged image sizes), scene sizes, active /
     max SH degree, background, scale modifier and precomputed colour / covariance inputs, in the
     exact numerics mode: image and radii bit-exact against the oracle (plus every forward
-    intermediate when scale_modifier is 1), gradients at the backward tolerance (covariance chain
-    at 1e-4 of its max: random scales include large splats)."""
+    intermediate when scale_modifier is 1), every gradient at the 1e-5 contract, the covariance
+    chain included (round 6: measured max 4.4e-7 of the max over the 24 cases; the chain bound was
+    1e-4 through round 5)."""
     cam, sc, bg, mod, deg, colors, cov = _random_case(seed, oracle)
     W, H = cam.image_width, cam.image_height
     cov_mod = 1.0 if cov is not None else mod  # a precomputed covariance already carries the modifier
@@ -731,7 +739,7 @@ def test_randomized_configurations_vs_oracle(oracle, device, seed):
     np.testing.assert_array_equal(radii.cpu().numpy(), ofw["radii"])
     np.testing.assert_array_equal(img.detach().cpu().numpy(), ofw["color"])
     gr = oracle.backward(osc, dpix)
-    _check_backward(gr, leaves, colors=colors, cov3D=cov, chain_frac=1e-4)
+    _check_backward(gr, leaves, colors=colors, cov3D=cov)
     _check_chain_noise(leaves, gr, oracle.backward_f32_acc(osc, dpix))
 
 
