@@ -491,7 +491,10 @@ class ShardedAdam:
         steps = [self.opt._advance(p)[2] for p in params]
         lrs = [float(g["lr"]) for g in groups]
         wds = [float(g.get("weight_decay", 0.0)) for g in groups]
-        chunks, Pm = self.plan(P)
+        local = not (dist.is_available() and dist.is_initialized())
+        # no process group (one replica): nothing to exchange, so nothing to chunk or overlap -- one
+        # update of every row, as FusedAdam.step
+        chunks, Pm = ([(0, P, P)], P) if local else self.plan(P)
         dev = b.flat.device
         on_dev = b.flat.is_cuda
         deferred = bool(b._deferred)
@@ -508,8 +511,7 @@ class ShardedAdam:
         data = [p.detach().view(P, -1) for p in params]
         mv = [(m.view(P, -1), v.view(P, -1)) for m, v in moments]
         works = []
-        local = not (dist.is_available() and dist.is_initialized())
-        overlap = self.overlap and on_dev
+        overlap = self.overlap and on_dev and not local
         pending = []
         zero_ev = None
         last = len(chunks) - 1
