@@ -539,8 +539,11 @@ def main():
 
     vp_train = None
     if args.vp_train_steps > 0:
-        vp_train = vp_train_bench(sc, cams, my_views, deg, dev, args.vp_train_steps, max(2, args.warmup // 3), world,
-                                  args.allreduce_chunks)
+        try:
+            vp_train = vp_train_bench(sc, cams, my_views, deg, dev, args.vp_train_steps, max(2, args.warmup // 3),
+                                      world, args.allreduce_chunks)
+        except Exception as e:  # a secondary measurement: report its failure in the line, keep the line
+            vp_train = {"error": f"{type(e).__name__}: {e}"[:400]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

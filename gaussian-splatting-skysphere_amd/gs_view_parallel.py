@@ -74,6 +74,7 @@ class GradBucket:
     def _bind(self, params):
         from diff_gaussian_rasterization import register_gradient_sink
 
+        self._hooks = []
         for p in params:
             if p.dtype != torch.float32:
                 raise TypeError("GradBucket: float32 parameters only")
@@ -89,6 +90,7 @@ class GradBucket:
             p.grad = v
             self.views[id(p)] = v
             register_gradient_sink(p, self)
+            self._hooks.append(p.register_hook(self._grad_hook))
         self._fresh = {}  # id(p) -> _version of the view at zero_grad (lazy mode: not written yet)
         self.zero_grad()
 
@@ -112,6 +114,18 @@ class GradBucket:
 
         for p in self.params:
             unregister_gradient_sink(p)
+        for h in getattr(self, "_hooks", []):
+            h.remove()
+        self._hooks = []
+
+    def _grad_hook(self, grad):
+        """A gradient about to be accumulated into a bucket view by autograd (outside the sink
+        protocol): its stream waits for a foreign zero-fill of the bucket first (after_foreign_read),
+        so no backward can race it even without before_backward()."""
+        ev = self._zero_wait
+        if ev is not None and grad.is_cuda:
+            torch.cuda.current_stream(grad.device).wait_event(ev)
+        return None
 
     def _check_bound(self):
         """Every parameter's .grad must be its bucket view.  optimizer.zero_grad(set_to_none=True)
@@ -135,13 +149,15 @@ class GradBucket:
 
     def before_backward(self) -> None:
         """Before a backward whose gradients reach the bucket outside the sink protocol (autograd's
-        accumulation into the .grad views): the current stream waits for a foreign zero-fill."""
-        ev, self._zero_wait = self._zero_wait, None
+        accumulation into the .grad views): the current stream waits for a foreign zero-fill now
+        (the parameters' gradient hooks also wait for it, on the accumulating stream)."""
+        ev = self._zero_wait
         if ev is not None and self.flat.is_cuda:
             torch.cuda.current_stream(self.flat.device).wait_event(ev)
 
     def zero_grad(self):
         self._check_bound()
+        self._zero_wait = None
         foreign, self._foreign = self._foreign, None
         if foreign is not None:
             ev, st, zeroed = foreign
