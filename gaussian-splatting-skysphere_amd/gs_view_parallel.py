@@ -123,7 +123,7 @@ class GradBucket:
         protocol): its stream waits for a foreign zero-fill of the bucket first (after_foreign_read),
         so no backward can race it even without before_backward()."""
         ev = self._zero_wait
-        if ev is not None and grad.is_cuda:
+        if ev is not None and grad is not None and grad.is_cuda:
             torch.cuda.current_stream(grad.device).wait_event(ev)
         return None
 
