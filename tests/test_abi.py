@@ -104,3 +104,68 @@ def test_numerics_mode_default_and_env():
     env["GSRAST_EXACT_EXP"] = "1"
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
     assert out.stdout.split() == ["1", "0"]
+
+
+def test_geom_flags_offset_lies_in_the_counters():
+    """gs_geom_flags_offset (ABI 17): a 4-aligned word inside the geometry buffer, in its 64-B
+    counters block (CNT_ERR = word 2), for every P."""
+    from diff_gaussian_rasterization import _native
+
+    lib = _native.load()
+    for P in (0, 1, 255, 256, 3000, 1_000_000, 5_000_000):
+        off = lib.gs_geom_flags_offset(P)
+        assert off % 4 == 0 and off + 4 <= lib.gs_geom_buffer_bytes(P), P
+        assert (off - 8) % 256 == 0, P  # the counters block is 256-B aligned, the flags are its word 2
+
+
+def test_row_waits_validation_on_the_host():
+    """gs_set_row_waits (ABI 17) checks its chunk bounds on the host (no GPU call): from row 0,
+    increasing, at most 64 chunks; n = 0 clears; null events are allowed (nothing to wait for)."""
+    import ctypes
+
+    from diff_gaussian_rasterization import _native
+
+    lib = _native.load()
+
+    def set_(bounds):
+        n = len(bounds) - 1
+        b = (ctypes.c_int * len(bounds))(*bounds)
+        e = (ctypes.c_void_p * max(n, 1))()
+        return lib.gs_set_row_waits(n, ctypes.cast(b, ctypes.c_void_p), ctypes.cast(e, ctypes.c_void_p))
+
+    assert set_([0, 100, 4096]) == 0
+    assert lib.gs_set_row_waits(0, None, None) == 0
+    assert set_([1, 100]) != 0 and b"row 0" in lib.gs_last_error()
+    assert set_([0, 100, 100]) != 0 and b"increase" in lib.gs_last_error()
+    assert set_(list(range(0, 66 * 10, 10))) != 0  # 65 chunks
+    assert lib.gs_set_row_waits(-1, None, None) != 0
+    assert lib.gs_set_row_waits(0, None, None) == 0
+
+
+def test_row_chunks_follow_the_preprocess_launch_rule():
+    """gs_train.row_chunks (the activation's chunks) uses the rasterizer's rule
+    (csrc/gs_forward.hip launch_row_chunks): 256-row blocks, a block in the chunk that holds its last
+    row; the chunks are contiguous, cover [0, P), and keep every event in order."""
+    import gs_train
+
+    evs = [object() for _ in range(4)]
+    for P in (1, 255, 256, 700, 1000, 5000, 100_000):
+        for cuts in ([0, P], [0, P // 3, 2 * P // 3, P], [0, 1, 2, P], [0, 256, 512, 768, P]):
+            cuts = sorted(set(min(max(c, 0), P) for c in cuts))
+            if len(cuts) < 2 or cuts[0] != 0 or cuts[-1] != P:
+                continue
+            waits = [(cuts[k], cuts[k + 1], evs[k % 4]) for k in range(len(cuts) - 1)]
+            out = gs_train.row_chunks(P, waits)
+            assert out[0][0] == 0 and out[-1][1] == P
+            assert all(out[k][1] == out[k + 1][0] for k in range(len(out) - 1))
+            assert all(lo % 256 == 0 for lo, _, _ in out)
+            # the block holding row r launches in a chunk whose waits include the chunk of r
+            seen = [e for _, _, e in out if e is not None]
+            assert seen == [e for _, _, e in waits][:len(seen)]
+            for lo, hi, _ in out:
+                for r in (lo, hi - 1):
+                    if lo < hi:
+                        last_row = min(256 * (r // 256) + 255, P - 1)
+                        k_needed = next(k for k, (a, b, _) in enumerate(waits) if a <= last_row < b)
+                        k_have = sum(1 for lo2, _, e in out if e is not None and lo2 <= lo)
+                        assert k_have >= k_needed + 1 or (k_needed == len(waits) - 1 and k_have == len(seen)), (P, cuts)
