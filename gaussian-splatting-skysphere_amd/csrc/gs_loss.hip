@@ -70,9 +70,16 @@ __device__ __forceinline__ void stage_tiles(float (*dst)[SS_IN][SS_LI], const fl
 }
 
 __device__ __forceinline__ void ld16(const float* row, float* v) {
+  // 16-B aligned (row strides and c0 are multiples of 4 floats): one ds_read_b128 per quarter.
+  // The empty asm keeps each 16-B load whole: otherwise the loads shrink to the used elements and
+  // are re-paired as ds_read2_b64 across the 16-B slots, which banks on (a/4) mod 32 and conflicts
+  // 2-way over the 16 rows a lane group reads.
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f* r4 = reinterpret_cast<const v4f*>(row);
 #pragma unroll
   for (int q = 0; q < 4; q++) {
-    const float4 t = reinterpret_cast<const float4*>(row)[q];
+    v4f t = r4[q];
+    asm volatile("" : "+v"(t));
     v[4 * q] = t.x, v[4 * q + 1] = t.y, v[4 * q + 2] = t.z, v[4 * q + 3] = t.w;
   }
 }
