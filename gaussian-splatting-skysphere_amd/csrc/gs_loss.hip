@@ -8,7 +8,7 @@
 // fused photometric loss, the |x - y| sum) and the three per-pixel partials dS/dmu1, dS/dE[x^2],
 // dS/dE[xy]; a second kernel filters those partials with the same window (the adjoint of a
 // symmetric, zero-padded correlation) and forms dL/dimg1 (fused loss: plus the L1 term).
-// 1080p x 3 planes: fwd 64 us, bwd 54 us (round 1's 16x16 tiles without register reuse: 103 / 79).
+// 1080p x 3 planes: fwd 64 us, bwd 52 us (round 1's 16x16 tiles without register reuse: 103 / 79).
 //
 //   S = (2 m1 m2 + C1)(2 s12 + C2) / ((m1^2 + m2^2 + C1)(s11 + s22 + C2)),
 //   s11 = E[x^2] - m1^2, s22 = E[y^2] - m2^2, s12 = E[xy] - m1 m2
@@ -22,7 +22,7 @@
 
 namespace gs {
 
-// 32x32 output tiles, 256 threads.  The window is applied as two 1-D passes through LDS with
+// 32x32 output tiles, 256 (forward) / 384 (backward) threads.  The window is applied as two 1-D passes through LDS with
 // register reuse: the horizontal pass gives each thread 4 adjacent outputs of one row (16 inputs
 // read as four 16-B LDS loads, products formed once per input), the vertical pass 4 adjacent
 // outputs of one column (14 row values per moment).  Row strides are chosen for conflict-free
@@ -35,7 +35,6 @@ constexpr int SS_LI = 44;                // input row stride (floats)
 constexpr int SS_LH = 36;                // horizontal-result row stride (floats)
 constexpr int SS_HG = SS_IN * (SS_T / 4);  // 336 horizontal groups of 4 outputs
 static_assert(SS_LI >= 4 * (SS_T / 4 - 1) + 16, "the last group's 16-B loads stay in the row");
-static_assert(SS_HG <= 512, "two horizontal groups per thread");
 constexpr int SS_FWD_LDS = 2 * SS_IN * SS_LI > 5 * SS_IN * SS_LH ? 2 * SS_IN * SS_LI : 5 * SS_IN * SS_LH;
 constexpr int SS_BWD_LDS = 3 * SS_IN * SS_LI > 3 * SS_IN * SS_LH ? 3 * SS_IN * SS_LI : 3 * SS_IN * SS_LH;
 
@@ -46,15 +45,24 @@ struct SsimWin {
 // stage a 42x42 halo tile of NP planes (zero outside the image: conv2d's padding).  Every load of
 // the thread is issued before the first LDS store, so the 7 x NP global loads are in flight
 // together (a load -> store loop waits out one memory latency per element).
-constexpr int SS_STAGE = (SS_IN * SS_IN + 255) / 256;  // 7 elements per thread and plane
-template <int NP>
+// The backward runs SS_BWD_NT = 384 threads (6 waves): one horizontal group per thread (336), the
+// first four waves take the vertical pass (53.1 -> 51.8 us at 1080p x 3, with the image loads
+// issued at the start).  The forward keeps 256 (two groups for the first two waves): its vertical
+// pass and epilogue are the long phase, and at 6 waves per workgroup (88 VGPRs) only 3 workgroups
+// share a CU in it against 4 -- measured 63.8 -> 73.4 us; nor did its moments 0-1 stored early
+// (102 VGPRs: 62.5-65.8 -> 65.0-66.1 us) or that at 5 waves per SIMD by attribute (36 B of
+// spills: 68.9-73.9 us) pay.
+constexpr int SS_BWD_NT = 384;
+static_assert(SS_HG <= SS_BWD_NT && SS_BWD_NT % 64 == 0, "one horizontal group per thread");
+template <int NP, int NT>
 __device__ __forceinline__ void stage_tiles(float (*dst)[SS_IN][SS_LI], const float* const* src, int H, int W, int y0,
                                             int x0) {
-  float v[NP][SS_STAGE];
-  int rr[SS_STAGE], cc[SS_STAGE];
+  constexpr int NS = (SS_IN * SS_IN + NT - 1) / NT;  // elements per thread and plane: 7 (256), 5 (384)
+  float v[NP][NS];
+  int rr[NS], cc[NS];
 #pragma unroll
-  for (int q = 0; q < SS_STAGE; q++) {
-    const int i = threadIdx.x + 256 * q;
+  for (int q = 0; q < NS; q++) {
+    const int i = threadIdx.x + NT * q;
     rr[q] = i / SS_IN;
     cc[q] = i - rr[q] * SS_IN;
     const int y = y0 - SS_R + rr[q], x = x0 - SS_R + cc[q];
@@ -63,8 +71,8 @@ __device__ __forceinline__ void stage_tiles(float (*dst)[SS_IN][SS_LI], const fl
     for (int p = 0; p < NP; p++) v[p][q] = ok ? src[p][(size_t)y * W + x] : 0.0f;
   }
 #pragma unroll
-  for (int q = 0; q < SS_STAGE; q++)
-    if (threadIdx.x + 256 * q < SS_IN * SS_IN)
+  for (int q = 0; q < NS; q++)
+    if (threadIdx.x + NT * q < SS_IN * SS_IN)
 #pragma unroll
       for (int p = 0; p < NP; p++) dst[p][rr[q]][cc[q]] = v[p][q];
 }
@@ -107,7 +115,7 @@ __global__ __launch_bounds__(256) void k_ssim_fwd(int H, int W, SsimWin win, con
   const int tid = threadIdx.x;
   {
     const float* src[2] = {img1 + plane * HW, img2 + plane * HW};
-    stage_tiles<2>(sxy, src, H, W, y0, x0);
+    stage_tiles<2, 256>(sxy, src, H, W, y0, x0);
   }
   lds_barrier();
   // horizontal pass: group g -> row g % 42, outputs 4 (g / 42) .. + 3 (consecutive lanes, consecutive
@@ -270,10 +278,10 @@ __global__ __launch_bounds__(256) void k_ssim_plane_sum(int tiles, const float* 
 // otherwise dimg1 = scale[plane / C] dSSIM-sum/dimg1.  Same tiling and passes as k_ssim_fwd, over
 // the three partial maps.
 template <bool FUSED>
-__global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, int C, SsimWin win, const float* __restrict__ img1,
-                                                  const float* __restrict__ img2, const float* __restrict__ dmaps,
-                                                  const float* __restrict__ scale, float kS, float kL,
-                                                  float* __restrict__ dimg1) {
+__global__ __launch_bounds__(SS_BWD_NT) void k_ssim_bwd(int H, int W, int C, SsimWin win, const float* __restrict__ img1,
+                                                    const float* __restrict__ img2, const float* __restrict__ dmaps,
+                                                    const float* __restrict__ scale, float kS, float kL,
+                                                    float* __restrict__ dimg1) {
   // the staged maps, then (after the horizontal pass) the filtered maps over them: 22 KB
   __shared__ __attribute__((aligned(16))) float s_lds[SS_BWD_LDS];
   float(*sd)[SS_IN][SS_LI] = reinterpret_cast<float(*)[SS_IN][SS_LI]>(s_lds);
@@ -284,15 +292,28 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, int C, SsimWin w
   const int tid = threadIdx.x;
   {
     const float* src[3] = {dmaps + plane * HW, dmaps + PHW + plane * HW, dmaps + 2 * PHW + plane * HW};
-    stage_tiles<3>(sd, src, H, W, y0, x0);
+    stage_tiles<3, SS_BWD_NT>(sd, src, H, W, y0, x0);
+  }
+  // the vertical pass's threads (the first four waves): column c, rows 4 j .. 4 j + 3; their 8
+  // image loads are issued now and land during the horizontal pass
+  const bool vt = tid < 256;
+  int c, j;
+  vmap(tid, c, j);
+  const int px = x0 + c;
+  float xs[4], ys[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int py = y0 + 4 * j + i;
+    const bool ok = vt && px < W && py < H;
+    const size_t o = ok ? plane * HW + (size_t)py * W + px : 0;
+    xs[i] = ok ? img1[o] : 0.f;
+    ys[i] = ok ? img2[o] : 0.f;
   }
   lds_barrier();
-  float o[2][3][4];
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const int g = tid + 256 * h;
-    if (g >= SS_HG) break;
-    const int r = g % SS_IN, c0 = 4 * (g / SS_IN);
+  const bool hg = tid < SS_HG;
+  const int r = tid % SS_IN, c0 = 4 * (tid / SS_IN);
+  float o[3][4];
+  if (hg) {
 #pragma unroll
     for (int m = 0; m < 3; m++) {
       float x[16];
@@ -302,23 +323,18 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, int C, SsimWin w
         float a = 0.f;
 #pragma unroll
         for (int k = 0; k < 2 * SS_R + 1; k++) a = __builtin_fmaf(win.w[k], x[i + k], a);
-        o[h][m][i] = a;
+        o[m][i] = a;
       }
     }
   }
   lds_barrier();
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const int g = tid + 256 * h;
-    if (g >= SS_HG) break;
-    const int r = g % SS_IN, c0 = 4 * (g / SS_IN);
+  if (hg) {
 #pragma unroll
     for (int m = 0; m < 3; m++)
-      *reinterpret_cast<float4*>(&sh[m][r][c0]) = make_float4(o[h][m][0], o[h][m][1], o[h][m][2], o[h][m][3]);
+      *reinterpret_cast<float4*>(&sh[m][r][c0]) = make_float4(o[m][0], o[m][1], o[m][2], o[m][3]);
   }
   lds_barrier();
-  int c, j;
-  vmap(tid, c, j);
+  if (!vt || px >= W) return;
   float gm[3][4];
 #pragma unroll
   for (int m = 0; m < 3; m++) {
@@ -333,17 +349,7 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(int H, int W, int C, SsimWin w
       gm[m][i] = a;
     }
   }
-  const int px = x0 + c;
-  if (px >= W) return;
   const float sc = FUSED ? scale[0] : scale[plane / C];
-  float xs[4], ys[4];  // the 8 image loads issued together
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int py = y0 + 4 * j + i;
-    const size_t o = plane * HW + (size_t)py * W + px;
-    xs[i] = py < H ? img1[o] : 0.f;
-    ys[i] = py < H ? img2[o] : 0.f;
-  }
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const int py = y0 + 4 * j + i;
@@ -387,7 +393,7 @@ void photometric_backward(int planes, int H, int W, const float* win11, const fl
   for (int k = 0; k < 2 * SS_R + 1; k++) w.w[k] = win11[k];
   const dim3 grid((W + SS_T - 1) / SS_T, (H + SS_T - 1) / SS_T, planes);
   const double n = (double)planes * (double)H * (double)W;
-  GS_LAUNCH("ssim_bwd", k_ssim_bwd<true>, grid, dim3(256), 0, st, H, W, 1, w, img, gt, dmaps, grad,
+  GS_LAUNCH("ssim_bwd", k_ssim_bwd<true>, grid, dim3(SS_BWD_NT), 0, st, H, W, 1, w, img, gt, dmaps, grad,
             (float)(-(double)lambda / n), (float)((1.0 - (double)lambda) / n), dimg);
 }
 
@@ -396,7 +402,7 @@ void ssim_backward(int planes, int C, int H, int W, const float* win11, const fl
   SsimWin w;
   for (int k = 0; k < 2 * SS_R + 1; k++) w.w[k] = win11[k];
   const dim3 grid((W + SS_T - 1) / SS_T, (H + SS_T - 1) / SS_T, planes);
-  GS_LAUNCH("ssim_bwd", k_ssim_bwd<false>, grid, dim3(256), 0, st, H, W, C, w, img1, img2, dmaps, scale, 0.0f, 0.0f,
+  GS_LAUNCH("ssim_bwd", k_ssim_bwd<false>, grid, dim3(SS_BWD_NT), 0, st, H, W, C, w, img1, img2, dmaps, scale, 0.0f, 0.0f,
             dimg1);
 }
 
