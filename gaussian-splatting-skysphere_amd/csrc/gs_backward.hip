@@ -939,7 +939,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd_stage(GaussianArgs g, Ca
     float row[KF];
 #pragma unroll
     for (int q = 0; q < Q; q++) {
-      const float4 r4 = *reinterpret_cast<const float4*>(&s_rows[t * SH_STAGE_ROW + 4 * q]);
+      const float4 r4 = lds_ld16(&s_rows[t * SH_STAGE_ROW + 4 * q]);
       row[4 * q] = r4.x, row[4 * q + 1] = r4.y, row[4 * q + 2] = r4.z, row[4 * q + 3] = r4.w;
     }
     // dL/dsh leaves through LDS: the per-Gaussian call must not store it (GS_ACC_SH set on its
@@ -1097,7 +1097,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd_adam(GaussianArgs g, Cam
     float row[KF];
 #pragma unroll
     for (int q = 0; q < Q; q++) {
-      const float4 r4 = *reinterpret_cast<const float4*>(&s_rows[t * SH_STAGE_ROW + 4 * q]);
+      const float4 r4 = lds_ld16(&s_rows[t * SH_STAGE_ROW + 4 * q]);
       row[4 * q] = r4.x, row[4 * q + 1] = r4.y, row[4 * q + 2] = r4.z, row[4 * q + 3] = r4.w;
     }
     RegSink gr;
@@ -1233,7 +1233,7 @@ __global__ __launch_bounds__(256) void k_backward_gaussians(GaussianArgs g, Fuse
     lds_barrier();
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-      const float4 t = *reinterpret_cast<const float4*>(&s_rows[threadIdx.x * BG_ROW + 4 * q]);
+      const float4 t = lds_ld16(&s_rows[threadIdx.x * BG_ROW + 4 * q]);
       row[4 * q] = t.x, row[4 * q + 1] = t.y, row[4 * q + 2] = t.z, row[4 * q + 3] = t.w;
     }
   }

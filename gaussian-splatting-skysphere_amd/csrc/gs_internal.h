@@ -76,6 +76,16 @@ struct __attribute__((aligned(4))) F3 {
 // instruction touching 64 cache lines.  SPLIT: features_dc's block (12 B per Gaussian, g.shs) and
 // features_rest's (180 B, g.shs_rest) are each contiguous; their 16-B pieces straddle rows and are
 // stored as dwords.  Needs 16-B aligned bases.  The caller puts a barrier after it.
+// A 16-B LDS read kept whole (one ds_read_b128): the compiler otherwise shrinks a float4 LDS load
+// to the elements it sees used and re-pairs the pieces as ds_read2_b32 / ds_read2_b64, which bank on
+// (a/4) mod 32 per 32-lane half and turn a row stride that is conflict-free for 16-B reads (52
+// floats here) into a 4-way conflict.
+__device__ __forceinline__ float4 lds_ld16(const float* p) {
+  typedef float v4f_t __attribute__((ext_vector_type(4)));
+  v4f_t t = *reinterpret_cast<const v4f_t*>(p);
+  asm volatile("" : "+v"(t));
+  return make_float4(t.x, t.y, t.z, t.w);
+}
 constexpr int SH_STAGE_ROW = 52;
 template <bool SPLIT>
 __device__ __forceinline__ void stage_sh_rows48(const GaussianArgs& g, int i0, int nG, float* s_rows) {
