@@ -27,6 +27,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c3")
 ap.add_argument("--reps", type=int, default=3, help="stamped launches (each one iteration after warm-up)")
 ap.add_argument("--out", default="")
+ap.add_argument("--raw", default="", help="also save the per-wave arrays of the last launch (npz)")
 a = ap.parse_args()
 P, deg, W, H = WL[a.workload]
 dev = torch.device("cuda:0")
@@ -134,6 +135,10 @@ for rep in range(a.reps):
         "per_xcd": per_xcd,
     }
     reports.append(rep_d)
+    if a.raw:
+        np.savez(a.raw, start_us=s_us, end_us=e_us, tile=(d[:, 2] >> 32).astype(np.int64), n_eff=n_eff, walked=walked,
+                 slots=nslots, xcc=xcc, simd_key=simd_key, launch_pos=np.nonzero(np.asarray(
+                     np.frombuffer(buf, dtype=np.uint64).reshape(slots, 5)[:, 1] != 0))[0])
     print(json.dumps(rep_d), flush=True)
 if a.out:
     with open(a.out, "w") as f:
