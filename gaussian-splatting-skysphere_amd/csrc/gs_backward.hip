@@ -1282,23 +1282,42 @@ __global__ __launch_bounds__(256) void k_backward_gaussians(GaussianArgs g, Fuse
     if (sr && !f_r)
       for (int k = 0; k < 4; k++) a_r[k] = out.drot[4 * i + k];
 
+    // a view's per-Gaussian inputs (visibility, record sum, clamp bits) are loaded one view ahead:
+    // the loop over the K views is not unrolled (K is a launch argument), so without it every view
+    // waited out its loads at 2 waves per SIMD
+    float an[GRAD_REC];
+    uint32_t tn = fv.v[0].tiles[i];
+    uint8_t cn = fv.v[0].clamped ? fv.v[0].clamped[i] : 0;
+    {
+      const float* rec = fv.v[0].gsum + (size_t)i * GRAD_REC;
+#pragma unroll
+      for (int k = 0; k < GRAD_REC; k++) an[k] = rec[k];
+    }
     for (int v = 0; v < fv.K; v++) {
       const ViewGrad& w = fv.v[v];
       float dcol[3] = {0.f, 0.f, 0.f}, dop = 0.f, dmean[3] = {0.f, 0.f, 0.f}, dcv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       float ds[3] = {0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f};
-      const bool vis = w.tiles[i] != 0;
-      if (vis) {
-        const float* rec = w.gsum + (size_t)i * GRAD_REC;
-        float a[GRAD_REC];
+      float a[GRAD_REC];
 #pragma unroll
-        for (int k = 0; k < GRAD_REC; k++) a[k] = rec[k];
+      for (int k = 0; k < GRAD_REC; k++) a[k] = an[k];
+      const bool vis = tn != 0;
+      const uint8_t clamp_bits = cn;
+      if (v + 1 < fv.K) {  // (uniform)
+        const ViewGrad& wn = fv.v[v + 1];
+        tn = wn.tiles[i];
+        cn = wn.clamped ? wn.clamped[i] : 0;
+        const float* rec = wn.gsum + (size_t)i * GRAD_REC;
+#pragma unroll
+        for (int k = 0; k < GRAD_REC; k++) an[k] = rec[k];
+      }
+      if (vis) {
         dcol[0] = a[0], dcol[1] = a[1], dcol[2] = a[2];
         dop = a[8];
         camera_grads(w.c, px, py, pz, cov3, a[5], a[6], a[7], a[3], a[4], dcv, dmean);
         if (DEG >= 0) {
           float shm[3];
           const float vx = px - w.c.campos[0], vy = py - w.c.campos[1], vz = pz - w.c.campos[2];
-          sh_backward<D, true, true>(row, g.M, vx, vy, vz, w.clamped[i], dcol, shm, dsh, f_sh);
+          sh_backward<D, true, true>(row, g.M, vx, vy, vz, clamp_bits, dcol, shm, dsh, f_sh);
           dmean[0] = dmean[0] + shm[0];
           dmean[1] = dmean[1] + shm[1];
           dmean[2] = dmean[2] + shm[2];
